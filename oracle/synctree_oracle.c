@@ -1,0 +1,701 @@
+/* synctree_oracle.c — CPU restatement of riak_ensemble's synctree.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library (as the checker); the
+ * product (riak_ensemble_amd, libsynctree_hip.so) never links or calls it.
+ *
+ * A literal, single-threaded restatement of src/synctree.erl over an ETS-like
+ * node store (src/synctree_ets.erl:32-66), in C for speed so that 100k–10M-key
+ * trees can be checked.  Citations (reference paths):
+ *   geometry            synctree.erl:151-170, 270-284
+ *   get_segment/hash    synctree.erl:251-259, ensure_binary 261-268
+ *   insert/update_path  synctree.erl:189-209
+ *   get                 synctree.erl:213-227
+ *   get_path/verify     synctree.erl:302-340
+ *   exchange_get        synctree.erl:231-237, verified_hashes 288-298
+ *   corrupt             synctree.erl:241-247
+ *   compare/exchange    synctree.erl:372-449, orddict_delta riak_ensemble_util.erl:115-141
+ *   rehash              synctree.erl:489-543
+ *   verify              synctree.erl:549-571
+ * plus ot_bulk_load(), which builds the segment level of a FRESH tree directly
+ * (equivalent to N sequential inserts: last writer wins, non-empty nodes only)
+ * followed by the restated rehash; tests pin that equivalence at small N.
+ *
+ * Key model: a key is (type, bytes) with type 0 = integer (bytes = <<K:64>>,
+ * i.e. ensure_binary, compared as signed int64), 1 = atom (utf8 text),
+ * 2 = binary.  Term order: integer < atom < binary; atoms/binaries compare
+ * bytewise with a proper prefix first (ERTS order).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include "md5_ref.h"
+
+#define OT_OK 0
+#define OT_NOTFOUND 1
+#define OT_CORRUPTED 2
+#define OT_EINVAL (-1)
+
+typedef struct {
+    const uint8_t *k, *v;
+    uint32_t klen, vlen;
+    uint8_t ktype;
+} oent;
+
+typedef struct {
+    uint64_t child;
+    uint8_t h[17];
+} ochild;
+
+typedef struct {
+    uint32_t n, cap;
+    oent *e;    /* segment level */
+    ochild *c;  /* inner levels */
+} onode;
+
+typedef struct arena_blk {
+    struct arena_blk *next;
+    size_t used, cap;
+    uint8_t data[];
+} arena_blk;
+
+typedef struct ot_tree {
+    uint64_t width, segments, shift, height, shift_max;
+    int rec_top_def;          /* #tree.top_hash field */
+    uint8_t rec_top[17];
+    int st_top_def;           /* stored {0,0} */
+    uint8_t st_top[17];
+    onode **lv;               /* lv[l][b] for l in 1..height+1 (dense) */
+    uint64_t *lvsize;
+    arena_blk *arena;
+} ot_tree;
+
+/* ------------------------------------------------------------------ */
+static uint8_t *arena_put(ot_tree *t, const uint8_t *p, size_t n) {
+    if (!t->arena || t->arena->used + n > t->arena->cap) {
+        size_t cap = n > (1u << 24) ? n : (1u << 24);
+        arena_blk *b = (arena_blk *)malloc(sizeof(arena_blk) + cap);
+        if (!b) abort();
+        b->next = t->arena; b->used = 0; b->cap = cap; t->arena = b;
+    }
+    uint8_t *d = t->arena->data + t->arena->used;
+    if (n) memcpy(d, p, n);
+    t->arena->used += n;
+    return d;
+}
+
+static int64_t be_i64(const uint8_t *p) {
+    uint64_t x = 0;
+    for (int i = 0; i < 8; i++) x = (x << 8) | p[i];
+    return (int64_t)x;
+}
+
+/* Erlang term order on the restated key domain. */
+static int key_cmp(uint8_t ta, const uint8_t *a, uint32_t la, uint8_t tb, const uint8_t *b, uint32_t lb) {
+    if (ta != tb) return ta < tb ? -1 : 1;
+    if (ta == 0) {
+        int64_t x = be_i64(a), y = be_i64(b);
+        return x < y ? -1 : (x > y ? 1 : 0);
+    }
+    uint32_t m = la < lb ? la : lb;
+    int c = memcmp(a, b, m);
+    if (c) return c < 0 ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+static void hash_seg(const onode *n, uint8_t out[17]) {
+    md5r_ctx c;
+    md5r_init(&c);
+    if (n)
+        for (uint32_t i = 0; i < n->n; i++) md5r_update(&c, n->e[i].v, n->e[i].vlen);
+    out[0] = 0;
+    md5r_final(&c, out + 1);
+}
+
+static void hash_inner(const onode *n, uint8_t out[17]) {
+    md5r_ctx c;
+    md5r_init(&c);
+    if (n)
+        for (uint32_t i = 0; i < n->n; i++) md5r_update(&c, n->c[i].h, 17);
+    out[0] = 0;
+    md5r_final(&c, out + 1);
+}
+
+/* ------------------------------------------------------------------ */
+ot_tree *ot_new(uint64_t width, uint64_t segments, int *err) {
+    *err = 0;
+    if (width < 2 || segments < 1) { *err = OT_EINVAL; return NULL; }
+    /* compute_height / compute_shift restated with the same libm calls */
+    double hd = log((double)segments) / log((double)width);
+    uint64_t height = (uint64_t)trunc(hd);
+    if ((uint64_t)trunc(pow((double)width, (double)height)) != segments) { *err = OT_EINVAL; return NULL; }
+    double sd = log((double)width) / log(2.0);
+    uint64_t shift = (uint64_t)trunc(sd);
+    if ((uint64_t)trunc(pow(2.0, (double)shift)) != width) { *err = OT_EINVAL; return NULL; }
+    if (segments > (1ull << 26)) { *err = OT_EINVAL; return NULL; }  /* dense store limit */
+    ot_tree *t = (ot_tree *)calloc(1, sizeof(ot_tree));
+    t->width = width; t->segments = segments; t->shift = shift; t->height = height;
+    t->shift_max = shift * height;
+    t->lv = (onode **)calloc(height + 2, sizeof(onode *));
+    t->lvsize = (uint64_t *)calloc(height + 2, sizeof(uint64_t));
+    uint64_t sz = 1;
+    for (uint64_t l = 1; l <= height + 1; l++) {
+        t->lvsize[l] = sz;
+        t->lv[l] = (onode *)calloc(sz, sizeof(onode));
+        sz *= width;
+    }
+    return t;
+}
+
+/* A node is "stored" when cap != 0 (allocated); n may be 0 (stored []). */
+static inline onode *node_at(ot_tree *t, uint64_t l, uint64_t b) { return &t->lv[l][b]; }
+static inline int node_stored(const onode *n) { return n->cap != 0; }
+
+static void node_clear(onode *n) {
+    free(n->e); free(n->c);
+    n->e = NULL; n->c = NULL; n->n = 0; n->cap = 0;
+}
+
+void ot_free(ot_tree *t) {
+    if (!t) return;
+    for (uint64_t l = 1; l <= t->height + 1; l++) {
+        for (uint64_t b = 0; b < t->lvsize[l]; b++) node_clear(&t->lv[l][b]);
+        free(t->lv[l]);
+    }
+    free(t->lv); free(t->lvsize);
+    while (t->arena) { arena_blk *n = t->arena->next; free(t->arena); t->arena = n; }
+    free(t);
+}
+
+uint64_t ot_height(ot_tree *t) { return t->height; }
+
+uint64_t ot_segment_of(ot_tree *t, const uint8_t *kbin, uint32_t klen) {
+    uint8_t d[16];
+    md5r(kbin, klen, d);
+    /* <<H:128>> rem Segments; Segments is a power of two (W^H, W = 2^shift) */
+    uint64_t lo = 0;
+    for (int i = 8; i < 16; i++) lo = (lo << 8) | d[i];
+    return t->segments == 1 ? 0 : (lo & (t->segments - 1));
+}
+
+/* orddict_find(Bucket, undefined, ParentContent) for inner content */
+static int inner_find(const onode *n, uint64_t child, const uint8_t **h) {
+    if (!n) return 0;
+    uint32_t lo = 0, hi = n->n;
+    while (lo < hi) {
+        uint32_t m = (lo + hi) / 2;
+        if (n->c[m].child < child) lo = m + 1; else hi = m;
+    }
+    if (lo < n->n && n->c[lo].child == child) { *h = n->c[lo].h; return 1; }
+    return 0;
+}
+
+/* verify_hash(Expected, Node) — synctree.erl:322-340 */
+static int verify_node(ot_tree *t, uint64_t l, const onode *n, int exp_def, const uint8_t *exp) {
+    uint32_t cnt = n ? n->n : 0;
+    if (!exp_def) return cnt == 0;
+    uint8_t h[17];
+    if (l == t->height + 1) hash_seg(n, h); else hash_inner(n, h);
+    return memcmp(h, exp, 17) == 0;
+}
+
+/* get_path restated: walks levels 1..target_level toward `bucket`
+ * (bucket is at target_level).  Returns OT_OK or OT_CORRUPTED. */
+static int get_path(ot_tree *t, uint64_t target_level, uint64_t bucket, uint32_t *cl, uint64_t *cb) {
+    int exp_def = t->rec_top_def;
+    const uint8_t *exp = t->rec_top;
+    for (uint64_t l = 1; l <= target_level; l++) {
+        uint64_t b = bucket >> (t->shift * (target_level - l));
+        onode *n = node_at(t, l, b);
+        if (!verify_node(t, l, n, exp_def, exp)) { *cl = (uint32_t)l; *cb = b; return OT_CORRUPTED; }
+        if (l == target_level) break;
+        uint64_t nb = bucket >> (t->shift * (target_level - l - 1));
+        const uint8_t *h = NULL;
+        exp_def = inner_find(n, nb, &h);
+        exp = h;
+    }
+    return OT_OK;
+}
+
+static void node_reserve_inner(onode *n, uint32_t want) {
+    if (want <= n->cap && n->cap) return;
+    uint32_t cap = n->cap ? n->cap * 2 : 4;
+    while (cap < want) cap *= 2;
+    n->c = (ochild *)realloc(n->c, cap * sizeof(ochild));
+    n->cap = cap;
+}
+
+static void node_reserve_seg(onode *n, uint32_t want) {
+    if (want <= n->cap && n->cap) return;
+    uint32_t cap = n->cap ? n->cap * 2 : 4;
+    while (cap < want) cap *= 2;
+    n->e = (oent *)realloc(n->e, cap * sizeof(oent));
+    n->cap = cap;
+}
+
+static void inner_store(onode *n, uint64_t child, const uint8_t h[17]) {
+    uint32_t lo = 0, hi = n->n;
+    while (lo < hi) {
+        uint32_t m = (lo + hi) / 2;
+        if (n->c[m].child < child) lo = m + 1; else hi = m;
+    }
+    if (lo < n->n && n->c[lo].child == child) { memcpy(n->c[lo].h, h, 17); return; }
+    node_reserve_inner(n, n->n + 1);
+    memmove(&n->c[lo + 1], &n->c[lo], (n->n - lo) * sizeof(ochild));
+    n->c[lo].child = child;
+    memcpy(n->c[lo].h, h, 17);
+    n->n++;
+}
+
+static int64_t seg_find(const onode *n, uint8_t kt, const uint8_t *k, uint32_t kl, uint32_t *pos) {
+    uint32_t lo = 0, hi = n ? n->n : 0;
+    while (lo < hi) {
+        uint32_t m = (lo + hi) / 2;
+        if (key_cmp(n->e[m].ktype, n->e[m].k, n->e[m].klen, kt, k, kl) < 0) lo = m + 1; else hi = m;
+    }
+    *pos = lo;
+    if (n && lo < n->n && key_cmp(n->e[lo].ktype, n->e[lo].k, n->e[lo].klen, kt, k, kl) == 0) return lo;
+    return -1;
+}
+
+/* insert/3 + update_path/4 (synctree.erl:189-209) */
+int ot_insert(ot_tree *t, uint8_t kt, const uint8_t *k, uint32_t kl, const uint8_t *v, uint32_t vl,
+              uint32_t *cl, uint64_t *cb) {
+    uint64_t seg = ot_segment_of(t, k, kl);
+    uint64_t H1 = t->height + 1;
+    if (get_path(t, H1, seg, cl, cb) != OT_OK) return OT_CORRUPTED;
+    /* segment: orddict:store(Key, Value) */
+    onode *sn = node_at(t, H1, seg);
+    uint32_t pos;
+    int64_t at = seg_find(sn, kt, k, kl, &pos);
+    const uint8_t *vc = arena_put(t, v, vl);
+    if (at >= 0) {
+        sn->e[at].v = vc; sn->e[at].vlen = vl;
+    } else {
+        node_reserve_seg(sn, sn->n + 1);
+        memmove(&sn->e[pos + 1], &sn->e[pos], (sn->n - pos) * sizeof(oent));
+        oent e; e.k = arena_put(t, k, kl); e.klen = kl; e.ktype = kt; e.v = vc; e.vlen = vl;
+        sn->e[pos] = e;
+        sn->n++;
+    }
+    uint8_t h[17];
+    hash_seg(sn, h);
+    uint64_t child = seg;
+    for (uint64_t l = t->height; l >= 1; l--) {
+        uint64_t b = child >> t->shift;
+        onode *n = node_at(t, l, b);
+        inner_store(n, child, h);
+        hash_inner(n, h);
+        child = b;
+    }
+    memcpy(t->rec_top, h, 17); t->rec_top_def = 1;
+    memcpy(t->st_top, h, 17); t->st_top_def = 1;
+    return OT_OK;
+}
+
+/* get/2 (synctree.erl:213-227) */
+int ot_get(ot_tree *t, uint8_t kt, const uint8_t *k, uint32_t kl, const uint8_t **vout, uint32_t *vlen,
+           uint32_t *cl, uint64_t *cb) {
+    if (!t->rec_top_def) return OT_NOTFOUND;
+    uint64_t seg = ot_segment_of(t, k, kl);
+    if (get_path(t, t->height + 1, seg, cl, cb) != OT_OK) return OT_CORRUPTED;
+    onode *sn = node_at(t, t->height + 1, seg);
+    uint32_t pos;
+    int64_t at = seg_find(sn, kt, k, kl, &pos);
+    if (at < 0) return OT_NOTFOUND;
+    *vout = sn->e[at].v; *vlen = sn->e[at].vlen;
+    return OT_OK;
+}
+
+/* corrupt/2 (synctree.erl:241-247): erase from the segment, no path update */
+void ot_corrupt(ot_tree *t, uint8_t kt, const uint8_t *k, uint32_t kl) {
+    uint64_t seg = ot_segment_of(t, k, kl);
+    onode *sn = node_at(t, t->height + 1, seg);
+    uint32_t pos;
+    int64_t at = seg_find(sn, kt, k, kl, &pos);
+    if (!node_stored(sn)) node_reserve_seg(sn, 1);   /* m_store of [] stores [] */
+    if (at >= 0) {
+        memmove(&sn->e[at], &sn->e[at + 1], (sn->n - at - 1) * sizeof(oent));
+        sn->n--;
+    }
+}
+
+/* rehash/4 (synctree.erl:511-535): returns #children; fills out[] hashes */
+static uint32_t rehash4(ot_tree *t, uint64_t level, uint64_t maxd, uint64_t bucket, onode **ret) {
+    if (level == maxd) {
+        onode *n = node_at(t, level, bucket);
+        *ret = n;
+        return n->n;
+    }
+    onode *me = node_at(t, level, bucket);
+    ochild buf[64];
+    ochild *ch = t->width <= 64 ? buf : (ochild *)malloc(t->width * sizeof(ochild));
+    uint32_t nc = 0;
+    uint64_t x0 = bucket * t->width;
+    for (uint64_t x = x0; x < x0 + t->width; x++) {
+        onode *cn;
+        uint32_t cnt = rehash4(t, level + 1, maxd, x, &cn);
+        if (cnt) {
+            ch[nc].child = x;
+            if (level + 1 == t->height + 1) hash_seg(cn, ch[nc].h); else hash_inner(cn, ch[nc].h);
+            nc++;
+        }
+    }
+    if (nc == 0) {
+        node_clear(me);                      /* delete_existing_batch */
+    } else {
+        node_reserve_inner(me, nc);
+        memcpy(me->c, ch, nc * sizeof(ochild));
+        me->n = nc;
+    }
+    if (ch != buf) free(ch);
+    *ret = me;
+    return nc;
+}
+
+/* rehash/2 (synctree.erl:497-509) */
+void ot_rehash(ot_tree *t, int upper) {
+    uint64_t maxd = upper ? t->height : t->height + 1;
+    if (maxd == 0) return;   /* rehash_upper at Height 0 never terminates in the reference */
+    onode *n;
+    uint32_t cnt = rehash4(t, 1, maxd, 0, &n);
+    if (cnt == 0) {
+        t->st_top_def = 0; t->rec_top_def = 0;
+    } else {
+        uint8_t h[17];
+        if (maxd == 1 && maxd == t->height + 1) hash_seg(n, h); else hash_inner(n, h);
+        memcpy(t->st_top, h, 17); memcpy(t->rec_top, h, 17);
+        t->st_top_def = 1; t->rec_top_def = 1;
+    }
+}
+
+/* verify/5 (synctree.erl:560-571) */
+static int verify5(ot_tree *t, uint64_t level, uint64_t maxd, uint64_t bucket, int exp_def, const uint8_t *exp) {
+    onode *n = node_at(t, level, bucket);
+    if (!verify_node(t, level, n, exp_def, exp)) return 0;
+    if (level == maxd) return 1;
+    for (uint32_t i = 0; i < n->n; i++)
+        if (!verify5(t, level + 1, maxd, n->c[i].child, 1, n->c[i].h)) return 0;
+    return 1;
+}
+
+int ot_verify(ot_tree *t, int upper) {
+    uint64_t maxd = upper ? t->height : t->height + 1;
+    if (maxd == 0) return -1;   /* verify_upper at Height 0 crashes in the reference */
+    return verify5(t, 1, maxd, 0, t->rec_top_def, t->rec_top);
+}
+
+int ot_top_hash(ot_tree *t, uint8_t out[17]) {
+    if (t->rec_top_def) memcpy(out, t->rec_top, 17);
+    return t->rec_top_def;
+}
+
+/* ------------------------------------------------------------------ */
+/* node images (what Mod:fetch({L,B}, [], State) returns) */
+int64_t ot_node_count(ot_tree *t, uint32_t level, uint64_t bucket) {
+    if (level < 1 || level > t->height + 1 || bucket >= t->lvsize[level]) return -1;
+    return node_at(t, level, bucket)->n;
+}
+int ot_node_stored(ot_tree *t, uint32_t level, uint64_t bucket) {
+    return node_stored(node_at(t, level, bucket));
+}
+void ot_node_child(ot_tree *t, uint32_t level, uint64_t bucket, uint32_t i, uint64_t *child, uint8_t h[17]) {
+    onode *n = node_at(t, level, bucket);
+    *child = n->c[i].child;
+    memcpy(h, n->c[i].h, 17);
+}
+void ot_node_entry(ot_tree *t, uint32_t level, uint64_t bucket, uint32_t i, uint8_t *kt, const uint8_t **k,
+                   uint32_t *kl, const uint8_t **v, uint32_t *vl) {
+    onode *n = node_at(t, level, bucket);
+    *kt = n->e[i].ktype; *k = n->e[i].k; *kl = n->e[i].klen; *v = n->e[i].v; *vl = n->e[i].vlen;
+}
+
+/* Entries recorded for every bucket of `level` in its parent node (level 1:
+ * the #tree top hash).  present[b] = 1 and hashes[17*b..] when recorded. */
+void ot_level_entries(ot_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes) {
+    uint64_t sz = t->lvsize[level];
+    memset(present, 0, sz);
+    memset(hashes, 0, sz * 17);
+    if (level == 1) {
+        if (t->rec_top_def) { present[0] = 1; memcpy(hashes, t->rec_top, 17); }
+        return;
+    }
+    for (uint64_t p = 0; p < t->lvsize[level - 1]; p++) {
+        onode *n = node_at(t, level - 1, p);
+        for (uint32_t i = 0; i < n->n; i++) {
+            uint64_t c = n->c[i].child;
+            if (c < sz) { present[c] = 1; memcpy(hashes + 17 * c, n->c[i].h, 17); }
+        }
+    }
+}
+
+/* raw backend stores (m_store/m_batch), used by corruption fixtures */
+void ot_store_inner(ot_tree *t, uint32_t level, uint64_t bucket, uint32_t n, const uint64_t *children,
+                    const uint8_t *hashes) {
+    onode *nd = node_at(t, level, bucket);
+    node_clear(nd);
+    node_reserve_inner(nd, n ? n : 1);
+    for (uint32_t i = 0; i < n; i++) { nd->c[i].child = children[i]; memcpy(nd->c[i].h, hashes + 17 * i, 17); }
+    nd->n = n;
+}
+void ot_store_segment(ot_tree *t, uint64_t seg, uint32_t n, const uint8_t *ktype, const uint8_t *kheap,
+                      const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff) {
+    onode *nd = node_at(t, t->height + 1, seg);
+    node_clear(nd);
+    node_reserve_seg(nd, n ? n : 1);
+    for (uint32_t i = 0; i < n; i++) {
+        oent e;
+        e.ktype = ktype[i];
+        e.klen = (uint32_t)(koff[i + 1] - koff[i]);
+        e.k = arena_put(t, kheap + koff[i], e.klen);
+        e.vlen = (uint32_t)(voff[i + 1] - voff[i]);
+        e.v = arena_put(t, vheap + voff[i], e.vlen);
+        nd->e[i] = e;
+    }
+    nd->n = n;
+}
+void ot_delete_node(ot_tree *t, uint32_t level, uint64_t bucket) { node_clear(node_at(t, level, bucket)); }
+void ot_store_top(ot_tree *t, const uint8_t *h, int also_record) {
+    if (h) { memcpy(t->st_top, h, 17); t->st_top_def = 1; } else t->st_top_def = 0;
+    if (also_record) { t->rec_top_def = t->st_top_def; memcpy(t->rec_top, t->st_top, 17); }
+}
+
+/* ------------------------------------------------------------------ */
+/* compare (synctree.erl:372-449) between two trees of the same geometry */
+typedef struct {
+    const uint8_t *k, *va, *vb;
+    uint32_t klen, vla, vlb;   /* vla/vlb == UINT32_MAX => '$none' */
+    uint8_t ktype;
+    uint64_t seg;
+} odiff_rec;
+
+typedef struct ot_diff {
+    odiff_rec *r;
+    uint64_t n, cap;
+} ot_diff;
+
+static void diff_push(ot_diff *d, odiff_rec r) {
+    if (d->n == d->cap) {
+        d->cap = d->cap ? d->cap * 2 : 64;
+        d->r = (odiff_rec *)realloc(d->r, d->cap * sizeof(odiff_rec));
+    }
+    d->r[d->n++] = r;
+}
+
+/* verified exchange_get of an inner or segment node; 0 ok / 2 corrupted */
+static int xget(ot_tree *t, uint64_t level, uint64_t bucket, onode **out, uint32_t *cl, uint64_t *cb) {
+    if (get_path(t, level, bucket, cl, cb) != OT_OK) return OT_CORRUPTED;
+    *out = node_at(t, level, bucket);
+    return OT_OK;
+}
+
+/* filter: 0 all, 1 local_only (drop remote-missing), 2 remote_only (drop local-missing) */
+ot_diff *ot_compare(ot_tree *a, ot_tree *b, int filter, int *status, uint32_t *clevel, uint64_t *cbucket,
+                    int *cside) {
+    ot_diff *res = (ot_diff *)calloc(1, sizeof(ot_diff));
+    *status = OT_OK;
+    /* level 0: [{0,TopA}] vs [{0,TopB}] — values compared exactly, never '$none' */
+    int same = (a->rec_top_def == b->rec_top_def) && (!a->rec_top_def || !memcmp(a->rec_top, b->rec_top, 17));
+    if (same) return res;
+    uint64_t *fr = (uint64_t *)malloc(sizeof(uint64_t));
+    uint64_t nf = 1;
+    fr[0] = 0;
+    uint64_t final = a->height + 1;
+    ot_diff *segd = (ot_diff *)calloc(1, sizeof(ot_diff));
+    uint64_t *segstart = NULL;
+    for (uint64_t level = 1; level <= final && nf; level++) {
+        uint64_t cap = nf * a->width, nn = 0;
+        uint64_t *nx = (uint64_t *)malloc((cap ? cap : 1) * sizeof(uint64_t));
+        if (level == final) segstart = (uint64_t *)calloc(nf + 1, sizeof(uint64_t));
+        for (uint64_t i = 0; i < nf; i++) {
+            onode *na, *nb;
+            if (xget(a, level, fr[i], &na, clevel, cbucket)) { *status = OT_CORRUPTED; *cside = 0; goto fail; }
+            if (xget(b, level, fr[i], &nb, clevel, cbucket)) { *status = OT_CORRUPTED; *cside = 1; goto fail; }
+            if (level < final) {
+                uint32_t x = 0, y = 0;
+                while (x < na->n || y < nb->n) {
+                    int c;
+                    if (x < na->n && y < nb->n) c = na->c[x].child < nb->c[y].child ? -1 : (na->c[x].child > nb->c[y].child ? 1 : 0);
+                    else c = x < na->n ? -1 : 1;
+                    if (c < 0) { if (filter != 1) nx[nn++] = na->c[x].child; x++; }
+                    else if (c > 0) { if (filter != 2) nx[nn++] = nb->c[y].child; y++; }
+                    else { if (memcmp(na->c[x].h, nb->c[y].h, 17)) nx[nn++] = na->c[x].child; x++; y++; }
+                }
+            } else {
+                segstart[i] = segd->n;
+                uint32_t x = 0, y = 0;
+                while (x < na->n || y < nb->n) {
+                    int c;
+                    if (x < na->n && y < nb->n)
+                        c = key_cmp(na->e[x].ktype, na->e[x].k, na->e[x].klen, nb->e[y].ktype, nb->e[y].k, nb->e[y].klen);
+                    else c = x < na->n ? -1 : 1;
+                    odiff_rec r;
+                    r.seg = fr[i];
+                    if (c < 0) {
+                        r.ktype = na->e[x].ktype; r.k = na->e[x].k; r.klen = na->e[x].klen;
+                        r.va = na->e[x].v; r.vla = na->e[x].vlen; r.vb = NULL; r.vlb = UINT32_MAX;
+                        if (filter != 1) diff_push(segd, r);
+                        x++;
+                    } else if (c > 0) {
+                        r.ktype = nb->e[y].ktype; r.k = nb->e[y].k; r.klen = nb->e[y].klen;
+                        r.va = NULL; r.vla = UINT32_MAX; r.vb = nb->e[y].v; r.vlb = nb->e[y].vlen;
+                        if (filter != 2) diff_push(segd, r);
+                        y++;
+                    } else {
+                        if (na->e[x].vlen != nb->e[y].vlen || memcmp(na->e[x].v, nb->e[y].v, na->e[x].vlen)) {
+                            r.ktype = na->e[x].ktype; r.k = na->e[x].k; r.klen = na->e[x].klen;
+                            r.va = na->e[x].v; r.vla = na->e[x].vlen; r.vb = nb->e[y].v; r.vlb = nb->e[y].vlen;
+                            diff_push(segd, r);
+                        }
+                        x++; y++;
+                    }
+                }
+            }
+        }
+        if (level == final) {
+            segstart[nf] = segd->n;
+            /* AccFun = Keys ++ Acc folded left => last segment's keys first */
+            for (uint64_t i = nf; i-- > 0;)
+                for (uint64_t j = segstart[i]; j < segstart[i + 1]; j++) diff_push(res, segd->r[j]);
+        }
+        free(fr);
+        fr = nx;
+        nf = nn;
+    }
+    free(fr);
+    free(segstart);
+    free(segd->r); free(segd);
+    return res;
+fail:
+    free(fr);
+    free(segstart);
+    free(segd->r); free(segd);
+    return res;
+}
+
+uint64_t ot_diff_count(ot_diff *d) { return d->n; }
+void ot_diff_get(ot_diff *d, uint64_t i, uint8_t *kt, const uint8_t **k, uint32_t *kl, const uint8_t **va,
+                 uint32_t *vla, const uint8_t **vb, uint32_t *vlb, uint64_t *seg) {
+    odiff_rec *r = &d->r[i];
+    *kt = r->ktype; *k = r->k; *kl = r->klen; *va = r->va; *vla = r->vla; *vb = r->vb; *vlb = r->vlb; *seg = r->seg;
+}
+void ot_diff_free(ot_diff *d) {
+    if (!d) return;
+    free(d->r); free(d);
+}
+
+/* ------------------------------------------------------------------ */
+/* Bulk load into a FRESH tree: sequential-insert semantics, then rehash. */
+static ot_tree *g_sort_tree;
+static const uint8_t *g_kt;
+static const uint8_t *g_kh;
+static const uint64_t *g_ko;
+
+static int cmp_idx(const void *x, const void *y) {
+    uint64_t i = *(const uint64_t *)x, j = *(const uint64_t *)y;
+    int c = key_cmp(g_kt[i], g_kh + g_ko[i], (uint32_t)(g_ko[i + 1] - g_ko[i]), g_kt[j], g_kh + g_ko[j],
+                    (uint32_t)(g_ko[j + 1] - g_ko[j]));
+    if (c) return c;
+    return i < j ? -1 : (i > j ? 1 : 0);
+}
+
+int ot_bulk_load(ot_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                 const uint8_t *vheap, const uint64_t *voff) {
+    uint64_t S = t->segments, H1 = t->height + 1;
+    for (uint64_t s = 0; s < S; s++)
+        if (node_stored(node_at(t, H1, s))) return OT_EINVAL;
+    if (t->rec_top_def) return OT_EINVAL;
+    uint32_t *seg = (uint32_t *)malloc(n * sizeof(uint32_t) + 1);
+    uint64_t *cnt = (uint64_t *)calloc(S + 1, sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; i++) {
+        seg[i] = (uint32_t)ot_segment_of(t, kheap + koff[i], (uint32_t)(koff[i + 1] - koff[i]));
+        cnt[seg[i] + 1]++;
+    }
+    for (uint64_t s = 0; s < S; s++) cnt[s + 1] += cnt[s];
+    uint64_t *order = (uint64_t *)malloc(n * sizeof(uint64_t) + 8);
+    uint64_t *fill = (uint64_t *)malloc((S + 1) * sizeof(uint64_t));
+    memcpy(fill, cnt, (S + 1) * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; i++) order[fill[seg[i]]++] = i;
+    /* copy payloads into the tree arena once */
+    uint8_t *kh = arena_put(t, kheap, koff[n]);
+    uint8_t *vh = arena_put(t, vheap, voff[n]);
+    g_sort_tree = t; g_kt = ktype; g_kh = kheap; g_ko = koff;
+    for (uint64_t s = 0; s < S; s++) {
+        uint64_t a = cnt[s], b = cnt[s + 1];
+        if (a == b) continue;
+        qsort(order + a, b - a, sizeof(uint64_t), cmp_idx);
+        onode *nd = node_at(t, H1, s);
+        node_reserve_seg(nd, (uint32_t)(b - a));
+        uint32_t m = 0;
+        for (uint64_t j = a; j < b; j++) {
+            uint64_t i = order[j];
+            /* last writer wins: skip i if the next one is the same key */
+            if (j + 1 < b) {
+                uint64_t i2 = order[j + 1];
+                if (key_cmp(ktype[i], kheap + koff[i], (uint32_t)(koff[i + 1] - koff[i]), ktype[i2], kheap + koff[i2],
+                            (uint32_t)(koff[i2 + 1] - koff[i2])) == 0)
+                    continue;
+            }
+            oent e;
+            e.ktype = ktype[i];
+            e.k = kh + koff[i]; e.klen = (uint32_t)(koff[i + 1] - koff[i]);
+            e.v = vh + voff[i]; e.vlen = (uint32_t)(voff[i + 1] - voff[i]);
+            nd->e[m++] = e;
+        }
+        nd->n = m;
+    }
+    free(seg); free(cnt); free(order); free(fill);
+    ot_rehash(t, 0);
+    return OT_OK;
+}
+
+/* Same, for 8-byte integer keys and fixed-width values (the bench inputs). */
+int ot_bulk_load_int64(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen) {
+    uint8_t *kt = (uint8_t *)calloc(n + 1, 1);
+    uint8_t *kh = (uint8_t *)malloc(n * 8 + 1);
+    uint64_t *ko = (uint64_t *)malloc((n + 1) * sizeof(uint64_t));
+    uint64_t *vo = (uint64_t *)malloc((n + 1) * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t x = (uint64_t)keys[i];
+        for (int j = 0; j < 8; j++) kh[8 * i + j] = (uint8_t)(x >> (56 - 8 * j));
+        ko[i] = 8 * i; vo[i] = (uint64_t)vlen * i;
+    }
+    ko[n] = 8 * n; vo[n] = (uint64_t)vlen * n;
+    int r = ot_bulk_load(t, n, kt, kh, ko, vals, vo);
+    free(kt); free(kh); free(ko); free(vo);
+    return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* Throughput-mode rehash for the CPU baseline: same result as ot_rehash(t,0)
+ * on a tree, with segment hashing spread over `threads` OpenMP threads. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+void ot_rehash_par(ot_tree *t, int threads) {
+    uint64_t H1 = t->height + 1;
+    uint64_t S = t->lvsize[H1];
+    if (t->height == 0 || t->width > 64) { ot_rehash(t, 0); return; }
+    /* level H entries from segments, in parallel over level-H parents */
+    uint64_t P = t->lvsize[H1 - 1];
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 64)
+#endif
+    for (int64_t p = 0; p < (int64_t)P; p++) {
+        onode *me = node_at(t, H1 - 1, (uint64_t)p);
+        ochild ch[64];
+        uint32_t nc = 0;
+        for (uint64_t x = (uint64_t)p * t->width; x < ((uint64_t)p + 1) * t->width && x < S; x++) {
+            onode *cn = node_at(t, H1, x);
+            if (cn->n) { ch[nc].child = x; hash_seg(cn, ch[nc].h); nc++; }
+        }
+        if (!nc) node_clear(me);
+        else { node_reserve_inner(me, nc); memcpy(me->c, ch, nc * sizeof(ochild)); me->n = nc; }
+    }
+    ot_rehash(t, 1);   /* levels 1..H-1 from the stored level-H nodes */
+}
+
+/* exported for the RFC 1321 known-answer tests */
+void ot_md5(const uint8_t *p, uint64_t n, uint8_t out[16]) { md5r(p, (size_t)n, out); }

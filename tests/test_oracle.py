@@ -1,0 +1,331 @@
+"""The oracle pinned: both CPU restatements vs RFC 1321, the reference's own
+synctree tests (test/synctree_pure.erl, test/synctree_remote.erl,
+test/synctree_eqc.erl property) and the committed golden fixtures.
+CPU only (no GPU needed)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_c as C
+import synctree_ref as R
+from riak_ensemble_amd import workload
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'synctree_golden.json')))
+
+
+def dec_key(d):
+    if d['t'] == 'int':
+        return int(d['v'])
+    if d['t'] == 'atom':
+        return d['v']
+    return bytes.fromhex(d['v'])
+
+
+def dec_val(v):
+    return v['atom'] if isinstance(v, dict) else bytes.fromhex(v)
+
+
+def dec_diff(lst):
+    return [(dec_key(k), (dec_val(a), dec_val(b))) for k, (a, b) in lst]
+
+
+def dec_result(r):
+    if isinstance(r, dict) and 'tuple' in r:
+        return tuple(r['tuple'])
+    if isinstance(r, dict):
+        return r['atom']
+    return bytes.fromhex(r)
+
+
+# ----------------------------------------------------------------- MD5 pins
+@pytest.mark.parametrize('msg,digest', GOLD['rfc1321'])
+def test_md5_rfc1321(msg, digest):
+    assert R.md5(msg.encode()).hex() == digest
+    assert C.md5(msg.encode()).hex() == digest
+
+
+def test_md5_c_vs_hashlib_lengths():
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 140)) + [255, 256, 1000, 4097]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert C.md5(b) == R.md5(b)
+
+
+# ----------------------------------------------------------------- segment map
+def test_segments_known():
+    segs = [R.get_segment(k, R.SEGMENTS) for k in range(1, 11)]
+    # keys 7..10 -> the descending segment order that test/synctree_remote.erl:37-39 relies on
+    assert segs[6:] == [744656, 431040, 393303, 166698]
+    assert segs == GOLD['segments_int_1_100'][:10]
+    t = C.OTree()
+    assert [t.segment_of(k) for k in range(1, 101)] == GOLD['segments_int_1_100']
+    for k, s in GOLD['segments_misc']:
+        assert R.get_segment(dec_key(k), R.SEGMENTS) == s
+        assert t.segment_of(dec_key(k)) == s
+
+
+# ----------------------------------------------------------------- synctree_pure
+@pytest.mark.parametrize('mod', ['synctree_ets', 'synctree_orddict'])
+def test_pure_basic(mod):
+    """test/synctree_pure.erl:28-37"""
+    t = R.build(100, mod)
+    assert R.get(42, t) == (420).to_bytes(8, 'big')
+    t2 = R.insert(42, (42).to_bytes(8, 'big'), t)
+    assert R.get(42, t2) == (42).to_bytes(8, 'big')
+    c = C.build(100)
+    assert c.get(42) == (420).to_bytes(8, 'big')
+    c.insert(42, (42).to_bytes(8, 'big'))
+    assert c.get(42) == (42).to_bytes(8, 'big')
+    assert c.top_hash().hex() == GOLD['basic']['top_after'] == t2.top_hash.hex()
+
+
+def test_pure_corrupt():
+    """test/synctree_pure.erl:43-54 (ets; orddict is disabled upstream too)"""
+    t = R.build(10)
+    assert R.get(4, t) == (40).to_bytes(8, 'big')
+    t2 = R.corrupt(4, t)
+    r = R.get(4, t2)
+    assert r[0] == 'corrupted'
+    t3 = R.rehash(t2)
+    assert R.get(4, t3) == 'notfound'
+    g = GOLD['corrupt']
+    c = C.build(10)
+    assert c.get(4) == dec_result(g['get4'])
+    c.corrupt(4)
+    assert c.get(4) == dec_result(g['get4_corrupt']) == r
+    assert c.insert(4, b'\x01') == dec_result(g['insert_into_corrupt'])
+    assert c.verify() == g['verify_corrupt'] and c.verify_upper() == g['verify_upper_corrupt']
+    c.rehash()
+    assert c.get(4) == dec_result(g['get4_rehashed']) == 'notfound'
+    assert c.top_hash().hex() == g['top_rehashed'] == t3.top_hash.hex()
+    assert c.verify() is True
+
+
+@pytest.mark.parametrize('mod', ['synctree_ets', 'synctree_orddict'])
+def test_pure_exchange(mod):
+    """test/synctree_pure.erl:60-68,82-84"""
+    t1, t2 = R.build(50, mod), R.build(40, mod)
+    res = R.local_compare(t1, t2)
+    assert sorted(res, key=lambda d: d[0]) == R.expected_diff(50, 10)
+    assert res == dec_diff(GOLD['exchange_50_40'])
+    assert C.build(50).compare(C.build(40)) == res
+    assert C.build(40).compare(C.build(50)) == dec_diff(GOLD['exchange_40_50'])
+
+
+def test_remote_exact_order():
+    """test/synctree_remote.erl:37-39 — unsorted result, exact order."""
+    exp = R.expected_diff(10, 4)
+    assert dec_diff(GOLD['remote_10_6']) == exp
+    assert C.build(10).compare(C.build(6)) == exp
+
+
+def test_top_hashes_and_levels():
+    for n, h in GOLD['top_build'].items():
+        assert R.build(int(n)).top_hash.hex() == h
+        assert C.build(int(n)).top_hash().hex() == h
+    c = C.build(100)
+    for lvl, nodes in GOLD['levels_build_100'].items():
+        lvl = int(lvl)
+        for b, content in nodes.items():
+            got = c.node(lvl, int(b))
+            if lvl <= c.height:
+                assert [[x, h.hex()] for x, h in got] == content
+            else:
+                assert [[{'t': 'int', 'v': str(k)}, v.hex()] for k, v in got] == content
+
+
+# ----------------------------------------------------------------- randomized cases
+def _c_tree(case, entries):
+    t = C.OTree(case['width'], case['segments'])
+    for k, v in entries:
+        t.insert(dec_key(k), bytes.fromhex(v))
+    return t
+
+
+@pytest.mark.parametrize('idx', range(len(GOLD['random_cases'])))
+def test_random_case_golden(idx):
+    case = GOLD['random_cases'][idx]
+    ta = _c_tree(case, case['a'])
+    tb = _c_tree(case, case['b_ops'])
+    top = ta.top_hash()
+    assert (top if isinstance(top, str) else top.hex()) == case['top_a']
+    top = tb.top_hash()
+    assert (top if isinstance(top, str) else top.hex()) == case['top_b']
+    assert ta.compare(tb) == dec_diff(case['diff_all'])
+    assert ta.compare(tb, ['local_only']) == dec_diff(case['diff_local_only'])
+    assert ta.compare(tb, ['remote_only']) == dec_diff(case['diff_remote_only'])
+    for lvl, nodes in case['levels_a'].items():
+        for b, content in nodes.items():
+            got = ta.node(int(lvl), int(b))
+            if int(lvl) <= ta.height:
+                assert [[x, h.hex()] for x, h in got] == content
+            else:
+                assert [[k, v] for k, v in got] == [[dec_key(k), bytes.fromhex(v)] for k, v in content]
+    assert ta.verify() and tb.verify()
+    if ta.height > 0:
+        assert ta.verify_upper()
+
+
+def test_both_filters_crash():
+    t = C.build(3)
+    with pytest.raises(ValueError):
+        t.compare(t, ['local_only', 'remote_only'])
+    with pytest.raises(R.ErlangCrash):
+        R.filter_type(['local_only', 'remote_only'])
+
+
+def test_bad_geometry():
+    for w, s in [(16, 1000), (3, 9), (16, 8)]:
+        with pytest.raises(ValueError):
+            C.OTree(w, s)
+        with pytest.raises(R.ErlangCrash):
+            R.new(None, w, s)
+
+
+def test_eqc_property_seeded():
+    """test/synctree_eqc.erl:42-97 as a seeded randomized property."""
+    rng = random.Random(11)
+    for trial in range(6):
+        n = rng.randrange(3, 60)
+        objs = [(str(k).encode(), bytes(rng.randrange(256) for _ in range(8))) for k in range(1, n + 1)]
+        rng.shuffle(objs)
+        m1 = rng.randrange(0, n + 1)
+        m2 = rng.randrange(0, n - m1 + 1)
+        dn = rng.randrange(0, n - m1 - m2 + 1)
+        remote_only, rest = objs[:m1], objs[m1:]
+        local_only, rest = rest[:m2], rest[m2:]
+        different, same = rest[:dn], rest[dn:]
+        different2 = [(k, bytes([(h[0] + 1) % 256]) + h[1:]) for k, h in different]
+        for w, s in [(16, 1 << 20), (4, 64)]:
+            a, b = C.OTree(w, s), C.OTree(w, s)
+            for k, v in same + local_only + different:
+                a.insert(k, v)
+            for k, v in same + remote_only + different2:
+                b.insert(k, v)
+            exp = sorted([('missing', k) for k, _ in remote_only] + [('remote_missing', k) for k, _ in local_only] +
+                         [('different', k) for k, _ in different])
+            got = sorted(('missing' if va == '$none' else 'remote_missing' if vb == '$none' else 'different', k)
+                         for k, (va, vb) in a.compare(b))
+            assert got == exp
+            for k, v in remote_only:
+                a.insert(k, v)
+            for k, v in local_only + different:
+                b.insert(k, v)
+            assert a.compare(b) == []
+            assert a.top_hash() == b.top_hash()
+
+
+def test_python_vs_c_random_corruptions():
+    """Raw backend corruption (test/synctree_intercepts.erl:96-104 mutation) on both restatements."""
+    rng = random.Random(3)
+    for w, s in [(4, 256), (16, 4096)]:
+        keys = list(range(1, 80))
+        tr = R.new(None, w, s)
+        tc = C.OTree(w, s)
+        for k in keys:
+            v = bytes(rng.randrange(256) for _ in range(17))
+            tr = R.insert(k, v, tr)
+            tc.insert(k, v)
+        # corrupt_segment: bump the first byte of the first value of a segment
+        seg = R.get_segment(keys[5], s)
+        node = R.m_fetch((tr.height + 1, seg), [], tr)
+        k0, v0 = node[0]
+        bad = [(k0, bytes([(v0[0] + 1) % 256]) + v0[1:])] + node[1:]
+        tr = R.m_store((tr.height + 1, seg), bad, tr)
+        tc.store_segment(seg, bad)
+        # corrupt_upper: two levels above the segment
+        lvl = tr.height - 1
+        if lvl >= 1:
+            seg2 = R.get_segment(keys[9], s)
+            b2 = seg2 >> (tr.shift * (tr.height + 1 - lvl))
+            nd = R.m_fetch((lvl, b2), [], tr)
+            c0, h0 = nd[0]
+            bad2 = [(c0, bytes([(h0[0] + 1) % 256]) + h0[1:])] + nd[1:]
+            tr = R.m_store((lvl, b2), bad2, tr)
+            tc.store_inner(lvl, b2, bad2)
+        for k in keys + [1000, 1001]:
+            assert tc.get(k) == R.get(k, tr)
+        assert tc.verify() == R.verify(tr)
+        assert tc.verify_upper() == R.verify_upper(tr)
+        clean = R.new(None, w, s)
+        for k in keys:
+            clean = R.insert(k, b'z', clean)
+        cc = C.OTree(w, s)
+        for k in keys:
+            cc.insert(k, b'z')
+        exp = _crash_or(lambda: R.local_compare(tr, clean))
+        got = tc.compare(cc)
+        if isinstance(exp, tuple):
+            assert got[0] == 'crash' and got[2] == exp
+        else:
+            assert got == exp
+        for k in keys[:20]:
+            r = R.insert(k, b'q', tr)
+            assert tc.insert(k, b'q') == _tuple_or_self(r, tc)
+            if not isinstance(r, tuple):
+                tr = r
+        tr = R.rehash(tr)
+        tc.rehash()
+        assert tc.top_hash() == tr.top_hash
+        assert tc.verify() and R.verify(tr)
+
+
+def _crash_or(f):
+    try:
+        return f()
+    except R.ErlangCrash as e:
+        msg = str(e)
+        import re
+        m = re.search(r"\('corrupted', (\d+), (\d+)\)", msg)
+        return ('corrupted', int(m.group(1)), int(m.group(2)))
+
+
+def _tuple_or_self(r, tc):
+    return r if isinstance(r, tuple) else tc
+
+
+def test_bulk_load_equals_sequential():
+    rng = random.Random(5)
+    for w, s, n in [(16, 1 << 20, 300), (4, 256, 400), (2, 2, 30)]:
+        keys = [rng.randrange(-(1 << 40), 1 << 40) for _ in range(n)] + [b'k%d' % i for i in range(20)] + ['at%d' % i
+                                                                                                          for i in range(5)]
+        keys += keys[:50]  # duplicates: last writer wins
+        vals = [bytes(rng.randrange(256) for _ in range(rng.randrange(0, 30))) for _ in keys]
+        seq = C.OTree(w, s)
+        for k, v in zip(keys, vals):
+            seq.insert(k, v)
+        bulk = C.OTree(w, s).bulk_load(keys, vals)
+        assert bulk.top_hash() == seq.top_hash()
+        for lvl in range(1, seq.height + 2):
+            pa, ha = seq.level_entries(lvl)
+            pb, hb = bulk.level_entries(lvl)
+            assert (pa == pb).all() and (ha == hb).all()
+        assert bulk.compare(seq) == []
+
+
+def test_splitmix_workload_golden():
+    g = GOLD['splitmix_1000']
+    keys = workload.keys_int63(1000)
+    assert [str(k) for k in keys[:8].tolist()] == g['first_keys']
+    vals = workload.obj_hash_values(1000)
+    t = C.OTree().bulk_load_int64(keys, vals)
+    assert t.top_hash().hex() == g['top']
+    import hashlib
+    for lvl, dg in g['level_digests'].items():
+        p, h = t.level_entries(int(lvl))
+        m = hashlib.md5()
+        for b in np.nonzero(p)[0]:
+            m.update(int(b).to_bytes(8, 'big') + h[b].tobytes())
+        assert m.hexdigest() == dg
+
+
+def test_rehash_par_equals_rehash():
+    keys = workload.keys_int63(20000)
+    vals = workload.obj_hash_values(20000)
+    t = C.OTree().bulk_load_int64(keys, vals)
+    top = t.top_hash()
+    t.rehash_par(4)
+    assert t.top_hash() == top and t.verify()
