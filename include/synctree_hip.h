@@ -1,0 +1,221 @@
+/* synctree_hip.h — C-ABI of libsynctree_hip.so, the MI355X (gfx950) synctree
+ * hashing & exchange path of riak_ensemble.
+ *
+ * Plain C types only (no torch / HIP types cross this boundary).  Every entry
+ * point names the reference interface it replaces (jrwest/riak_ensemble,
+ * paths relative to the repository root).  The Erlang-side binding a
+ * maintainer would add (a NIF + a synctree backend module) is shown in
+ * INTEGRATION.md; the Python mirror used by this repo's tests lives in
+ * riak_ensemble_amd/synctree.py.
+ *
+ * Conventions:
+ *  - Trees are device-resident; a handle is used by one caller at a time
+ *    (like the owning gen_server, src/riak_ensemble_peer_tree.erl:58-59);
+ *    different handles may be used concurrently (each has its own stream).
+ *  - Corruption is a VALUE, not an error: ST_CORRUPTED plus the (Level,
+ *    Bucket) of the first node on the root->leaf path whose hash does not
+ *    match its parent's entry, exactly like {corrupted, Level, Bucket}
+ *    (src/synctree.erl:306-320).
+ *  - Keys are passed as (type, ensure_binary bytes) (src/synctree.erl:261-268):
+ *      ST_KEY_INT    bytes = <<Key:64/big>>  (integer keys in int64 range;
+ *                    ordered numerically)
+ *      ST_KEY_ATOM   bytes = atom_to_binary(Key, utf8)
+ *      ST_KEY_BINARY bytes = the binary
+ *    Erlang term order on that domain: integer < atom < binary; atoms and
+ *    binaries compare bytewise with a proper prefix first.  Other terms (which
+ *    the reference hashes via term_to_binary) are rejected with ST_EINVAL.
+ *  - Packed variable-length arrays: element i of a heap is
+ *    heap[off[i] .. off[i+1]) with off[] of n+1 entries.
+ *  - Hashes are 17 bytes: <<?H_MD5 = 0, md5/binary>> (src/synctree.erl:255-259).
+ */
+#ifndef SYNCTREE_HIP_H
+#define SYNCTREE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ST_OK 0
+#define ST_NOTFOUND 1
+#define ST_CORRUPTED 2
+#define ST_EINVAL (-1)   /* bad argument / geometry (reference: crash) */
+#define ST_EDEVICE (-2)  /* HIP runtime error */
+#define ST_ENOMEM (-3)
+
+#define ST_KEY_INT 0
+#define ST_KEY_ATOM 1
+#define ST_KEY_BINARY 2
+
+#define ST_FILTER_ALL 0
+#define ST_FILTER_LOCAL_ONLY 1   /* drops {K,{_, '$none'}}  (synctree.erl:438-442) */
+#define ST_FILTER_REMOTE_ONLY 2  /* drops {K,{'$none', _}}  (synctree.erl:445-449) */
+
+#define ST_DIFF_BOTH 0        /* {K, {A, B}}       */
+#define ST_DIFF_LOCAL_ONLY 1  /* {K, {A, '$none'}} */
+#define ST_DIFF_REMOTE_ONLY 2 /* {K, {'$none', B}} */
+
+typedef struct st_tree st_tree;
+
+/* ---- lifecycle ------------------------------------------------------ */
+
+/* synctree:new/3..5 (src/synctree.erl:143-170): Height = log_W(Segments),
+ * Shift = log2(W).  Returns ST_EINVAL where the reference crashes
+ * (compute_height/compute_shift case_clause, synctree.erl:270-284).
+ * device: HIP device ordinal. */
+int st_create(uint64_t width, uint64_t segments, int device, st_tree **out);
+void st_destroy(st_tree *t);
+
+/* Enqueue this tree's work on an external hipStream_t (e.g. torch's
+ * current stream); NULL restores the tree's own stream. */
+int st_set_stream(st_tree *t, void *hip_stream);
+int st_sync(st_tree *t);
+
+/* synctree:height/1 (synctree.erl:179-181) */
+uint32_t st_height(const st_tree *t);
+uint64_t st_width(const st_tree *t);
+uint64_t st_segments(const st_tree *t);
+/* number of {Key,Value} entries over all segments */
+uint64_t st_num_entries(st_tree *t);
+/* the last error message of this thread */
+const char *st_last_error(void);
+
+/* ---- writes --------------------------------------------------------- */
+
+/* insert/3 (synctree.erl:189-209) for n keys, with the semantics of n
+ * sequential inserts: last writer wins; a key whose root->segment path fails
+ * verification is not inserted and reports ST_CORRUPTED + (level, bucket);
+ * other keys are inserted and their paths rehashed (dirty-path update).
+ * status/clevel/cbucket: per-key outputs (may be NULL).  Host pointers. */
+int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                    const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel,
+                    uint64_t *cbucket);
+
+/* Same for integer keys (ST_KEY_INT) and fixed-width values.
+ * keys[n] (int64), vals[n*vlen].  inputs_on_device != 0: both pointers are
+ * device memory on this tree's device (no host staging).  *n_corrupted
+ * (may be NULL) receives the number of rejected keys. */
+int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                    int inputs_on_device, uint64_t *n_corrupted);
+
+/* corrupt/2 (synctree.erl:241-247): erase Key from its segment without
+ * updating the path (test aid). */
+int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen);
+
+/* Raw backend writes (Mod:store/2,3 of synctree_ets.erl:51-66, used through
+ * m_batch/m_flush by riak_ensemble_peer_tree repair, peer_tree.erl:264-277,
+ * and by the corruption intercepts, test/synctree_intercepts.erl).
+ * Inner node content = [{ChildId, Hash17}] with ChildId in
+ * [bucket*W, bucket*W+W) (n may be 0 = store []).  Segment content is
+ * [{Key,Value}] and must be strictly ascending in key order. */
+int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint32_t n, const uint64_t *children,
+                   const uint8_t *hashes17);
+int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
+                     const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff);
+int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket);
+/* store {0,0}: hash17 or NULL (delete); also_record != 0 also sets the
+ * #tree.top_hash field (as insert/rehash do) */
+int st_store_top(st_tree *t, const uint8_t *hash17, int also_record);
+/* Set only the #tree.top_hash record field (hash17 NULL = undefined).  An
+ * Erlang tree record is a value: a caller holding an older record of the same
+ * backend (e.g. the ETS table) verifies against ITS top hash
+ * (synctree.erl:302-304); this lets a host mirror reproduce that exactly. */
+int st_set_record_top(st_tree *t, const uint8_t *hash17);
+
+/* ---- rehash / verify ------------------------------------------------ */
+
+/* rehash/1 (upper = 0) and rehash_upper/1 (upper = 1), synctree.erl:489-543:
+ * recompute every inner node and the top hash from the segments (or from the
+ * stored level-Height nodes).  Kernels K1 segment_hash + K2 level_rehash. */
+int st_rehash(st_tree *t, int upper);
+
+/* verify/1 (upper = 0) and verify_upper/1 (upper = 1), synctree.erl:549-571 */
+int st_verify(st_tree *t, int upper, int *ok);
+
+/* top_hash/1 (synctree.erl:183-185): *present = 0 <=> undefined */
+int st_top_hash(st_tree *t, uint8_t out17[17], int *present);
+
+/* Entries recorded for every bucket of `level` (1..Height+1) in its parent
+ * node (level 1: the #tree top hash): present[W^(level-1)],
+ * hashes17[W^(level-1) * 17].  Used for per-level parity checks. */
+int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes17);
+
+/* ---- reads ---------------------------------------------------------- */
+
+/* Library-allocated result blocks; free with st_free_result(). */
+typedef struct st_result {
+    uint64_t n;          /* records */
+    int32_t *status;     /* ST_OK / ST_NOTFOUND / ST_CORRUPTED */
+    uint32_t *clevel;    /* corruption level (status == ST_CORRUPTED) */
+    uint64_t *cbucket;   /* corruption bucket */
+    uint64_t *eoff;      /* n+1: entries of record i are [eoff[i], eoff[i+1]) */
+    uint64_t n_entries;
+    /* inner-level entries */
+    uint64_t *child;     /* n_entries */
+    uint8_t *hash17;     /* n_entries * 17 */
+    /* key/value entries (segments, get, compare) */
+    uint8_t *ktype;      /* n_entries */
+    uint64_t *koff;      /* n_entries + 1 */
+    uint8_t *kheap;
+    uint64_t *aoff;      /* n_entries + 1 (value, or local value for diffs) */
+    uint8_t *aheap;
+    uint64_t *boff;      /* n_entries + 1 (remote value for diffs) */
+    uint8_t *bheap;
+    uint8_t *kind;       /* n_entries: ST_DIFF_* for compare results */
+    uint64_t *seg;       /* n_entries: segment of each diff record */
+} st_result;
+void st_free_result(st_result *r);
+
+/* get/2 (synctree.erl:213-227) for n keys: per key ST_OK (value = entry
+ * eoff[i] of aoff/aheap), ST_NOTFOUND, or ST_CORRUPTED. */
+int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                 st_result **out);
+
+/* exchange_get/3 (synctree.erl:231-237) at one level for n buckets, each
+ * verified root->node (verified_hashes, synctree.erl:288-298).  Level 0
+ * (bucket 0) is answered as [{0, TopHash}] by the caller from st_top_hash.
+ * Inner levels fill child/hash17; the segment level fills ktype/koff/kheap
+ * and aoff/aheap.  This is also the batched form of the streaming
+ * start_exchange_level protocol (test/synctree_remote.erl:25-35). */
+int st_exchange_get_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out);
+
+/* Mod:fetch({Level,Bucket}, [], State) (synctree_ets.erl:38-44) for n
+ * buckets of one level, WITHOUT verification (the raw backend image).
+ * Level 0 returns the stored {0,0} top hash as one inner entry (child 0). */
+int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out);
+
+/* compare/3,5 between two trees on the same device (local_compare/2,
+ * synctree.erl:361-382, with filters :421-449): level-synchronous tree
+ * diff (kernel K3).  On success returns ST_OK and the diff records in
+ * reference order (AccFun = Keys ++ Acc: descending segment, ascending key)
+ * in out->ktype/koff/kheap, out->kind, out->aoff/aheap (local value),
+ * out->boff/bheap (remote value), out->seg.  If a visited node fails
+ * verification the reference crashes (orddict_delta has no clause for the
+ * {corrupted,L,B} tuple): returns ST_CORRUPTED with the first such node in
+ * reference visiting order in *clevel, *cbucket and *cside (0 local,
+ * 1 remote) and no records. */
+int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
+               uint64_t *cbucket, int *cside);
+
+/* The same compare with every result kept in device memory (bench path):
+ * *n_diffs receives the number of diff records.  Records are built on the
+ * device exactly as st_compare's; st_compare = this + the D2H copy. */
+int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
+                      uint64_t *cbucket, int *cside);
+
+/* ---- diagnostics ---------------------------------------------------- */
+
+/* Key -> segment (get_segment/2, synctree.erl:251-253) on the device. */
+int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
+                        const uint64_t *koff, uint64_t *segments_out);
+
+/* Enable per-kernel HIP-event timing on this tree's stream; st_kernel_stats
+ * returns the accumulated launch count and milliseconds of the named
+ * kernel ("segment_hash", "level_rehash", "key_segment", "tree_compare"...). */
+int st_set_timing(st_tree *t, int enabled);
+int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,180 @@
+// md5_dev.h — RFC 1321 MD5 for gfx950 (one message per lane).
+//
+// The reference hashes with OTP `crypto:hash(md5, IoList)` (src/synctree.erl:
+// 252, 258): segment ids from md5(ensure_binary(Key)) and node hashes from the
+// md5 of the concatenated child values.  MD5 is serial within a message, so
+// the device parallelism is across messages: every lane owns one message.
+//
+// Codegen notes (check the .s with -save-temps):
+//  * rotl(x, s) is __builtin_amdgcn_alignbit(x, x, 32 - s)   -> v_alignbit_b32
+//  * F = bfi(b, c, d), G = bfi(d, b, c)                     -> v_bfi_b32
+//  * H = b ^ c ^ d                                           -> v_xor3_b32
+//  * a + F + K + M                                           -> v_add3_u32 + v_add
+//  so a step is ~5 VALU ops; a 64-byte block ~330-360 ops.
+//  * message blocks from global memory are fetched with four unaligned
+//    global_load_dwordx4 (gfx950 runs with unaligned access enabled; hipcc
+//    emits the wide loads for byte pointers) — no shuffling in registers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace stmd5 {
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+#define STMD5_F(b, c, d) bfi((b), (c), (d))
+#define STMD5_G(b, c, d) bfi((d), (b), (c))
+#define STMD5_H(b, c, d) ((b) ^ (c) ^ (d))
+#define STMD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
+#define STMD5_STEP(f, a, b, c, d, m, k, s) a = (b) + rotl((a) + f((b), (c), (d)) + ((m) + (k)), (s))
+
+__device__ __forceinline__ void init(uint32_t s[4]) {
+    s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
+}
+
+__device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    STMD5_STEP(STMD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    STMD5_STEP(STMD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    STMD5_STEP(STMD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    STMD5_STEP(STMD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    STMD5_STEP(STMD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    STMD5_STEP(STMD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    STMD5_STEP(STMD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    STMD5_STEP(STMD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    STMD5_STEP(STMD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    STMD5_STEP(STMD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    STMD5_STEP(STMD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    STMD5_STEP(STMD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    STMD5_STEP(STMD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    STMD5_STEP(STMD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    STMD5_STEP(STMD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    STMD5_STEP(STMD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+    STMD5_STEP(STMD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    STMD5_STEP(STMD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    STMD5_STEP(STMD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    STMD5_STEP(STMD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    STMD5_STEP(STMD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    STMD5_STEP(STMD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    STMD5_STEP(STMD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    STMD5_STEP(STMD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    STMD5_STEP(STMD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    STMD5_STEP(STMD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    STMD5_STEP(STMD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    STMD5_STEP(STMD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    STMD5_STEP(STMD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    STMD5_STEP(STMD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    STMD5_STEP(STMD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    STMD5_STEP(STMD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    STMD5_STEP(STMD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+    STMD5_STEP(STMD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
+    STMD5_STEP(STMD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    STMD5_STEP(STMD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+    STMD5_STEP(STMD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+    STMD5_STEP(STMD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    STMD5_STEP(STMD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    STMD5_STEP(STMD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    STMD5_STEP(STMD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    STMD5_STEP(STMD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+    STMD5_STEP(STMD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    STMD5_STEP(STMD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
+    STMD5_STEP(STMD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    STMD5_STEP(STMD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    STMD5_STEP(STMD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    STMD5_STEP(STMD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+    STMD5_STEP(STMD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    STMD5_STEP(STMD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    STMD5_STEP(STMD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    STMD5_STEP(STMD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    STMD5_STEP(STMD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    STMD5_STEP(STMD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    STMD5_STEP(STMD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    STMD5_STEP(STMD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    STMD5_STEP(STMD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    STMD5_STEP(STMD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    STMD5_STEP(STMD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    STMD5_STEP(STMD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    STMD5_STEP(STMD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    STMD5_STEP(STMD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    STMD5_STEP(STMD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    STMD5_STEP(STMD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+// Keep the `valid` leading bytes of little-endian word w (0..4 valid), put
+// the 0x80 terminator right after them when they end inside this word.
+__device__ __forceinline__ uint32_t tail_word(uint32_t w, int valid) {
+    if (valid >= 4) return w;
+    if (valid < 0) return 0u;
+    uint32_t keep = valid == 0 ? 0u : (0xffffffffu >> (32 - 8 * valid));
+    return (w & keep) | (0x80u << (8 * valid));
+}
+
+// Apply MD5 padding to block k of a `len`-byte message whose raw words
+// (possibly garbage beyond len) are in m[].  rem = len - 64k.
+__device__ __forceinline__ void pad_block(uint32_t m[16], int64_t rem, bool last, uint64_t len) {
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        int64_t v = rem - 4 * w;
+        m[w] = tail_word(m[w], v > 4 ? 4 : (int)v);
+    }
+    if (last) {
+        m[14] = (uint32_t)(len << 3);
+        m[15] = (uint32_t)(len >> 29);
+    }
+}
+
+__device__ __forceinline__ void load_block_global(const uint8_t *p, uint32_t m[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint4 v;
+        __builtin_memcpy(&v, p + 16 * q, 16);
+        m[4 * q + 0] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
+    }
+}
+
+// MD5 of p[0..len) in global memory, any alignment.  The buffer must stay
+// readable for 64 bytes past p+len (heaps are allocated with slack).
+__device__ __forceinline__ void md5_global(const uint8_t *p, uint64_t len, uint32_t out[4]) {
+    uint32_t st[4];
+    init(st);
+    const uint64_t nblk = (len + 8) / 64 + 1;
+    for (uint64_t k = 0; k < nblk; k++) {
+        uint32_t m[16];
+        const int64_t rem = (int64_t)len - (int64_t)(64 * k);
+        if (rem >= 64) {
+            load_block_global(p + 64 * k, m);
+        } else {
+            if (rem > 0) {
+                load_block_global(p + 64 * k, m);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 16; w++) m[w] = 0u;
+            }
+            pad_block(m, rem, k + 1 == nblk, len);
+        }
+        compress(st, m);
+    }
+    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+}
+
+// MD5 of a message of `len` bytes staged in LDS at a 4-byte aligned address
+// (bytes beyond len are ignored).
+__device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t out[4]) {
+    uint32_t st[4];
+    init(st);
+    const uint32_t nblk = (len + 8) / 64 + 1;
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(p);
+    for (uint32_t k = 0; k < nblk; k++) {
+        uint32_t m[16];
+        const int64_t rem = (int64_t)len - (int64_t)(64 * k);
+#pragma unroll
+        for (int w = 0; w < 16; w++) m[w] = (rem - 4 * w > 0) ? pw[16 * k + w] : 0u;
+        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
+        compress(st, m);
+    }
+    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+}
+
+}  // namespace stmd5

@@ -1,0 +1,795 @@
+// st_kernels.h — gfx950 kernels of the synctree path (included once, by
+// synctree_hip.hip).  Reference: src/synctree.erl (jrwest/riak_ensemble).
+//
+// Device layout of one tree:
+//  * node entries: one slot per (Level, Bucket) for Level 1..H+1 plus slot 0
+//    for the #tree.top_hash record field.  slot(l, b) = base[l] + b.  A slot
+//    holds the 17-byte entry the PARENT node records for that child:
+//    md5[slot] (16 B) + tag[slot] (bit 8 = present, bits 0..7 = prefix byte).
+//    slot(1,0) is the stored {0,0}; slot 0 the cached record (they only
+//    differ after raw backend writes).  The content of inner node (l, b) is
+//    the present slots among children (l+1, b*W .. b*W+W-1) — exactly the
+//    [{ChildId, Hash}] orddict of synctree.erl:516-533.
+//  * segments: CSR.  seg_off[S+1] entry offsets; key records (tag byte +
+//    ensure_binary payload, integer payload with its sign bit flipped so that
+//    memcmp-then-length IS Erlang term order) in kheap/koff; values in
+//    vheap/voff; seg_voff[S+1] = voff[seg_off[s]] so that a segment's hash
+//    input (the concatenation of its values, synctree.erl:255-259) is ONE
+//    contiguous byte range.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "md5_dev.h"
+
+#define ST_MAXLEV 33
+#define TAG_PRESENT 0x100u
+#define KEYTAG_INT 0
+#define KEYTAG_ATOM 1
+#define KEYTAG_BINARY 2
+
+#define MODE_STORE 0
+#define MODE_VERIFY 1
+
+struct DevTree {
+    uint32_t W, shift, H, pad0;
+    uint64_t S;
+    uint64_t base[ST_MAXLEV + 2];
+    uint4 *md5;
+    uint16_t *tag;
+    const uint64_t *seg_off;
+    const uint64_t *seg_voff;
+    const uint64_t *koff;
+    const uint8_t *kheap;
+    const uint64_t *voff;
+    const uint8_t *vheap;
+};
+
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+
+// Erlang term order on key records: memcmp over the common prefix, then length.
+__device__ __forceinline__ int rec_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    uint64_t m = la < lb ? la : lb;
+    uint64_t i = 0;
+    for (; i + 8 <= m; i += 8) {
+        uint64_t x, y;
+        __builtin_memcpy(&x, a + i, 8);
+        __builtin_memcpy(&y, b + i, 8);
+        if (x != y) {
+            x = __builtin_bswap64(x);
+            y = __builtin_bswap64(y);
+            return x < y ? -1 : 1;
+        }
+    }
+    for (; i < m; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    if (la != lb) return false;
+    uint64_t i = 0;
+    for (; i + 8 <= la; i += 8) {
+        uint64_t x, y;
+        __builtin_memcpy(&x, a + i, 8);
+        __builtin_memcpy(&y, b + i, 8);
+        if (x != y) return false;
+    }
+    for (; i < la; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+__device__ __forceinline__ void copy_bytes(uint8_t *d, const uint8_t *s, uint64_t n) {
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        uint4 v;
+        __builtin_memcpy(&v, s + i, 16);
+        __builtin_memcpy(d + i, &v, 16);
+    }
+    if (i + 8 <= n) {
+        uint64_t v;
+        __builtin_memcpy(&v, s + i, 8);
+        __builtin_memcpy(d + i, &v, 8);
+        i += 8;
+    }
+    if (i + 4 <= n) {
+        uint32_t v;
+        __builtin_memcpy(&v, s + i, 4);
+        __builtin_memcpy(d + i, &v, 4);
+        i += 4;
+    }
+    for (; i < n; i++) d[i] = s[i];
+}
+
+// ---------------------------------------------------------------------------
+// Ingest helpers
+
+// int64 keys -> key records (9 bytes: tag 0, <<K:64/big>> with sign bit flipped)
+__global__ void k_pack_int64(const int64_t *keys, uint64_t n, uint8_t *kheap, uint64_t *koff, uint64_t *voff,
+                             uint32_t vlen) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        koff[i] = 9 * i;
+        voff[i] = (uint64_t)vlen * i;
+        if (i == n) break;
+        uint64_t k = (uint64_t)keys[i] ^ 0x8000000000000000ull;
+        uint8_t *p = kheap + 9 * i;
+        p[0] = KEYTAG_INT;
+        uint64_t be = __builtin_bswap64(k);
+        __builtin_memcpy(p + 1, &be, 8);
+    }
+}
+
+// K1a key_segment: get_segment/2 (synctree.erl:251-253) — md5 of the key's
+// ensure_binary bytes read as a big-endian 128-bit integer, rem Segments
+// (a power of two: the low bits of digest bytes 8..15).
+__global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64_t n, uint64_t segmask,
+                              uint32_t *seg_out) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t o = koff[i];
+        const uint64_t len = koff[i + 1] - o;
+        const uint8_t *p = kheap + o;
+        uint32_t d[4];
+        if (p[0] == KEYTAG_INT && len == 9) {
+            uint2 x;
+            __builtin_memcpy(&x, p + 1, 8);
+            uint32_t m[16];
+            m[0] = x.x ^ 0x80u;  // unflip the sign bit: message = <<Key:64/big>>
+            m[1] = x.y;
+            m[2] = 0x80u;
+#pragma unroll
+            for (int w = 3; w < 16; w++) m[w] = 0u;
+            m[14] = 64u;
+            stmd5::init(d);
+            stmd5::compress(d, m);
+        } else {
+            stmd5::md5_global(p + 1, len - 1, d);
+        }
+        const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
+        seg_out[i] = (uint32_t)(lo & segmask);
+    }
+}
+
+__global__ void k_iota(uint32_t *v, uint64_t n) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) v[i] = (uint32_t)i;
+}
+
+// bseg_off[s] = first position of segment s in the sorted batch (S+1 entries)
+__global__ void k_run_bounds(const uint32_t *sseg, uint64_t n, uint64_t S, uint64_t *bseg_off) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        const uint64_t cur = i < n ? sseg[i] : S;
+        const int64_t prev = i > 0 ? (int64_t)sseg[i - 1] : -1;
+        for (int64_t s = prev + 1; s <= (int64_t)cur; s++) bseg_off[s] = i;
+    }
+}
+
+struct BatchView {
+    const uint8_t *kheap;
+    const uint64_t *koff;
+};
+
+__device__ __forceinline__ int batch_cmp(const BatchView &b, uint32_t x, uint32_t y) {
+    int c = rec_cmp(b.kheap + b.koff[x], b.koff[x + 1] - b.koff[x], b.kheap + b.koff[y], b.koff[y + 1] - b.koff[y]);
+    if (c) return c;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+__device__ void heap_sift(const BatchView &bv, uint32_t *a, uint64_t start, uint64_t end) {
+    uint64_t root = start;
+    while (2 * root + 1 < end) {
+        uint64_t child = 2 * root + 1, sw = root;
+        if (batch_cmp(bv, a[sw], a[child]) < 0) sw = child;
+        if (child + 1 < end && batch_cmp(bv, a[sw], a[child + 1]) < 0) sw = child + 1;
+        if (sw == root) return;
+        uint32_t t = a[root]; a[root] = a[sw]; a[sw] = t;
+        root = sw;
+    }
+}
+
+// Sort each segment's run of the batch by (key record, batch index) and mark
+// the last writer of every key (sequential insert semantics: last wins).
+__global__ void k_run_sort(BatchView bv, uint32_t *perm, const uint64_t *bseg_off, uint64_t S, uint8_t *keep) {
+    for (uint64_t s = gtid(); s < S; s += gstride()) {
+        const uint64_t a = bseg_off[s], b = bseg_off[s + 1];
+        if (a == b) continue;
+        uint32_t *r = perm + a;
+        const uint64_t n = b - a;
+        if (n <= 32) {
+            for (uint64_t i = 1; i < n; i++) {
+                uint32_t x = r[i];
+                uint64_t j = i;
+                while (j > 0 && batch_cmp(bv, r[j - 1], x) > 0) { r[j] = r[j - 1]; j--; }
+                r[j] = x;
+            }
+        } else {
+            for (uint64_t st = n / 2; st-- > 0;) heap_sift(bv, r, st, n);
+            for (uint64_t e = n - 1; e > 0; e--) {
+                uint32_t t = r[0]; r[0] = r[e]; r[e] = t;
+                heap_sift(bv, r, 0, e);
+            }
+        }
+        for (uint64_t i = 0; i < n; i++) {
+            bool last = (i + 1 == n);
+            if (!last) {
+                const uint32_t x = r[i], y = r[i + 1];
+                last = rec_cmp(bv.kheap + bv.koff[x], bv.koff[x + 1] - bv.koff[x], bv.kheap + bv.koff[y],
+                               bv.koff[y + 1] - bv.koff[y]) != 0;
+            }
+            keep[a + i] = last ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Paths: marks, verification status
+
+// Mark every node on the root->target path (levels 1..L) of each target.
+// Targets are either the segments with a batch run (bseg_off != NULL) or an
+// explicit list of buckets at level L.
+__global__ void k_mark_paths(DevTree t, uint32_t L, const uint64_t *bseg_off, const uint64_t *targets,
+                             uint64_t ntargets, uint8_t *mark) {
+    for (uint64_t i = gtid(); i < ntargets; i += gstride()) {
+        uint64_t tb;
+        if (bseg_off) {
+            if (bseg_off[i] == bseg_off[i + 1]) continue;
+            tb = i;
+        } else {
+            tb = targets[i];
+        }
+        for (uint32_t l = 1; l <= L; l++) {
+            const uint64_t b = tb >> (t.shift * (L - l));
+            mark[t.base[l] + b] = 1;
+        }
+    }
+}
+
+// Mark the ancestors (levels 1..H+1) of segments flagged in segflag[].
+__global__ void k_mark_from_segments(DevTree t, const uint8_t *segflag, uint8_t *mark) {
+    const uint32_t L = t.H + 1;
+    for (uint64_t s = gtid(); s < t.S; s += gstride()) {
+        if (!segflag[s]) continue;
+        for (uint32_t l = 1; l <= L; l++) mark[t.base[l] + (s >> (t.shift * (L - l)))] = 1;
+    }
+}
+
+// Reachability for verify/5 (synctree.erl:560-571): node (l,b) is visited iff
+// every entry on its path from level 2 down is present; (1,0) always is.
+__global__ void k_mark_reachable(DevTree t, uint32_t maxd, uint8_t *mark) {
+    const uint64_t lo = t.base[1], hi = t.base[maxd + 1];
+    for (uint64_t slot = lo + gtid(); slot < hi; slot += gstride()) {
+        uint32_t l = 1;
+        while (t.base[l + 1] <= slot) l++;
+        const uint64_t b = slot - t.base[l];
+        bool r = true;
+        for (uint32_t q = 2; q <= l && r; q++) r = (t.tag[t.base[q] + (b >> (t.shift * (l - q)))] & TAG_PRESENT) != 0;
+        mark[slot] = r ? 1 : 0;
+    }
+}
+
+// First failing level on each target's root->target path (0 = verified).
+__global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, const uint64_t *targets,
+                              uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus) {
+    for (uint64_t i = gtid(); i < ntargets; i += gstride()) {
+        uint64_t tb;
+        if (bseg_off) {
+            if (bseg_off[i] == bseg_off[i + 1]) { seg_reject[i] = 0; continue; }
+            tb = i;
+        } else {
+            tb = targets[i];
+        }
+        uint32_t bad = 0;
+        for (uint32_t l = 1; l <= L; l++) {
+            const uint64_t b = tb >> (t.shift * (L - l));
+            if (!ok[t.base[l] + b]) { bad = l; break; }
+        }
+        if (seg_reject) seg_reject[i] = (uint8_t)bad;
+        if (tstatus) tstatus[i] = bad;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1 segment_hash: hash(Segment) = <<0, md5(V1 ‖ … ‖ Vn)>> (synctree.erl:255-259)
+// one lane per segment; the values of a segment are one contiguous range.
+// MODE_STORE writes the parent's entry (rehash, synctree.erl:515-527);
+// MODE_VERIFY checks it like verify_hash/2 (synctree.erl:322-340).
+template <int MODE>
+__global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *list, const uint32_t *list_cnt,
+                               uint8_t *ok, uint32_t *fail) {
+    const uint32_t L = t.H + 1;
+    const uint64_t n = list ? (uint64_t)*list_cnt : t.S;
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t s = list ? list[i] : i;
+        const uint64_t slot = t.base[L] + s;
+        if (mask && !mask[slot]) continue;
+        const uint64_t e0 = t.seg_off[s], e1 = t.seg_off[s + 1];
+        const uint64_t eslot = (L == 1) ? 0 : slot;
+        if (MODE == MODE_VERIFY) {
+            const uint16_t et = t.tag[eslot];
+            bool good;
+            if (!(et & TAG_PRESENT)) {
+                good = (e0 == e1);
+            } else {
+                uint32_t d[4];
+                const uint64_t v0 = t.seg_voff[s];
+                stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                const uint4 e = t.md5[eslot];
+                good = (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+            }
+            if (ok) ok[slot] = good ? 1 : 0;
+            if (!good && fail) atomicOr(fail, 1u);
+        } else {
+            if (e0 == e1) {
+                t.tag[slot] = 0;
+                if (L == 1) t.tag[0] = 0;
+            } else {
+                uint32_t d[4];
+                const uint64_t v0 = t.seg_voff[s];
+                stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
+                t.md5[slot] = e;
+                t.tag[slot] = TAG_PRESENT;
+                if (L == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+            }
+        }
+    }
+}
+
+// Stage the content of inner node (l, b) — the present child entries, 17
+// bytes each in child order — into this lane's LDS region; returns its length.
+__device__ __forceinline__ uint32_t stage_inner(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
+    const uint64_t c0 = t.base[l + 1] + b * t.W;
+    uint32_t len = 0;
+    for (uint32_t j = 0; j < t.W; j++) {
+        const uint16_t ct = t.tag[c0 + j];
+        if (!(ct & TAG_PRESENT)) continue;
+        const uint4 h = t.md5[c0 + j];
+        uint8_t *q = reg + len;
+        q[0] = (uint8_t)(ct & 0xff);
+        const uint32_t w[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) q[1 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        len += 17;
+    }
+    return len;
+}
+
+// Bytes of LDS per lane for inner-node staging (odd dword stride).
+__host__ __device__ __forceinline__ uint32_t lane_region_bytes(uint32_t W) {
+    uint32_t dw = (W * 17 + 72 + 3) / 4;
+    if ((dw & 1) == 0) dw++;
+    return dw * 4;
+}
+
+// K2 level_rehash: one lane per inner node of a level (rehash/4 inner part,
+// synctree.erl:515-535), children staged in LDS.  Nodes of level l are
+// processed after level l+1.  With levels == 0 the kernel covers every level
+// in [lmin, lmax] in one launch (only valid for MODE_VERIFY, whose nodes are
+// independent).
+template <int MODE>
+__global__ void k_level_hash(DevTree t, uint32_t lmin, uint32_t lmax, const uint8_t *mask, const uint32_t *list,
+                             const uint32_t *list_cnt, uint8_t *ok, uint32_t *fail) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(t.W);
+    const uint64_t lo = t.base[lmin], hi = t.base[lmax + 1];
+    const uint64_t n = list ? (uint64_t)*list_cnt : (hi - lo);
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        uint64_t slot;
+        uint32_t l = lmin;
+        if (list) {
+            slot = t.base[lmin] + list[i];
+        } else {
+            slot = lo + i;
+            while (t.base[l + 1] <= slot) l++;
+        }
+        if (mask && !mask[slot]) continue;
+        const uint64_t b = slot - t.base[l];
+        const uint32_t len = stage_inner(t, l, b, reg);
+        const uint64_t eslot = (l == 1) ? 0 : slot;
+        if (MODE == MODE_VERIFY) {
+            const uint16_t et = t.tag[eslot];
+            bool good;
+            if (!(et & TAG_PRESENT)) {
+                good = (len == 0);
+            } else {
+                uint32_t d[4];
+                stmd5::md5_lds(reg, len, d);
+                const uint4 e = t.md5[eslot];
+                good = (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+            }
+            if (ok) ok[slot] = good ? 1 : 0;
+            if (!good && fail) atomicOr(fail, 1u);
+        } else {
+            if (len == 0) {
+                t.tag[slot] = 0;
+                if (l == 1) t.tag[0] = 0;
+            } else {
+                uint32_t d[4];
+                stmd5::md5_lds(reg, len, d);
+                const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
+                t.md5[slot] = e;
+                t.tag[slot] = TAG_PRESENT;
+                if (l == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Merge a sorted batch into the segment CSR (insert/3's orddict:store,
+// synctree.erl:206, applied per segment with last-writer-wins).
+
+struct MergeArgs {
+    // old tree
+    const uint64_t *seg_off;
+    const uint64_t *koff;
+    const uint8_t *kheap;
+    // batch (sorted order = perm, runs = bseg_off, keep = last writer)
+    const uint32_t *perm;
+    const uint64_t *bseg_off;
+    const uint8_t *keep;
+    const uint8_t *bop;         // NULL: all PUT; else 1 = ERASE
+    const uint8_t *seg_reject;  // NULL or per segment: nonzero => batch run ignored
+    const uint8_t *seg_replace; // NULL or per segment: nonzero => old run dropped
+    BatchView bv;
+    uint64_t S;
+};
+
+template <bool WRITE>
+__global__ void k_merge(MergeArgs a, uint64_t *cnt_or_off, uint64_t *src, uint8_t *dirty) {
+    for (uint64_t s = gtid(); s < a.S; s += gstride()) {
+        uint64_t i = a.seg_off ? a.seg_off[s] : 0, ie = a.seg_off ? a.seg_off[s + 1] : 0;
+        uint64_t j = a.bseg_off[s], je = a.bseg_off[s + 1];
+        if (a.seg_reject && a.seg_reject[s]) j = je;
+        if (a.seg_replace && a.seg_replace[s]) i = ie;
+        uint64_t out = WRITE ? cnt_or_off[s] : 0;
+        bool changed = false;
+        while (i < ie || j < je) {
+            if (j < je && !a.keep[j]) { j++; continue; }
+            int c;
+            uint32_t bi = 0;
+            if (j < je) bi = a.perm[j];
+            if (i < ie && j < je) {
+                c = rec_cmp(a.kheap + a.koff[i], a.koff[i + 1] - a.koff[i], a.bv.kheap + a.bv.koff[bi],
+                            a.bv.koff[bi + 1] - a.bv.koff[bi]);
+            } else {
+                c = (i < ie) ? -1 : 1;
+            }
+            if (c < 0) {
+                if (WRITE) src[out] = i;
+                out++;
+                i++;
+            } else {
+                const bool erase = a.bop && a.bop[bi];
+                if (!erase) {
+                    if (WRITE) src[out] = (1ull << 63) | bi;
+                    out++;
+                }
+                changed = true;
+                if (c == 0) i++;
+                j++;
+            }
+        }
+        if (!WRITE) {
+            cnt_or_off[s] = out;
+            if (dirty) dirty[s] = changed ? 1 : 0;
+        }
+    }
+}
+
+// Per new entry: key/value byte lengths (for the offset scans).
+__global__ void k_src_lengths(const uint64_t *src, uint64_t n, const uint64_t *okoff, const uint64_t *ovoff,
+                              const uint64_t *bkoff, const uint64_t *bvoff, uint64_t *klen, uint64_t *vlen) {
+    for (uint64_t j = gtid(); j <= n; j += gstride()) {
+        if (j == n) { klen[j] = 0; vlen[j] = 0; break; }
+        const uint64_t s = src[j];
+        if (s >> 63) {
+            const uint64_t b = s & 0x7fffffffffffffffull;
+            klen[j] = bkoff[b + 1] - bkoff[b];
+            vlen[j] = bvoff[b + 1] - bvoff[b];
+        } else {
+            klen[j] = okoff[s + 1] - okoff[s];
+            vlen[j] = ovoff[s + 1] - ovoff[s];
+        }
+    }
+}
+
+__global__ void k_gather_entries(const uint64_t *src, uint64_t n, const uint64_t *okoff, const uint8_t *okheap,
+                                 const uint64_t *ovoff, const uint8_t *ovheap, const uint64_t *bkoff,
+                                 const uint8_t *bkheap, const uint64_t *bvoff, const uint8_t *bvheap,
+                                 const uint64_t *nkoff, uint8_t *nkheap, const uint64_t *nvoff, uint8_t *nvheap) {
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        const uint64_t s = src[j];
+        const uint8_t *kp, *vp;
+        uint64_t kl, vl;
+        if (s >> 63) {
+            const uint64_t b = s & 0x7fffffffffffffffull;
+            kp = bkheap + bkoff[b]; kl = bkoff[b + 1] - bkoff[b];
+            vp = bvheap + bvoff[b]; vl = bvoff[b + 1] - bvoff[b];
+        } else {
+            kp = okheap + okoff[s]; kl = okoff[s + 1] - okoff[s];
+            vp = ovheap + ovoff[s]; vl = ovoff[s + 1] - ovoff[s];
+        }
+        copy_bytes(nkheap + nkoff[j], kp, kl);
+        copy_bytes(nvheap + nvoff[j], vp, vl);
+    }
+}
+
+__global__ void k_seg_voff(const uint64_t *seg_off, const uint64_t *voff, uint64_t S, uint64_t *seg_voff) {
+    for (uint64_t s = gtid(); s <= S; s += gstride()) seg_voff[s] = voff[seg_off[s]];
+}
+
+// Per batch key: insert status from its segment's path status.
+__global__ void k_key_status(const uint32_t *seg, uint64_t n, const uint8_t *seg_reject, uint32_t *clevel) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) clevel[i] = seg_reject[seg[i]];
+}
+
+__global__ void k_count_nonzero(const uint8_t *flags, uint64_t n, unsigned long long *cnt) {
+    uint32_t c = 0;
+    for (uint64_t i = gtid(); i < n; i += gstride()) c += flags[i] ? 1u : 0u;
+    if (c) atomicAdd(cnt, (unsigned long long)c);
+}
+
+// ---------------------------------------------------------------------------
+// Reads: get/2 lookups and exchange_get node images
+
+// For each key (segment seg[i], record i of the batch): index of the entry in
+// the tree with an equal key, or UINT64_MAX.  (orddict_find, synctree.erl:342-348)
+__global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t n, uint64_t *found) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t s = seg[i];
+        uint64_t lo = t.seg_off[s], hi = t.seg_off[s + 1];
+        const uint8_t *k = bv.kheap + bv.koff[i];
+        const uint64_t kl = bv.koff[i + 1] - bv.koff[i];
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) / 2;
+            if (rec_cmp(t.kheap + t.koff[m], t.koff[m + 1] - t.koff[m], k, kl) < 0) lo = m + 1; else hi = m;
+        }
+        uint64_t r = ~0ull;
+        if (lo < t.seg_off[s + 1] && rec_cmp(t.kheap + t.koff[lo], t.koff[lo + 1] - t.koff[lo], k, kl) == 0) r = lo;
+        found[i] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3 tree_compare: level-synchronous diff (exchange/exchange_level,
+// synctree.erl:386-406) of two trees of the same geometry.  One lane per
+// frontier node: verify the node on both sides against its parent's entry
+// (exchange_get's verified path; ancestors were verified at earlier levels),
+// then diff the W child entries (orddict_delta, riak_ensemble_util.erl:115-141)
+// under the filter and set the differing children in the next frontier bitmap.
+// err: min over (level, bucket, side) of a failed verification — the
+// reference's first crash in visiting order (local before remote).
+
+__device__ __forceinline__ bool verify_inner_node(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
+    const uint64_t slot = t.base[l] + b;
+    const uint64_t eslot = (l == 1) ? 0 : slot;
+    const uint32_t len = stage_inner(t, l, b, reg);
+    const uint16_t et = t.tag[eslot];
+    if (!(et & TAG_PRESENT)) return len == 0;
+    uint32_t d[4];
+    stmd5::md5_lds(reg, len, d);
+    const uint4 e = t.md5[eslot];
+    return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+}
+
+__device__ __forceinline__ bool verify_segment(const DevTree &t, uint64_t s) {
+    const uint32_t L = t.H + 1;
+    const uint64_t slot = t.base[L] + s;
+    const uint64_t eslot = (L == 1) ? 0 : slot;
+    const uint16_t et = t.tag[eslot];
+    if (!(et & TAG_PRESENT)) return t.seg_off[s] == t.seg_off[s + 1];
+    uint32_t d[4];
+    const uint64_t v0 = t.seg_voff[s];
+    stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+    const uint4 e = t.md5[eslot];
+    return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+}
+
+__device__ __forceinline__ uint64_t err_code(uint32_t level, uint64_t bucket, uint32_t side) {
+    return ((uint64_t)level << 56) | (bucket << 1) | side;
+}
+
+// level 0: [{0,TopA}] vs [{0,TopB}] (exchange_get(0,0) is not verified)
+__global__ void k_cmp_top(DevTree A, DevTree B, uint32_t *list, uint32_t *cnt) {
+    if (gtid() != 0) return;
+    const uint16_t ta = A.tag[0], tb = B.tag[0];
+    bool same = (ta == tb);
+    if (same && (ta & TAG_PRESENT)) {
+        const uint4 x = A.md5[0], y = B.md5[0];
+        same = x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
+    }
+    list[0] = 0;
+    *cnt = same ? 0u : 1u;
+}
+
+__global__ void k_cmp_inner(DevTree A, DevTree B, uint32_t level, const uint32_t *list, const uint32_t *cnt,
+                            unsigned long long *bitmap, int filter, unsigned long long *err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(A.W);
+    if (*err != ~0ull) return;
+    const uint64_t n = *cnt;
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t b = list[i];
+        if (!verify_inner_node(A, level, b, reg)) { atomicMin(err, err_code(level, b, 0)); continue; }
+        if (!verify_inner_node(B, level, b, reg)) { atomicMin(err, err_code(level, b, 1)); continue; }
+        const uint64_t c0 = A.base[level + 1] + b * A.W;
+        unsigned long long word = 0;
+        uint64_t cur_w = ~0ull;
+        for (uint32_t j = 0; j < A.W; j++) {
+            const uint16_t ta = A.tag[c0 + j], tb = B.tag[c0 + j];
+            const bool pa = ta & TAG_PRESENT, pb = tb & TAG_PRESENT;
+            bool d = false;
+            if (pa && pb) {
+                const uint4 x = A.md5[c0 + j], y = B.md5[c0 + j];
+                d = ta != tb || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+            } else if (pa) {
+                d = filter != 1;   // {C,{H,'$none'}} dropped by local_only
+            } else if (pb) {
+                d = filter != 2;   // {C,{'$none',H}} dropped by remote_only
+            }
+            if (!d) continue;
+            const uint64_t child = b * A.W + j;
+            const uint64_t w = child >> 6;
+            if (w != cur_w) {
+                if (word) atomicOr(bitmap + cur_w, word);
+                word = 0;
+                cur_w = w;
+            }
+            word |= 1ull << (child & 63);
+        }
+        if (word) atomicOr(bitmap + cur_w, word);
+    }
+}
+
+// bitmap (nwords 64-bit words) -> ascending list of set bit indices; clears
+// the bitmap.  One workgroup of 1024 threads.
+__global__ void __launch_bounds__(1024) k_bitmap_to_list(unsigned long long *bitmap, uint64_t nwords, uint32_t *list,
+                                                         uint32_t *cnt) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    const uint64_t per = 16;
+    for (uint64_t base = 0; base < nwords; base += 1024 * per) {
+        const uint64_t w0 = base + tid * per;
+        uint32_t c = 0;
+        for (uint64_t w = w0; w < w0 + per && w < nwords; w++) c += __popcll(bitmap[w]);
+        part[tid] = c;
+        __syncthreads();
+        for (uint32_t off = 1; off < 1024; off <<= 1) {
+            uint32_t v = tid >= off ? part[tid - off] : 0;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        uint32_t pos = carry + part[tid] - c;
+        for (uint64_t w = w0; w < w0 + per && w < nwords; w++) {
+            unsigned long long x = bitmap[w];
+            if (!x) continue;
+            bitmap[w] = 0;
+            while (x) {
+                const int bit = __ffsll((long long)x) - 1;
+                list[pos++] = (uint32_t)(w * 64 + bit);
+                x &= x - 1;
+            }
+        }
+        __syncthreads();
+        if (tid == 1023) carry += part[1023];
+        __syncthreads();
+    }
+    if (tid == 0) *cnt = carry;
+}
+
+// Final level (exchange_final, synctree.erl:408-417): verify both segments,
+// merge-join their key lists, count (WRITE=false) or emit (WRITE=true) the
+// diff records.  Output order: AccFun = Keys ++ Acc over ascending segments
+// => records of the LAST frontier segment first.
+struct DiffRec {
+    uint64_t a, b, seg;   // entry indices (~0 = '$none')
+    uint32_t kind, pad;
+};
+
+template <bool WRITE>
+__global__ void k_cmp_segments(DevTree A, DevTree B, const uint32_t *list, uint64_t n, int filter,
+                               uint64_t *dcnt, const uint64_t *doff, uint64_t total, DiffRec *out,
+                               unsigned long long *err) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t s = list[i];
+        if (!WRITE) {
+            if (!verify_segment(A, s)) { atomicMin(err, err_code(A.H + 1, s, 0)); dcnt[i] = 0; continue; }
+            if (!verify_segment(B, s)) { atomicMin(err, err_code(A.H + 1, s, 1)); dcnt[i] = 0; continue; }
+        }
+        uint64_t x = A.seg_off[s], xe = A.seg_off[s + 1];
+        uint64_t y = B.seg_off[s], ye = B.seg_off[s + 1];
+        uint64_t c = 0;
+        uint64_t pos = WRITE ? (total - doff[i] - dcnt[i]) : 0;
+        while (x < xe || y < ye) {
+            int cmp;
+            if (x < xe && y < ye)
+                cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y],
+                              B.koff[y + 1] - B.koff[y]);
+            else
+                cmp = x < xe ? -1 : 1;
+            DiffRec r;
+            r.seg = s;
+            r.pad = 0;
+            bool emit = false;
+            if (cmp < 0) {
+                r.a = x; r.b = ~0ull; r.kind = 1;
+                emit = filter != 1;
+                x++;
+            } else if (cmp > 0) {
+                r.a = ~0ull; r.b = y; r.kind = 2;
+                emit = filter != 2;
+                y++;
+            } else {
+                const uint64_t la = A.voff[x + 1] - A.voff[x], lb = B.voff[y + 1] - B.voff[y];
+                emit = !bytes_eq(A.vheap + A.voff[x], la, B.vheap + B.voff[y], lb);
+                r.a = x; r.b = y; r.kind = 0;
+                x++; y++;
+            }
+            if (emit) {
+                if (WRITE) out[pos] = r;
+                pos++;
+                c++;
+            }
+        }
+        if (!WRITE) dcnt[i] = c;
+    }
+}
+
+// Diff records -> byte lengths of key / local value / remote value
+__global__ void k_diff_lengths(DevTree A, DevTree B, const DiffRec *r, uint64_t n, uint64_t *kl, uint64_t *al,
+                               uint64_t *bl) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        if (i == n) { kl[i] = al[i] = bl[i] = 0; break; }
+        const DiffRec d = r[i];
+        if (d.a != ~0ull) {
+            kl[i] = A.koff[d.a + 1] - A.koff[d.a];
+            al[i] = A.voff[d.a + 1] - A.voff[d.a];
+        } else {
+            kl[i] = B.koff[d.b + 1] - B.koff[d.b];
+            al[i] = 0;
+        }
+        bl[i] = d.b != ~0ull ? B.voff[d.b + 1] - B.voff[d.b] : 0;
+    }
+}
+
+__global__ void k_diff_gather(DevTree A, DevTree B, const DiffRec *r, uint64_t n, const uint64_t *koff,
+                              uint8_t *kheap, const uint64_t *aoff, uint8_t *aheap, const uint64_t *boff,
+                              uint8_t *bheap, uint8_t *kind, uint64_t *seg) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const DiffRec d = r[i];
+        if (d.a != ~0ull) {
+            copy_bytes(kheap + koff[i], A.kheap + A.koff[d.a], A.koff[d.a + 1] - A.koff[d.a]);
+            copy_bytes(aheap + aoff[i], A.vheap + A.voff[d.a], A.voff[d.a + 1] - A.voff[d.a]);
+        } else {
+            copy_bytes(kheap + koff[i], B.kheap + B.koff[d.b], B.koff[d.b + 1] - B.koff[d.b]);
+        }
+        if (d.b != ~0ull) copy_bytes(bheap + boff[i], B.vheap + B.voff[d.b], B.voff[d.b + 1] - B.voff[d.b]);
+        kind[i] = (uint8_t)d.kind;
+        seg[i] = d.seg;
+    }
+}
+
+// Gather entries by index list (get results / segment images) into packed heaps.
+__global__ void k_entry_lengths(DevTree t, const uint64_t *idx, uint64_t n, uint64_t *kl, uint64_t *vl) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        if (i == n) { kl[i] = vl[i] = 0; break; }
+        const uint64_t e = idx[i];
+        if (e == ~0ull) { kl[i] = vl[i] = 0; continue; }
+        kl[i] = t.koff[e + 1] - t.koff[e];
+        vl[i] = t.voff[e + 1] - t.voff[e];
+    }
+}
+
+__global__ void k_entry_gather(DevTree t, const uint64_t *idx, uint64_t n, const uint64_t *koff, uint8_t *kheap,
+                               const uint64_t *voff, uint8_t *vheap) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t e = idx[i];
+        if (e == ~0ull) continue;
+        if (kheap) copy_bytes(kheap + koff[i], t.kheap + t.koff[e], t.koff[e + 1] - t.koff[e]);
+        copy_bytes(vheap + voff[i], t.vheap + t.voff[e], t.voff[e + 1] - t.voff[e]);
+    }
+}

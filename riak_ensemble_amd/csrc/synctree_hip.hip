@@ -1,0 +1,1365 @@
+// synctree_hip.hip — libsynctree_hip.so: C-ABI (include/synctree_hip.h) over
+// the gfx950 kernels in st_kernels.h.  Host code only orchestrates: every
+// hash, comparison, sort and merge of tree data runs on the device.
+//
+// Reference: src/synctree.erl (jrwest/riak_ensemble); see the header for the
+// per-function mapping and DESIGN.md for layouts and rooflines.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/synctree_hip.h"
+#include "st_kernels.h"
+
+static thread_local std::string g_err;
+static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past a range
+
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            g_err = std::string(#x) + ": " + hipGetErrorString(e_);                       \
+            return ST_EDEVICE;                                                            \
+        }                                                                                 \
+    } while (0)
+
+#define CHK(x)                                     \
+    do {                                           \
+        int r_ = (x);                              \
+        if (r_ != ST_OK) return r_;                \
+    } while (0)
+
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+};
+
+struct st_tree {
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    uint64_t W = 16, S = 1 << 20;
+    uint32_t shift = 4, H = 5;
+    uint64_t base[ST_MAXLEV + 2] = {0};
+    uint64_t nslots = 0;
+    uint4 *md5 = nullptr;
+    uint16_t *tag = nullptr;
+    uint8_t *mark = nullptr, *ok = nullptr;
+    uint32_t *flag = nullptr;
+    unsigned long long *cnt64 = nullptr;
+    // segment CSR
+    uint64_t n = 0, kbytes = 0, vbytes = 0;
+    uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
+    uint8_t *kheap = nullptr, *vheap = nullptr;
+    bool fresh = true;
+    // timing
+    bool timing = false;
+    std::vector<Pending> pending;
+    std::map<std::string, std::pair<uint64_t, double>> stats;
+};
+
+// ------------------------------------------------------------------ helpers
+static int dalloc(st_tree *t, void **p, uint64_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMallocAsync(p, bytes, t->stream);
+    if (e != hipSuccess) {
+        g_err = std::string("hipMallocAsync: ") + hipGetErrorString(e);
+        return e == hipErrorOutOfMemory ? ST_ENOMEM : ST_EDEVICE;
+    }
+    return ST_OK;
+}
+template <typename T>
+static int dalloc_t(st_tree *t, T **p, uint64_t count) {
+    return dalloc(t, (void **)p, count * sizeof(T));
+}
+static void dfree(st_tree *t, void *p) {
+    if (p) (void)hipFreeAsync(p, t->stream);
+}
+
+static DevTree view(const st_tree *t) {
+    DevTree d;
+    memset(&d, 0, sizeof(d));
+    d.W = (uint32_t)t->W;
+    d.shift = t->shift;
+    d.H = t->H;
+    d.S = t->S;
+    for (int i = 0; i < ST_MAXLEV + 2; i++) d.base[i] = t->base[i];
+    d.md5 = t->md5;
+    d.tag = t->tag;
+    d.seg_off = t->seg_off;
+    d.seg_voff = t->seg_voff;
+    d.koff = t->koff;
+    d.kheap = t->kheap;
+    d.voff = t->voff;
+    d.vheap = t->vheap;
+    return d;
+}
+
+static uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t cap = 16384) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (uint32_t)g;
+}
+
+struct TimedLaunch {
+    st_tree *t;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(st_tree *t_, const char *n) : t(t_), name(n) {
+        if (t->timing) {
+            (void)hipEventCreate(&a);
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(a, t->stream);
+        }
+    }
+    ~TimedLaunch() {
+        if (t->timing) {
+            (void)hipEventRecord(b, t->stream);
+            t->pending.push_back({name, a, b});
+        }
+    }
+};
+
+#define LAUNCH(t, name, kern, grid, block, shmem, ...)                            \
+    do {                                                                          \
+        TimedLaunch tl_(t, name);                                                 \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(block), shmem, (t)->stream, __VA_ARGS__); \
+        hipError_t e_ = hipGetLastError();                                        \
+        if (e_ != hipSuccess) {                                                   \
+            g_err = std::string("launch ") + name + ": " + hipGetErrorString(e_); \
+            return ST_EDEVICE;                                                    \
+        }                                                                         \
+    } while (0)
+
+static int use_device(st_tree *t) {
+    HIPCHK(hipSetDevice(t->device));
+    return ST_OK;
+}
+
+template <typename T>
+static int exclusive_scan(st_tree *t, const T *in, T *out, uint64_t n) {
+    size_t bytes = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), t->stream));
+    void *tmp;
+    CHK(dalloc(t, &tmp, bytes));
+    hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), t->stream);
+    dfree(t, tmp);
+    HIPCHK(e);
+    return ST_OK;
+}
+
+static int d2h(st_tree *t, void *dst, const void *src, uint64_t bytes) {
+    if (!bytes) return ST_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
+}
+static int h2d(st_tree *t, void *dst, const void *src, uint64_t bytes) {
+    if (!bytes) return ST_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, t->stream));
+    return ST_OK;
+}
+
+static uint32_t inner_block(const st_tree *t) { return 64; }
+static size_t inner_shmem(const st_tree *t) { return (size_t)inner_block(t) * lane_region_bytes((uint32_t)t->W); }
+
+// ------------------------------------------------------------------ lifecycle
+extern "C" const char *st_last_error(void) { return g_err.c_str(); }
+
+extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree **out) {
+    *out = nullptr;
+    if (width < 2 || segments < 1) { g_err = "bad geometry"; return ST_EINVAL; }
+    // compute_height / compute_shift (synctree.erl:270-284), same libm math
+    const double hd = std::log((double)segments) / std::log((double)width);
+    const uint64_t height = (uint64_t)std::trunc(hd);
+    if ((uint64_t)std::trunc(std::pow((double)width, (double)height)) != segments) {
+        g_err = "segments is not a power of width (case_clause)";
+        return ST_EINVAL;
+    }
+    const double sd = std::log((double)width) / std::log(2.0);
+    const uint64_t shift = (uint64_t)std::trunc(sd);
+    if ((uint64_t)std::trunc(std::pow(2.0, (double)shift)) != width) {
+        g_err = "width is not a power of 2 (case_clause)";
+        return ST_EINVAL;
+    }
+    if (width > 64 || segments > (1ull << 31) || height + 1 > ST_MAXLEV) {
+        g_err = "geometry outside the device domain (W <= 64, Segments <= 2^31)";
+        return ST_EINVAL;
+    }
+    st_tree *t = new st_tree();
+    t->device = device;
+    t->W = width;
+    t->S = segments;
+    t->shift = (uint32_t)shift;
+    t->H = (uint32_t)height;
+    // slot 0: #tree.top_hash; levels 1..H+1
+    t->base[0] = 0;
+    t->base[1] = 1;
+    uint64_t sz = 1;
+    for (uint32_t l = 1; l <= t->H + 1; l++) {
+        t->base[l + 1] = t->base[l] + sz;
+        sz *= width;
+    }
+    for (uint32_t l = t->H + 3; l < ST_MAXLEV + 2; l++) t->base[l] = t->base[t->H + 2];
+    t->nslots = t->base[t->H + 2];
+    int r = ST_OK;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        g_err = "hipSetDevice/hipStreamCreate failed";
+        delete t;
+        return ST_EDEVICE;
+    }
+    t->stream = t->own_stream;
+    {
+        // keep freed pool memory cached (no release to the OS at every sync)
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+    }
+    if ((r = dalloc_t(t, &t->md5, t->nslots)) || (r = dalloc_t(t, &t->tag, t->nslots)) ||
+        (r = dalloc_t(t, &t->mark, t->nslots)) || (r = dalloc_t(t, &t->ok, t->nslots)) ||
+        (r = dalloc_t(t, &t->flag, 4)) || (r = dalloc_t(t, &t->cnt64, 2)) ||
+        (r = dalloc_t(t, &t->seg_off, t->S + 1)) || (r = dalloc_t(t, &t->seg_voff, t->S + 1)) ||
+        (r = dalloc_t(t, &t->koff, 1)) || (r = dalloc_t(t, &t->voff, 1)) || (r = dalloc(t, (void **)&t->kheap, HEAP_SLACK)) ||
+        (r = dalloc(t, (void **)&t->vheap, HEAP_SLACK))) {
+        st_destroy(t);
+        return r;
+    }
+    (void)hipMemsetAsync(t->md5, 0, t->nslots * sizeof(uint4), t->stream);
+    (void)hipMemsetAsync(t->tag, 0, t->nslots * sizeof(uint16_t), t->stream);
+    (void)hipMemsetAsync(t->seg_off, 0, (t->S + 1) * 8, t->stream);
+    (void)hipMemsetAsync(t->seg_voff, 0, (t->S + 1) * 8, t->stream);
+    (void)hipMemsetAsync(t->koff, 0, 8, t->stream);
+    (void)hipMemsetAsync(t->voff, 0, 8, t->stream);
+    (void)hipMemsetAsync(t->kheap, 0, HEAP_SLACK, t->stream);
+    (void)hipMemsetAsync(t->vheap, 0, HEAP_SLACK, t->stream);
+    if (hipStreamSynchronize(t->stream) != hipSuccess) {
+        g_err = "init failed";
+        st_destroy(t);
+        return ST_EDEVICE;
+    }
+    *out = t;
+    return ST_OK;
+}
+
+extern "C" void st_destroy(st_tree *t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap};
+    for (void *p : ps) dfree(t, p);
+    for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
+    delete t;
+}
+
+extern "C" int st_set_stream(st_tree *t, void *s) {
+    CHK(use_device(t));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    t->stream = s ? (hipStream_t)s : t->own_stream;
+    return ST_OK;
+}
+
+extern "C" int st_sync(st_tree *t) {
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
+}
+
+extern "C" uint32_t st_height(const st_tree *t) { return t->H; }
+extern "C" uint64_t st_width(const st_tree *t) { return t->W; }
+extern "C" uint64_t st_segments(const st_tree *t) { return t->S; }
+extern "C" uint64_t st_num_entries(st_tree *t) { return t->n; }
+
+extern "C" int st_set_timing(st_tree *t, int enabled) {
+    t->timing = enabled != 0;
+    return ST_OK;
+}
+
+extern "C" int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *total_ms) {
+    HIPCHK(hipStreamSynchronize(t->stream));
+    for (auto &p : t->pending) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
+        auto &s = t->stats[p.name];
+        s.first += 1;
+        s.second += ms;
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    t->pending.clear();
+    auto it = t->stats.find(kernel ? kernel : "");
+    if (kernel && std::string(kernel) == "*reset*") {
+        t->stats.clear();
+        return ST_OK;
+    }
+    *launches = it == t->stats.end() ? 0 : it->second.first;
+    *total_ms = it == t->stats.end() ? 0.0 : it->second.second;
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ key records
+// Host packing of (type, ensure_binary bytes) into device key records.
+struct HostRecords {
+    std::vector<uint8_t> heap;
+    std::vector<uint64_t> off;
+};
+
+static int pack_records(uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff, HostRecords &r) {
+    r.off.resize(n + 1);
+    r.heap.clear();
+    r.heap.reserve((koff ? koff[n] : 0) + n + HEAP_SLACK);
+    for (uint64_t i = 0; i < n; i++) {
+        r.off[i] = r.heap.size();
+        const uint8_t ty = ktype[i];
+        const uint64_t len = koff[i + 1] - koff[i];
+        const uint8_t *p = kheap + koff[i];
+        if (ty == ST_KEY_INT) {
+            if (len != 8) { g_err = "integer key must be 8 bytes (<<K:64>>)"; return ST_EINVAL; }
+            r.heap.push_back(KEYTAG_INT);
+            r.heap.push_back(p[0] ^ 0x80);
+            r.heap.insert(r.heap.end(), p + 1, p + 8);
+        } else if (ty == ST_KEY_ATOM || ty == ST_KEY_BINARY) {
+            r.heap.push_back(ty);
+            r.heap.insert(r.heap.end(), p, p + len);
+        } else {
+            g_err = "key type outside the device domain (term_to_binary keys)";
+            return ST_EINVAL;
+        }
+    }
+    r.off[n] = r.heap.size();
+    r.heap.resize(r.heap.size() + HEAP_SLACK, 0);
+    return ST_OK;
+}
+
+static int host_rec_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    uint64_t m = la < lb ? la : lb;
+    int c = m ? memcmp(a, b, m) : 0;
+    if (c) return c < 0 ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// ------------------------------------------------------------------ rehash pieces
+static int rehash_levels(st_tree *t, uint32_t top_level, const uint8_t *mask) {
+    DevTree d = view(t);
+    for (uint32_t l = top_level; l >= 1; l--) {
+        const uint64_t nodes = t->base[l + 1] - t->base[l];
+        LAUNCH(t, "level_rehash", (k_level_hash<MODE_STORE>), grid_for(nodes, inner_block(t)), inner_block(t),
+               inner_shmem(t), d, l, l, mask, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr,
+               (uint32_t *)nullptr);
+    }
+    return ST_OK;
+}
+
+// Verify every node marked in t->mark (levels 1..L); results in t->ok.
+static int verify_marked(st_tree *t, uint32_t L) {
+    DevTree d = view(t);
+    if (L == t->H + 1)
+        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
+               (const uint32_t *)nullptr, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+    const uint32_t lmax = L < t->H ? L : t->H;
+    if (lmax >= 1) {
+        const uint64_t nodes = t->base[lmax + 1] - t->base[1];
+        LAUNCH(t, "level_verify", (k_level_hash<MODE_VERIFY>), grid_for(nodes, inner_block(t)), inner_block(t),
+               inner_shmem(t), d, 1u, lmax, (const uint8_t *)t->mark, (const uint32_t *)nullptr,
+               (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+    }
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ ingest
+// Merge n device key records (+ values) into the tree.
+//  seg_given: precomputed segment per record (raw segment store) or NULL
+//  bop: per-record ERASE flags (device) or NULL
+//  seg_replace: per-segment replace flags (device) or NULL
+//  verify_rehash: insert semantics (path verification + dirty-path rehash)
+//  clevel_out: per-record corruption level (device, n) or NULL
+//  seg_out: per-record segment (device, n) or NULL
+struct IngestIn {
+    uint64_t n;
+    const uint8_t *krec;
+    const uint64_t *koff;
+    const uint8_t *vheap;
+    const uint64_t *voff;
+    const uint32_t *seg_given;
+    const uint8_t *bop;
+    const uint8_t *seg_replace;
+    bool verify_rehash;
+    uint32_t *clevel_out;
+    uint32_t *seg_out;
+    uint64_t n_rejected;
+};
+
+static int ingest(st_tree *t, IngestIn &in) {
+    const uint64_t n = in.n, S = t->S;
+    in.n_rejected = 0;
+    if (n == 0) return ST_OK;
+    DevTree d = view(t);
+    uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr;
+    uint64_t *bseg_off = nullptr, *cnt = nullptr, *nseg_off = nullptr, *src = nullptr, *klen = nullptr, *vlen = nullptr;
+    uint64_t *nkoff = nullptr, *nvoff = nullptr, *nseg_voff = nullptr;
+    uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr, *nkheap = nullptr, *nvheap = nullptr;
+    int r = ST_OK;
+    auto cleanup = [&]() {
+        void *ps[] = {seg, sseg, idx, perm, bseg_off, cnt, src, klen, vlen, keep, reject, dirty};
+        for (void *p : ps) dfree(t, p);
+    };
+#define ICHK(x)                        \
+    do {                               \
+        r = (x);                       \
+        if (r != ST_OK) { cleanup(); return r; } \
+    } while (0)
+    ICHK(dalloc_t(t, &seg, n));
+    ICHK(dalloc_t(t, &sseg, n));
+    ICHK(dalloc_t(t, &idx, n));
+    ICHK(dalloc_t(t, &perm, n));
+    ICHK(dalloc_t(t, &bseg_off, S + 1));
+    ICHK(dalloc_t(t, &keep, n));
+    if (in.seg_given) {
+        HIPCHK(hipMemcpyAsync(seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
+    } else {
+        LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, seg);
+    }
+    if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
+    LAUNCH(t, "iota", k_iota, grid_for(n), 256, 0, idx, n);
+    if (S > 1) {
+        unsigned end_bit = 0;
+        while ((1ull << end_bit) < S) end_bit++;
+        size_t bytes = 0;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream));
+        void *tmp;
+        ICHK(dalloc(t, &tmp, bytes));
+        {
+            TimedLaunch tl(t, "radix_sort");
+            hipError_t e = rocprim::radix_sort_pairs(tmp, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream);
+            if (e != hipSuccess) { dfree(t, tmp); cleanup(); g_err = "radix_sort_pairs failed"; return ST_EDEVICE; }
+        }
+        dfree(t, tmp);
+    } else {
+        HIPCHK(hipMemcpyAsync(sseg, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
+        HIPCHK(hipMemcpyAsync(perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
+    }
+    LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
+    BatchView bv{in.krec, in.koff};
+    LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, perm, (const uint64_t *)bseg_off, S, keep);
+
+    // path verification of touched segments (insert semantics)
+    if (in.verify_rehash) {
+        ICHK(dalloc_t(t, &reject, S));
+        if (t->fresh) {
+            HIPCHK(hipMemsetAsync(reject, 0, S, t->stream));
+        } else {
+            HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+            LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
+                   (const uint64_t *)nullptr, S, t->mark);
+            ICHK(verify_marked(t, t->H + 1));
+            LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
+                   (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
+        }
+        if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)seg, n,
+                                  (const uint8_t *)reject, in.clevel_out);
+    }
+
+    // merge: count, scan, write
+    MergeArgs ma;
+    ma.seg_off = t->seg_off;
+    ma.koff = t->koff;
+    ma.kheap = t->kheap;
+    ma.perm = perm;
+    ma.bseg_off = bseg_off;
+    ma.keep = keep;
+    ma.bop = in.bop;
+    ma.seg_reject = reject;
+    ma.seg_replace = in.seg_replace;
+    ma.bv = bv;
+    ma.S = S;
+    ICHK(dalloc_t(t, &cnt, S + 1));
+    ICHK(dalloc_t(t, &dirty, S));
+    HIPCHK(hipMemsetAsync(cnt + S, 0, 8, t->stream));
+    LAUNCH(t, "merge_count", (k_merge<false>), grid_for(S), 256, 0, ma, cnt, (uint64_t *)nullptr, dirty);
+    ICHK(dalloc_t(t, &nseg_off, S + 1));
+    ICHK(exclusive_scan<uint64_t>(t, cnt, nseg_off, S + 1));
+    uint64_t n_new = 0;
+    ICHK(d2h(t, &n_new, nseg_off + S, 8));
+    ICHK(dalloc_t(t, &src, n_new + 1));
+    LAUNCH(t, "merge_write", (k_merge<true>), grid_for(S), 256, 0, ma, nseg_off, src, (uint8_t *)nullptr);
+    ICHK(dalloc_t(t, &klen, n_new + 1));
+    ICHK(dalloc_t(t, &vlen, n_new + 1));
+    LAUNCH(t, "src_lengths", k_src_lengths, grid_for(n_new + 1), 256, 0, (const uint64_t *)src, n_new,
+           (const uint64_t *)t->koff, (const uint64_t *)t->voff, in.koff, in.voff, klen, vlen);
+    ICHK(dalloc_t(t, &nkoff, n_new + 1));
+    ICHK(dalloc_t(t, &nvoff, n_new + 1));
+    ICHK(exclusive_scan<uint64_t>(t, klen, nkoff, n_new + 1));
+    ICHK(exclusive_scan<uint64_t>(t, vlen, nvoff, n_new + 1));
+    uint64_t tot[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&tot[0], nkoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[1], nvoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    ICHK(dalloc(t, (void **)&nkheap, tot[0] + HEAP_SLACK));
+    ICHK(dalloc(t, (void **)&nvheap, tot[1] + HEAP_SLACK));
+    HIPCHK(hipMemsetAsync(nkheap + tot[0], 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(nvheap + tot[1], 0, HEAP_SLACK, t->stream));
+    LAUNCH(t, "gather_entries", k_gather_entries, grid_for(n_new), 256, 0, (const uint64_t *)src, n_new,
+           (const uint64_t *)t->koff, (const uint8_t *)t->kheap, (const uint64_t *)t->voff, (const uint8_t *)t->vheap,
+           in.koff, in.krec, in.voff, in.vheap, (const uint64_t *)nkoff, nkheap, (const uint64_t *)nvoff, nvheap);
+    ICHK(dalloc_t(t, &nseg_voff, S + 1));
+    LAUNCH(t, "seg_voff", k_seg_voff, grid_for(S + 1), 256, 0, (const uint64_t *)nseg_off, (const uint64_t *)nvoff, S,
+           nseg_voff);
+    // swap in the new CSR
+    dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
+    t->seg_off = nseg_off; t->seg_voff = nseg_voff; t->koff = nkoff; t->voff = nvoff; t->kheap = nkheap; t->vheap = nvheap;
+    t->n = n_new; t->kbytes = tot[0]; t->vbytes = tot[1];
+
+    if (in.verify_rehash) {
+        // dirty-path rehash: segments whose content changed and their ancestors
+        HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+        d = view(t);
+        LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
+        LAUNCH(t, "segment_hash", (k_segment_hash<MODE_STORE>), grid_for(S), 256, 0, d, (const uint8_t *)t->mark,
+               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint32_t *)nullptr);
+        ICHK(rehash_levels(t, t->H, t->mark));
+    }
+    t->fresh = false;
+    cleanup();
+#undef ICHK
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ writes
+static int upload_records(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                          uint8_t **d_krec, uint64_t **d_koff) {
+    HostRecords hr;
+    CHK(pack_records(n, ktype, kheap, koff, hr));
+    CHK(dalloc(t, (void **)d_krec, hr.heap.size()));
+    CHK(dalloc_t(t, d_koff, n + 1));
+    CHK(h2d(t, *d_krec, hr.heap.data(), hr.heap.size()));
+    CHK(h2d(t, *d_koff, hr.off.data(), (n + 1) * 8));
+    HIPCHK(hipStreamSynchronize(t->stream));   // host vectors die here
+    return ST_OK;
+}
+
+static int upload_values(st_tree *t, uint64_t n, const uint8_t *vheap, const uint64_t *voff, uint8_t **d_vheap,
+                         uint64_t **d_voff) {
+    const uint64_t vb = voff[n] - voff[0];
+    CHK(dalloc(t, (void **)d_vheap, vb + HEAP_SLACK));
+    CHK(dalloc_t(t, d_voff, n + 1));
+    std::vector<uint64_t> vo(n + 1);
+    for (uint64_t i = 0; i <= n; i++) vo[i] = voff[i] - voff[0];
+    CHK(h2d(t, *d_vheap, vheap + voff[0], vb));
+    HIPCHK(hipMemsetAsync(*d_vheap + vb, 0, HEAP_SLACK, t->stream));
+    CHK(h2d(t, *d_voff, vo.data(), (n + 1) * 8));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
+}
+
+extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                               const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel,
+                               uint64_t *cbucket) {
+    CHK(use_device(t));
+    if (n == 0) return ST_OK;
+    uint8_t *krec = nullptr, *dv = nullptr;
+    uint64_t *dko = nullptr, *dvo = nullptr;
+    uint32_t *dcl = nullptr, *dseg = nullptr;
+    int r = upload_records(t, n, ktype, kheap, koff, &krec, &dko);
+    if (!r) r = upload_values(t, n, vheap, voff, &dv, &dvo);
+    if (!r && (status || clevel || cbucket)) {
+        r = dalloc_t(t, &dcl, n);
+        if (!r) r = dalloc_t(t, &dseg, n);
+    }
+    if (!r) {
+        IngestIn in{};
+        in.n = n; in.krec = krec; in.koff = dko; in.vheap = dv; in.voff = dvo;
+        in.verify_rehash = true; in.clevel_out = dcl; in.seg_out = dseg;
+        r = ingest(t, in);
+    }
+    if (!r && dcl) {
+        std::vector<uint32_t> cl(n), sg(n);
+        r = d2h(t, cl.data(), dcl, n * 4);
+        if (!r) r = d2h(t, sg.data(), dseg, n * 4);
+        if (!r)
+            for (uint64_t i = 0; i < n; i++) {
+                if (status) status[i] = cl[i] ? ST_CORRUPTED : ST_OK;
+                if (clevel) clevel[i] = cl[i];
+                if (cbucket) cbucket[i] = cl[i] ? ((uint64_t)sg[i] >> (t->shift * (t->H + 1 - cl[i]))) : 0;
+            }
+    }
+    dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, dcl); dfree(t, dseg);
+    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    return r;
+}
+
+extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                               int on_device, uint64_t *n_corrupted) {
+    CHK(use_device(t));
+    if (n_corrupted) *n_corrupted = 0;
+    if (n == 0) return ST_OK;
+    const int64_t *dkeys = keys;
+    const uint8_t *dvals = vals;
+    int64_t *tk = nullptr;
+    uint8_t *tv = nullptr, *krec = nullptr;
+    uint64_t *dko = nullptr, *dvo = nullptr;
+    uint32_t *dcl = nullptr;
+    int r = ST_OK;
+    if (!on_device) {
+        r = dalloc_t(t, &tk, n);
+        if (!r) r = dalloc(t, (void **)&tv, (uint64_t)n * vlen + HEAP_SLACK);
+        if (!r) r = h2d(t, tk, keys, n * 8);
+        if (!r) r = h2d(t, tv, vals, (uint64_t)n * vlen);
+        dkeys = tk;
+        dvals = tv;
+    }
+    if (!r) r = dalloc(t, (void **)&krec, 9 * n + HEAP_SLACK);
+    if (!r) r = dalloc_t(t, &dko, n + 1);
+    if (!r) r = dalloc_t(t, &dvo, n + 1);
+    if (!r && n_corrupted) r = dalloc_t(t, &dcl, n);
+    if (!r) {
+        (void)hipMemsetAsync(krec + 9 * n, 0, HEAP_SLACK, t->stream);
+        TimedLaunch tl(t, "pack_int64");
+        hipLaunchKernelGGL(k_pack_int64, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, dkeys, n, krec, dko, dvo, vlen);
+        if (hipGetLastError() != hipSuccess) { r = ST_EDEVICE; g_err = "pack_int64 launch"; }
+    }
+    if (!r) {
+        IngestIn in{};
+        in.n = n; in.krec = krec; in.koff = dko; in.vheap = dvals; in.voff = dvo;
+        in.verify_rehash = true; in.clevel_out = dcl;
+        r = ingest(t, in);
+    }
+    if (!r && n_corrupted && dcl) {
+        // count per-key rejections
+        std::vector<uint32_t> cl(n);
+        r = d2h(t, cl.data(), dcl, n * 4);
+        uint64_t c = 0;
+        for (uint64_t i = 0; i < n && !r; i++) c += cl[i] != 0;
+        *n_corrupted = c;
+    }
+    dfree(t, tk); dfree(t, tv); dfree(t, krec); dfree(t, dko); dfree(t, dvo); dfree(t, dcl);
+    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    return r;
+}
+
+extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen) {
+    CHK(use_device(t));
+    uint64_t koff[2] = {0, klen};
+    uint8_t *krec = nullptr, *dv = nullptr, *bop = nullptr;
+    uint64_t *dko = nullptr, *dvo = nullptr;
+    int r = upload_records(t, 1, &ktype, kbytes, koff, &krec, &dko);
+    uint64_t voff[2] = {0, 0};
+    uint8_t dummy = 0;
+    if (!r) r = upload_values(t, 1, &dummy, voff, &dv, &dvo);
+    if (!r) r = dalloc_t(t, &bop, 1);
+    if (!r) {
+        (void)hipMemsetAsync(bop, 1, 1, t->stream);
+        IngestIn in{};
+        in.n = 1; in.krec = krec; in.koff = dko; in.vheap = dv; in.voff = dvo; in.bop = bop;
+        in.verify_rehash = false;
+        r = ingest(t, in);
+    }
+    dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, bop);
+    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    return r;
+}
+
+extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
+                                const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff) {
+    CHK(use_device(t));
+    if (segment >= t->S) { g_err = "segment out of range"; return ST_EINVAL; }
+    HostRecords hr;
+    CHK(pack_records(n, ktype, kheap, koff, hr));
+    for (uint64_t i = 1; i < n; i++)
+        if (host_rec_cmp(hr.heap.data() + hr.off[i - 1], hr.off[i] - hr.off[i - 1], hr.heap.data() + hr.off[i],
+                         hr.off[i + 1] - hr.off[i]) >= 0) {
+            g_err = "segment content must be strictly ascending in key order";
+            return ST_EINVAL;
+        }
+    uint8_t *krec = nullptr, *dv = nullptr, *rep = nullptr;
+    uint64_t *dko = nullptr, *dvo = nullptr;
+    uint32_t *dseg = nullptr;
+    int r = ST_OK;
+    uint64_t nn = n;
+    // an empty store still needs one (erased) record to drive the replace
+    std::vector<uint64_t> vz;
+    if (n == 0) {
+        uint8_t kt = ST_KEY_BINARY;
+        uint64_t ko[2] = {0, 0};
+        CHK(pack_records(1, &kt, nullptr, ko, hr));
+        nn = 1;
+    }
+    r = dalloc(t, (void **)&krec, hr.heap.size());
+    if (!r) r = dalloc_t(t, &dko, nn + 1);
+    if (!r) r = h2d(t, krec, hr.heap.data(), hr.heap.size());
+    if (!r) r = h2d(t, dko, hr.off.data(), (nn + 1) * 8);
+    if (!r) {
+        if (n) {
+            r = upload_values(t, n, vheap, voff, &dv, &dvo);
+        } else {
+            uint64_t vo[2] = {0, 0};
+            uint8_t z = 0;
+            r = upload_values(t, 1, &z, vo, &dv, &dvo);
+        }
+    }
+    uint8_t *bop = nullptr;
+    if (!r) r = dalloc_t(t, &dseg, nn);
+    if (!r) r = dalloc_t(t, &rep, t->S);
+    if (!r && n == 0) {
+        r = dalloc_t(t, &bop, 1);
+        if (!r) (void)hipMemsetAsync(bop, 1, 1, t->stream);
+    }
+    if (!r) {
+        std::vector<uint32_t> sg(nn, (uint32_t)segment);
+        r = h2d(t, dseg, sg.data(), nn * 4);
+        (void)hipMemsetAsync(rep, 0, t->S, t->stream);
+        (void)hipMemsetAsync(rep + segment, 1, 1, t->stream);
+        if (!r) {
+            HIPCHK(hipStreamSynchronize(t->stream));
+            IngestIn in{};
+            in.n = nn; in.krec = krec; in.koff = dko; in.vheap = dv; in.voff = dvo;
+            in.seg_given = dseg; in.seg_replace = rep; in.bop = bop;
+            in.verify_rehash = false;
+            r = ingest(t, in);
+        }
+    }
+    dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, dseg); dfree(t, rep); dfree(t, bop);
+    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    return r;
+}
+
+static void set_entry_host(uint16_t &tag, uint4 &m, const uint8_t *h17) {
+    tag = (uint16_t)(TAG_PRESENT | h17[0]);
+    uint32_t w[4];
+    for (int k = 0; k < 4; k++)
+        w[k] = (uint32_t)h17[1 + 4 * k] | ((uint32_t)h17[2 + 4 * k] << 8) | ((uint32_t)h17[3 + 4 * k] << 16) |
+               ((uint32_t)h17[4 + 4 * k] << 24);
+    m = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint32_t n, const uint64_t *children,
+                              const uint8_t *hashes17) {
+    CHK(use_device(t));
+    if (level < 1 || level > t->H) { g_err = "inner level out of range"; return ST_EINVAL; }
+    if (bucket >= t->base[level + 1] - t->base[level]) { g_err = "bucket out of range"; return ST_EINVAL; }
+    std::vector<uint16_t> tags(t->W, 0);
+    std::vector<uint4> md(t->W, make_uint4(0, 0, 0, 0));
+    for (uint32_t i = 0; i < n; i++) {
+        if (children[i] < bucket * t->W || children[i] >= (bucket + 1) * t->W || (i && children[i] <= children[i - 1])) {
+            g_err = "child ids must be ascending and within the node's range";
+            return ST_EINVAL;
+        }
+        const uint64_t j = children[i] - bucket * t->W;
+        set_entry_host(tags[j], md[j], hashes17 + 17 * i);
+    }
+    const uint64_t c0 = t->base[level + 1] + bucket * t->W;
+    CHK(h2d(t, t->tag + c0, tags.data(), t->W * 2));
+    CHK(h2d(t, t->md5 + c0, md.data(), t->W * 16));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    t->fresh = false;
+    return ST_OK;
+}
+
+extern "C" int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket) {
+    if (level == 0) return st_store_top(t, nullptr, 0);
+    if (level == t->H + 1) return st_store_segment(t, bucket, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+    return st_store_inner(t, level, bucket, 0, nullptr, nullptr);
+}
+
+extern "C" int st_store_top(st_tree *t, const uint8_t *hash17, int also_record) {
+    CHK(use_device(t));
+    uint16_t tg = 0;
+    uint4 m = make_uint4(0, 0, 0, 0);
+    if (hash17) set_entry_host(tg, m, hash17);
+    CHK(h2d(t, t->tag + 1, &tg, 2));
+    CHK(h2d(t, t->md5 + 1, &m, 16));
+    if (also_record) {
+        CHK(h2d(t, t->tag, &tg, 2));
+        CHK(h2d(t, t->md5, &m, 16));
+    }
+    HIPCHK(hipStreamSynchronize(t->stream));
+    t->fresh = false;
+    return ST_OK;
+}
+
+extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
+    CHK(use_device(t));
+    uint16_t tg = 0;
+    uint4 m = make_uint4(0, 0, 0, 0);
+    if (hash17) set_entry_host(tg, m, hash17);
+    CHK(h2d(t, t->tag, &tg, 2));
+    CHK(h2d(t, t->md5, &m, 16));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    if (hash17) t->fresh = false;
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ rehash / verify
+extern "C" int st_rehash(st_tree *t, int upper) {
+    CHK(use_device(t));
+    if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
+    DevTree d = view(t);
+    if (!upper)
+        LAUNCH(t, "segment_hash", (k_segment_hash<MODE_STORE>), grid_for(t->S), 256, 0, d, (const uint8_t *)nullptr,
+               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint32_t *)nullptr);
+    CHK(rehash_levels(t, t->H, nullptr));
+    t->fresh = false;
+    return ST_OK;
+}
+
+extern "C" int st_verify(st_tree *t, int upper, int *ok) {
+    CHK(use_device(t));
+    const uint32_t maxd = upper ? t->H : t->H + 1;
+    if (maxd == 0) { g_err = "verify_upper at Height 0 crashes in the reference"; return ST_EINVAL; }
+    DevTree d = view(t);
+    HIPCHK(hipMemsetAsync(t->flag, 0, 4, t->stream));
+    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+    LAUNCH(t, "mark_reachable", k_mark_reachable, grid_for(t->base[maxd + 1] - 1), 256, 0, d, maxd, t->mark);
+    if (maxd == t->H + 1)
+        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
+               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, t->flag);
+    const uint32_t lmax = maxd < t->H ? maxd : t->H;
+    if (lmax >= 1) {
+        const uint64_t nodes = t->base[lmax + 1] - t->base[1];
+        LAUNCH(t, "level_verify", (k_level_hash<MODE_VERIFY>), grid_for(nodes, inner_block(t)), inner_block(t),
+               inner_shmem(t), d, 1u, lmax, (const uint8_t *)t->mark, (const uint32_t *)nullptr,
+               (const uint32_t *)nullptr, (uint8_t *)nullptr, t->flag);
+    }
+    uint32_t f = 0;
+    CHK(d2h(t, &f, t->flag, 4));
+    *ok = f == 0;
+    return ST_OK;
+}
+
+static void entry_to_h17(uint16_t tg, const uint4 &m, uint8_t *out) {
+    out[0] = (uint8_t)(tg & 0xff);
+    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+    for (int k = 0; k < 16; k++) out[1 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
+    CHK(use_device(t));
+    uint16_t tg = 0;
+    uint4 m;
+    HIPCHK(hipMemcpyAsync(&tg, t->tag, 2, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&m, t->md5, 16, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    *present = (tg & TAG_PRESENT) ? 1 : 0;
+    if (*present) entry_to_h17(tg, m, out17);
+    return ST_OK;
+}
+
+extern "C" int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes17) {
+    CHK(use_device(t));
+    if (level < 1 || level > t->H + 1) { g_err = "level out of range"; return ST_EINVAL; }
+    const uint64_t n = t->base[level + 1] - t->base[level];
+    std::vector<uint16_t> tg(n);
+    std::vector<uint4> m(n);
+    HIPCHK(hipMemcpyAsync(tg.data(), t->tag + t->base[level], n * 2, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(m.data(), t->md5 + t->base[level], n * 16, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    for (uint64_t i = 0; i < n; i++) {
+        present[i] = (tg[i] & TAG_PRESENT) ? 1 : 0;
+        if (present[i]) entry_to_h17(tg[i], m[i], hashes17 + 17 * i);
+        else memset(hashes17 + 17 * i, 0, 17);
+    }
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ result blocks
+static st_result *new_result(uint64_t n) {
+    st_result *r = (st_result *)calloc(1, sizeof(st_result));
+    r->n = n;
+    r->status = (int32_t *)calloc(n + 1, 4);
+    r->clevel = (uint32_t *)calloc(n + 1, 4);
+    r->cbucket = (uint64_t *)calloc(n + 1, 8);
+    r->eoff = (uint64_t *)calloc(n + 1, 8);
+    return r;
+}
+
+extern "C" void st_free_result(st_result *r) {
+    if (!r) return;
+    void *ps[] = {r->status, r->clevel, r->cbucket, r->eoff, r->child, r->hash17, r->ktype, r->koff, r->kheap,
+                  r->aoff, r->aheap, r->boff, r->bheap, r->kind, r->seg};
+    for (void *p : ps) free(p);
+    free(r);
+}
+
+// Device entries (by index, ~0 = none) -> host key/value heaps of a result.
+static int fetch_entries(st_tree *t, const uint64_t *d_idx, uint64_t n, st_result *res, bool keys) {
+    DevTree d = view(t);
+    uint64_t *kl = nullptr, *vl = nullptr, *ko = nullptr, *vo = nullptr;
+    uint8_t *kh = nullptr, *vh = nullptr;
+    int r = ST_OK;
+    auto done = [&]() { dfree(t, kl); dfree(t, vl); dfree(t, ko); dfree(t, vo); dfree(t, kh); dfree(t, vh); };
+    if ((r = dalloc_t(t, &kl, n + 1)) || (r = dalloc_t(t, &vl, n + 1)) || (r = dalloc_t(t, &ko, n + 1)) ||
+        (r = dalloc_t(t, &vo, n + 1))) { done(); return r; }
+    LAUNCH(t, "entry_lengths", k_entry_lengths, grid_for(n + 1), 256, 0, d, d_idx, n, kl, vl);
+    if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, vl, vo, n + 1))) { done(); return r; }
+    res->koff = (uint64_t *)calloc(n + 1, 8);
+    res->aoff = (uint64_t *)calloc(n + 1, 8);
+    if ((r = d2h(t, res->koff, ko, (n + 1) * 8)) || (r = d2h(t, res->aoff, vo, (n + 1) * 8))) { done(); return r; }
+    const uint64_t kb = res->koff[n], vb = res->aoff[n];
+    if ((r = dalloc(t, (void **)&kh, kb + 16)) || (r = dalloc(t, (void **)&vh, vb + 16))) { done(); return r; }
+    LAUNCH(t, "entry_gather", k_entry_gather, grid_for(n), 256, 0, d, d_idx, n, (const uint64_t *)ko, kh,
+           (const uint64_t *)vo, vh);
+    res->kheap = (uint8_t *)malloc(kb + 1);
+    res->aheap = (uint8_t *)malloc(vb + 1);
+    if ((r = d2h(t, res->kheap, kh, kb)) || (r = d2h(t, res->aheap, vh, vb))) { done(); return r; }
+    done();
+    (void)keys;
+    return ST_OK;
+}
+
+// Convert device key records (tag + payload') of a result into (ktype, ensure_binary bytes).
+static void records_to_keys(st_result *res, uint64_t n) {
+    res->ktype = (uint8_t *)calloc(n + 1, 1);
+    uint64_t *nk = (uint64_t *)calloc(n + 1, 8);
+    uint8_t *nh = (uint8_t *)malloc(res->koff[n] + 1);
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *p = res->kheap + res->koff[i];
+        const uint64_t len = res->koff[i + 1] - res->koff[i];
+        nk[i] = o;
+        if (len == 0) continue;
+        res->ktype[i] = p[0];
+        memcpy(nh + o, p + 1, len - 1);
+        if (p[0] == KEYTAG_INT) nh[o] ^= 0x80;
+        o += len - 1;
+    }
+    nk[n] = o;
+    free(res->koff);
+    free(res->kheap);
+    res->koff = nk;
+    res->kheap = nh;
+}
+
+// Verify the root->target paths (targets at level L, device list) and
+// return the first failing level per target (device, n).
+static int verify_paths(st_tree *t, uint32_t L, const uint64_t *d_targets, uint64_t n, uint32_t *d_status) {
+    DevTree d = view(t);
+    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+    LAUNCH(t, "mark_paths", k_mark_paths, grid_for(n), 256, 0, d, L, (const uint64_t *)nullptr, d_targets, n, t->mark);
+    CHK(verify_marked(t, L));
+    LAUNCH(t, "path_status", k_path_status, grid_for(n), 256, 0, d, L, (const uint64_t *)nullptr, d_targets, n,
+           (const uint8_t *)t->ok, (uint8_t *)nullptr, d_status);
+    return ST_OK;
+}
+
+__global__ void k_u32_to_u64(const uint32_t *a, uint64_t n, uint64_t *b) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) b[i] = a[i];
+}
+
+extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                            st_result **out) {
+    CHK(use_device(t));
+    *out = nullptr;
+    st_result *res = new_result(n);
+    int present = 0;
+    uint8_t top[17];
+    CHK(st_top_hash(t, top, &present));
+    if (!present || n == 0) {   // get/2: undefined top => notfound (synctree.erl:216-218)
+        for (uint64_t i = 0; i < n; i++) res->status[i] = ST_NOTFOUND;
+        res->koff = (uint64_t *)calloc(n + 1, 8);
+        res->aoff = (uint64_t *)calloc(n + 1, 8);
+        res->kheap = (uint8_t *)malloc(1);
+        res->aheap = (uint8_t *)malloc(1);
+        res->ktype = (uint8_t *)calloc(n + 1, 1);
+        *out = res;
+        return ST_OK;
+    }
+    uint8_t *krec = nullptr;
+    uint64_t *dko = nullptr, *tg64 = nullptr, *found = nullptr;
+    uint32_t *seg = nullptr, *pst = nullptr;
+    int r = upload_records(t, n, ktype, kheap, koff, &krec, &dko);
+    if (!r) r = dalloc_t(t, &seg, n);
+    if (!r) r = dalloc_t(t, &tg64, n);
+    if (!r) r = dalloc_t(t, &pst, n);
+    if (!r) r = dalloc_t(t, &found, n);
+    DevTree d = view(t);
+    if (!r) {
+        hipLaunchKernelGGL(k_key_segment, dim3(grid_for(n)), dim3(256), 0, t->stream, krec, dko, n, t->S - 1, seg);
+        hipLaunchKernelGGL(k_u32_to_u64, dim3(grid_for(n)), dim3(256), 0, t->stream, seg, n, tg64);
+        r = verify_paths(t, t->H + 1, tg64, n, pst);
+    }
+    if (!r) {
+        BatchView bv{krec, dko};
+        hipLaunchKernelGGL(k_lookup, dim3(grid_for(n)), dim3(256), 0, t->stream, d, bv, seg, n, found);
+        std::vector<uint32_t> ps(n), sg(n);
+        std::vector<uint64_t> fd(n);
+        r = d2h(t, ps.data(), pst, n * 4);
+        if (!r) r = d2h(t, sg.data(), seg, n * 4);
+        if (!r) r = d2h(t, fd.data(), found, n * 8);
+        if (!r) {
+            for (uint64_t i = 0; i < n; i++) {
+                if (ps[i]) {
+                    res->status[i] = ST_CORRUPTED;
+                    res->clevel[i] = ps[i];
+                    res->cbucket[i] = (uint64_t)sg[i] >> (t->shift * (t->H + 1 - ps[i]));
+                    fd[i] = ~0ull;
+                } else {
+                    res->status[i] = fd[i] == ~0ull ? ST_NOTFOUND : ST_OK;
+                }
+                res->eoff[i + 1] = i + 1;   // entry i <-> key i (value valid iff ST_OK)
+            }
+            res->n_entries = n;
+            r = h2d(t, found, fd.data(), n * 8);
+            if (!r) r = fetch_entries(t, found, n, res, false);
+            if (!r) records_to_keys(res, n);
+        }
+    }
+    dfree(t, krec); dfree(t, dko); dfree(t, seg); dfree(t, tg64); dfree(t, pst); dfree(t, found);
+    if (r) { st_free_result(res); return r; }
+    HIPCHK(hipStreamSynchronize(t->stream));
+    *out = res;
+    return ST_OK;
+}
+
+__global__ void k_gather_children(DevTree t, uint32_t level, const uint64_t *targets, uint64_t n, uint16_t *tags,
+                                  uint4 *md) {
+    const uint64_t total = n * t.W;
+    for (uint64_t i = gtid(); i < total; i += gstride()) {
+        const uint64_t k = i / t.W, j = i % t.W;
+        const uint64_t slot = t.base[level + 1] + targets[k] * t.W + j;
+        tags[i] = t.tag[slot];
+        md[i] = t.md5[slot];
+    }
+}
+
+__global__ void k_target_counts(DevTree t, const uint64_t *targets, uint64_t n, const uint32_t *status, uint64_t *cnt) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        if (i == n) { cnt[i] = 0; break; }
+        const uint64_t s = targets[i];
+        cnt[i] = status[i] ? 0 : t.seg_off[s + 1] - t.seg_off[s];
+    }
+}
+
+__global__ void k_expand_ranges(DevTree t, const uint64_t *targets, uint64_t n, const uint32_t *status,
+                                const uint64_t *eoff, uint64_t *idx) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        if (status[i]) continue;
+        const uint64_t s = targets[i], e0 = t.seg_off[s];
+        const uint64_t m = eoff[i + 1] - eoff[i];
+        for (uint64_t k = 0; k < m; k++) idx[eoff[i] + k] = e0 + k;
+    }
+}
+
+static int node_images(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out, bool verify) {
+    *out = nullptr;
+    if (level < 1 || level > t->H + 1) { g_err = "level out of range (level 0 is answered from the top hash)"; return ST_EINVAL; }
+    const uint64_t lsize = t->base[level + 1] - t->base[level];
+    for (uint64_t i = 0; i < n; i++)
+        if (buckets[i] >= lsize) { g_err = "bucket out of range"; return ST_EINVAL; }
+    st_result *res = new_result(n);
+    uint64_t *dt = nullptr, *cnt = nullptr, *eo = nullptr, *idx = nullptr;
+    uint32_t *pst = nullptr;
+    uint16_t *tg = nullptr;
+    uint4 *md = nullptr;
+    DevTree d = view(t);
+    int r = dalloc_t(t, &dt, n ? n : 1);
+    if (!r) r = dalloc_t(t, &pst, n ? n : 1);
+    if (!r) r = h2d(t, dt, buckets, n * 8);
+    if (!r && n) {
+        if (verify) r = verify_paths(t, level, dt, n, pst);
+        else HIPCHK(hipMemsetAsync(pst, 0, n * 4, t->stream));
+    }
+    std::vector<uint32_t> ps(n);
+    if (!r) r = d2h(t, ps.data(), pst, n * 4);
+    for (uint64_t i = 0; i < n && !r; i++)
+        if (ps[i]) {
+            res->status[i] = ST_CORRUPTED;
+            res->clevel[i] = ps[i];
+            res->cbucket[i] = buckets[i] >> (t->shift * (level - ps[i]));
+        }
+    if (!r && level <= t->H) {
+        const uint64_t m = n * t->W;
+        r = dalloc_t(t, &tg, m ? m : 1);
+        if (!r) r = dalloc_t(t, &md, m ? m : 1);
+        if (!r && m) hipLaunchKernelGGL(k_gather_children, dim3(grid_for(m)), dim3(256), 0, t->stream, d, level, dt, n, tg, md);
+        std::vector<uint16_t> htg(m);
+        std::vector<uint4> hmd(m);
+        if (!r) r = d2h(t, htg.data(), tg, m * 2);
+        if (!r) r = d2h(t, hmd.data(), md, m * 16);
+        if (!r) {
+            uint64_t tot = 0;
+            for (uint64_t i = 0; i < n; i++) {
+                res->eoff[i] = tot;
+                if (!ps[i])
+                    for (uint64_t j = 0; j < t->W; j++) tot += (htg[i * t->W + j] & TAG_PRESENT) != 0;
+            }
+            res->eoff[n] = tot;
+            res->n_entries = tot;
+            res->child = (uint64_t *)calloc(tot + 1, 8);
+            res->hash17 = (uint8_t *)calloc(tot + 1, 17);
+            uint64_t e = 0;
+            for (uint64_t i = 0; i < n; i++) {
+                if (ps[i]) continue;
+                for (uint64_t j = 0; j < t->W; j++) {
+                    const uint64_t q = i * t->W + j;
+                    if (!(htg[q] & TAG_PRESENT)) continue;
+                    res->child[e] = buckets[i] * t->W + j;
+                    entry_to_h17(htg[q], hmd[q], res->hash17 + 17 * e);
+                    e++;
+                }
+            }
+        }
+    } else if (!r) {
+        r = dalloc_t(t, &cnt, n + 1);
+        if (!r) r = dalloc_t(t, &eo, n + 1);
+        if (!r) hipLaunchKernelGGL(k_target_counts, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, d, dt, n, pst, cnt);
+        if (!r) r = exclusive_scan<uint64_t>(t, cnt, eo, n + 1);
+        if (!r) r = d2h(t, res->eoff, eo, (n + 1) * 8);
+        const uint64_t tot = r ? 0 : res->eoff[n];
+        res->n_entries = tot;
+        if (!r) r = dalloc_t(t, &idx, tot + 1);
+        if (!r && n) hipLaunchKernelGGL(k_expand_ranges, dim3(grid_for(n)), dim3(256), 0, t->stream, d, dt, n, pst, eo, idx);
+        if (!r) r = fetch_entries(t, idx, tot, res, true);
+        if (!r) records_to_keys(res, tot);
+    }
+    dfree(t, dt); dfree(t, pst); dfree(t, tg); dfree(t, md); dfree(t, cnt); dfree(t, eo); dfree(t, idx);
+    if (r) { st_free_result(res); return r; }
+    HIPCHK(hipStreamSynchronize(t->stream));
+    *out = res;
+    return ST_OK;
+}
+
+extern "C" int st_exchange_get_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
+    CHK(use_device(t));
+    return node_images(t, level, n, buckets, out, true);
+}
+
+extern "C" int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
+    CHK(use_device(t));
+    if (level == 0) {
+        st_result *res = new_result(n);
+        uint16_t tg = 0;
+        uint4 m;
+        HIPCHK(hipMemcpyAsync(&tg, t->tag + 1, 2, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipMemcpyAsync(&m, t->md5 + 1, 16, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        const uint64_t e = (tg & TAG_PRESENT) ? 1 : 0;
+        res->child = (uint64_t *)calloc(n + 1, 8);
+        res->hash17 = (uint8_t *)calloc(n + 1, 17);
+        for (uint64_t i = 0; i < n; i++) {
+            res->eoff[i + 1] = res->eoff[i] + e;
+            if (e) entry_to_h17(tg, m, res->hash17 + 17 * i);
+        }
+        res->n_entries = res->eoff[n];
+        *out = res;
+        return ST_OK;
+    }
+    return node_images(t, level, n, buckets, out, false);
+}
+
+extern "C" int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
+                                   const uint64_t *koff, uint64_t *segments_out) {
+    CHK(use_device(t));
+    if (n == 0) return ST_OK;
+    uint8_t *krec = nullptr;
+    uint64_t *dko = nullptr;
+    uint32_t *seg = nullptr;
+    int r = upload_records(t, n, ktype, kheap, koff, &krec, &dko);
+    if (!r) r = dalloc_t(t, &seg, n);
+    std::vector<uint32_t> sg(n);
+    if (!r) {
+        hipLaunchKernelGGL(k_key_segment, dim3(grid_for(n)), dim3(256), 0, t->stream, krec, dko, n, t->S - 1, seg);
+        r = d2h(t, sg.data(), seg, n * 4);
+    }
+    for (uint64_t i = 0; i < n && !r; i++) segments_out[i] = sg[i];
+    dfree(t, krec); dfree(t, dko); dfree(t, seg);
+    return r;
+}
+
+// ------------------------------------------------------------------ compare (K3)
+struct CompareOut {
+    uint64_t n = 0;
+    DiffRec *rec = nullptr;   // device
+};
+
+static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint32_t *clevel, uint64_t *cbucket,
+                        int *cside, int *status) {
+    *status = ST_OK;
+    if (A->W != B->W || A->S != B->S) { g_err = "trees of different shape"; return ST_EINVAL; }
+    if (filter < 0 || filter > 2) { g_err = "both local_only and remote_only (case_clause)"; return ST_EINVAL; }
+    if (A->device != B->device) { g_err = "trees on different devices"; return ST_EINVAL; }
+    st_tree *t = A;   // work is enqueued on the local tree's stream
+    if (B->stream != A->stream) HIPCHK(hipStreamSynchronize(B->stream));
+    DevTree da = view(A), db = view(B);
+    const uint64_t S = A->S;
+    uint32_t *list[2] = {nullptr, nullptr}, *cnt = nullptr;
+    unsigned long long *bitmap = nullptr, *err = nullptr;
+    uint64_t *dcnt = nullptr, *doff = nullptr;
+    const uint64_t nwords = (S + 63) / 64;
+    int r = ST_OK;
+    auto done = [&]() {
+        dfree(t, list[0]); dfree(t, list[1]); dfree(t, cnt); dfree(t, bitmap); dfree(t, err); dfree(t, dcnt); dfree(t, doff);
+    };
+#define CCHK(x)                               \
+    do {                                      \
+        r = (x);                              \
+        if (r != ST_OK) { done(); return r; } \
+    } while (0)
+    CCHK(dalloc_t(t, &list[0], S + 1));
+    CCHK(dalloc_t(t, &list[1], S + 1));
+    CCHK(dalloc_t(t, &cnt, 2));
+    CCHK(dalloc_t(t, &bitmap, nwords + 1));
+    CCHK(dalloc_t(t, &err, 1));
+    HIPCHK(hipMemsetAsync(bitmap, 0, (nwords + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(err, 0xff, 8, t->stream));
+    LAUNCH(t, "tree_compare", k_cmp_top, 1, 64, 0, da, db, list[0], cnt);
+    int cur = 0;
+    for (uint32_t l = 1; l <= A->H; l++) {
+        const uint64_t lsize = A->base[l + 1] - A->base[l];
+        const uint64_t nsize = A->base[l + 2] - A->base[l + 1];
+        LAUNCH(t, "tree_compare", k_cmp_inner, grid_for(lsize, inner_block(t)), inner_block(t), inner_shmem(t), da, db, l,
+               (const uint32_t *)list[cur], (const uint32_t *)(cnt + cur), bitmap, filter, err);
+        LAUNCH(t, "tree_compare_list", k_bitmap_to_list, 1, 1024, 0, bitmap, (nsize + 63) / 64, list[cur ^ 1],
+               cnt + (cur ^ 1));
+        cur ^= 1;
+    }
+    uint32_t nf = 0;
+    unsigned long long e = ~0ull;
+    HIPCHK(hipMemcpyAsync(&nf, cnt + cur, 4, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&e, err, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    if (e == ~0ull && nf > 0) {
+        CCHK(dalloc_t(t, &dcnt, (uint64_t)nf + 1));
+        CCHK(dalloc_t(t, &doff, (uint64_t)nf + 1));
+        HIPCHK(hipMemsetAsync(dcnt + nf, 0, 8, t->stream));
+        LAUNCH(t, "tree_compare", (k_cmp_segments<false>), grid_for(nf), 256, 0, da, db, (const uint32_t *)list[cur],
+               (uint64_t)nf, filter, dcnt, (const uint64_t *)nullptr, (uint64_t)0, (DiffRec *)nullptr, err);
+        CCHK(exclusive_scan<uint64_t>(t, dcnt, doff, (uint64_t)nf + 1));
+        uint64_t total = 0;
+        HIPCHK(hipMemcpyAsync(&total, doff + nf, 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipMemcpyAsync(&e, err, 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        if (e == ~0ull && total > 0) {
+            CCHK(dalloc_t(t, &co.rec, total));
+            LAUNCH(t, "tree_compare", (k_cmp_segments<true>), grid_for(nf), 256, 0, da, db, (const uint32_t *)list[cur],
+                   (uint64_t)nf, filter, dcnt, (const uint64_t *)doff, total, co.rec, err);
+            co.n = total;
+        }
+    }
+    if (e != ~0ull) {
+        *status = ST_CORRUPTED;
+        *clevel = (uint32_t)(e >> 56);
+        *cbucket = (e & ((1ull << 56) - 1)) >> 1;
+        *cside = (int)(e & 1);
+        dfree(t, co.rec);
+        co.rec = nullptr;
+        co.n = 0;
+    }
+    done();
+#undef CCHK
+    return ST_OK;
+}
+
+extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
+                                 uint64_t *cbucket, int *cside) {
+    CHK(use_device(local));
+    CompareOut co;
+    int status = ST_OK;
+    CHK(compare_core(local, remote, filter, co, clevel, cbucket, cside, &status));
+    *n_diffs = co.n;
+    if (co.rec) {
+        // materialise the diff records' keys/values on the device, as st_compare does
+        st_tree *t = local;
+        DevTree da = view(local), db = view(remote);
+        uint64_t *kl, *al, *bl, *ko, *ao, *bo;
+        uint8_t *kind;
+        uint64_t *seg;
+        int r = ST_OK;
+        if ((r = dalloc_t(t, &kl, co.n + 1)) || (r = dalloc_t(t, &al, co.n + 1)) || (r = dalloc_t(t, &bl, co.n + 1)) ||
+            (r = dalloc_t(t, &ko, co.n + 1)) || (r = dalloc_t(t, &ao, co.n + 1)) || (r = dalloc_t(t, &bo, co.n + 1)) ||
+            (r = dalloc_t(t, &kind, co.n)) || (r = dalloc_t(t, &seg, co.n)))
+            return r;
+        LAUNCH(t, "diff_lengths", k_diff_lengths, grid_for(co.n + 1), 256, 0, da, db, (const DiffRec *)co.rec, co.n, kl, al, bl);
+        CHK(exclusive_scan<uint64_t>(t, kl, ko, co.n + 1));
+        CHK(exclusive_scan<uint64_t>(t, al, ao, co.n + 1));
+        CHK(exclusive_scan<uint64_t>(t, bl, bo, co.n + 1));
+        uint64_t tot[3];
+        HIPCHK(hipMemcpyAsync(&tot[0], ko + co.n, 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipMemcpyAsync(&tot[1], ao + co.n, 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipMemcpyAsync(&tot[2], bo + co.n, 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        uint8_t *kh, *ah, *bh;
+        CHK(dalloc(t, (void **)&kh, tot[0] + 16));
+        CHK(dalloc(t, (void **)&ah, tot[1] + 16));
+        CHK(dalloc(t, (void **)&bh, tot[2] + 16));
+        LAUNCH(t, "diff_gather", k_diff_gather, grid_for(co.n), 256, 0, da, db, (const DiffRec *)co.rec, co.n,
+               (const uint64_t *)ko, kh, (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
+        HIPCHK(hipStreamSynchronize(t->stream));
+        void *ps[] = {kl, al, bl, ko, ao, bo, kind, seg, kh, ah, bh, co.rec};
+        for (void *p : ps) dfree(t, p);
+    }
+    HIPCHK(hipStreamSynchronize(local->stream));
+    return status;
+}
+
+extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
+                          uint64_t *cbucket, int *cside) {
+    CHK(use_device(local));
+    *out = nullptr;
+    CompareOut co;
+    int status = ST_OK;
+    CHK(compare_core(local, remote, filter, co, clevel, cbucket, cside, &status));
+    if (status != ST_OK) return status;
+    st_tree *t = local;
+    const uint64_t n = co.n;
+    st_result *res = new_result(0);
+    res->n = 1;
+    res->eoff[0] = 0;
+    res->eoff[1] = n;
+    res->n_entries = n;
+    if (n == 0) {
+        res->ktype = (uint8_t *)calloc(1, 1);
+        res->koff = (uint64_t *)calloc(1, 8);
+        res->aoff = (uint64_t *)calloc(1, 8);
+        res->boff = (uint64_t *)calloc(1, 8);
+        res->kheap = (uint8_t *)malloc(1);
+        res->aheap = (uint8_t *)malloc(1);
+        res->bheap = (uint8_t *)malloc(1);
+        res->kind = (uint8_t *)calloc(1, 1);
+        res->seg = (uint64_t *)calloc(1, 8);
+        *out = res;
+        return ST_OK;
+    }
+    DevTree da = view(local), db = view(remote);
+    uint64_t *kl = nullptr, *al = nullptr, *bl = nullptr, *ko = nullptr, *ao = nullptr, *bo = nullptr, *seg = nullptr;
+    uint8_t *kind = nullptr, *kh = nullptr, *ah = nullptr, *bh = nullptr;
+    int r = ST_OK;
+    auto done = [&]() {
+        void *ps[] = {kl, al, bl, ko, ao, bo, seg, kind, kh, ah, bh, co.rec};
+        for (void *p : ps) dfree(t, p);
+    };
+    if ((r = dalloc_t(t, &kl, n + 1)) || (r = dalloc_t(t, &al, n + 1)) || (r = dalloc_t(t, &bl, n + 1)) ||
+        (r = dalloc_t(t, &ko, n + 1)) || (r = dalloc_t(t, &ao, n + 1)) || (r = dalloc_t(t, &bo, n + 1)) ||
+        (r = dalloc_t(t, &kind, n)) || (r = dalloc_t(t, &seg, n))) { done(); st_free_result(res); return r; }
+    hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, da, db, (const DiffRec *)co.rec, n, kl, al, bl);
+    if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, al, ao, n + 1)) ||
+        (r = exclusive_scan<uint64_t>(t, bl, bo, n + 1))) { done(); st_free_result(res); return r; }
+    res->koff = (uint64_t *)calloc(n + 1, 8);
+    res->aoff = (uint64_t *)calloc(n + 1, 8);
+    res->boff = (uint64_t *)calloc(n + 1, 8);
+    if ((r = d2h(t, res->koff, ko, (n + 1) * 8)) || (r = d2h(t, res->aoff, ao, (n + 1) * 8)) ||
+        (r = d2h(t, res->boff, bo, (n + 1) * 8))) { done(); st_free_result(res); return r; }
+    const uint64_t kb = res->koff[n], ab = res->aoff[n], bb = res->boff[n];
+    if ((r = dalloc(t, (void **)&kh, kb + 16)) || (r = dalloc(t, (void **)&ah, ab + 16)) || (r = dalloc(t, (void **)&bh, bb + 16))) {
+        done(); st_free_result(res); return r;
+    }
+    hipLaunchKernelGGL(k_diff_gather, dim3(grid_for(n)), dim3(256), 0, t->stream, da, db, (const DiffRec *)co.rec, n,
+                       (const uint64_t *)ko, kh, (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
+    res->kheap = (uint8_t *)malloc(kb + 1);
+    res->aheap = (uint8_t *)malloc(ab + 1);
+    res->bheap = (uint8_t *)malloc(bb + 1);
+    res->kind = (uint8_t *)malloc(n);
+    res->seg = (uint64_t *)malloc(n * 8);
+    if ((r = d2h(t, res->kheap, kh, kb)) || (r = d2h(t, res->aheap, ah, ab)) || (r = d2h(t, res->bheap, bh, bb)) ||
+        (r = d2h(t, res->kind, kind, n)) || (r = d2h(t, res->seg, seg, n * 8))) { done(); st_free_result(res); return r; }
+    done();
+    records_to_keys(res, n);
+    *out = res;
+    return ST_OK;
+}

@@ -1,0 +1,296 @@
+"""synctree_hip — the device-resident synctree backend.
+
+Mirrors the synctree backend behaviour (``new/1, fetch/3, exists/2,
+store/3, store/2``: src/synctree_ets.erl:22-66, src/synctree_orddict.erl:22-66)
+over libsynctree_hip.so, and adds the bulk callbacks the synctree module uses
+when they exist (insert_batch, rehash, verify, exchange_get, compare): the
+plug point SURVEY.md §8b recommends.  State is a :class:`DeviceTree`.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import terms
+
+name = 'synctree_hip'
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _bytes(p, o0, o1):
+    n = int(o1 - o0)
+    if n <= 0:
+        return b''
+    return ctypes.string_at(ctypes.addressof(p.contents) + int(o0), n)
+
+
+class DeviceTree:
+    """One device-resident tree (a C-ABI st_tree handle)."""
+
+    def __init__(self, width=16, segments=1 << 20, device=0):
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(L.st_create(width, segments, device, ctypes.byref(h)), 'st_create')
+        self.h = h
+        self.L = L
+        self.device = device
+        self.width = int(L.st_width(h))
+        self.segments = int(L.st_segments(h))
+        self.height = int(L.st_height(h))
+        self.shift = self.width.bit_length() - 1
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.L.st_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ writes
+    def insert_batch(self, keys, values):
+        """Sequential-insert semantics; returns per-key status: None (ok) or
+        ('corrupted', Level, Bucket)."""
+        n = len(keys)
+        if n == 0:
+            return []
+        kt, kh, ko = terms.pack_keys(keys)
+        vh, vo = terms.pack_values(values)
+        st = np.zeros(n, np.int32)
+        cl = np.zeros(n, np.uint32)
+        cb = np.zeros(n, np.uint64)
+        _lib.check(self.L.st_insert_batch(self.h, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vh), _ptr(vo), _ptr(st),
+                                          _ptr(cl), _ptr(cb)), 'st_insert_batch')
+        return [None if st[i] == _lib.ST_OK else (terms.CORRUPTED, int(cl[i]), int(cb[i])) for i in range(n)]
+
+    def insert_int64(self, keys, values, on_device=False):
+        """keys: int64 array [n]; values: uint8 [n, vlen] (numpy, or device
+        pointers when on_device).  Returns the number of rejected keys."""
+        nc = ctypes.c_uint64(0)
+        if on_device:
+            kp, vp, n, vlen = keys
+            _lib.check(self.L.st_insert_int64(self.h, n, ctypes.c_void_p(kp), ctypes.c_void_p(vp), vlen, 1,
+                                              ctypes.byref(nc)), 'st_insert_int64')
+        else:
+            keys = np.ascontiguousarray(keys, np.int64)
+            values = np.ascontiguousarray(values, np.uint8)
+            _lib.check(self.L.st_insert_int64(self.h, len(keys), _ptr(keys), _ptr(values), values.shape[1], 0,
+                                              ctypes.byref(nc)), 'st_insert_int64')
+        return int(nc.value)
+
+    def corrupt(self, key):
+        kt, kb = terms.key_parts(key)
+        _lib.check(self.L.st_corrupt(self.h, kt, kb, len(kb)), 'st_corrupt')
+
+    def store_node(self, level, bucket, node):
+        """Raw Mod:store({Level,Bucket}, Node): no verification, no rehash."""
+        if level == 0:
+            if node in (terms.UNDEFINED, None):
+                _lib.check(self.L.st_store_top(self.h, None, 0), 'st_store_top')
+            else:
+                _lib.check(self.L.st_store_top(self.h, bytes(node), 0), 'st_store_top')
+        elif level == self.height + 1:
+            keys = [k for k, _ in node]
+            vals = [v for _, v in node]
+            kt, kh, ko = terms.pack_keys(keys)
+            vh, vo = terms.pack_values(vals)
+            _lib.check(self.L.st_store_segment(self.h, bucket, len(node), _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vh),
+                                               _ptr(vo)), 'st_store_segment')
+        else:
+            ch = np.array([c for c, _ in node], np.uint64)
+            hs = np.frombuffer(b''.join(bytes(h) for _, h in node) + b'\0', np.uint8).copy()
+            for _, h in node:
+                if len(h) != 17:
+                    raise ValueError('inner entries are 17-byte hashes on the device path')
+            _lib.check(self.L.st_store_inner(self.h, level, bucket, len(node), _ptr(ch), _ptr(hs)), 'st_store_inner')
+
+    def delete_node(self, level, bucket):
+        _lib.check(self.L.st_delete_node(self.h, level, bucket), 'st_delete_node')
+
+    def set_record_top(self, top):
+        _lib.check(self.L.st_set_record_top(self.h, None if top == terms.UNDEFINED else bytes(top)),
+                   'st_set_record_top')
+
+    # ------------------------------------------------------------ rehash / verify
+    def rehash(self, upper=False):
+        _lib.check(self.L.st_rehash(self.h, 1 if upper else 0), 'st_rehash')
+
+    def verify(self, upper=False):
+        ok = ctypes.c_int(0)
+        _lib.check(self.L.st_verify(self.h, 1 if upper else 0, ctypes.byref(ok)), 'st_verify')
+        return bool(ok.value)
+
+    def top_hash(self):
+        buf = ctypes.create_string_buffer(17)
+        p = ctypes.c_int(0)
+        _lib.check(self.L.st_top_hash(self.h, buf, ctypes.byref(p)), 'st_top_hash')
+        return buf.raw if p.value else terms.UNDEFINED
+
+    def level_entries(self, level):
+        n = self.width ** (level - 1)
+        present = np.zeros(n, np.uint8)
+        hashes = np.zeros((n, 17), np.uint8)
+        _lib.check(self.L.st_level_entries(self.h, level, _ptr(present), _ptr(hashes)), 'st_level_entries')
+        return present, hashes
+
+    def num_entries(self):
+        return int(self.L.st_num_entries(self.h))
+
+    def sync(self):
+        _lib.check(self.L.st_sync(self.h), 'st_sync')
+
+    # ------------------------------------------------------------ reads
+    def _take(self, rp):
+        try:
+            return rp.contents
+        except ValueError:
+            raise _lib.DeviceError('null result')
+
+    def get_batch(self, keys):
+        n = len(keys)
+        if n == 0:
+            return []
+        kt, kh, ko = terms.pack_keys(keys)
+        rp = ctypes.POINTER(_lib.StResult)()
+        _lib.check(self.L.st_get_batch(self.h, n, _ptr(kt), _ptr(kh), _ptr(ko), ctypes.byref(rp)), 'st_get_batch')
+        try:
+            r = self._take(rp)
+            out = []
+            for i in range(n):
+                s = r.status[i]
+                if s == _lib.ST_OK:
+                    out.append(_bytes(r.aheap, r.aoff[i], r.aoff[i + 1]))
+                elif s == _lib.ST_NOTFOUND:
+                    out.append(terms.NOTFOUND)
+                else:
+                    out.append((terms.CORRUPTED, int(r.clevel[i]), int(r.cbucket[i])))
+            return out
+        finally:
+            self.L.st_free_result(rp)
+
+    def _images(self, fn, level, buckets):
+        n = len(buckets)
+        bk = np.array(buckets, np.uint64)
+        rp = ctypes.POINTER(_lib.StResult)()
+        _lib.check(fn(self.h, level, n, _ptr(bk), ctypes.byref(rp)), 'node images')
+        try:
+            r = self._take(rp)
+            out = []
+            for i in range(n):
+                if r.status[i] == _lib.ST_CORRUPTED:
+                    out.append((terms.CORRUPTED, int(r.clevel[i]), int(r.cbucket[i])))
+                    continue
+                e0, e1 = r.eoff[i], r.eoff[i + 1]
+                if level == 0:
+                    out.append(_bytes(r.hash17, 17 * e0, 17 * e1) if e1 > e0 else terms.UNDEFINED)
+                elif level <= self.height:
+                    out.append([(int(r.child[e]), _bytes(r.hash17, 17 * e, 17 * e + 17)) for e in range(e0, e1)])
+                else:
+                    out.append([(terms.key_from_parts(r.ktype[e], _bytes(r.kheap, r.koff[e], r.koff[e + 1])),
+                                 _bytes(r.aheap, r.aoff[e], r.aoff[e + 1])) for e in range(e0, e1)])
+            return out
+        finally:
+            self.L.st_free_result(rp)
+
+    def exchange_get_batch(self, level, buckets):
+        """Verified node images (exchange_get/3 for level >= 1)."""
+        return self._images(self.L.st_exchange_get_batch, level, buckets)
+
+    def fetch_batch(self, level, buckets):
+        """Raw node images (Mod:fetch/3, no verification)."""
+        return self._images(self.L.st_fetch_batch, level, buckets)
+
+    def segments_of(self, keys):
+        kt, kh, ko = terms.pack_keys(keys)
+        out = np.zeros(len(keys), np.uint64)
+        _lib.check(self.L.st_segment_of_batch(self.h, len(keys), _ptr(kt), _ptr(kh), _ptr(ko), _ptr(out)),
+                   'st_segment_of_batch')
+        return [int(x) for x in out]
+
+    def compare(self, remote, filt=_lib.ST_FILTER_ALL):
+        """Device compare (K3).  Returns ('ok', [(seg, key, (va, vb))...]) in
+        reference order, or ('corrupted', side, (corrupted, L, B))."""
+        rp = ctypes.POINTER(_lib.StResult)()
+        cl, cb, cs = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int()
+        rc = _lib.check(self.L.st_compare(self.h, remote.h, filt, ctypes.byref(rp), ctypes.byref(cl), ctypes.byref(cb),
+                                          ctypes.byref(cs)), 'st_compare')
+        if rc == _lib.ST_CORRUPTED:
+            return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
+        try:
+            r = self._take(rp)
+            out = []
+            for i in range(int(r.n_entries)):
+                kind = r.kind[i]
+                k = terms.key_from_parts(r.ktype[i], _bytes(r.kheap, r.koff[i], r.koff[i + 1]))
+                va = terms.NONE if kind == _lib.ST_DIFF_REMOTE_ONLY else _bytes(r.aheap, r.aoff[i], r.aoff[i + 1])
+                vb = terms.NONE if kind == _lib.ST_DIFF_LOCAL_ONLY else _bytes(r.bheap, r.boff[i], r.boff[i + 1])
+                out.append((int(r.seg[i]), k, (va, vb)))
+            return ('ok', out)
+        finally:
+            self.L.st_free_result(rp)
+
+    def compare_device(self, remote, filt=_lib.ST_FILTER_ALL):
+        """Device compare with results left on the device: number of diffs or
+        ('corrupted', ...)."""
+        nd, cl, cb, cs = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int()
+        rc = _lib.check(self.L.st_compare_device(self.h, remote.h, filt, ctypes.byref(nd), ctypes.byref(cl),
+                                                 ctypes.byref(cb), ctypes.byref(cs)), 'st_compare_device')
+        if rc == _lib.ST_CORRUPTED:
+            return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
+        return int(nd.value)
+
+    # ------------------------------------------------------------ timing
+    def set_timing(self, on=True):
+        _lib.check(self.L.st_set_timing(self.h, 1 if on else 0), 'st_set_timing')
+
+    def kernel_stats(self, kernel):
+        n, ms = ctypes.c_uint64(), ctypes.c_double()
+        _lib.check(self.L.st_kernel_stats(self.h, kernel.encode(), ctypes.byref(n), ctypes.byref(ms)), 'stats')
+        return int(n.value), float(ms.value)
+
+    def set_stream(self, stream_handle):
+        _lib.check(self.L.st_set_stream(self.h, ctypes.c_void_p(stream_handle)), 'st_set_stream')
+
+
+# ---------------------------------------------------------------------------
+# The backend behaviour (synctree_ets.erl:22-66) over a DeviceTree state.
+
+def new(opts=()):
+    opts = dict(opts) if opts else {}
+    return DeviceTree(opts.get('width', 16), opts.get('segments', 1 << 20), opts.get('device', 0))
+
+
+def fetch(key, default, state):
+    level, bucket = key
+    img = state.fetch_batch(level, [bucket])[0]
+    if level == 0:
+        return default if img == terms.UNDEFINED else img
+    return img if img else default
+
+
+def exists(key, state):
+    level, bucket = key
+    img = state.fetch_batch(level, [bucket])[0]
+    return img != terms.UNDEFINED and img != []
+
+
+def store(key, val, state):
+    state.store_node(key[0], key[1], val)
+    return state
+
+
+def store_batch(updates, state):
+    """Mod:store/2: puts (deletes as 'deleted' markers) then deletes."""
+    for u in updates:
+        if u[0] == 'put':
+            state.store_node(u[1][0], u[1][1], u[2])
+    for u in updates:
+        if u[0] == 'delete':
+            state.delete_node(u[1][0], u[1][1])
+    return state
