@@ -69,19 +69,21 @@ class DeviceTree:
                                           _ptr(cl), _ptr(cb)), 'st_insert_batch')
         return [None if st[i] == _lib.ST_OK else (terms.CORRUPTED, int(cl[i]), int(cb[i])) for i in range(n)]
 
-    def insert_int64(self, keys, values, on_device=False):
-        """keys: int64 array [n]; values: uint8 [n, vlen] (numpy, or device
-        pointers when on_device).  Returns the number of rejected keys."""
+    def insert_int64(self, keys, values):
+        """keys: int64 ndarray [n]; values: uint8 ndarray [n, vlen] (host).
+        Returns the number of keys rejected by path verification."""
         nc = ctypes.c_uint64(0)
-        if on_device:
-            kp, vp, n, vlen = keys
-            _lib.check(self.L.st_insert_int64(self.h, n, ctypes.c_void_p(kp), ctypes.c_void_p(vp), vlen, 1,
-                                              ctypes.byref(nc)), 'st_insert_int64')
-        else:
-            keys = np.ascontiguousarray(keys, np.int64)
-            values = np.ascontiguousarray(values, np.uint8)
-            _lib.check(self.L.st_insert_int64(self.h, len(keys), _ptr(keys), _ptr(values), values.shape[1], 0,
-                                              ctypes.byref(nc)), 'st_insert_int64')
+        keys = np.ascontiguousarray(keys, np.int64)
+        values = np.ascontiguousarray(values, np.uint8)
+        _lib.check(self.L.st_insert_int64(self.h, len(keys), _ptr(keys), _ptr(values), values.shape[1], 0,
+                                          ctypes.byref(nc)), 'st_insert_int64')
+        return int(nc.value)
+
+    def insert_int64_device(self, keys_ptr, vals_ptr, n, vlen):
+        """Same with device-resident inputs (int64 keys, n*vlen value bytes)."""
+        nc = ctypes.c_uint64(0)
+        _lib.check(self.L.st_insert_int64(self.h, n, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(vals_ptr), vlen, 1,
+                                          ctypes.byref(nc)), 'st_insert_int64')
         return int(nc.value)
 
     def corrupt(self, key):

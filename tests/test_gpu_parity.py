@@ -385,11 +385,19 @@ def test_exchange_corrupt_segments_1m():
     assert r[0] == 'ok'
     assert [(k, vv) for _, k, vv in r[1]] == exp
     assert da.compare_device(db) == len(segs)
-    # without rehash: B is inconsistent -> the reference crashes at the first
-    # corrupted segment
-    db2 = synctree_hip.DeviceTree()
-    db2.insert_int64(keys, vals)
+    # A2 = A with segs[3] corrupted WITHOUT rehash (inconsistent): the frontier
+    # of A2 vs B reaches segs[3], whose verification fails -> the reference
+    # crashes in orddict_delta there (local side)
+    da2 = synctree_hip.DeviceTree()
+    da2.insert_int64(keys, vals)
+    oa2 = C.OTree().bulk_load_int64(keys, vals)
     node = oa.node(6, int(segs[3]))
-    db2.store_node(6, int(segs[3]), [(node[0][0], _corrupt_value(node[0][1]))] + node[1:])
-    r = da.compare(db2)
-    assert r[0] == 'corrupted' and r[1] == 'remote' and r[2] == ('corrupted', 6, int(segs[3]))
+    bad = [(node[0][0], _corrupt_value(_corrupt_value(node[0][1])))] + node[1:]
+    da2.store_node(6, int(segs[3]), bad)
+    oa2.store_segment(int(segs[3]), bad)
+    exp = oa2.compare(ob)
+    assert exp == ('crash', 'local', ('corrupted', 6, int(segs[3])))
+    r = da2.compare(db)
+    assert r == ('corrupted', 'local', ('corrupted', 6, int(segs[3])))
+    # an identical-top pair never descends (level 0 equal): no crash, no diffs
+    assert da2.compare(da)[0] == 'ok' and oa2.compare(oa) == []
