@@ -334,23 +334,48 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
     }
 }
 
+// Appends bytes to a lane's LDS message with a 64-bit shift accumulator,
+// emitting aligned dwords (instead of one ds_write_b8 per byte).
+struct MsgWriter {
+    uint32_t *w;
+    uint64_t acc;
+    uint32_t nb, nw;
+    __device__ __forceinline__ void init(uint8_t *reg) { w = reinterpret_cast<uint32_t *>(reg); acc = 0; nb = 0; nw = 0; }
+    __device__ __forceinline__ void push(uint32_t x, uint32_t bits) {
+        acc |= (uint64_t)x << nb;
+        nb += bits;
+        if (nb >= 32) { w[nw++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+    }
+    __device__ __forceinline__ void entry(uint32_t tag, const uint4 &h) {
+        push(tag & 0xffu, 8); push(h.x, 32); push(h.y, 32); push(h.z, 32); push(h.w, 32);
+    }
+    __device__ __forceinline__ uint32_t finish() {
+        if (nb) w[nw] = (uint32_t)acc;
+        return nw * 4 + nb / 8;
+    }
+};
+
 // Stage the content of inner node (l, b) — the present child entries, 17
 // bytes each in child order — into this lane's LDS region; returns its length.
+// All W child entries are loaded before any is inspected (one memory round
+// trip per 16 children, not one per child).
 __device__ __forceinline__ uint32_t stage_inner(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
     const uint64_t c0 = t.base[l + 1] + b * t.W;
-    uint32_t len = 0;
-    for (uint32_t j = 0; j < t.W; j++) {
-        const uint16_t ct = t.tag[c0 + j];
-        if (!(ct & TAG_PRESENT)) continue;
-        const uint4 h = t.md5[c0 + j];
-        uint8_t *q = reg + len;
-        q[0] = (uint8_t)(ct & 0xff);
-        const uint32_t w[4] = {h.x, h.y, h.z, h.w};
+    MsgWriter mw;
+    mw.init(reg);
+    for (uint32_t j0 = 0; j0 < t.W; j0 += 16) {
+        uint32_t tg[16];
+        uint4 h[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) q[1 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-        len += 17;
+        for (int j = 0; j < 16; j++) {
+            if (j0 + j < t.W) { tg[j] = t.tag[c0 + j0 + j]; h[j] = t.md5[c0 + j0 + j]; }
+            else tg[j] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (tg[j] & TAG_PRESENT) mw.entry(tg[j], h[j]);
     }
-    return len;
+    return mw.finish();
 }
 
 // Bytes of LDS per lane for inner-node staging (odd dword stride).
@@ -792,4 +817,732 @@ __global__ void k_entry_gather(DevTree t, const uint64_t *idx, uint64_t n, const
         if (kheap) copy_bytes(kheap + koff[i], t.kheap + t.koff[e], t.koff[e + 1] - t.koff[e]);
         copy_bytes(vheap + voff[i], t.vheap + t.voff[e], t.voff[e + 1] - t.voff[e]);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Fused rehash (K1 + the first d levels of K2 in one launch).
+//
+// One workgroup per subtree of SEGS = W^d consecutive segments (W^d <= 256,
+// d <= H): every lane hashes one segment (the lanes are assigned segments in
+// order of their MD5 block count, so the 64 lanes of a wave run loops of
+// (nearly) equal length), the entries stay in LDS, and the workgroup then
+// reduces the d levels above them (rehash/4, synctree.erl:515-535) with one
+// lane per node.  With a mask (dirty-path rehash after inserts) only marked
+// nodes are recomputed; unmarked ones keep their stored entry, exactly like
+// update_path leaves untouched siblings alone.
+
+struct SubtreeLds {
+    uint4 *md5;      // SEGS entries of the current level (then SEGS/W, ...)
+    uint32_t *tag;
+    uint4 *md5b;     // next level
+    uint32_t *tagb;
+    uint32_t *hist;  // 64 bins
+    uint32_t *perm;  // SEGS
+    uint8_t *stage;  // per-lane inner-node staging
+};
+
+__host__ __device__ __forceinline__ uint32_t subtree_lds_bytes(uint32_t W, uint32_t segs) {
+    uint32_t b = segs * 16 * 2 + segs * 4 * 2 + 64 * 4 + segs * 4;
+    const uint32_t inner_lanes = segs / W > 0 ? segs / W : 1;
+    b = (b + 15) & ~15u;
+    return b + inner_lanes * lane_region_bytes(W);
+}
+
+__device__ __forceinline__ uint32_t stage_entries(uint32_t W, const uint4 *md5, const uint32_t *tag, uint32_t c0,
+                                                  uint8_t *reg) {
+    MsgWriter mw;
+    mw.init(reg);
+    for (uint32_t j = 0; j < W; j++) {
+        const uint32_t ct = tag[c0 + j];
+        if (ct & TAG_PRESENT) mw.entry(ct, md5[c0 + j]);
+    }
+    return mw.finish();
+}
+
+__global__ void __launch_bounds__(256) k_rehash_subtree(DevTree t, uint32_t dseg, uint32_t segs, uint32_t d,
+                                                        const uint8_t *mask, uint32_t ilp2) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    SubtreeLds L;
+    L.md5 = reinterpret_cast<uint4 *>(lds);
+    L.md5b = L.md5 + segs;
+    L.tag = reinterpret_cast<uint32_t *>(L.md5b + segs);
+    L.tagb = L.tag + segs;
+    L.hist = L.tagb + segs;
+    L.perm = L.hist + 64;
+    L.stage = lds + ((segs * 16 * 2 + segs * 4 * 2 + 64 * 4 + segs * 4 + 15) & ~15u);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t H1 = t.H + 1;
+    const uint64_t s0 = (uint64_t)blockIdx.x * segs;
+    // subtree root (level H1-d, bucket blockIdx.x): nothing to do when unmarked
+    if (mask && !mask[t.base[H1 - dseg] + blockIdx.x]) return;
+
+    // ---- lane -> segment assignment by MD5 block count (LDS counting sort)
+    if (tid < 64) L.hist[tid] = 0;
+    __syncthreads();
+    uint32_t mybin[2] = {0, 0};
+    for (uint32_t q = 0, i = tid; q < 2 && i < segs; q++, i += blockDim.x) {
+        const uint64_t s = s0 + i;
+        const uint64_t bytes = t.seg_voff[s + 1] - t.seg_voff[s];
+        uint64_t blocks = (bytes + 8) / 64 + 1;
+        mybin[q] = 63 - (blocks > 63 ? 63u : (uint32_t)blocks);   // longest first
+        atomicAdd(&L.hist[mybin[q]], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < 64; b++) { const uint32_t c = L.hist[b]; L.hist[b] = acc; acc += c; }
+    }
+    __syncthreads();
+    for (uint32_t q = 0, i = tid; q < 2 && i < segs; q++, i += blockDim.x) L.perm[atomicAdd(&L.hist[mybin[q]], 1u)] = i;
+    __syncthreads();
+
+    // ---- K1: segment hashes.  ilp2: a lane takes two neighbouring positions
+    // of the block-count order (two equally long messages, interleaved).
+    const uint32_t per = ilp2 ? 2 : 1;
+    for (uint32_t pos = tid * per; pos < segs && pos < (tid + 1) * per; pos += per) {
+        uint32_t li[2] = {L.perm[pos], per == 2 && pos + 1 < segs ? L.perm[pos + 1] : L.perm[pos]};
+        const uint32_t cnt = (per == 2 && pos + 1 < segs) ? 2 : 1;
+        uint64_t s_[2], slot[2];
+        bool work[2];
+        for (uint32_t q = 0; q < 2; q++) {
+            s_[q] = s0 + li[q];
+            slot[q] = t.base[H1] + s_[q];
+            work[q] = q < cnt && !(mask && !mask[slot[q]]) && t.seg_off[s_[q]] != t.seg_off[s_[q] + 1];
+        }
+        uint32_t d1[4] = {0, 0, 0, 0}, d2[4] = {0, 0, 0, 0};
+        if (cnt == 2 && work[0] && work[1]) {
+            const uint64_t a0 = t.seg_voff[s_[0]], b0 = t.seg_voff[s_[1]];
+            stmd5::md5_global_x2(t.vheap + a0, t.seg_voff[s_[0] + 1] - a0, t.vheap + b0, t.seg_voff[s_[1] + 1] - b0,
+                                 d1, d2);
+        } else {
+            if (work[0]) {
+                const uint64_t a0 = t.seg_voff[s_[0]];
+                stmd5::md5_global_pf(t.vheap + a0, t.seg_voff[s_[0] + 1] - a0, d1);
+            }
+            if (cnt == 2 && work[1]) {
+                const uint64_t b0 = t.seg_voff[s_[1]];
+                stmd5::md5_global_pf(t.vheap + b0, t.seg_voff[s_[1] + 1] - b0, d2);
+            }
+        }
+        for (uint32_t q = 0; q < cnt; q++) {
+            const uint32_t *dg = q == 0 ? d1 : d2;
+            uint4 e;
+            uint32_t tg;
+            if (mask && !mask[slot[q]]) {
+                e = t.md5[slot[q]];
+                tg = t.tag[slot[q]];
+            } else if (!work[q]) {
+                e = make_uint4(0, 0, 0, 0);
+                tg = 0;
+                t.tag[slot[q]] = 0;
+                if (H1 == 1) t.tag[0] = 0;
+            } else {
+                e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+                tg = TAG_PRESENT;
+                t.md5[slot[q]] = e;
+                t.tag[slot[q]] = TAG_PRESENT;
+                if (H1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+            }
+            L.md5[li[q]] = e;
+            L.tag[li[q]] = tg;
+        }
+    }
+    __syncthreads();
+
+    // ---- the d levels above, one lane per node.  Only wave 0 stays (the
+    // widest of these levels has segs/W <= 64 nodes when W >= 4); the other
+    // waves leave so their slots go to other workgroups' segment hashing.
+    if (d == 0) return;
+    const bool one_wave = (segs / t.W) <= 64;
+    if (one_wave && tid >= 64) return;
+    uint32_t nodes = segs;
+    uint4 *cm = L.md5, *nm = L.md5b;
+    uint32_t *ct = L.tag, *nt = L.tagb;
+    for (uint32_t q = 1; q <= d; q++) {
+        nodes /= t.W;
+        const uint32_t lvl = H1 - q;
+        if (tid < nodes) {
+            const uint64_t b = ((uint64_t)blockIdx.x * nodes) + tid;
+            const uint64_t slot = t.base[lvl] + b;
+            uint4 e;
+            uint32_t tg;
+            if (mask && !mask[slot]) {
+                e = t.md5[slot];
+                tg = t.tag[slot];
+            } else {
+                uint8_t *reg = L.stage + tid * lane_region_bytes(t.W);
+                const uint32_t len = stage_entries(t.W, cm, ct, tid * t.W, reg);
+                if (len == 0) {
+                    e = make_uint4(0, 0, 0, 0);
+                    tg = 0;
+                } else {
+                    uint32_t dg[4];
+                    stmd5::md5_lds(reg, len, dg);
+                    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+                    tg = TAG_PRESENT;
+                    t.md5[slot] = e;
+                }
+                t.tag[slot] = (uint16_t)tg;
+                if (lvl == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
+            }
+            nm[tid] = e;
+            nt[tid] = tg;
+        }
+        if (one_wave) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            __syncthreads();
+        }
+        uint4 *xm = cm; cm = nm; nm = xm;
+        uint32_t *xt = ct; ct = nt; nt = xt;
+    }
+}
+
+// The remaining upper levels [lmin, lmax] (at most 256 nodes each) in ONE
+// workgroup, level by level (entries of level lmax+1 come from the previous
+// launch).  Dynamic LDS: 256 lane regions.
+__global__ void __launch_bounds__(256) k_rehash_upper_levels(DevTree t, uint32_t lmin, uint32_t lmax,
+                                                             const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(t.W);
+    for (uint32_t l = lmax; l >= lmin; l--) {
+        const uint64_t nodes = t.base[l + 1] - t.base[l];
+        for (uint64_t b = threadIdx.x; b < nodes; b += blockDim.x) {
+            const uint64_t slot = t.base[l] + b;
+            if (mask && !mask[slot]) continue;
+            const uint32_t len = stage_inner(t, l, b, reg);
+            uint32_t tg = 0;
+            uint4 e = make_uint4(0, 0, 0, 0);
+            if (len) {
+                uint32_t dg[4];
+                stmd5::md5_lds(reg, len, dg);
+                e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+                tg = TAG_PRESENT;
+                t.md5[slot] = e;
+            }
+            t.tag[slot] = (uint16_t)tg;
+            if (l == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
+        }
+        __syncthreads();
+        if (l == lmin) break;
+    }
+}
+
+// Levels [H+1-dl, H] in one launch: one single-wave workgroup per subtree of
+// W^(dl-1) <= 64 level-H nodes.  Lanes stage their node's W child entries from
+// global memory, hash, keep the result in LDS for the next level up; the
+// wave reduces dl levels with wave-level syncs only.  Serial-MD5 latency per
+// level is what bounds this, so every workgroup is one short wave.
+__global__ void __launch_bounds__(64) k_rehash_levels_wave(DevTree t, uint32_t dl, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x;
+    uint32_t nodes = 1;
+    for (uint32_t q = 1; q < dl; q++) nodes *= t.W;      // level-H nodes of this subtree
+    uint4 *em = reinterpret_cast<uint4 *>(lds);           // 64 entries (current level)
+    uint32_t *et = reinterpret_cast<uint32_t *>(em + 64);
+    uint8_t *reg = lds + 64 * 20 + lane * lane_region_bytes(t.W);
+    const uint32_t H = t.H;
+    for (uint32_t q = 0; q < dl; q++) {
+        const uint32_t lvl = H - q;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        uint32_t tg = 0;
+        const bool act = lane < nodes;
+        const uint64_t b = (uint64_t)blockIdx.x * nodes + lane;
+        const uint64_t slot = t.base[lvl] + b;
+        if (act) {
+            if (mask && !mask[slot]) {
+                e = t.md5[slot];
+                tg = t.tag[slot];
+            } else {
+                const uint32_t len = (q == 0) ? stage_inner(t, lvl, b, reg)
+                                              : stage_entries(t.W, em, et, lane * t.W, reg);
+                if (len) {
+                    uint32_t dg[4];
+                    stmd5::md5_lds(reg, len, dg);
+                    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+                    tg = TAG_PRESENT;
+                    t.md5[slot] = e;
+                }
+                t.tag[slot] = (uint16_t)tg;
+                if (lvl == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (act) { em[lane] = e; et[lane] = tg; }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        nodes /= t.W;
+        if (nodes == 0) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1 segment_hash, LDS-staged (the rehash hot loop).
+//
+// One wave per 64 consecutive segments.  Their values are ONE contiguous byte
+// range of the value heap (CSR order), so the wave first copies that range
+// into its LDS slice with coalesced 16-byte loads (every HBM byte read once,
+// full lines, many bytes in flight), then each lane hashes one segment out of
+// LDS.  Lanes take segments in order of MD5 block count (wave bitonic sort)
+// so a wave's 64 loops have (nearly) equal trip counts.  A wave whose range
+// does not fit its slice hashes straight from global memory instead.
+#define K1_WAVES 4
+#define K1_SLICE 13312   // bytes of LDS per wave (the 64-segment range + 80 B)
+
+__device__ __forceinline__ uint32_t wave_sort_key(uint32_t key) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t o = __shfl_xor(key, j, 64);
+            const bool up = ((lane & k) == 0);
+            const bool lower = (lane & j) == 0;
+            const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
+            key = (lower == up) ? mn : mx;
+        }
+    }
+    return key;
+}
+
+__global__ void __launch_bounds__(64 * K1_WAVES) k_segment_hash_lds(DevTree t, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *slice = lds + wave * K1_SLICE;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t s0 = ((uint64_t)blockIdx.x * K1_WAVES + wave) * 64;
+    if (s0 >= t.S) return;
+    const uint64_t nseg = (t.S - s0) < 64 ? (t.S - s0) : 64;
+    // this lane's own segment (natural order) -> sort key = (255 - blocks) << 6 | lane
+    const uint64_t my = s0 + (lane < nseg ? lane : 0);
+    const uint64_t mv0 = t.seg_voff[my], mv1 = t.seg_voff[my + 1];
+    uint32_t blocks = (uint32_t)((mv1 - mv0 + 8) / 64 + 1);
+    blocks = blocks > 255 ? 255 : blocks;
+    uint32_t key = lane < nseg ? (((255u - blocks) << 6) | lane) : (0xffffffu);
+    key = wave_sort_key(key);
+    const uint32_t src = key & 63;                       // lane whose segment I hash
+    const bool act = key != 0xffffffu;
+    const uint64_t v0 = __shfl(mv0, 0, 64);
+    const uint64_t vend = __shfl(mv1, (int)(nseg - 1), 64);
+    const uint64_t a0 = v0 & ~15ull;
+    const uint64_t need = vend - a0 + 80;
+    const bool staged = need <= K1_SLICE;
+    if (staged) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(t.vheap + a0);
+        uint4 *l = reinterpret_cast<uint4 *>(slice);
+        const uint32_t chunks = (uint32_t)((need + 15) / 16);
+        for (uint32_t c = lane; c < chunks; c += 64) l[c] = g[c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint64_t s = s0 + src;
+    const uint64_t sv0 = __shfl(mv0, (int)src, 64), sv1 = __shfl(mv1, (int)src, 64);
+    if (!act) return;
+    const uint64_t slot = t.base[L1] + s;
+    if (mask && !mask[slot]) return;
+    if (t.seg_off[s] == t.seg_off[s + 1]) {
+        t.tag[slot] = 0;
+        if (L1 == 1) t.tag[0] = 0;
+        return;
+    }
+    uint32_t dg[4];
+    if (staged) stmd5::md5_lds_at(reinterpret_cast<const uint32_t *>(slice), (uint32_t)(sv0 - a0), (uint32_t)(sv1 - sv0), dg);
+    else stmd5::md5_global_pf(t.vheap + sv0, sv1 - sv0, dg);
+    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    t.md5[slot] = e;
+    t.tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+}
+
+// ---------------------------------------------------------------------------
+// Rehash v3 kernels.
+//
+// k_seg_perm_*: order segments by MD5 block count (descending; empty last),
+// computed once per ingest and kept in the tree, so that the 64 lanes of every
+// K1 wave run loops of equal length (K1 is VALU-bound: divergence is waste).
+
+#define PERM_BINS 256
+__device__ __forceinline__ uint32_t perm_bin(const DevTree &t, uint64_t s) {
+    if (t.seg_off[s] == t.seg_off[s + 1]) return PERM_BINS - 1;
+    const uint64_t blocks = (t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1;
+    return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
+}
+
+// Pass 1: per-workgroup histograms reserved from global bin counters.
+__global__ void __launch_bounds__(256) k_seg_perm_count(DevTree t, uint32_t *gcount) {
+    __shared__ uint32_t h[PERM_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t s = gtid(); s < t.S; s += gstride()) atomicAdd(&h[perm_bin(t, s)], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&gcount[threadIdx.x], h[threadIdx.x]);
+}
+
+// Pass 2: exclusive scan of the 256 bin counts into cursors (one workgroup).
+__global__ void __launch_bounds__(256) k_seg_perm_scan(uint32_t *gcount) {
+    __shared__ uint32_t h[PERM_BINS];
+    h[threadIdx.x] = gcount[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < PERM_BINS; b++) { const uint32_t c = h[b]; h[b] = acc; acc += c; }
+    }
+    __syncthreads();
+    gcount[threadIdx.x] = h[threadIdx.x];
+}
+
+// Pass 3: scatter (one global atomic per workgroup and bin).
+__global__ void __launch_bounds__(256) k_seg_perm_scatter(DevTree t, uint32_t *gcur, uint32_t *perm) {
+    __shared__ uint32_t h[PERM_BINS], base[PERM_BINS];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t chunk = (t.S + gridDim.x - 1) / gridDim.x;
+    const uint64_t a = blockIdx.x * chunk, b = (a + chunk < t.S) ? a + chunk : t.S;
+    for (uint64_t s = a + threadIdx.x; s < b; s += blockDim.x) atomicAdd(&h[perm_bin(t, s)], 1u);
+    __syncthreads();
+    base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&gcur[threadIdx.x], h[threadIdx.x]) : 0;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t s = a + threadIdx.x; s < b; s += blockDim.x) {
+        const uint32_t bin = perm_bin(t, s);
+        perm[base[bin] + atomicAdd(&h[bin], 1u)] = (uint32_t)s;
+    }
+}
+
+// K1 segment_hash over the block-count order.
+__global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint32_t *perm, const uint8_t *mask) {
+    const uint32_t L1 = t.H + 1;
+    for (uint64_t i = gtid(); i < t.S; i += gstride()) {
+        const uint64_t s = perm[i];
+        const uint64_t slot = t.base[L1] + s;
+        if (mask && !mask[slot]) continue;
+        if (t.seg_off[s] == t.seg_off[s + 1]) {
+            t.tag[slot] = 0;
+            if (L1 == 1) t.tag[0] = 0;
+            continue;
+        }
+        uint32_t dg[4];
+        const uint64_t v0 = t.seg_voff[s];
+        stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, dg);
+        const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+        t.md5[slot] = e;
+        t.tag[slot] = TAG_PRESENT;
+        if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+    }
+}
+
+// Hash inner node (l, b) of a W == 16 tree into its parent's entry.  Nodes
+// with all 16 children present hash from registers (md5_node16); others stage
+// the present entries in the lane's LDS region.
+__device__ __forceinline__ void hash_node16(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
+    const uint64_t slot = t.base[l] + b;
+    const uint64_t c0 = t.base[l + 1] + b * 16;
+    uint32_t tg[16];
+    uint4 h[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) { tg[j] = t.tag[c0 + j]; h[j] = t.md5[c0 + j]; }
+    uint32_t full = 1;
+#pragma unroll
+    for (int j = 0; j < 16; j++) full &= (tg[j] >> 8) & 1u;
+    uint32_t dg[4];
+    uint32_t len = 1;
+    if (full) {
+        uint32_t pf[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) pf[j] = tg[j] & 0xffu;
+        stmd5::md5_node16(pf, h, dg);
+    } else {
+        MsgWriter mw;
+        mw.init(reg);
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (tg[j] & TAG_PRESENT) mw.entry(tg[j], h[j]);
+        len = mw.finish();
+        if (len) stmd5::md5_lds(reg, len, dg);
+    }
+    uint32_t ot = 0;
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (len) {
+        e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+        ot = TAG_PRESENT;
+        t.md5[slot] = e;
+    }
+    t.tag[slot] = (uint16_t)ot;
+    if (l == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)ot; }
+}
+
+// One inner level (W == 16), one lane per node.
+__global__ void __launch_bounds__(64) k_level16(DevTree t, uint32_t l, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
+    const uint64_t nodes = t.base[l + 1] - t.base[l];
+    for (uint64_t b = gtid(); b < nodes; b += gstride()) {
+        if (mask && !mask[t.base[l] + b]) continue;
+        hash_node16(t, l, b, reg);
+    }
+}
+
+// Levels lmax..lmin (W == 16, <= 256 nodes each) in one workgroup.
+__global__ void __launch_bounds__(256) k_upper16(DevTree t, uint32_t lmin, uint32_t lmax, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
+    for (uint32_t l = lmax; l >= lmin; l--) {
+        const uint64_t nodes = t.base[l + 1] - t.base[l];
+        for (uint64_t b = threadIdx.x; b < nodes; b += blockDim.x) {
+            if (mask && !mask[t.base[l] + b]) continue;
+            hash_node16(t, l, b, reg);
+        }
+        __syncthreads();
+        if (l == lmin) break;
+    }
+}
+
+// K1 segment_hash v4: block-count order + coalesced gather into LDS.
+// One wave per 64 consecutive positions of the block-count order (so its 64
+// segments need (nearly) the same number of MD5 blocks B).  Each segment gets
+// an aligned LDS slot of 64*B bytes; the wave copies all slots with
+// consecutive lanes on consecutive 16-byte chunks of a segment (a few cache
+// lines per instruction instead of 64), then every lane hashes its segment out
+// of its slot.  Waves whose slots exceed the slice hash from global memory.
+#define K1G_SLICE 20480
+
+__global__ void __launch_bounds__(64) k_segment_hash_gather(DevTree t, const uint32_t *perm, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *pre = reinterpret_cast<uint32_t *>(lds + K1G_SLICE);        // 65 words after the slots
+    uint64_t *src = reinterpret_cast<uint64_t *>(lds + K1G_SLICE + 272);  // 64 source offsets
+    const uint32_t lane = threadIdx.x;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
+    const bool inr = p < t.S;
+    const uint64_t s = inr ? perm[p] : 0;
+    const uint64_t slot = t.base[L1] + s;
+    const bool nonempty = inr && t.seg_off[s] != t.seg_off[s + 1];
+    const bool work = nonempty && !(mask && !mask[slot]);
+    const uint64_t v0 = t.seg_voff[s];
+    const uint32_t len = work ? (uint32_t)(t.seg_voff[s + 1] - v0) : 0u;
+    const uint32_t nblk = work ? (len + 8) / 64 + 1 : 0u;
+    // wave-inclusive scan of chunk counts (4 chunks of 16 B per 64 B block)
+    uint32_t c = nblk * 4, x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    pre[lane + 1] = x;
+    src[lane] = v0;
+    if (lane == 0) pre[0] = 0;
+    uint32_t dg[4];
+    const bool staged = total * 16 <= K1G_SLICE;
+    __syncthreads();
+    if (staged) {
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        for (uint32_t q = lane; q < total; q += 64) {
+            uint32_t lo = 0, hi = 64;   // segment j with pre[j] <= q < pre[j+1]
+#pragma unroll
+            for (int it = 0; it < 6; it++) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pre[mid] <= q) lo = mid; else hi = mid;
+            }
+            const uint64_t vj = src[lo];   // (a shuffle here would read inactive lanes as 0)
+            uint4 v;
+            __builtin_memcpy(&v, t.vheap + vj + 16ull * (q - pre[lo]), 16);
+            dst[q] = v;
+        }
+        __syncthreads();
+        if (work) stmd5::md5_lds(lds + 16u * (x - c), len, dg);
+    } else if (work) {
+        stmd5::md5_global_pf(t.vheap + v0, len, dg);
+    }
+    if (!inr || (mask && !mask[slot])) return;
+    if (!nonempty) {
+        t.tag[slot] = 0;
+        if (L1 == 1) t.tag[0] = 0;
+        return;
+    }
+    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    t.md5[slot] = e;
+    t.tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+}
+
+// K1 segment_hash v5: block-count order; a wave whose 64 segments all need
+// the same B <= 4 blocks (the common case in that order) gathers them into
+// 64-byte-aligned LDS slots with fully coalesced loads (consecutive lanes on
+// consecutive 16 B of a segment) and hashes from LDS; any other wave loads
+// directly from global memory.
+#define K1U_MAXB 4
+__global__ void __launch_bounds__(64) k_segment_hash_v5(DevTree t, const uint32_t *perm, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
+    const bool inr = p < t.S;
+    const uint64_t s = inr ? perm[p] : 0;
+    const uint64_t slot = t.base[L1] + s;
+    const bool nonempty = inr && t.seg_off[s] != t.seg_off[s + 1];
+    const bool work = nonempty && !(mask && !mask[slot]);
+    const uint64_t v0 = t.seg_voff[s];
+    const uint32_t len = work ? (uint32_t)(t.seg_voff[s + 1] - v0) : 0u;
+    const uint32_t nblk = work ? (len + 8) / 64 + 1 : 0u;
+    const uint32_t B = __shfl(nblk, 0, 64);
+    const bool uniform = (__ballot(nblk == B) == ~0ull) && B >= 1 && B <= K1U_MAXB;
+    uint32_t dg[4];
+    if (uniform) {
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        const uint32_t per = 4 * B;            // 16-byte chunks per segment
+        for (uint32_t it = 0; it < per; it++) {
+            const uint32_t q = it * 64 + lane;
+            const uint32_t j = q / per, k = q - j * per;
+            const uint64_t vj = __shfl(v0, (int)j, 64);   // every lane active here
+            uint4 v;
+            __builtin_memcpy(&v, t.vheap + vj + 16ull * k, 16);
+            dst[q] = v;
+        }
+        __syncthreads();
+        stmd5::md5_lds_a16(lds + 64u * B * lane, len, dg);
+    } else if (work) {
+        stmd5::md5_global_pf(t.vheap + v0, len, dg);
+    }
+    if (!inr || (mask && !mask[slot])) return;
+    if (!nonempty) {
+        t.tag[slot] = 0;
+        if (L1 == 1) t.tag[0] = 0;
+        return;
+    }
+    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    t.md5[slot] = e;
+    t.tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+}
+
+// ---------------------------------------------------------------------------
+// K2 level_rehash for W == 16: levels H, H-1, H-2 of one level-(H-2) subtree
+// per workgroup (256 threads), all in LDS.
+//
+// The subtree's 4096 child entries (level H+1) are contiguous in the slot
+// arrays: they are staged with coalesced 16-byte loads into per-node blocks
+// of 16 x 16 B (+16 B pad: conflict-free ds_read_b128 by node).  Each level
+// is then one lane per node: full nodes hash from registers (md5_node16),
+// others write their message over their own (already consumed) child block
+// and hash it from LDS.  Results go to global memory and to the next level's
+// LDS blocks.  With a mask (dirty-path rehash) unmarked nodes keep their
+// stored entry.
+#define NB16 272           // bytes per staged node block (16 x 16 B + pad)
+#define TB16 48            // bytes per staged tag block (16 x u16 + pad)
+
+__device__ __forceinline__ void node_lds16(uint8_t *blk, const uint16_t *tags, uint32_t dg[4], uint32_t &present) {
+    const uint4 *hb = reinterpret_cast<const uint4 *>(blk);
+    uint4 h[16];
+    uint32_t tg[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) { h[j] = hb[j]; tg[j] = tags[j]; }
+    uint32_t full = 1, any = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) { full &= (tg[j] >> 8) & 1u; any |= (tg[j] >> 8) & 1u; }
+    present = any;
+    if (!any) return;
+    if (full) {
+        uint32_t pf[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) pf[j] = tg[j] & 0xffu;
+        stmd5::md5_node16(pf, h, dg);
+    } else {
+        MsgWriter mw;
+        mw.init(blk);             // own block: its entries are in registers now
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (tg[j] & TAG_PRESENT) mw.entry(tg[j], h[j]);
+        stmd5::md5_lds(blk, mw.finish(), dg);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *mask) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *A = lds;                                        // 256 node blocks (level H children)
+    uint16_t *At = reinterpret_cast<uint16_t *>(A + 256 * NB16);
+    uint8_t *Bb = A + 256 * NB16 + 256 * TB16;               // 16 node blocks (level H-1 children)
+    uint16_t *Bt = reinterpret_cast<uint16_t *>(Bb + 16 * NB16);
+    uint8_t *Cb = Bb + 16 * NB16 + 16 * TB16;                // 1 node block (level H-2 children)
+    uint16_t *Ct = reinterpret_cast<uint16_t *>(Cb + NB16);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t H = t.H;
+    const uint64_t root = blockIdx.x;                        // bucket at level H-2
+    if (mask && !mask[t.base[H - 2] + root]) return;
+    // ---- stage the 4096 level-(H+1) entries
+    const uint64_t c0 = t.base[H + 1] + root * 4096;
+#pragma unroll 4
+    for (uint32_t it = 0; it < 16; it++) {
+        const uint32_t e = it * 256 + tid;
+        *reinterpret_cast<uint4 *>(A + (e >> 4) * NB16 + (e & 15) * 16) = t.md5[c0 + e];
+    }
+    {
+        const uint4 *tg = reinterpret_cast<const uint4 *>(t.tag + c0);   // 8 tags per 16 B
+        for (uint32_t it = 0; it < 2; it++) {
+            const uint32_t q = it * 256 + tid;                             // 512 chunks
+            *reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(At) + (q >> 1) * TB16 + (q & 1) * 16) = tg[q];
+        }
+    }
+    __syncthreads();
+    // ---- level H: lane = node
+    {
+        const uint64_t b = root * 256 + tid;
+        const uint64_t slot = t.base[H] + b;
+        uint4 e;
+        uint32_t tg;
+        if (mask && !mask[slot]) {
+            e = t.md5[slot];
+            tg = t.tag[slot];
+        } else {
+            uint32_t dg[4], pr;
+            node_lds16(A + tid * NB16, reinterpret_cast<const uint16_t *>(reinterpret_cast<uint8_t *>(At) + tid * TB16), dg, pr);
+            e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+            tg = pr ? TAG_PRESENT : 0u;
+            if (pr) t.md5[slot] = e;
+            t.tag[slot] = (uint16_t)tg;
+        }
+        *reinterpret_cast<uint4 *>(Bb + (tid >> 4) * NB16 + (tid & 15) * 16) = e;
+        *reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(Bt) + (tid >> 4) * TB16 + (tid & 15) * 2) = (uint16_t)tg;
+    }
+    __syncthreads();
+    // ---- level H-1: 16 nodes
+    if (tid < 16) {
+        const uint64_t b = root * 16 + tid;
+        const uint64_t slot = t.base[H - 1] + b;
+        uint4 e;
+        uint32_t tg;
+        if (mask && !mask[slot]) {
+            e = t.md5[slot];
+            tg = t.tag[slot];
+        } else {
+            uint32_t dg[4], pr;
+            node_lds16(Bb + tid * NB16, reinterpret_cast<const uint16_t *>(reinterpret_cast<uint8_t *>(Bt) + tid * TB16), dg, pr);
+            e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+            tg = pr ? TAG_PRESENT : 0u;
+            if (pr) t.md5[slot] = e;
+            t.tag[slot] = (uint16_t)tg;
+        }
+        *reinterpret_cast<uint4 *>(Cb + tid * 16) = e;
+        Ct[tid] = (uint16_t)tg;
+    }
+    __syncthreads();
+    // ---- level H-2: the root
+    if (tid == 0) {
+        const uint64_t slot = t.base[H - 2] + root;
+        uint32_t dg[4], pr;
+        node_lds16(Cb, Ct, dg, pr);
+        const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+        if (pr) t.md5[slot] = e;
+        t.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
+        if (H - 2 == 1) { t.md5[0] = e; t.tag[0] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0; }
+    }
+}
+
+__host__ __device__ __forceinline__ uint32_t levels3_16_lds_bytes() {
+    return 256 * NB16 + 256 * TB16 + 16 * NB16 + 16 * TB16 + NB16 + TB16 + 128;
 }

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -57,6 +58,8 @@ struct st_tree {
     uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
     uint8_t *kheap = nullptr, *vheap = nullptr;
     bool fresh = true;
+    uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
+    bool perm_valid = false;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -229,7 +232,7 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
         (r = dalloc_t(t, &t->flag, 4)) || (r = dalloc_t(t, &t->cnt64, 2)) ||
         (r = dalloc_t(t, &t->seg_off, t->S + 1)) || (r = dalloc_t(t, &t->seg_voff, t->S + 1)) ||
         (r = dalloc_t(t, &t->koff, 1)) || (r = dalloc_t(t, &t->voff, 1)) || (r = dalloc(t, (void **)&t->kheap, HEAP_SLACK)) ||
-        (r = dalloc(t, (void **)&t->vheap, HEAP_SLACK))) {
+        (r = dalloc(t, (void **)&t->vheap, HEAP_SLACK)) || (r = dalloc_t(t, &t->seg_perm, t->S))) {
         st_destroy(t);
         return r;
     }
@@ -253,7 +256,8 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
 extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
-    void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap};
+    void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
+                  t->seg_perm};
     for (void *p : ps) dfree(t, p);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
@@ -355,6 +359,104 @@ static int rehash_levels(st_tree *t, uint32_t top_level, const uint8_t *mask) {
                inner_shmem(t), d, l, l, mask, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr,
                (uint32_t *)nullptr);
     }
+    return ST_OK;
+}
+
+// Full or dirty (mask) rehash of segments + every inner level:
+// k_rehash_subtree covers the segments and the d levels above them (W^d <= 256
+// segments per workgroup), per-level kernels any level still wider than 256
+// nodes, and k_rehash_upper_levels the rest in one workgroup.
+static int ensure_perm(st_tree *t) {
+    if (t->perm_valid) return ST_OK;
+    DevTree d = view(t);
+    uint32_t *cnt = nullptr;
+    CHK(dalloc_t(t, &cnt, PERM_BINS));
+    HIPCHK(hipMemsetAsync(cnt, 0, PERM_BINS * 4, t->stream));
+    LAUNCH(t, "seg_perm", k_seg_perm_count, grid_for(t->S, 256, 1024), 256, 0, d, cnt);
+    LAUNCH(t, "seg_perm", k_seg_perm_scan, 1, 256, 0, cnt);
+    LAUNCH(t, "seg_perm", k_seg_perm_scatter, grid_for(t->S, 256, 1024), 256, 0, d, cnt, t->seg_perm);
+    dfree(t, cnt);
+    t->perm_valid = true;
+    return ST_OK;
+}
+
+static int rehash_all(st_tree *t, const uint8_t *mask) {
+    DevTree d = view(t);
+    uint32_t depth = 0;
+    uint64_t segs = 1;
+    while (depth < t->H && segs * t->W <= 256) { segs *= t->W; depth++; }
+    // K1 variant (env ST_K1: A/B knob): 3 = block-count order (default),
+    // 2 = LDS-staged waves, 1 = subtree kernel (optional in-kernel levels)
+    static const int k1 = getenv("ST_K1") ? atoi(getenv("ST_K1")) : 3;
+    static const int knob = getenv("ST_FUSED_LEVELS") ? atoi(getenv("ST_FUSED_LEVELS")) : 0;
+    uint32_t dlev = 0;
+    if (k1 == 3 || k1 == 4 || k1 == 5) {
+        CHK(ensure_perm(t));
+        if (k1 == 5)
+            LAUNCH(t, "segment_hash", k_segment_hash_v5, (uint32_t)((t->S + 63) / 64), 64, 64 * 64 * K1U_MAXB, d,
+                   (const uint32_t *)t->seg_perm, mask);
+        else if (k1 == 4)
+            LAUNCH(t, "segment_hash", k_segment_hash_gather, (uint32_t)((t->S + 63) / 64), 64, K1G_SLICE + 272 + 512, d,
+                   (const uint32_t *)t->seg_perm, mask);
+        else
+            LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
+        static const int k2 = getenv("ST_K2") ? atoi(getenv("ST_K2")) : 2;
+        if (k2 == 2 && t->W == 16 && t->H >= 3) {
+            LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
+                   levels3_16_lds_bytes(), d, mask);
+            uint32_t l = t->H - 3;
+            for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
+                LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
+                       (size_t)64 * lane_region_bytes(16), d, l, mask);
+            if (l >= 1)
+                LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, mask);
+            return ST_OK;
+        }
+        if (t->W == 16 && t->H >= 1) {
+            uint32_t l = t->H;
+            for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
+                LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
+                       (size_t)64 * lane_region_bytes(16), d, l, mask);
+            if (l >= 1)
+                LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, mask);
+            return ST_OK;
+        }
+    } else if (k1 == 2) {
+        const uint64_t waves = (t->S + 63) / 64;
+        LAUNCH(t, "segment_hash", k_segment_hash_lds, (uint32_t)((waves + K1_WAVES - 1) / K1_WAVES), 64 * K1_WAVES,
+               (size_t)K1_WAVES * K1_SLICE, d, mask);
+    } else {
+        dlev = (int)depth < knob ? depth : (uint32_t)(knob < 0 ? 0 : knob);
+        static const int ilp_knob = getenv("ST_K1_ILP") ? atoi(getenv("ST_K1_ILP")) : 1;
+        const uint32_t ilp2 = (ilp_knob == 2 && segs >= 128 && dlev == 0) ? 1 : 0;
+        uint32_t block = segs < 64 ? 64 : (uint32_t)segs;
+        if (ilp2) block = (uint32_t)segs / 2;
+        LAUNCH(t, "segment_hash", k_rehash_subtree, (uint32_t)(t->S / segs), block,
+               subtree_lds_bytes((uint32_t)t->W, (uint32_t)segs), d, depth, (uint32_t)segs, dlev, mask, ilp2);
+    }
+    if (t->H <= dlev) return ST_OK;
+    uint32_t l = t->H - dlev;   // highest level not yet recomputed
+    if (l == t->H && t->H >= 1) {
+        // levels H .. H+1-dl in single-wave subtrees of <= 64 level-H nodes
+        uint32_t dl = 1;
+        uint64_t nh = 1;
+        while (dl < t->H && nh * t->W <= 64) { nh *= t->W; dl++; }
+        const uint64_t wgs = (t->base[t->H + 1] - t->base[t->H]) / nh;
+        LAUNCH(t, "level_rehash", k_rehash_levels_wave, (uint32_t)wgs, 64, 64 * 20 + nh * lane_region_bytes((uint32_t)t->W),
+               d, dl, mask);
+        l = t->H - dl;
+        if (l == 0) return ST_OK;
+    }
+    while (l >= 1 && t->base[l + 1] - t->base[l] > 256) {
+        const uint64_t nodes = t->base[l + 1] - t->base[l];
+        LAUNCH(t, "level_rehash", (k_level_hash<MODE_STORE>), grid_for(nodes, inner_block(t)), inner_block(t),
+               inner_shmem(t), d, l, l, mask, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr,
+               (uint32_t *)nullptr);
+        l--;
+    }
+    if (l >= 1)
+        LAUNCH(t, "level_rehash", k_rehash_upper_levels, 1, 256, (size_t)256 * lane_region_bytes((uint32_t)t->W), d, 1u, l,
+               mask);
     return ST_OK;
 }
 
@@ -516,15 +618,14 @@ static int ingest(st_tree *t, IngestIn &in) {
     dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
     t->seg_off = nseg_off; t->seg_voff = nseg_voff; t->koff = nkoff; t->voff = nvoff; t->kheap = nkheap; t->vheap = nvheap;
     t->n = n_new; t->kbytes = tot[0]; t->vbytes = tot[1];
+    t->perm_valid = false;
 
     if (in.verify_rehash) {
         // dirty-path rehash: segments whose content changed and their ancestors
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         d = view(t);
         LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
-        LAUNCH(t, "segment_hash", (k_segment_hash<MODE_STORE>), grid_for(S), 256, 0, d, (const uint8_t *)t->mark,
-               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint32_t *)nullptr);
-        ICHK(rehash_levels(t, t->H, t->mark));
+        ICHK(rehash_all(t, t->mark));
     }
     t->fresh = false;
     cleanup();
@@ -800,11 +901,8 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 extern "C" int st_rehash(st_tree *t, int upper) {
     CHK(use_device(t));
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
-    DevTree d = view(t);
-    if (!upper)
-        LAUNCH(t, "segment_hash", (k_segment_hash<MODE_STORE>), grid_for(t->S), 256, 0, d, (const uint8_t *)nullptr,
-               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint32_t *)nullptr);
-    CHK(rehash_levels(t, t->H, nullptr));
+    if (upper) CHK(rehash_levels(t, t->H, nullptr));
+    else CHK(rehash_all(t, nullptr));
     t->fresh = false;
     return ST_OK;
 }
