@@ -29,11 +29,23 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X peaks (opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec;
-# int32 VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s.
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec.
+# Integer VALU, measured on gfx950 (tools/microbench/valu_peak.cpp,
+# profiles/r01_valu_peak.txt): v_add_u32 / v_xor_b32 / v_bitop3_b32 issue a
+# wave64 in 2 SIMD cycles, v_add3_u32 / v_alignbit_b32 in 4.  The MD5 block
+# loop of k_segment_hash_perm (ISA dump) is 100 add +
+# 48 bitop3 + 32 and + 29 xor + ~10 moves (2 cyc) and 97 add3 + 64 alignbit
+# (4 cyc) = 1082 SIMD cycles per wave = 16.9 SIMD-cycles per 64-B block.
 HBM_PEAK_GBS = 8000.0
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
-MD5_OPS_PER_BLOCK = 400   # measured from the ISA of k_segment_hash
+SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9
+MD5_SIMD_CYCLES_PER_BLOCK = 1082.0 / 64
+# HBM bytes of one K1 launch from rocprofv3 PMC (profiles/r01_pmc_k1_session2.txt):
+# (FETCH_SIZE + WRITE_SIZE) x 1 KiB, averaged over 12 launches.  No x2
+# correction: K1's reads are per-lane 16-B loads of scattered segments (not the
+# wide coalesced stream the gfx950 1/2-count applies to), and the raw count
+# already equals the algorithmic read bytes.
+K1_PMC_TRAFFIC_BYTES = (200211.9 + 36959.0) * 1024
 METRIC = 'synctree keys rehashed/sec + exchange tree-diffs/sec at 10M keys, 1–8 GPUs'
 
 
@@ -143,20 +155,27 @@ def main():
             seg_of = _segment_histogram(tree, keys_h)
         except Exception as e:  # pragma: no cover
             log('histogram failed', e)
-        k1_bytes = n * 17 + (S + 1) * 8 * 2 + S * 18
+        # algorithmic bytes of one K1 launch: values (n x 17 B) + seg_off and
+        # seg_voff (2 x (S+1) x 8 B) + the block-count order (S x 4 B) read;
+        # S x (16 B md5 + 2 B tag) node entries written.
+        k1_bytes = n * 17 + (S + 1) * 8 * 2 + S * 4 + S * 18
         if seg_of is not None:
             blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
         else:
             blocks = int(n * 17 / 64 + nseg)
         k1_avg_ms = k1_ms / max(k1_n, 1)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
-        valu_tops = blocks * MD5_OPS_PER_BLOCK / (k1_avg_ms / 1e3) / 1e12
-        roof = {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
-                'kernel': 'k_segment_hash (K1)', 'kernel_avg_ms': round(k1_avg_ms, 4),
+        t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
+        t_valu = blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
+        roof = {'bound': 'hbm' if t_hbm >= t_valu else 'valu', 'achieved': round(achieved_gbs, 1),
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
+                'traffic': int(K1_PMC_TRAFFIC_BYTES),
+                'kernel': 'k_segment_hash_perm (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
                 'bytes_per_launch': k1_bytes, 'md5_blocks_per_launch': blocks,
-                'valu': {'achieved_tops': round(valu_tops, 2), 'peak_tops': round(VALU_PEAK_TOPS, 1),
-                         'frac': round(valu_tops / VALU_PEAK_TOPS, 4), 'ops_per_block': MD5_OPS_PER_BLOCK},
+                't_min_hbm_us': round(t_hbm * 1e6, 2),
+                'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),
+                         'simd_cycles_per_block': round(MD5_SIMD_CYCLES_PER_BLOCK, 2),
+                         'peak': '1024 SIMDs x 2.4 GHz'},
                 'level_rehash_avg_ms_per_step': round(k2_ms / max(args.steps, 1), 4)}
         out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'keys/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
