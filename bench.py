@@ -45,7 +45,7 @@ MD5_SIMD_CYCLES_PER_BLOCK = 1082.0 / 64
 # correction: K1's reads are per-lane 16-B loads of scattered segments (not the
 # wide coalesced stream the gfx950 1/2-count applies to), and the raw count
 # already equals the algorithmic read bytes.
-K1_PMC_TRAFFIC_BYTES = (200211.9 + 36959.0) * 1024
+K1_PMC_TRAFFIC_BYTES = None   # re-collected for k_rehash_fused16 (tools/profile_round.sh)
 METRIC = 'synctree keys rehashed/sec + exchange tree-diffs/sec at 10M keys, 1–8 GPUs'
 
 
@@ -124,7 +124,7 @@ def main():
     tree.kernel_stats('*reset*')
     for _ in range(args.steps):
         tree.rehash()
-    k1_n, k1_ms = tree.kernel_stats('segment_hash')
+    k1_n, k1_ms = tree.kernel_stats('rehash_fused')
     k2_n, k2_ms = tree.kernel_stats('level_rehash')
     tree.set_timing(False)
 
@@ -155,22 +155,27 @@ def main():
             seg_of = _segment_histogram(tree, keys_h)
         except Exception as e:  # pragma: no cover
             log('histogram failed', e)
-        # algorithmic bytes of one K1 launch: values (n x 17 B) + seg_off and
-        # seg_voff (2 x (S+1) x 8 B) + the block-count order (S x 4 B) read;
-        # S x (16 B md5 + 2 B tag) node entries written.
-        k1_bytes = n * 17 + (S + 1) * 8 * 2 + S * 4 + S * 18
+        # Algorithmic work of one k_rehash_fused16 launch (K1 + levels H, H-1):
+        # reads the padded MD5 messages of every segment (64 B per block),
+        # tile order + block counts (2 x 4 B per segment) and tile info
+        # (16 B per 64 segments); writes 18 B (md5 + tag) per segment, level-H
+        # and level-(H-1) node.  MD5 blocks: segment messages + 5 per full
+        # inner node (16 x 17 B children).
         if seg_of is not None:
-            blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
+            seg_blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
         else:
-            blocks = int(n * 17 / 64 + nseg)
+            seg_blocks = int(n * 17 / 64 + nseg)
+        inner_nodes = (S >> 4) + (S >> 8)
+        blocks = seg_blocks + 5 * inner_nodes
+        k1_bytes = 64 * seg_blocks + S * 8 + (S // 64) * 16 + (S + inner_nodes) * 18
         k1_avg_ms = k1_ms / max(k1_n, 1)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
         t_valu = blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
         roof = {'bound': 'hbm' if t_hbm >= t_valu else 'valu', 'achieved': round(achieved_gbs, 1),
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
-                'traffic': int(K1_PMC_TRAFFIC_BYTES),
-                'kernel': 'k_segment_hash_perm (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
+                'traffic': K1_PMC_TRAFFIC_BYTES,
+                'kernel': 'k_rehash_fused16 (K1 segment_hash + K2 levels H, H-1)', 'kernel_avg_ms': round(k1_avg_ms, 4),
                 'bytes_per_launch': k1_bytes, 'md5_blocks_per_launch': blocks,
                 't_min_hbm_us': round(t_hbm * 1e6, 2),
                 'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),

@@ -1546,3 +1546,183 @@ __global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *ma
 __host__ __device__ __forceinline__ uint32_t levels3_16_lds_bytes() {
     return 256 * NB16 + 256 * TB16 + 16 * NB16 + 16 * TB16 + NB16 + TB16 + 128;
 }
+
+// ---------------------------------------------------------------------------
+// Hash-ready tiled layout + fused rehash (W == 16, full rehash).
+//
+// The tree keeps, next to the CSR, every segment's hash input as its padded
+// MD5 message (values in key order, 0x80, zeros, 64-bit bit length; RFC 1321
+// §3.1-3.2) in a TILED layout built at ingest: the 256 segments of each level-H
+// node's parent subtree (a level-(H-1) node) are ordered by MD5 block count
+// (descending) and cut into 4 tiles of 64; tile t stores 16-byte chunk q of
+// block k of its lane j at tiles[tbase[t] + (k*4 + q)*64 + j].  A wave hashing
+// one tile then reads 1 KiB contiguous per load instruction, its 64 lanes run
+// (nearly) equal-length MD5 loops, and no padding logic runs in the hot loop.
+// The layout is rebuilt whenever the CSR changes (every mutation goes through
+// ingest), so a rehash always hashes the current segments.
+struct TileInfo {
+    uint64_t base;   // in uint4 units
+    uint32_t B;      // blocks of the longest message in the tile
+    uint32_t pad;
+};
+
+// One workgroup (256 threads) per level-(H-1) subtree of 256 segments: block
+// counts, counting sort (descending), tile block maxima.
+__global__ void __launch_bounds__(256) k_tile_order(const uint64_t *__restrict__ seg_off, const uint64_t *__restrict__ seg_voff,
+                                                    uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
+                                                    uint64_t *__restrict__ tsize) {
+    __shared__ uint32_t hist[16];
+    __shared__ uint32_t bmax[4];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + tid;
+    if (tid < 16) hist[tid] = 0;
+    if (tid < 4) bmax[tid] = 0;
+    __syncthreads();
+    const uint64_t len = seg_voff[s + 1] - seg_voff[s];
+    const uint32_t nb = seg_off[s] == seg_off[s + 1] ? 0u : (uint32_t)((len + 8) / 64 + 1);
+    const uint32_t bin = nb > 15 ? 15u : nb;
+    const uint32_t pos = atomicAdd(&hist[bin], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int b = 15; b >= 0; b--) { const uint32_t c = hist[b]; hist[b] = acc; acc += c; }
+    }
+    __syncthreads();
+    const uint32_t r = hist[bin] + pos;     // rank in descending block-count order
+    const uint64_t o = (uint64_t)blockIdx.x * 256 + r;
+    tseg[o] = (uint32_t)s;
+    tnb[o] = nb;
+    atomicMax(&bmax[r >> 6], nb);
+    __syncthreads();
+    if (tid < 4) tsize[(uint64_t)blockIdx.x * 4 + tid] = (uint64_t)bmax[tid] * 256;   // uint4 units
+}
+
+// One workgroup per tile: write the padded messages in tiled order.
+__global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ seg_voff, const uint8_t *__restrict__ vheap,
+                                                   const uint32_t *__restrict__ tseg, const uint64_t *__restrict__ tbase,
+                                                   const uint64_t *__restrict__ tsize, uint4 *__restrict__ tiles) {
+    const uint32_t tid = threadIdx.x, q = tid >> 6, j = tid & 63;
+    const uint64_t tl = blockIdx.x;
+    const uint32_t B = (uint32_t)(tsize[tl] / 256);
+    if (B == 0) return;
+    const uint32_t s = tseg[tl * 64 + j];
+    const uint64_t v0 = seg_voff[s];
+    const uint64_t len = seg_voff[s + 1] - v0;
+    const uint32_t nb = len ? (uint32_t)((len + 8) / 64 + 1) : 0u;
+    uint4 *dst = tiles + tbase[tl] + q * 64 + j;
+    for (uint32_t k = 0; k < B; k++) {
+        uint4 c = make_uint4(0, 0, 0, 0);
+        if (k < nb) {
+            const uint64_t off = 64ull * k + 16ull * q;
+            if (off < len) __builtin_memcpy(&c, vheap + v0 + off, 16);
+            const int64_t rem = (int64_t)len - (int64_t)off;
+            c.x = stmd5::tail_word(c.x, rem >= 4 ? 4 : (int)rem);
+            c.y = stmd5::tail_word(c.y, rem - 4 >= 4 ? 4 : (int)(rem - 4));
+            c.z = stmd5::tail_word(c.z, rem - 8 >= 4 ? 4 : (int)(rem - 8));
+            c.w = stmd5::tail_word(c.w, rem - 12 >= 4 ? 4 : (int)(rem - 12));
+            if (k + 1 == nb && q == 3) { c.z = (uint32_t)(len << 3); c.w = (uint32_t)(len >> 29); }
+        }
+        dst[(uint64_t)k * 256] = c;
+    }
+}
+
+// Fused rehash of one level-(H-1) subtree per workgroup (4 waves, one tile
+// each): K1 segment hashes from the tiles, then the 16 level-H nodes and the
+// level-(H-1) node (rehash/4 inner part, synctree.erl:515-535) from LDS.
+// Levels H-2..1 follow in k_level16 / k_upper16.
+struct FusedArgs {
+    uint4 *md5;
+    uint16_t *tag;
+    uint64_t b_seg, b_h, b_h1;   // slot bases of levels H+1, H, H-1
+    uint32_t top;                // H - 1 == 1: also set the #tree.top_hash slot
+};
+
+// Hash an inner node whose 16 child entries are staged in LDS (entries in a
+// 272-B block, tags in a 48-B block) through a separate per-lane message
+// region (MsgWriter + md5_lds): few registers, so the fused kernel keeps the
+// occupancy of its K1 part.
+__device__ __forceinline__ void node_lds16_lean(const uint8_t *blk, const uint16_t *tags, uint8_t *msg, uint32_t dg[4],
+                                                uint32_t &present) {
+    MsgWriter mw;
+    mw.init(msg);
+#pragma unroll 1
+    for (int j = 0; j < 16; j++) {
+        const uint32_t tg = tags[j];
+        if (tg & TAG_PRESENT) mw.entry(tg, *reinterpret_cast<const uint4 *>(blk + 16 * j));
+    }
+    const uint32_t len = mw.finish();
+    present = len != 0;
+    if (len) stmd5::md5_lds(msg, len, dg);
+}
+
+#define FUSED_MSG 328   // per-lane message region (>= 5 blocks + 8, odd dword stride)
+__global__ void __launch_bounds__(256) k_rehash_fused16(FusedArgs a, const TileInfo *__restrict__ tinfo,
+                                                        const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ tnb,
+                                                        const uint4 *__restrict__ tiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t E6[16 * NB16];
+    __shared__ __attribute__((aligned(16))) uint8_t T6[16 * TB16];
+    __shared__ __attribute__((aligned(16))) uint8_t E5[NB16];
+    __shared__ __attribute__((aligned(16))) uint8_t T5[TB16];
+    __shared__ __attribute__((aligned(16))) uint8_t MS[16 * FUSED_MSG];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint64_t g = blockIdx.x;
+    const uint64_t tl = g * 4 + (tid >> 6);
+    const TileInfo ti = tinfo[tl];
+    const uint32_t seg = tseg[tl * 64 + lane];
+    const uint32_t nb = tnb[tl * 64 + lane];
+    uint32_t st[4];
+    stmd5::init(st);
+    if (ti.B) {
+        const uint4 *b = tiles + ti.base + lane;
+        uint4 n0 = b[0], n1 = b[64], n2 = b[128], n3 = b[192];
+        for (uint32_t k = 0; k < ti.B; k++) {
+            uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+            if (k + 1 < ti.B) {
+                const uint4 *p = b + 256 * (k + 1);
+                n0 = p[0]; n1 = p[64]; n2 = p[128]; n3 = p[192];
+            }
+            if (k < nb) stmd5::compress(st, m);
+        }
+    }
+    const uint32_t i = seg - (uint32_t)(g * 256);
+    const uint4 e = nb ? make_uint4(st[0], st[1], st[2], st[3]) : make_uint4(0, 0, 0, 0);
+    const uint16_t tg = nb ? (uint16_t)TAG_PRESENT : (uint16_t)0;
+    if (nb) a.md5[a.b_seg + seg] = e;
+    a.tag[a.b_seg + seg] = tg;
+    *reinterpret_cast<uint4 *>(E6 + (i >> 4) * NB16 + (i & 15) * 16) = e;
+    *reinterpret_cast<uint16_t *>(T6 + (i >> 4) * TB16 + (i & 15) * 2) = tg;
+    __syncthreads();
+    if (tid >= 64) return;   // levels H and H-1: wave 0 only; the other waves free their slots
+    if (tid < 16) {
+        uint32_t dg[4], pr;
+        node_lds16_lean(E6 + tid * NB16, reinterpret_cast<const uint16_t *>(T6 + tid * TB16), MS + tid * FUSED_MSG, dg, pr);
+        const uint4 h = pr ? make_uint4(dg[0], dg[1], dg[2], dg[3]) : make_uint4(0, 0, 0, 0);
+        const uint64_t slot = a.b_h + g * 16 + tid;
+        if (pr) a.md5[slot] = h;
+        a.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
+        *reinterpret_cast<uint4 *>(E5 + tid * 16) = h;
+        *reinterpret_cast<uint16_t *>(T5 + tid * 2) = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (tid == 0) {
+        uint32_t dg[4], pr;
+        node_lds16_lean(E5, reinterpret_cast<const uint16_t *>(T5), MS, dg, pr);
+        const uint4 h = pr ? make_uint4(dg[0], dg[1], dg[2], dg[3]) : make_uint4(0, 0, 0, 0);
+        const uint64_t slot = a.b_h1 + g;
+        if (pr) a.md5[slot] = h;
+        a.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
+        if (a.top) { a.md5[0] = h; a.tag[0] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0; }
+    }
+}
+
+__global__ void k_tile_info(const uint64_t *tbase, const uint64_t *tsize, uint64_t ntiles, TileInfo *info) {
+    for (uint64_t i = gtid(); i < ntiles; i += gstride()) {
+        TileInfo x;
+        x.base = tbase[i];
+        x.B = (uint32_t)(tsize[i] / 256);
+        x.pad = 0;
+        info[i] = x;
+    }
+}

@@ -60,6 +60,12 @@ struct st_tree {
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
+    // hash-ready tiled messages (W == 16 fused rehash; st_kernels.h)
+    uint4 *tiles = nullptr;
+    uint64_t tiles_cap = 0;         // uint4 units
+    uint32_t *tseg = nullptr, *tnb = nullptr;
+    TileInfo *tinfo = nullptr;
+    bool tiles_valid = false;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -257,7 +263,7 @@ extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm};
+                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo};
     for (void *p : ps) dfree(t, p);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
@@ -380,7 +386,74 @@ static int ensure_perm(st_tree *t) {
     return ST_OK;
 }
 
+static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 2; }
+
+// Build the hash-ready tiled messages from the CSR (k_tile_order, scan,
+// k_tile_fill).  Called at the end of every ingest and lazily by rehash.
+static int ensure_tiles(st_tree *t) {
+    if (t->tiles_valid || !fused_geometry(t)) return ST_OK;
+    const uint64_t ngroups = t->S / 256, ntiles = ngroups * 4;
+    if (!t->tseg) {
+        CHK(dalloc_t(t, &t->tseg, t->S));
+        CHK(dalloc_t(t, &t->tnb, t->S));
+        CHK(dalloc_t(t, &t->tinfo, ntiles));
+    }
+    uint64_t *tsize = nullptr, *tbase = nullptr;
+    int r = ST_OK;
+    auto done = [&]() { dfree(t, tsize); dfree(t, tbase); };
+    if ((r = dalloc_t(t, &tsize, ntiles + 1)) || (r = dalloc_t(t, &tbase, ntiles + 1))) { done(); return r; }
+    HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
+    LAUNCH(t, "tile_build", k_tile_order, (uint32_t)ngroups, 256, 0, (const uint64_t *)t->seg_off, (const uint64_t *)t->seg_voff,
+           t->tseg, t->tnb, tsize);
+    if ((r = exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1))) { done(); return r; }
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    if (total + 1 > t->tiles_cap) {
+        dfree(t, t->tiles);
+        t->tiles = nullptr;
+        t->tiles_cap = 0;
+        const uint64_t cap = total + total / 8 + 1;
+        if ((r = dalloc_t(t, &t->tiles, cap))) { done(); return r; }
+        t->tiles_cap = cap;
+    }
+    LAUNCH(t, "tile_build", k_tile_fill, (uint32_t)ntiles, 256, 0, (const uint64_t *)t->seg_voff, (const uint8_t *)t->vheap,
+           (const uint32_t *)t->tseg, (const uint64_t *)tbase, (const uint64_t *)tsize, t->tiles);
+    LAUNCH(t, "tile_build", k_tile_info, grid_for(ntiles), 256, 0, (const uint64_t *)tbase, (const uint64_t *)tsize, ntiles,
+           t->tinfo);
+    done();
+    t->tiles_valid = true;
+    return ST_OK;
+}
+
+// Full rehash, W == 16: fused K1 + levels H, H-1 per level-(H-1) subtree,
+// then the remaining levels (k_level16 while a level is wider than 256 nodes,
+// k_upper16 for the rest).
+static int rehash_fused(st_tree *t) {
+    CHK(ensure_tiles(t));
+    DevTree d = view(t);
+    FusedArgs a;
+    a.md5 = t->md5;
+    a.tag = t->tag;
+    a.b_seg = t->base[t->H + 1];
+    a.b_h = t->base[t->H];
+    a.b_h1 = t->base[t->H - 1];
+    a.top = t->H - 1 == 1 ? 1u : 0u;
+    LAUNCH(t, "rehash_fused", k_rehash_fused16, (uint32_t)(t->S / 256), 256, 0, a, (const TileInfo *)t->tinfo,
+           (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
+    if (t->H - 1 == 1) return ST_OK;
+    uint32_t l = t->H - 2;
+    for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
+        LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64, (size_t)64 * lane_region_bytes(16),
+               d, l, (const uint8_t *)nullptr);
+    if (l >= 1)
+        LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, (const uint8_t *)nullptr);
+    return ST_OK;
+}
+
 static int rehash_all(st_tree *t, const uint8_t *mask) {
+    static const int fused_knob = getenv("ST_FUSED") ? atoi(getenv("ST_FUSED")) : 1;
+    if (!mask && fused_knob && fused_geometry(t)) return rehash_fused(t);
     DevTree d = view(t);
     uint32_t depth = 0;
     uint64_t segs = 1;
@@ -619,6 +692,7 @@ static int ingest(st_tree *t, IngestIn &in) {
     t->seg_off = nseg_off; t->seg_voff = nseg_voff; t->koff = nkoff; t->voff = nvoff; t->kheap = nkheap; t->vheap = nvheap;
     t->n = n_new; t->kbytes = tot[0]; t->vbytes = tot[1];
     t->perm_valid = false;
+    t->tiles_valid = false;
 
     if (in.verify_rehash) {
         // dirty-path rehash: segments whose content changed and their ancestors
@@ -628,6 +702,9 @@ static int ingest(st_tree *t, IngestIn &in) {
         ICHK(rehash_all(t, t->mark));
     }
     t->fresh = false;
+    // bulk batches rebuild the hash-ready tiles now (the build pays for the
+    // layout); small ones leave it to the next full rehash
+    if (n >= 65536) ICHK(ensure_tiles(t));
     cleanup();
 #undef ICHK
     return ST_OK;
