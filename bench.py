@@ -45,7 +45,7 @@ MD5_SIMD_CYCLES_PER_BLOCK = 1082.0 / 64
 # correction: K1's reads are per-lane 16-B loads of scattered segments (not the
 # wide coalesced stream the gfx950 1/2-count applies to), and the raw count
 # already equals the algorithmic read bytes.
-K1_PMC_TRAFFIC_BYTES = None   # re-collected for k_rehash_fused16 (tools/profile_round.sh)
+K1_PMC_TRAFFIC_BYTES = None   # re-collected for k_segment_hash_tiled (tools/profile_round.sh)
 METRIC = 'synctree keys rehashed/sec + exchange tree-diffs/sec at 10M keys, 1–8 GPUs'
 
 
@@ -124,7 +124,7 @@ def main():
     tree.kernel_stats('*reset*')
     for _ in range(args.steps):
         tree.rehash()
-    k1_n, k1_ms = tree.kernel_stats('rehash_fused')
+    k1_n, k1_ms = tree.kernel_stats('segment_hash')
     k2_n, k2_ms = tree.kernel_stats('level_rehash')
     tree.set_timing(False)
 
@@ -155,33 +155,34 @@ def main():
             seg_of = _segment_histogram(tree, keys_h)
         except Exception as e:  # pragma: no cover
             log('histogram failed', e)
-        # Algorithmic work of one k_rehash_fused16 launch (K1 + levels H, H-1):
-        # reads the padded MD5 messages of every segment (64 B per block),
-        # tile order + block counts (2 x 4 B per segment) and tile info
-        # (16 B per 64 segments); writes 18 B (md5 + tag) per segment, level-H
-        # and level-(H-1) node.  MD5 blocks: segment messages + 5 per full
-        # inner node (16 x 17 B children).
+        # Algorithmic work of one K1 launch (k_segment_hash_tiled): the hash
+        # input of every segment (its values, 17 B per key: MD5 padding is
+        # computed, not data), the tile metadata (segment id + block count,
+        # 2 x 4 B per segment; 16 B per 64-segment tile) and the 18-B entry
+        # (md5 + tag) written per segment.  The tiles K1 actually streams hold
+        # each message padded to whole 64-B blocks (64 B x blocks, reported
+        # as tile_bytes); the PMC traffic shows what HBM really served.
         if seg_of is not None:
             seg_blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
         else:
             seg_blocks = int(n * 17 / 64 + nseg)
-        inner_nodes = (S >> 4) + (S >> 8)
-        blocks = seg_blocks + 5 * inner_nodes
-        k1_bytes = 64 * seg_blocks + S * 8 + (S // 64) * 16 + (S + inner_nodes) * 18
-        k1_avg_ms = k1_ms / max(k1_n, 1)
+        blocks = seg_blocks
+        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S * 18
+        k1_avg_ms = max(k1_ms / max(k1_n, 1), 1e-9)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
         t_valu = blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
         roof = {'bound': 'hbm' if t_hbm >= t_valu else 'valu', 'achieved': round(achieved_gbs, 1),
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
                 'traffic': K1_PMC_TRAFFIC_BYTES,
-                'kernel': 'k_rehash_fused16 (K1 segment_hash + K2 levels H, H-1)', 'kernel_avg_ms': round(k1_avg_ms, 4),
-                'bytes_per_launch': k1_bytes, 'md5_blocks_per_launch': blocks,
+                'kernel': 'k_segment_hash_tiled (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
+                'bytes_per_launch': k1_bytes, 'tile_bytes_per_launch': 64 * seg_blocks, 'md5_blocks_per_launch': blocks,
                 't_min_hbm_us': round(t_hbm * 1e6, 2),
                 'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),
                          'simd_cycles_per_block': round(MD5_SIMD_CYCLES_PER_BLOCK, 2),
                          'peak': '1024 SIMDs x 2.4 GHz'},
-                'level_rehash_avg_ms_per_step': round(k2_ms / max(args.steps, 1), 4)}
+                'level_rehash_avg_ms_per_step': round(k2_ms / max(args.steps, 1), 4),
+                'level_rehash_kernel': 'k_levels3_16<true> (levels 5..1 + top, one launch)'}
         out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'keys/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',

@@ -1462,7 +1462,14 @@ __device__ __forceinline__ void node_lds16(uint8_t *blk, const uint16_t *tags, u
     }
 }
 
-__global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *mask) {
+// CHAIN (full rehash only): the workgroup that finishes the last of the 16
+// children of a level-(l-1) node hashes that node too, up to level 1 and the
+// top hash, so levels H-3..1 need no further launch.  cnt[slot] counts the
+// finished children of inner node `slot` (levels 1..H-3); the last arriver
+// resets it to 0.  Release/acquire at agent scope make the children's entries,
+// written by workgroups on other XCDs (other L2s), visible to the reader.
+template <bool CHAIN>
+__global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *mask, uint32_t *cnt) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *A = lds;                                        // 256 node blocks (level H children)
     uint16_t *At = reinterpret_cast<uint16_t *>(A + 256 * NB16);
@@ -1540,6 +1547,22 @@ __global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *ma
         if (pr) t.md5[slot] = e;
         t.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
         if (H - 2 == 1) { t.md5[0] = e; t.tag[0] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0; }
+        if (CHAIN) {
+            uint32_t l = H - 2;
+            uint64_t b = root;
+            while (l > 1) {
+                const uint64_t p = b >> 4;
+                uint32_t *c = cnt + t.base[l - 1] + p;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                const uint32_t old = atomicAdd(c, 1u);
+                if (old != 15u) break;
+                *c = 0u;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                hash_node16(t, l - 1, p, A);   // A: consumed staging, reused as the message region
+                l--;
+                b = p;
+            }
+        }
     }
 }
 
@@ -1606,8 +1629,9 @@ __global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ 
     const uint32_t B = (uint32_t)(tsize[tl] / 256);
     if (B == 0) return;
     const uint32_t s = tseg[tl * 64 + j];
-    const uint64_t v0 = seg_voff[s];
-    const uint64_t len = seg_voff[s + 1] - v0;
+    const bool pad = s == 0xffffffffu;
+    const uint64_t v0 = pad ? 0 : seg_voff[s];
+    const uint64_t len = pad ? 0 : seg_voff[s + 1] - v0;
     const uint32_t nb = len ? (uint32_t)((len + 8) / 64 + 1) : 0u;
     uint4 *dst = tiles + tbase[tl] + q * 64 + j;
     for (uint32_t k = 0; k < B; k++) {
@@ -1725,4 +1749,72 @@ __global__ void k_tile_info(const uint64_t *tbase, const uint64_t *tsize, uint64
         x.pad = 0;
         info[i] = x;
     }
+}
+
+// ---------------------------------------------------------------------------
+// K1 over tiles in the GLOBAL block-count order (seg_perm): tile tl holds the
+// segments at positions [64 tl, 64 tl + 64) of seg_perm, so a wave's 64 lanes
+// run (nearly) equal-length MD5 loops across the whole tree, and every load
+// instruction reads 1 KiB contiguous.  Positions past S are padding
+// (tseg = 0xffffffff, nb = 0).
+__global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint32_t *__restrict__ perm,
+                                                           uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
+                                                           uint64_t *__restrict__ tsize, uint64_t ntiles) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t tl = i >> 6;
+    uint32_t s = 0xffffffffu, nb = 0;
+    if (i < t.S) {
+        s = perm[i];
+        if (t.seg_off[s] != t.seg_off[s + 1]) nb = (uint32_t)((t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1);
+    }
+    if (tl < ntiles) {
+        tseg[i] = s;
+        tnb[i] = nb;
+    }
+    uint32_t m = nb;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t y = __shfl_xor(m, o, 64);
+        m = y > m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0 && tl < ntiles) tsize[tl] = (uint64_t)m * 256;
+}
+
+// One wave per tile.  Writes every segment's entry (absent segments: tag 0).
+__global__ void __launch_bounds__(64) k_segment_hash_tiled(DevTree t, const TileInfo *__restrict__ tinfo,
+                                                           const uint32_t *__restrict__ tseg,
+                                                           const uint32_t *__restrict__ tnb,
+                                                           const uint4 *__restrict__ tiles) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t tl = blockIdx.x;
+    const TileInfo ti = tinfo[tl];
+    const uint32_t seg = tseg[tl * 64 + lane];
+    const uint32_t nb = tnb[tl * 64 + lane];
+    const uint32_t B = ti.B;
+    uint32_t st[4];
+    stmd5::init(st);
+    if (B) {
+        const uint4 *b = tiles + ti.base + lane;
+        uint4 n0 = b[0], n1 = b[64], n2 = b[128], n3 = b[192];
+        for (uint32_t k = 0; k < B; k++) {
+            uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+            if (k + 1 < B) {
+                const uint4 *q = b + 256 * (k + 1);
+                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+            }
+            if (k < nb) stmd5::compress(st, m);
+        }
+    }
+    if (seg == 0xffffffffu) return;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t slot = t.base[L1] + seg;
+    if (!nb) {
+        t.tag[slot] = 0;
+        if (L1 == 1) t.tag[0] = 0;
+        return;
+    }
+    const uint4 e = make_uint4(st[0], st[1], st[2], st[3]);
+    t.md5[slot] = e;
+    t.tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
 }

@@ -66,6 +66,8 @@ struct st_tree {
     uint32_t *tseg = nullptr, *tnb = nullptr;
     TileInfo *tinfo = nullptr;
     bool tiles_valid = false;
+    bool tiles_global = false;      // tiles in seg_perm order (else per level-(H-1) group)
+    uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_levels3_16<true>)
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -263,7 +265,7 @@ extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo};
+                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt};
     for (void *p : ps) dfree(t, p);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
@@ -388,14 +390,37 @@ static int ensure_perm(st_tree *t) {
 
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 2; }
 
+// Full-rehash strategy (env ST_REHASH, A/B knob): 2 = tiled K1 in global
+// block-count order + one-launch level dataflow (default), 1 = fused K1 +
+// levels H, H-1 per subtree, 0 = K1 over seg_perm from the CSR.
+static int rehash_mode() {
+    static const int m = getenv("ST_REHASH") ? atoi(getenv("ST_REHASH")) : 2;
+    return m;
+}
+static bool want_tiles(const st_tree *t) {
+    return rehash_mode() == 2 || (rehash_mode() == 1 && fused_geometry(t));
+}
+static int ensure_perm(st_tree *t);
+
 // Build the hash-ready tiled messages from the CSR (k_tile_order, scan,
 // k_tile_fill).  Called at the end of every ingest and lazily by rehash.
+static uint64_t num_tiles(const st_tree *t) { return t->tiles_global ? (t->S + 63) / 64 : t->S / 64; }
+
 static int ensure_tiles(st_tree *t) {
-    if (t->tiles_valid || !fused_geometry(t)) return ST_OK;
-    const uint64_t ngroups = t->S / 256, ntiles = ngroups * 4;
+    if (!want_tiles(t)) return ST_OK;
+    const bool global = rehash_mode() == 2;
+    if (t->tiles_valid && t->tiles_global == global) return ST_OK;
+    if (global) CHK(ensure_perm(t));
+    if (t->tseg && t->tiles_global != global) {
+        dfree(t, t->tseg); dfree(t, t->tnb); dfree(t, t->tinfo);
+        t->tseg = t->tnb = nullptr;
+        t->tinfo = nullptr;
+    }
+    t->tiles_global = global;
+    const uint64_t ntiles = num_tiles(t);
     if (!t->tseg) {
-        CHK(dalloc_t(t, &t->tseg, t->S));
-        CHK(dalloc_t(t, &t->tnb, t->S));
+        CHK(dalloc_t(t, &t->tseg, ntiles * 64));
+        CHK(dalloc_t(t, &t->tnb, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
     uint64_t *tsize = nullptr, *tbase = nullptr;
@@ -403,8 +428,12 @@ static int ensure_tiles(st_tree *t) {
     auto done = [&]() { dfree(t, tsize); dfree(t, tbase); };
     if ((r = dalloc_t(t, &tsize, ntiles + 1)) || (r = dalloc_t(t, &tbase, ntiles + 1))) { done(); return r; }
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
-    LAUNCH(t, "tile_build", k_tile_order, (uint32_t)ngroups, 256, 0, (const uint64_t *)t->seg_off, (const uint64_t *)t->seg_voff,
-           t->tseg, t->tnb, tsize);
+    if (global)
+        LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
+               (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
+    else
+        LAUNCH(t, "tile_build", k_tile_order, (uint32_t)(t->S / 256), 256, 0, (const uint64_t *)t->seg_off,
+               (const uint64_t *)t->seg_voff, t->tseg, t->tnb, tsize);
     if ((r = exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1))) { done(); return r; }
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
@@ -451,9 +480,40 @@ static int rehash_fused(st_tree *t) {
     return ST_OK;
 }
 
+// Full rehash, default strategy: K1 k_segment_hash_tiled over the global
+// block-count tiles, then (W == 16, H >= 3) every inner level and the top hash
+// in ONE launch of k_levels3_16<true> (levels H..H-2 per workgroup, the rest
+// by last-arriving workgroups).  Other geometries use the per-level kernels.
+static int rehash_tiled(st_tree *t) {
+    CHK(ensure_tiles(t));
+    DevTree d = view(t);
+    LAUNCH(t, "segment_hash", k_segment_hash_tiled, (uint32_t)num_tiles(t), 64, 0, d, (const TileInfo *)t->tinfo,
+           (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
+    if (t->H == 0) return ST_OK;
+    if (t->W == 16 && t->H >= 3) {
+        if (!t->lvl_cnt) {
+            CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
+            HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
+        }
+        LAUNCH(t, "level_rehash", k_levels3_16<true>, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
+               levels3_16_lds_bytes(), d, (const uint8_t *)nullptr, t->lvl_cnt);
+        return ST_OK;
+    }
+    if (t->W == 16) {
+        uint32_t l = t->H;
+        for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
+            LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
+                   (size_t)64 * lane_region_bytes(16), d, l, (const uint8_t *)nullptr);
+        if (l >= 1)
+            LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, (const uint8_t *)nullptr);
+        return ST_OK;
+    }
+    return rehash_levels(t, t->H, nullptr);
+}
+
 static int rehash_all(st_tree *t, const uint8_t *mask) {
-    static const int fused_knob = getenv("ST_FUSED") ? atoi(getenv("ST_FUSED")) : 1;
-    if (!mask && fused_knob && fused_geometry(t)) return rehash_fused(t);
+    if (!mask && rehash_mode() == 2) return rehash_tiled(t);
+    if (!mask && rehash_mode() == 1 && fused_geometry(t)) return rehash_fused(t);
     DevTree d = view(t);
     uint32_t depth = 0;
     uint64_t segs = 1;
@@ -475,8 +535,8 @@ static int rehash_all(st_tree *t, const uint8_t *mask) {
             LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
         static const int k2 = getenv("ST_K2") ? atoi(getenv("ST_K2")) : 2;
         if (k2 == 2 && t->W == 16 && t->H >= 3) {
-            LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
-                   levels3_16_lds_bytes(), d, mask);
+            LAUNCH(t, "level_rehash", k_levels3_16<false>, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
+                   levels3_16_lds_bytes(), d, mask, (uint32_t *)nullptr);
             uint32_t l = t->H - 3;
             for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
                 LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
