@@ -182,7 +182,7 @@ def main():
                          'simd_cycles_per_block': round(MD5_SIMD_CYCLES_PER_BLOCK, 2),
                          'peak': '1024 SIMDs x 2.4 GHz'},
                 'level_rehash_avg_ms_per_step': round(k2_ms / max(args.steps, 1), 4),
-                'level_rehash_kernel': 'k_levels3_16<true> (levels 5..1 + top, one launch)'}
+                'level_rehash_kernel': 'k_levels_flow16 (levels 5..1 + top, one launch)'}
         out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'keys/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',

@@ -1462,14 +1462,7 @@ __device__ __forceinline__ void node_lds16(uint8_t *blk, const uint16_t *tags, u
     }
 }
 
-// CHAIN (full rehash only): the workgroup that finishes the last of the 16
-// children of a level-(l-1) node hashes that node too, up to level 1 and the
-// top hash, so levels H-3..1 need no further launch.  cnt[slot] counts the
-// finished children of inner node `slot` (levels 1..H-3); the last arriver
-// resets it to 0.  Release/acquire at agent scope make the children's entries,
-// written by workgroups on other XCDs (other L2s), visible to the reader.
-template <bool CHAIN>
-__global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *mask, uint32_t *cnt) {
+__global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *mask) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *A = lds;                                        // 256 node blocks (level H children)
     uint16_t *At = reinterpret_cast<uint16_t *>(A + 256 * NB16);
@@ -1547,22 +1540,6 @@ __global__ void __launch_bounds__(256) k_levels3_16(DevTree t, const uint8_t *ma
         if (pr) t.md5[slot] = e;
         t.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
         if (H - 2 == 1) { t.md5[0] = e; t.tag[0] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0; }
-        if (CHAIN) {
-            uint32_t l = H - 2;
-            uint64_t b = root;
-            while (l > 1) {
-                const uint64_t p = b >> 4;
-                uint32_t *c = cnt + t.base[l - 1] + p;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                const uint32_t old = atomicAdd(c, 1u);
-                if (old != 15u) break;
-                *c = 0u;
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                hash_node16(t, l - 1, p, A);   // A: consumed staging, reused as the message region
-                l--;
-                b = p;
-            }
-        }
     }
 }
 
@@ -1571,54 +1548,23 @@ __host__ __device__ __forceinline__ uint32_t levels3_16_lds_bytes() {
 }
 
 // ---------------------------------------------------------------------------
-// Hash-ready tiled layout + fused rehash (W == 16, full rehash).
+// Hash-ready tiled layout (full rehash, K1).
 //
 // The tree keeps, next to the CSR, every segment's hash input as its padded
 // MD5 message (values in key order, 0x80, zeros, 64-bit bit length; RFC 1321
-// §3.1-3.2) in a TILED layout built at ingest: the 256 segments of each level-H
-// node's parent subtree (a level-(H-1) node) are ordered by MD5 block count
-// (descending) and cut into 4 tiles of 64; tile t stores 16-byte chunk q of
-// block k of its lane j at tiles[tbase[t] + (k*4 + q)*64 + j].  A wave hashing
-// one tile then reads 1 KiB contiguous per load instruction, its 64 lanes run
-// (nearly) equal-length MD5 loops, and no padding logic runs in the hot loop.
-// The layout is rebuilt whenever the CSR changes (every mutation goes through
-// ingest), so a rehash always hashes the current segments.
+// §3.1-3.2) in a TILED layout built at ingest: segments in seg_perm order
+// (descending MD5 block count) are cut into tiles of 64; tile t stores 16-byte
+// chunk q of block k of its lane j at tiles[tbase[t] + (k*4 + q)*64 + j].  A
+// wave hashing one tile then reads 1 KiB contiguous per load instruction, its
+// 64 lanes run (nearly) equal-length MD5 loops, and no padding logic runs in
+// the hot loop.  The layout is rebuilt whenever the CSR changes (every
+// mutation goes through ingest), so a rehash always hashes the current
+// segments.
 struct TileInfo {
     uint64_t base;   // in uint4 units
     uint32_t B;      // blocks of the longest message in the tile
     uint32_t pad;
 };
-
-// One workgroup (256 threads) per level-(H-1) subtree of 256 segments: block
-// counts, counting sort (descending), tile block maxima.
-__global__ void __launch_bounds__(256) k_tile_order(const uint64_t *__restrict__ seg_off, const uint64_t *__restrict__ seg_voff,
-                                                    uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
-                                                    uint64_t *__restrict__ tsize) {
-    __shared__ uint32_t hist[16];
-    __shared__ uint32_t bmax[4];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t s = (uint64_t)blockIdx.x * 256 + tid;
-    if (tid < 16) hist[tid] = 0;
-    if (tid < 4) bmax[tid] = 0;
-    __syncthreads();
-    const uint64_t len = seg_voff[s + 1] - seg_voff[s];
-    const uint32_t nb = seg_off[s] == seg_off[s + 1] ? 0u : (uint32_t)((len + 8) / 64 + 1);
-    const uint32_t bin = nb > 15 ? 15u : nb;
-    const uint32_t pos = atomicAdd(&hist[bin], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int b = 15; b >= 0; b--) { const uint32_t c = hist[b]; hist[b] = acc; acc += c; }
-    }
-    __syncthreads();
-    const uint32_t r = hist[bin] + pos;     // rank in descending block-count order
-    const uint64_t o = (uint64_t)blockIdx.x * 256 + r;
-    tseg[o] = (uint32_t)s;
-    tnb[o] = nb;
-    atomicMax(&bmax[r >> 6], nb);
-    __syncthreads();
-    if (tid < 4) tsize[(uint64_t)blockIdx.x * 4 + tid] = (uint64_t)bmax[tid] * 256;   // uint4 units
-}
 
 // One workgroup per tile: write the padded messages in tiled order.
 __global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ seg_voff, const uint8_t *__restrict__ vheap,
@@ -1647,97 +1593,6 @@ __global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ 
             if (k + 1 == nb && q == 3) { c.z = (uint32_t)(len << 3); c.w = (uint32_t)(len >> 29); }
         }
         dst[(uint64_t)k * 256] = c;
-    }
-}
-
-// Fused rehash of one level-(H-1) subtree per workgroup (4 waves, one tile
-// each): K1 segment hashes from the tiles, then the 16 level-H nodes and the
-// level-(H-1) node (rehash/4 inner part, synctree.erl:515-535) from LDS.
-// Levels H-2..1 follow in k_level16 / k_upper16.
-struct FusedArgs {
-    uint4 *md5;
-    uint16_t *tag;
-    uint64_t b_seg, b_h, b_h1;   // slot bases of levels H+1, H, H-1
-    uint32_t top;                // H - 1 == 1: also set the #tree.top_hash slot
-};
-
-// Hash an inner node whose 16 child entries are staged in LDS (entries in a
-// 272-B block, tags in a 48-B block) through a separate per-lane message
-// region (MsgWriter + md5_lds): few registers, so the fused kernel keeps the
-// occupancy of its K1 part.
-__device__ __forceinline__ void node_lds16_lean(const uint8_t *blk, const uint16_t *tags, uint8_t *msg, uint32_t dg[4],
-                                                uint32_t &present) {
-    MsgWriter mw;
-    mw.init(msg);
-#pragma unroll 1
-    for (int j = 0; j < 16; j++) {
-        const uint32_t tg = tags[j];
-        if (tg & TAG_PRESENT) mw.entry(tg, *reinterpret_cast<const uint4 *>(blk + 16 * j));
-    }
-    const uint32_t len = mw.finish();
-    present = len != 0;
-    if (len) stmd5::md5_lds(msg, len, dg);
-}
-
-#define FUSED_MSG 328   // per-lane message region (>= 5 blocks + 8, odd dword stride)
-__global__ void __launch_bounds__(256) k_rehash_fused16(FusedArgs a, const TileInfo *__restrict__ tinfo,
-                                                        const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ tnb,
-                                                        const uint4 *__restrict__ tiles) {
-    __shared__ __attribute__((aligned(16))) uint8_t E6[16 * NB16];
-    __shared__ __attribute__((aligned(16))) uint8_t T6[16 * TB16];
-    __shared__ __attribute__((aligned(16))) uint8_t E5[NB16];
-    __shared__ __attribute__((aligned(16))) uint8_t T5[TB16];
-    __shared__ __attribute__((aligned(16))) uint8_t MS[16 * FUSED_MSG];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint64_t g = blockIdx.x;
-    const uint64_t tl = g * 4 + (tid >> 6);
-    const TileInfo ti = tinfo[tl];
-    const uint32_t seg = tseg[tl * 64 + lane];
-    const uint32_t nb = tnb[tl * 64 + lane];
-    uint32_t st[4];
-    stmd5::init(st);
-    if (ti.B) {
-        const uint4 *b = tiles + ti.base + lane;
-        uint4 n0 = b[0], n1 = b[64], n2 = b[128], n3 = b[192];
-        for (uint32_t k = 0; k < ti.B; k++) {
-            uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
-            if (k + 1 < ti.B) {
-                const uint4 *p = b + 256 * (k + 1);
-                n0 = p[0]; n1 = p[64]; n2 = p[128]; n3 = p[192];
-            }
-            if (k < nb) stmd5::compress(st, m);
-        }
-    }
-    const uint32_t i = seg - (uint32_t)(g * 256);
-    const uint4 e = nb ? make_uint4(st[0], st[1], st[2], st[3]) : make_uint4(0, 0, 0, 0);
-    const uint16_t tg = nb ? (uint16_t)TAG_PRESENT : (uint16_t)0;
-    if (nb) a.md5[a.b_seg + seg] = e;
-    a.tag[a.b_seg + seg] = tg;
-    *reinterpret_cast<uint4 *>(E6 + (i >> 4) * NB16 + (i & 15) * 16) = e;
-    *reinterpret_cast<uint16_t *>(T6 + (i >> 4) * TB16 + (i & 15) * 2) = tg;
-    __syncthreads();
-    if (tid >= 64) return;   // levels H and H-1: wave 0 only; the other waves free their slots
-    if (tid < 16) {
-        uint32_t dg[4], pr;
-        node_lds16_lean(E6 + tid * NB16, reinterpret_cast<const uint16_t *>(T6 + tid * TB16), MS + tid * FUSED_MSG, dg, pr);
-        const uint4 h = pr ? make_uint4(dg[0], dg[1], dg[2], dg[3]) : make_uint4(0, 0, 0, 0);
-        const uint64_t slot = a.b_h + g * 16 + tid;
-        if (pr) a.md5[slot] = h;
-        a.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
-        *reinterpret_cast<uint4 *>(E5 + tid * 16) = h;
-        *reinterpret_cast<uint16_t *>(T5 + tid * 2) = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    if (tid == 0) {
-        uint32_t dg[4], pr;
-        node_lds16_lean(E5, reinterpret_cast<const uint16_t *>(T5), MS, dg, pr);
-        const uint4 h = pr ? make_uint4(dg[0], dg[1], dg[2], dg[3]) : make_uint4(0, 0, 0, 0);
-        const uint64_t slot = a.b_h1 + g;
-        if (pr) a.md5[slot] = h;
-        a.tag[slot] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0;
-        if (a.top) { a.md5[0] = h; a.tag[0] = pr ? (uint16_t)TAG_PRESENT : (uint16_t)0; }
     }
 }
 
@@ -1817,4 +1672,147 @@ __global__ void __launch_bounds__(64) k_segment_hash_tiled(DevTree t, const Tile
     t.md5[slot] = e;
     t.tag[slot] = TAG_PRESENT;
     if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+}
+
+// ---------------------------------------------------------------------------
+// K2 full level rehash (W == 16, H >= 3) in ONE launch with ONE inlined copy
+// of the node-hash code.  A workgroup per level-(H-2) subtree stages its 4096
+// segment entries in LDS (as k_levels3_16), then loops: phase 0 = 256 level-H
+// nodes (one per lane), phase 1 = 16 level-(H-1) nodes, phase 2 = the
+// level-(H-2) node; after that lane 0 climbs while it is the last of 16
+// siblings to finish (cnt[slot] counts the finished children of inner node
+// `slot`, levels 1..H-3; the last arriver resets it to 0), hashing the parent from
+// global memory, up to level 1 and the top hash.  Children come through
+// generic pointers (LDS for phases 0-2, global for the climb), so every level
+// runs the same instructions: the code a CU warms at level H stays in its
+// instruction cache for the latency-bound single-lane levels above it.
+// Release/acquire fences at agent scope around the counter make the
+// children's entries, written by workgroups on other XCDs (other L2s),
+// visible to the climbing lane.
+__device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tags, uint8_t *reg, uint4 &e, uint32_t &tg) {
+    uint4 h[16];
+    uint32_t t16[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) { h[j] = ent[j]; t16[j] = tags[j]; }
+    uint32_t full = 1;
+#pragma unroll
+    for (int j = 0; j < 16; j++) full &= (t16[j] >> 8) & 1u;
+    uint32_t dg[4];
+    // The path is chosen per WAVE, not per lane: a wave whose active lanes
+    // all hold full nodes hashes from registers (md5_node16, the common case
+    // in big trees); otherwise every lane packs its present entries into its
+    // LDS region and hashes from there.  Lanes of one wave never split
+    // between the two paths (that would run both, one after the other).
+    if (__ballot(!full) == 0) {
+        uint32_t pf[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) pf[j] = t16[j] & 0xffu;
+        stmd5::md5_node16(pf, h, dg);
+        tg = TAG_PRESENT;
+        e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+        return;
+    }
+    MsgWriter mw;
+    mw.init(reg);
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if (t16[j] & TAG_PRESENT) mw.entry(t16[j], h[j]);
+    const uint32_t len = mw.finish();
+    tg = len ? TAG_PRESENT : 0u;
+    e = make_uint4(0, 0, 0, 0);
+    if (!len) return;
+    stmd5::md5_lds(reg, len, dg);
+    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+}
+
+template <bool STAMP>
+__global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt, uint64_t *stamps) {
+#define FLOW_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    FLOW_STAMP(0);
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *A = lds;
+    uint8_t *At = A + 256 * NB16;
+    uint8_t *Bb = At + 256 * TB16;
+    uint8_t *Bt = Bb + 16 * NB16;
+    uint8_t *Cb = Bt + 16 * TB16;
+    uint8_t *Ct = Cb + NB16;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t H = t.H;
+    const uint64_t root = blockIdx.x;
+    const uint64_t c0 = t.base[H + 1] + root * 4096;
+#pragma unroll 4
+    for (uint32_t it = 0; it < 16; it++) {
+        const uint32_t e = it * 256 + tid;
+        *reinterpret_cast<uint4 *>(A + (e >> 4) * NB16 + (e & 15) * 16) = t.md5[c0 + e];
+    }
+    {
+        const uint4 *tg = reinterpret_cast<const uint4 *>(t.tag + c0);
+        for (uint32_t it = 0; it < 2; it++) {
+            const uint32_t q = it * 256 + tid;
+            *reinterpret_cast<uint4 *>(At + (q >> 1) * TB16 + (q & 1) * 16) = tg[q];
+        }
+    }
+    __syncthreads();
+    FLOW_STAMP(1);
+    uint32_t l = H;
+    uint64_t b = root * 256 + tid;
+    const uint4 *ent = reinterpret_cast<const uint4 *>(A + tid * NB16);
+    const uint16_t *tgs = reinterpret_cast<const uint16_t *>(At + tid * TB16);
+    uint8_t *reg = A + tid * NB16;
+    uint8_t *nxE = Bb + (tid >> 4) * NB16 + (tid & 15) * 16;
+    uint8_t *nxT = Bt + (tid >> 4) * TB16 + (tid & 15) * 2;
+    bool act = true;
+#pragma unroll 1
+    for (uint32_t phase = 0;; phase++) {
+        if (act) {
+            uint4 e;
+            uint32_t tg;
+            node16_any(ent, tgs, reg, e, tg);
+            const uint64_t slot = t.base[l] + b;
+            if (tg) t.md5[slot] = e;
+            t.tag[slot] = (uint16_t)tg;
+            if (l == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
+            if (phase < 2) {
+                *reinterpret_cast<uint4 *>(nxE) = e;
+                *reinterpret_cast<uint16_t *>(nxT) = (uint16_t)tg;
+            }
+        }
+        FLOW_STAMP(2 + 2 * phase);
+        if (phase < 2) {
+            __syncthreads();
+            l--;
+            if (phase == 0) {
+                act = tid < 16;
+                b = root * 16 + tid;
+                ent = reinterpret_cast<const uint4 *>(Bb + tid * NB16);
+                tgs = reinterpret_cast<const uint16_t *>(Bt + tid * TB16);
+                reg = Bb + tid * NB16;
+                nxE = Cb + tid * 16;
+                nxT = Ct + tid * 2;
+            } else {
+                act = tid == 0;
+                b = root;
+                ent = reinterpret_cast<const uint4 *>(Cb);
+                tgs = reinterpret_cast<const uint16_t *>(Ct);
+                reg = Cb;
+            }
+            continue;
+        }
+        if (tid != 0 || l == 1) break;
+        const uint64_t p = b >> 4;
+        uint32_t *c = cnt + t.base[l - 1] + p;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const uint32_t old = atomicAdd(c, 1u);
+        if (old != 15u) break;
+        *c = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        FLOW_STAMP(3 + 2 * phase);
+        l--;
+        b = p;
+        const uint64_t cc = t.base[l + 1] + p * 16;
+        ent = t.md5 + cc;
+        tgs = t.tag + cc;
+        reg = A;
+    }
+#undef FLOW_STAMP
 }

@@ -14,6 +14,7 @@
 #include <map>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
@@ -60,14 +61,13 @@ struct st_tree {
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
-    // hash-ready tiled messages (W == 16 fused rehash; st_kernels.h)
+    // hash-ready tiled messages in seg_perm order (K1; st_kernels.h)
     uint4 *tiles = nullptr;
     uint64_t tiles_cap = 0;         // uint4 units
     uint32_t *tseg = nullptr, *tnb = nullptr;
     TileInfo *tinfo = nullptr;
     bool tiles_valid = false;
-    bool tiles_global = false;      // tiles in seg_perm order (else per level-(H-1) group)
-    uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_levels3_16<true>)
+    uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_levels_flow16)
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -388,35 +388,25 @@ static int ensure_perm(st_tree *t) {
     return ST_OK;
 }
 
-static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 2; }
-
 // Full-rehash strategy (env ST_REHASH, A/B knob): 2 = tiled K1 in global
-// block-count order + one-launch level dataflow (default), 1 = fused K1 +
-// levels H, H-1 per subtree, 0 = K1 over seg_perm from the CSR.
+// block-count order + level dataflow (default), 0 = K1 over seg_perm straight
+// from the CSR + per-level kernels.
 static int rehash_mode() {
     static const int m = getenv("ST_REHASH") ? atoi(getenv("ST_REHASH")) : 2;
     return m;
-}
-static bool want_tiles(const st_tree *t) {
-    return rehash_mode() == 2 || (rehash_mode() == 1 && fused_geometry(t));
 }
 static int ensure_perm(st_tree *t);
 
 // Build the hash-ready tiled messages from the CSR (k_tile_order, scan,
 // k_tile_fill).  Called at the end of every ingest and lazily by rehash.
-static uint64_t num_tiles(const st_tree *t) { return t->tiles_global ? (t->S + 63) / 64 : t->S / 64; }
+static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 
+// Build the hash-ready tiled messages from the CSR in seg_perm order
+// (k_tile_order_global, scan, k_tile_fill).  Called at the end of every bulk
+// ingest and lazily by rehash.
 static int ensure_tiles(st_tree *t) {
-    if (!want_tiles(t)) return ST_OK;
-    const bool global = rehash_mode() == 2;
-    if (t->tiles_valid && t->tiles_global == global) return ST_OK;
-    if (global) CHK(ensure_perm(t));
-    if (t->tseg && t->tiles_global != global) {
-        dfree(t, t->tseg); dfree(t, t->tnb); dfree(t, t->tinfo);
-        t->tseg = t->tnb = nullptr;
-        t->tinfo = nullptr;
-    }
-    t->tiles_global = global;
+    if (rehash_mode() != 2 || t->tiles_valid) return ST_OK;
+    CHK(ensure_perm(t));
     const uint64_t ntiles = num_tiles(t);
     if (!t->tseg) {
         CHK(dalloc_t(t, &t->tseg, ntiles * 64));
@@ -428,12 +418,8 @@ static int ensure_tiles(st_tree *t) {
     auto done = [&]() { dfree(t, tsize); dfree(t, tbase); };
     if ((r = dalloc_t(t, &tsize, ntiles + 1)) || (r = dalloc_t(t, &tbase, ntiles + 1))) { done(); return r; }
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
-    if (global)
-        LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
-               (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
-    else
-        LAUNCH(t, "tile_build", k_tile_order, (uint32_t)(t->S / 256), 256, 0, (const uint64_t *)t->seg_off,
-               (const uint64_t *)t->seg_voff, t->tseg, t->tnb, tsize);
+    LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
+           (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
     if ((r = exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1))) { done(); return r; }
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
@@ -455,35 +441,10 @@ static int ensure_tiles(st_tree *t) {
     return ST_OK;
 }
 
-// Full rehash, W == 16: fused K1 + levels H, H-1 per level-(H-1) subtree,
-// then the remaining levels (k_level16 while a level is wider than 256 nodes,
-// k_upper16 for the rest).
-static int rehash_fused(st_tree *t) {
-    CHK(ensure_tiles(t));
-    DevTree d = view(t);
-    FusedArgs a;
-    a.md5 = t->md5;
-    a.tag = t->tag;
-    a.b_seg = t->base[t->H + 1];
-    a.b_h = t->base[t->H];
-    a.b_h1 = t->base[t->H - 1];
-    a.top = t->H - 1 == 1 ? 1u : 0u;
-    LAUNCH(t, "rehash_fused", k_rehash_fused16, (uint32_t)(t->S / 256), 256, 0, a, (const TileInfo *)t->tinfo,
-           (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
-    if (t->H - 1 == 1) return ST_OK;
-    uint32_t l = t->H - 2;
-    for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
-        LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64, (size_t)64 * lane_region_bytes(16),
-               d, l, (const uint8_t *)nullptr);
-    if (l >= 1)
-        LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, (const uint8_t *)nullptr);
-    return ST_OK;
-}
-
 // Full rehash, default strategy: K1 k_segment_hash_tiled over the global
 // block-count tiles, then (W == 16, H >= 3) every inner level and the top hash
-// in ONE launch of k_levels3_16<true> (levels H..H-2 per workgroup, the rest
-// by last-arriving workgroups).  Other geometries use the per-level kernels.
+// in ONE launch of k_levels_flow16 (levels H..H-2 per workgroup, the rest by
+// last-arriving workgroups).  Other geometries use the per-level kernels.
 static int rehash_tiled(st_tree *t) {
     CHK(ensure_tiles(t));
     DevTree d = view(t);
@@ -495,8 +456,31 @@ static int rehash_tiled(st_tree *t) {
             CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
             HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
         }
-        LAUNCH(t, "level_rehash", k_levels3_16<true>, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
-               levels3_16_lds_bytes(), d, (const uint8_t *)nullptr, t->lvl_cnt);
+        static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
+        const uint32_t nwg = (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]);
+        if (!stamp)
+            LAUNCH(t, "level_rehash", k_levels_flow16<false>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt,
+                   (uint64_t *)nullptr);
+        else {   // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
+            uint64_t *st = nullptr;
+            CHK(dalloc_t(t, &st, (uint64_t)nwg * 16));
+            HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
+            LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st);
+            std::vector<uint64_t> h((uint64_t)nwg * 16);
+            HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(hipStreamSynchronize(t->stream));
+            dfree(t, st);
+            uint64_t t0 = ~0ull;
+            for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
+            for (int k = 0; k < 12; k++) {
+                std::vector<double> v;
+                for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, "flow stamp %2d: n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, v.size(), v[0], v[v.size() / 2],
+                        v.back());
+            }
+        }
         return ST_OK;
     }
     if (t->W == 16) {
@@ -513,7 +497,6 @@ static int rehash_tiled(st_tree *t) {
 
 static int rehash_all(st_tree *t, const uint8_t *mask) {
     if (!mask && rehash_mode() == 2) return rehash_tiled(t);
-    if (!mask && rehash_mode() == 1 && fused_geometry(t)) return rehash_fused(t);
     DevTree d = view(t);
     uint32_t depth = 0;
     uint64_t segs = 1;
@@ -535,8 +518,8 @@ static int rehash_all(st_tree *t, const uint8_t *mask) {
             LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
         static const int k2 = getenv("ST_K2") ? atoi(getenv("ST_K2")) : 2;
         if (k2 == 2 && t->W == 16 && t->H >= 3) {
-            LAUNCH(t, "level_rehash", k_levels3_16<false>, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
-                   levels3_16_lds_bytes(), d, mask, (uint32_t *)nullptr);
+            LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
+                   levels3_16_lds_bytes(), d, mask);
             uint32_t l = t->H - 3;
             for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
                 LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
