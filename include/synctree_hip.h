@@ -140,6 +140,22 @@ int st_top_hash(st_tree *t, uint8_t out17[17], int *present);
  * hashes17[W^(level-1) * 17].  Used for per-level parity checks. */
 int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes17);
 
+/* ---- multi-GPU: segment-range partition of one tree ------
+ * No reference counterpart: riak_ensemble keeps a tree on one node.  This is
+ * the sharding of a single huge tree across the GPUs of one node.
+ *
+ * st_set_partition: this handle owns segments [seg_lo, seg_hi) only (width
+ * 16, height >= 4, whole level-2 subtrees: S/16-aligned; call before the
+ * first insert; [0, S) clears it).  Inserts keep the owned keys and drop the
+ * rest; st_rehash (upper = 0) hashes the owned subtrees up to level 2 and
+ * leaves level 1 + top to st_combine_upper.
+ *
+ * st_combine_upper: store the 16 level-2 entries (present16[16],
+ * hashes17[16*17], all-gathered from every partition) and recompute level 1
+ * and the top hash, so every partition holds the global tree's top hash. */
+int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi);
+int st_combine_upper(st_tree *t, const uint8_t *present16, const uint8_t *hashes17);
+
 /* ---- reads ---------------------------------------------------------- */
 
 /* Library-allocated result blocks; free with st_free_result(). */

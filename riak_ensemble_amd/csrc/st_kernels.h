@@ -1173,6 +1173,17 @@ __device__ __forceinline__ uint32_t perm_bin(const DevTree &t, uint64_t s) {
     return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
 }
 
+// Segment-range partition: empty the batch runs of segments outside
+// [lo, hi) (clamp the run bounds), so ingest keeps only the owned keys.
+__global__ void k_clamp_runs(uint64_t *bseg_off, uint64_t S, uint64_t lo, uint64_t hi) {
+    const uint64_t a = bseg_off[lo], b = bseg_off[hi];
+    for (uint64_t s = gtid(); s <= S; s += gstride()) {
+        if (s == lo || s == hi) continue;
+        const uint64_t x = bseg_off[s];
+        bseg_off[s] = x < a ? a : (x > b ? b : x);
+    }
+}
+
 // Pass 1: per-workgroup histograms reserved from global bin counters.
 __global__ void __launch_bounds__(256) k_seg_perm_count(DevTree t, uint32_t *gcount) {
     __shared__ uint32_t h[PERM_BINS];
@@ -1725,8 +1736,12 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
     e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
 }
 
+// root0: first level-(H-2) bucket (a segment-range partition hashes only its
+// own subtrees); lmin: the climb stops once level lmin is hashed (1 = up to
+// the top hash; 2 = a partition stops at its level-2 entries).
 template <bool STAMP>
-__global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt, uint64_t *stamps) {
+__global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt, uint64_t *stamps, uint64_t root0,
+                                                       uint32_t lmin) {
 #define FLOW_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     FLOW_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1738,7 +1753,7 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
     uint8_t *Ct = Cb + NB16;
     const uint32_t tid = threadIdx.x;
     const uint32_t H = t.H;
-    const uint64_t root = blockIdx.x;
+    const uint64_t root = root0 + blockIdx.x;
     const uint64_t c0 = t.base[H + 1] + root * 4096;
 #pragma unroll 4
     for (uint32_t it = 0; it < 16; it++) {
@@ -1798,7 +1813,7 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
             }
             continue;
         }
-        if (tid != 0 || l == 1) break;
+        if (tid != 0 || l <= lmin) break;
         const uint64_t p = b >> 4;
         uint32_t *c = cnt + t.base[l - 1] + p;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

@@ -68,6 +68,9 @@ struct st_tree {
     TileInfo *tinfo = nullptr;
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_levels_flow16)
+    // segment-range partition (st_set_partition): owned segments [part_lo, part_hi)
+    bool partitioned = false;
+    uint64_t part_lo = 0, part_hi = 0;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -457,15 +460,23 @@ static int rehash_tiled(st_tree *t) {
             HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
         }
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
-        const uint32_t nwg = (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]);
+        // a partition hashes only its own level-(H-2) subtrees (4096 segments
+        // each) and stops at level 2; st_combine_upper finishes level 1 + top
+        const uint64_t nroots = t->base[t->H - 1] - t->base[t->H - 2];   // 16^(H-3) level-(H-2) nodes
+        const uint64_t sub = t->S / nroots;                                // segments per subtree
+        const uint64_t root0 = t->partitioned ? t->part_lo / sub : 0;
+        const uint32_t nwg = t->partitioned ? (uint32_t)((t->part_hi - t->part_lo) / sub) : (uint32_t)nroots;
+        if (root0 + nwg > nroots || nwg == 0) { g_err = "level rehash range out of bounds"; return ST_EINVAL; }
+        const uint32_t lmin = t->partitioned ? 2u : 1u;
         if (!stamp)
             LAUNCH(t, "level_rehash", k_levels_flow16<false>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt,
-                   (uint64_t *)nullptr);
+                   (uint64_t *)nullptr, root0, lmin);
         else {   // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
             uint64_t *st = nullptr;
             CHK(dalloc_t(t, &st, (uint64_t)nwg * 16));
             HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
-            LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st);
+            LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st, root0,
+                   lmin);
             std::vector<uint64_t> h((uint64_t)nwg * 16);
             HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
             HIPCHK(hipStreamSynchronize(t->stream));
@@ -665,6 +676,7 @@ static int ingest(st_tree *t, IngestIn &in) {
         HIPCHK(hipMemcpyAsync(perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
     }
     LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
+    if (t->partitioned) LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bseg_off, S, t->part_lo, t->part_hi);
     BatchView bv{in.krec, in.koff};
     LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, perm, (const uint64_t *)bseg_off, S, keep);
 
@@ -1021,6 +1033,10 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 extern "C" int st_rehash(st_tree *t, int upper) {
     CHK(use_device(t));
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
+    if (t->partitioned && (upper || rehash_mode() != 2)) {
+        g_err = "a segment-range partition supports the full rehash (st_rehash upper = 0) only";
+        return ST_EINVAL;
+    }
     if (upper) CHK(rehash_levels(t, t->H, nullptr));
     else CHK(rehash_all(t, nullptr));
     t->fresh = false;
@@ -1066,6 +1082,40 @@ extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
     HIPCHK(hipStreamSynchronize(t->stream));
     *present = (tg & TAG_PRESENT) ? 1 : 0;
     if (*present) entry_to_h17(tg, m, out17);
+    return ST_OK;
+}
+
+extern "C" int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi) {
+    CHK(use_device(t));
+    if (seg_lo == 0 && seg_hi == t->S) { t->partitioned = false; return ST_OK; }
+    const uint64_t l2 = t->W == 16 && t->H >= 4 ? t->S / 16 : 0;
+    if (!l2 || seg_lo >= seg_hi || seg_hi > t->S || seg_lo % l2 || seg_hi % l2) {
+        g_err = "partition needs width 16, height >= 4 and a range of whole level-2 subtrees";
+        return ST_EINVAL;
+    }
+    if (t->n) { g_err = "set the partition before the first insert"; return ST_EINVAL; }
+    t->partitioned = true;
+    t->part_lo = seg_lo;
+    t->part_hi = seg_hi;
+    return ST_OK;
+}
+
+extern "C" int st_combine_upper(st_tree *t, const uint8_t *present16, const uint8_t *hashes17) {
+    CHK(use_device(t));
+    if (t->W != 16 || t->H < 2) { g_err = "combine needs width 16 and height >= 2"; return ST_EINVAL; }
+    uint16_t tg[16];
+    uint4 m[16];
+    for (int b = 0; b < 16; b++) {
+        tg[b] = 0;
+        m[b] = make_uint4(0, 0, 0, 0);
+        if (present16[b]) set_entry_host(tg[b], m[b], hashes17 + 17 * b);
+    }
+    CHK(h2d(t, t->tag + t->base[2], tg, sizeof(tg)));
+    CHK(h2d(t, t->md5 + t->base[2], m, sizeof(m)));
+    DevTree d = view(t);
+    LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, 1u, (const uint8_t *)nullptr);
+    HIPCHK(hipStreamSynchronize(t->stream));
+    t->fresh = false;
     return ST_OK;
 }
 

@@ -141,6 +141,17 @@ class DeviceTree:
         _lib.check(self.L.st_level_entries(self.h, level, _ptr(present), _ptr(hashes)), 'st_level_entries')
         return present, hashes
 
+    # ------------------------------------------------------------ partition
+    def set_partition(self, seg_lo, seg_hi):
+        """Own segments [seg_lo, seg_hi) only (st_set_partition)."""
+        _lib.check(self.L.st_set_partition(self.h, int(seg_lo), int(seg_hi)), 'st_set_partition')
+
+    def combine_upper(self, present16, hashes17):
+        """Store the 16 level-2 entries and recompute level 1 + top (st_combine_upper)."""
+        present16 = np.ascontiguousarray(present16, np.uint8)
+        hashes17 = np.ascontiguousarray(hashes17, np.uint8).reshape(16, 17)
+        _lib.check(self.L.st_combine_upper(self.h, _ptr(present16), _ptr(hashes17)), 'st_combine_upper')
+
     def num_entries(self):
         return int(self.L.st_num_entries(self.h))
 
