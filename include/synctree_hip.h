@@ -140,6 +140,21 @@ int st_top_hash(st_tree *t, uint8_t out17[17], int *present);
  * hashes17[W^(level-1) * 17].  Used for per-level parity checks. */
 int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes17);
 
+/* ---- exchange diff application -------------------
+ * riak_ensemble_exchange.erl:71-97 for one remote peer: compare(local,
+ * remote) with default options, then for each diff in reference order
+ * {K,{'$none',B}} -> insert B; {K,{_, '$none'}} -> nothing; {K,{A,B}} ->
+ * insert B iff valid_obj_hash(B, A) (B >= A, riak_ensemble_peer.erl:1726-1729),
+ * all as ONE batched insert/3 into the local tree.  valid_obj_hash has no
+ * clause unless both hashes start with ?H_OBJ_NONE (0): such a pair is the
+ * exchange's function_clause crash, reported as *crashed = 1 with the diffs
+ * before it (only) applied.  A corrupted node met during the compare returns
+ * ST_CORRUPTED (+ level/bucket/side) and applies nothing (the reference
+ * throws out of compare/3).  n_rejected: inserts refused by path
+ * verification (insert/3 -> corrupted, ignored by the exchange). */
+int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
+                      uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside);
+
 /* ---- multi-GPU: segment-range partition of one tree ------
  * No reference counterpart: riak_ensemble keeps a tree on one node.  This is
  * the sharding of a single huge tree across the GPUs of one node.

@@ -7,10 +7,11 @@
 //
 // Codegen notes (check the .s with -save-temps):
 //  * rotl(x, s) is __builtin_amdgcn_alignbit(x, x, 32 - s)   -> v_alignbit_b32
-//  * F = bfi(b, c, d), G = bfi(d, b, c)                     -> v_bfi_b32
-//  * H = b ^ c ^ d                                           -> v_xor3_b32
-//  * a + F + K + M                                           -> v_add3_u32 + v_add
-//  so a step is ~5 VALU ops; a 64-byte block ~330-360 ops.
+//  * F, G, H, I are one v_bitop3_b32 each (__builtin_amdgcn_bitop3_b32)
+//  * (a + M + K) + F                                        -> v_add3_u32 + v_add_u32
+//  so a step is 5 VALU ops, 14 SIMD cycles per wave64 (add / bitop3 2,
+//  add3 / alignbit 4, measured: profiles/r01_valu_peak.txt); a 64-byte block
+//  ~916 SIMD cycles (k_segment_hash_tiled's loop, ISA count).
 //  * message blocks from global memory are fetched with four unaligned
 //    global_load_dwordx4 (gfx950 runs with unaligned access enabled; hipcc
 //    emits the wide loads for byte pointers) — no shuffling in registers.
@@ -21,13 +22,16 @@
 namespace stmd5 {
 
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
-#define STMD5_F(b, c, d) bfi((b), (c), (d))
-#define STMD5_G(b, c, d) bfi((d), (b), (c))
-#define STMD5_H(b, c, d) ((b) ^ (c) ^ (d))
-#define STMD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
-#define STMD5_STEP(f, a, b, c, d, m, k, s) a = (b) + rotl((a) + f((b), (c), (d)) + ((m) + (k)), (s))
+// The four round functions as single v_bitop3_b32 (gfx950): truth tables
+// over (b, c, d) = (0xF0, 0xCC, 0xAA).  Written as plain and/or/xor the
+// compiler splits F and G into and + andn + two adds (18 SIMD cycles a
+// step instead of 14).
+#define STMD5_F(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xCA)   // (b & c) | (~b & d)
+#define STMD5_G(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xE4)   // (b & d) | (c & ~d)
+#define STMD5_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)   // b ^ c ^ d
+#define STMD5_I(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x39)   // c ^ (b | ~d)
+#define STMD5_STEP(f, a, b, c, d, m, k, s) a = (b) + rotl(((a) + (m) + (k)) + f((b), (c), (d)), (s))
 
 __device__ __forceinline__ void init(uint32_t s[4]) {
     s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;

@@ -798,6 +798,77 @@ __global__ void k_diff_gather(DevTree A, DevTree B, const DiffRec *r, uint64_t n
     }
 }
 
+// ---------------------------------------------------------------------------
+// Diff application (riak_ensemble_exchange.erl:85-97): for every diff record
+// in reference order decide whether the local tree takes the remote value:
+//   {K, {'$none', B}} -> insert B;  {K, {_, '$none'}} -> nothing;
+//   {K, {A, B}}       -> insert B iff valid_obj_hash(B, A), i.e. B >= A as
+//                        Erlang binaries (riak_ensemble_peer.erl:1726-1729).
+// valid_obj_hash has a clause only for two <<?H_OBJ_NONE, _>> hashes: any
+// other pair is a function_clause crash of the exchange, which has applied
+// the diffs before it (list comprehension order) and none after: first_bad
+// records the smallest such index.
+__device__ __forceinline__ bool erl_bin_ge(const uint8_t *x, uint64_t lx, const uint8_t *y, uint64_t ly) {
+    const uint64_t m = lx < ly ? lx : ly;
+    for (uint64_t i = 0; i < m; i++)
+        if (x[i] != y[i]) return x[i] > y[i];
+    return lx >= ly;
+}
+
+__global__ void k_diff_apply_select(DevTree A, DevTree B, const DiffRec *r, uint64_t n, uint8_t *take,
+                                    unsigned long long *first_bad) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const DiffRec d = r[i];
+        bool tk = false;
+        if (d.b != ~0ull) {
+            if (d.a == ~0ull) {
+                tk = true;
+            } else {
+                const uint8_t *va = A.vheap + A.voff[d.a], *vb = B.vheap + B.voff[d.b];
+                const uint64_t la = A.voff[d.a + 1] - A.voff[d.a], lb = B.voff[d.b + 1] - B.voff[d.b];
+                if (la == 0 || lb == 0 || va[0] != 0 || vb[0] != 0)
+                    atomicMin(first_bad, (unsigned long long)i);
+                else
+                    tk = erl_bin_ge(vb, lb, va, la);
+            }
+        }
+        take[i] = tk ? 1 : 0;
+    }
+}
+
+// Lengths of the records to insert (0 for skipped diffs and for every diff at
+// or after the first crash), n + 1 entries with a zero terminator.
+__global__ void k_diff_apply_lengths(DevTree B, const DiffRec *r, uint64_t n, const uint8_t *take,
+                                     const unsigned long long *first_bad, uint64_t *one, uint64_t *kl, uint64_t *vl) {
+    const unsigned long long fb = *first_bad;
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        const bool tk = i < n && i < fb && take[i];
+        one[i] = tk ? 1 : 0;
+        if (tk) {
+            const DiffRec d = r[i];
+            kl[i] = B.koff[d.b + 1] - B.koff[d.b];
+            vl[i] = B.voff[d.b + 1] - B.voff[d.b];
+        } else {
+            kl[i] = vl[i] = 0;
+        }
+    }
+}
+
+// Pack the taken remote entries as an ingest batch (key records + values).
+__global__ void k_diff_apply_gather(DevTree B, const DiffRec *r, uint64_t n, const uint64_t *pos, const uint64_t *ko,
+                                    const uint64_t *vo, uint8_t *kheap, uint64_t *koff, uint8_t *vheap, uint64_t *voff) {
+    for (uint64_t i = gtid(); i <= n; i += gstride()) {
+        const uint64_t p = pos[i];
+        if (i == n) { koff[p] = ko[n]; voff[p] = vo[n]; break; }
+        if (pos[i + 1] == p) continue;   // not taken
+        const DiffRec d = r[i];
+        koff[p] = ko[i];
+        voff[p] = vo[i];
+        copy_bytes(kheap + ko[i], B.kheap + B.koff[d.b], B.koff[d.b + 1] - B.koff[d.b]);
+        copy_bytes(vheap + vo[i], B.vheap + B.voff[d.b], B.voff[d.b + 1] - B.voff[d.b]);
+    }
+}
+
 // Gather entries by index list (get results / segment images) into packed heaps.
 __global__ void k_entry_lengths(DevTree t, const uint64_t *idx, uint64_t n, uint64_t *kl, uint64_t *vl) {
     for (uint64_t i = gtid(); i <= n; i += gstride()) {
@@ -1830,4 +1901,114 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
         reg = A;
     }
 #undef FLOW_STAMP
+}
+
+// K1 variants over the same tiles (A/B, env ST_K1T):
+//  1: persistent waves, grid-stride over tiles; the next tile's info and first
+//     block are fetched while the current tile's last block is hashed.
+//  2: two adjacent tiles per wave (2 x 64 segments), their MD5 chains
+//     interleaved in every lane (ILP 2).
+__device__ __forceinline__ void tile_store(const DevTree &t, uint32_t seg, uint32_t nb, const uint32_t st[4]) {
+    if (seg == 0xffffffffu) return;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t slot = t.base[L1] + seg;
+    if (!nb) {
+        t.tag[slot] = 0;
+        if (L1 == 1) t.tag[0] = 0;
+        return;
+    }
+    const uint4 e = make_uint4(st[0], st[1], st[2], st[3]);
+    t.md5[slot] = e;
+    t.tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+}
+
+__global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, const TileInfo *__restrict__ tinfo,
+                                                              const uint32_t *__restrict__ tseg,
+                                                              const uint32_t *__restrict__ tnb,
+                                                              const uint4 *__restrict__ tiles, uint64_t ntiles) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    uint64_t tl = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tl >= ntiles) return;
+    TileInfo ti = tinfo[tl];
+    uint32_t seg = tseg[tl * 64 + lane], nb = tnb[tl * 64 + lane];
+    uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
+    if (ti.B) {
+        const uint4 *b = tiles + ti.base + lane;
+        n0 = b[0]; n1 = b[64]; n2 = b[128]; n3 = b[192];
+    }
+    for (;;) {
+        const uint64_t nx = tl + nw;
+        TileInfo tn;
+        tn.base = 0; tn.B = 0; tn.pad = 0;
+        uint32_t segn = 0xffffffffu, nbn = 0;
+        if (nx < ntiles) {
+            tn = tinfo[nx];
+            segn = tseg[nx * 64 + lane];
+            nbn = tnb[nx * 64 + lane];
+        }
+        uint32_t st[4];
+        stmd5::init(st);
+        const uint4 *b = tiles + ti.base + lane;
+        for (uint32_t k = 0; k < ti.B; k++) {
+            uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
+            if (k + 1 < ti.B) {
+                const uint4 *q = b + 256 * (k + 1);
+                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+            } else if (tn.B) {
+                const uint4 *q = tiles + tn.base + lane;
+                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+            }
+            if (k < nb) stmd5::compress(st, m);
+        }
+        tile_store(t, seg, nb, st);
+        if (nx >= ntiles) break;
+        if (ti.B == 0 && tn.B) {
+            const uint4 *q = tiles + tn.base + lane;
+            n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+        }
+        tl = nx;
+        ti = tn;
+        seg = segn;
+        nb = nbn;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_segment_hash_tiled_x2(DevTree t, const TileInfo *__restrict__ tinfo,
+                                                              const uint32_t *__restrict__ tseg,
+                                                              const uint32_t *__restrict__ tnb,
+                                                              const uint4 *__restrict__ tiles, uint64_t ntiles) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * 2, t1 = t0 + 1;
+    const bool has1 = t1 < ntiles;
+    const TileInfo i0 = tinfo[t0];
+    TileInfo i1;
+    i1.base = 0; i1.B = 0; i1.pad = 0;
+    if (has1) i1 = tinfo[t1];
+    const uint32_t s0 = tseg[t0 * 64 + lane], b0 = tnb[t0 * 64 + lane];
+    const uint32_t s1 = has1 ? tseg[t1 * 64 + lane] : 0xffffffffu, b1 = has1 ? tnb[t1 * 64 + lane] : 0u;
+    const uint32_t B = i0.B > i1.B ? i0.B : i1.B;
+    uint32_t st0[4], st1[4];
+    stmd5::init(st0);
+    stmd5::init(st1);
+    const uint4 *p0 = tiles + i0.base + lane, *p1 = tiles + i1.base + lane;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 a0 = z, a1 = z, a2 = z, a3 = z, c0 = z, c1 = z, c2 = z, c3 = z;
+    if (i0.B) { a0 = p0[0]; a1 = p0[64]; a2 = p0[128]; a3 = p0[192]; }
+    if (i1.B) { c0 = p1[0]; c1 = p1[64]; c2 = p1[128]; c3 = p1[192]; }
+    for (uint32_t k = 0; k < B; k++) {
+        uint32_t m0[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+        uint32_t m1[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        if (k + 1 < i0.B) { const uint4 *q = p0 + 256 * (k + 1); a0 = q[0]; a1 = q[64]; a2 = q[128]; a3 = q[192]; }
+        if (k + 1 < i1.B) { const uint4 *q = p1 + 256 * (k + 1); c0 = q[0]; c1 = q[64]; c2 = q[128]; c3 = q[192]; }
+        uint32_t u0[4] = {st0[0], st0[1], st0[2], st0[3]}, u1[4] = {st1[0], st1[1], st1[2], st1[3]};
+        stmd5::compress(u0, m0);
+        stmd5::compress(u1, m1);
+        const bool g0 = k < b0, g1 = k < b1;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { st0[i] = g0 ? u0[i] : st0[i]; st1[i] = g1 ? u1[i] : st1[i]; }
+    }
+    tile_store(t, s0, b0, st0);
+    tile_store(t, s1, b1, st1);
 }

@@ -451,8 +451,21 @@ static int ensure_tiles(st_tree *t) {
 static int rehash_tiled(st_tree *t) {
     CHK(ensure_tiles(t));
     DevTree d = view(t);
-    LAUNCH(t, "segment_hash", k_segment_hash_tiled, (uint32_t)num_tiles(t), 64, 0, d, (const TileInfo *)t->tinfo,
-           (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
+    // K1 variant (env ST_K1T, A/B knob): 1 = persistent waves with cross-tile
+    // prefetch (default; 1024 workgroups x 4 waves), 0 = one wave per tile,
+    // 2 = two tiles per wave interleaved (ILP 2).
+    static const int k1t = getenv("ST_K1T") ? atoi(getenv("ST_K1T")) : 1;
+    static const uint32_t k1wgs = getenv("ST_K1_WGS") ? (uint32_t)atoi(getenv("ST_K1_WGS")) : 1024u;
+    const uint64_t ntl = num_tiles(t);
+    if (k1t == 1)
+        LAUNCH(t, "segment_hash", k_segment_hash_tiled_p, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, k1wgs), 256, 0, d,
+               (const TileInfo *)t->tinfo, (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles, ntl);
+    else if (k1t == 2)
+        LAUNCH(t, "segment_hash", k_segment_hash_tiled_x2, (uint32_t)((ntl + 1) / 2), 64, 0, d, (const TileInfo *)t->tinfo,
+               (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles, ntl);
+    else
+        LAUNCH(t, "segment_hash", k_segment_hash_tiled, (uint32_t)ntl, 64, 0, d, (const TileInfo *)t->tinfo,
+               (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         if (!t->lvl_cnt) {
@@ -1564,6 +1577,94 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
     }
     HIPCHK(hipStreamSynchronize(local->stream));
     return status;
+}
+
+// Exchange diff application (riak_ensemble_exchange.erl:71-97): compare the
+// local tree against the remote one (K3, default options), then insert into
+// the local tree, with insert/3 semantics, every remote value the exchange
+// would take (k_diff_apply_*), as ONE device batch instead of one
+// peer_tree:insert gen_server call per diff.
+extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
+                                 uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
+    CHK(use_device(local));
+    *n_diffs = 0;
+    *n_applied = 0;
+    *n_rejected = 0;
+    *crashed = 0;
+    CompareOut co;
+    int status = ST_OK;
+    CHK(compare_core(local, remote, ST_FILTER_ALL, co, clevel, cbucket, cside, &status));
+    *n_diffs = co.n;
+    if (status != ST_OK || !co.rec || co.n == 0) {
+        if (co.rec) dfree(local, co.rec);
+        HIPCHK(hipStreamSynchronize(local->stream));
+        return status;
+    }
+    st_tree *t = local;
+    const uint64_t n = co.n;
+    DevTree da = view(local), db = view(remote);
+    uint8_t *take = nullptr, *kh = nullptr, *vh = nullptr;
+    unsigned long long *fb = nullptr;
+    uint64_t *one = nullptr, *kl = nullptr, *vl = nullptr, *pos = nullptr, *ko = nullptr, *vo = nullptr, *bko = nullptr,
+             *bvo = nullptr;
+    uint32_t *dcl = nullptr;
+    int r = ST_OK;
+    auto done = [&]() {
+        void *ps[] = {take, kh, vh, fb, one, kl, vl, pos, ko, vo, bko, bvo, dcl, co.rec};
+        for (void *p : ps) dfree(t, p);
+    };
+#define XCHK(x)                               \
+    do {                                      \
+        r = (x);                              \
+        if (r != ST_OK) { done(); return r; } \
+    } while (0)
+    XCHK(dalloc_t(t, &take, n));
+    XCHK(dalloc_t(t, &fb, 1));
+    XCHK(dalloc_t(t, &one, n + 1));
+    XCHK(dalloc_t(t, &kl, n + 1));
+    XCHK(dalloc_t(t, &vl, n + 1));
+    XCHK(dalloc_t(t, &pos, n + 1));
+    XCHK(dalloc_t(t, &ko, n + 1));
+    XCHK(dalloc_t(t, &vo, n + 1));
+    HIPCHK(hipMemsetAsync(fb, 0xff, 8, t->stream));
+    LAUNCH(t, "diff_apply", k_diff_apply_select, grid_for(n), 256, 0, da, db, (const DiffRec *)co.rec, n, take, fb);
+    LAUNCH(t, "diff_apply", k_diff_apply_lengths, grid_for(n + 1), 256, 0, db, (const DiffRec *)co.rec, n,
+           (const uint8_t *)take, (const unsigned long long *)fb, one, kl, vl);
+    XCHK(exclusive_scan<uint64_t>(t, one, pos, n + 1));
+    XCHK(exclusive_scan<uint64_t>(t, kl, ko, n + 1));
+    XCHK(exclusive_scan<uint64_t>(t, vl, vo, n + 1));
+    uint64_t tot[3] = {0, 0, 0};
+    unsigned long long hfb = 0;
+    HIPCHK(hipMemcpyAsync(&tot[0], pos + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[1], ko + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[2], vo + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&hfb, fb, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    *crashed = hfb != ~0ull ? 1 : 0;
+    const uint64_t m = tot[0];
+    if (m) {
+        XCHK(dalloc(t, (void **)&kh, tot[1] + HEAP_SLACK));
+        XCHK(dalloc(t, (void **)&vh, tot[2] + HEAP_SLACK));
+        XCHK(dalloc_t(t, &bko, m + 1));
+        XCHK(dalloc_t(t, &bvo, m + 1));
+        XCHK(dalloc_t(t, &dcl, m));
+        LAUNCH(t, "diff_apply", k_diff_apply_gather, grid_for(n + 1), 256, 0, db, (const DiffRec *)co.rec, n,
+               (const uint64_t *)pos, (const uint64_t *)ko, (const uint64_t *)vo, kh, bko, vh, bvo);
+        IngestIn in{};
+        in.n = m; in.krec = kh; in.koff = bko; in.vheap = vh; in.voff = bvo;
+        in.verify_rehash = true; in.clevel_out = dcl;
+        XCHK(ingest(t, in));
+        std::vector<uint32_t> cl(m);
+        XCHK(d2h(t, cl.data(), dcl, m * 4));
+        uint64_t rej = 0;
+        for (uint64_t i = 0; i < m; i++) rej += cl[i] != 0;
+        *n_rejected = rej;
+        *n_applied = m - rej;
+    }
+    done();
+#undef XCHK
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
 }
 
 extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,

@@ -258,6 +258,22 @@ class DeviceTree:
             return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
         return int(nd.value)
 
+    def exchange_apply(self, remote):
+        """riak_ensemble_exchange.erl:71-97 against one remote tree, as one
+        device batch (st_exchange_apply).  Returns ('ok', info),
+        ('exchange_failed', info) for the valid_obj_hash function_clause
+        crash (diffs before it applied), or ('corrupted', side, tuple) when
+        the compare meets a corrupted node (nothing applied)."""
+        nd, na, nr, cr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        cl, cb, cs = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int()
+        rc = _lib.check(self.L.st_exchange_apply(self.h, remote.h, ctypes.byref(nd), ctypes.byref(na), ctypes.byref(nr),
+                                                 ctypes.byref(cr), ctypes.byref(cl), ctypes.byref(cb), ctypes.byref(cs)),
+                        'st_exchange_apply')
+        if rc == _lib.ST_CORRUPTED:
+            return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
+        info = {'diffs': int(nd.value), 'applied': int(na.value), 'rejected': int(nr.value)}
+        return ('exchange_failed' if cr.value else 'ok', info)
+
     # ------------------------------------------------------------ timing
     def set_timing(self, on=True):
         _lib.check(self.L.st_set_timing(self.h, 1 if on else 0), 'st_set_timing')
