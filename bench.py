@@ -31,15 +31,15 @@ sys.path.insert(0, ROOT)
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec.
 # Integer VALU, measured on gfx950 (tools/microbench/valu_peak.cpp,
-# profiles/r01_valu_peak.txt): v_add_u32 / v_xor_b32 / v_bitop3_b32 issue a
-# wave64 in 2 SIMD cycles, v_add3_u32 / v_alignbit_b32 in 4.  The MD5 block
-# loop of k_segment_hash_perm (ISA dump) is 100 add +
-# 48 bitop3 + 32 and + 29 xor + ~10 moves (2 cyc) and 97 add3 + 64 alignbit
-# (4 cyc) = 1082 SIMD cycles per wave = 16.9 SIMD-cycles per 64-B block.
+# profiles/r01_valu_peak.txt): v_add_u32 / v_bitop3_b32 issue a wave64 in 2
+# SIMD cycles, v_add3_u32 / v_alignbit_b32 in 4.  The MD5 block loop of
+# k_segment_hash_tiled (ISA count) is 130 add + 64 bitop3
+# (2 cyc) and 65 add3 + 64 alignbit (4 cyc) = 916 SIMD cycles per wave =
+# 14.3 SIMD-cycles per 64-B block.
 HBM_PEAK_GBS = 8000.0
 SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9
-MD5_SIMD_CYCLES_PER_BLOCK = 1082.0 / 64
+MD5_SIMD_CYCLES_PER_BLOCK = 916.0 / 64
 # HBM bytes of one K1 launch from rocprofv3 PMC (profiles/r01_pmc_k1_session2.txt):
 # (FETCH_SIZE + WRITE_SIZE) x 1 KiB, averaged over 12 launches.  No x2
 # correction: K1's reads are per-lane 16-B loads of scattered segments (not the
@@ -64,7 +64,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--keys', type=int, default=10_000_000)
     ap.add_argument('--no-cpu', action='store_true', help='skip the CPU baseline leg')
-    ap.add_argument('--no-extras', action='store_true', help='skip build/compare legs')
+    ap.add_argument('--no-extras', action='store_true', help='skip build/compare/ensemble legs')
+    ap.add_argument('--ensembles', type=int, default=32, help='config-4 leg: ensembles (trees) per GPU')
+    ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
     args = ap.parse_args()
 
     import torch
@@ -131,10 +133,9 @@ def main():
     # cross-GPU combine of the ensembles' top hashes (RCCL all-gather, untimed)
     tops_ok = True
     if dist:
-        mine = torch.frombuffer(bytearray(top0), dtype=torch.uint8).to(dev)
-        allt = torch.empty(world * 17, dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(allt, mine)
-        tops_ok = bytes(allt[rank * 17:(rank + 1) * 17].cpu().numpy()) == top0
+        from riak_ensemble_amd import parallel
+        tops = parallel.gather_tops(dist, [top0], device=dev)
+        tops_ok = len(tops) == world and tops[rank] == top0
 
     ms_per_step = el * 1000.0 / args.steps
     value = world * n * args.steps / el
@@ -175,7 +176,7 @@ def main():
         roof = {'bound': 'hbm' if t_hbm >= t_valu else 'valu', 'achieved': round(achieved_gbs, 1),
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
                 'traffic': K1_PMC_TRAFFIC_BYTES,
-                'kernel': 'k_segment_hash_tiled (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
+                'kernel': 'k_segment_hash_tiled_p (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
                 'bytes_per_launch': k1_bytes, 'tile_bytes_per_launch': 64 * seg_blocks, 'md5_blocks_per_launch': blocks,
                 't_min_hbm_us': round(t_hbm * 1e6, 2),
                 'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),
@@ -198,6 +199,9 @@ def main():
         if not args.no_extras:
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, local, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_h, vals_h, keys_d, vals_d, n, local, torch)
+            del keys_d, vals_d
+            tree.close()
+            out['ensembles'] = _bench_ensembles(synctree_hip, workload, args.ensembles, args.ensemble_keys, local, torch)
         if not args.no_cpu:
             out['cpu_baseline'] = _cpu_baseline(keys_h, vals_h, top0)
     if dist:
@@ -256,12 +260,73 @@ def _bench_compare(synctree_hip, tree_a, keys_h, vals_h, keys_d, vals_d, n, loca
     res = tree_a.compare(tb)
     dt_host = time.perf_counter() - t0
     assert res[0] == 'ok' and len(res[1]) == len(segs)
+    # (B's bumped FIRST byte is the ?H_OBJ_NONE prefix: the reference exchange
+    # would crash in valid_obj_hash on these diffs, and so does ours)
+    assert tree_a.exchange_apply(tb)[0] == 'exchange_failed'
     tb.close()
+    # riak_ensemble_exchange.erl:71-97 as one device batch: B2 = A with the
+    # same keys' Seq advanced (last byte + 1, so B2 > A: valid_obj_hash holds);
+    # compare + apply into a fresh copy of A, which then equals B2
+    mut2 = [(k, v[:-1] + bytes([v[-1] + 1])) for k, v in
+            ((img[0][0], img[0][1]) for img in imgs) if v[-1] < 255]
+    tb2 = synctree_hip.DeviceTree(device=local)
+    tb2.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    tb2.insert_batch([k for k, _ in mut2], [v for _, v in mut2])
+    ta = synctree_hip.DeviceTree(device=local)
+    ta.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res_apply = ta.exchange_apply(tb2)
+    torch.cuda.synchronize()
+    dt_apply = time.perf_counter() - t0
+    assert res_apply[0] == 'ok' and res_apply[1]['applied'] == len(mut2), res_apply
+    assert ta.top_hash() == tb2.top_hash(), 'exchange did not converge the trees'
+    ta.close()
+    tb2.close()
     return {'tree_compares_per_s': round(1.0 / dt, 1), 'ms_per_compare': round(dt * 1e3, 4),
             'diff_keys': nd, 'diff_keys_per_s': round(nd / dt, 1),
             'ms_per_compare_incl_d2h_records': round(dt_host * 1e3, 4),
+            'exchange_apply_ms': round(dt_apply * 1e3, 4),
+            'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
+                              'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),
             'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 with per-node '
                     'self-verification, diff records materialised on device'}
+
+
+def _bench_ensembles(synctree_hip, workload, E, nk, local, torch, reps=10):
+    """Config 4 shape on one GPU: E independent ensembles x nk keys (keys
+    seeded SEED ^ e), all rehashed as ONE batch (st_rehash_group) vs one
+    st_rehash per tree."""
+    trees = []
+    for e in range(E):
+        k = torch.from_numpy(workload.keys_int63(nk, workload.SEED ^ (e + 1))).to(torch.device('cuda', local))
+        v = torch.from_numpy(workload.obj_hash_values(nk)).to(k.device)
+        t = synctree_hip.DeviceTree(device=local)
+        t.insert_int64_device(k.data_ptr(), v.data_ptr(), nk, 17)
+        trees.append(t)
+    torch.cuda.synchronize()
+    tops = [t.top_hash() for t in trees]
+    synctree_hip.rehash_group(trees)
+    assert [t.top_hash() for t in trees] == tops
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        synctree_hip.rehash_group(trees)
+    torch.cuda.synchronize()
+    dt_g = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for t in trees:
+            t.rehash()
+    for t in trees:
+        t.sync()
+    dt_s = (time.perf_counter() - t0) / reps
+    assert [t.top_hash() for t in trees] == tops
+    for t in trees:
+        t.close()
+    return {'keys_per_s': round(E * nk / dt_g, 1), 'ms_per_batch': round(dt_g * 1e3, 4),
+            'per_tree_rehash_keys_per_s': round(E * nk / dt_s, 1), 'ensembles': E, 'keys_per_ensemble': nk,
+            'what': 'config4 shape per GPU: %d ensembles x %d keys rehashed as one st_rehash_group batch '
+                    '(K1 over all trees\' tiles + one level-dataflow launch), vs st_rehash per tree' % (E, nk)}
 
 
 def _cpu_baseline(keys_h, vals_h, top0, reps=2):

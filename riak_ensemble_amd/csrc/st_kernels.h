@@ -1648,6 +1648,18 @@ struct TileInfo {
     uint32_t pad;
 };
 
+// Per-tree pointers of a batched (multi-tree) rehash: trees of one geometry,
+// e.g. the ensembles one GPU hosts.
+struct TreeTiles {
+    uint4 *md5;
+    uint16_t *tag;
+    uint32_t *cnt;
+    const TileInfo *tinfo;
+    const uint32_t *tseg, *tnb;
+    const uint4 *tiles;
+};
+
+
 // One workgroup per tile: write the padded messages in tiled order.
 __global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ seg_voff, const uint8_t *__restrict__ vheap,
                                                    const uint32_t *__restrict__ tseg, const uint64_t *__restrict__ tbase,
@@ -1908,67 +1920,77 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
 //     block are fetched while the current tile's last block is hashed.
 //  2: two adjacent tiles per wave (2 x 64 segments), their MD5 chains
 //     interleaved in every lane (ILP 2).
-__device__ __forceinline__ void tile_store(const DevTree &t, uint32_t seg, uint32_t nb, const uint32_t st[4]) {
+__device__ __forceinline__ void tile_store(const DevTree &t, uint4 *md5, uint16_t *tag, uint32_t seg, uint32_t nb,
+                                           const uint32_t st[4]) {
     if (seg == 0xffffffffu) return;
     const uint32_t L1 = t.H + 1;
     const uint64_t slot = t.base[L1] + seg;
     if (!nb) {
-        t.tag[slot] = 0;
-        if (L1 == 1) t.tag[0] = 0;
+        tag[slot] = 0;
+        if (L1 == 1) tag[0] = 0;
         return;
     }
     const uint4 e = make_uint4(st[0], st[1], st[2], st[3]);
-    t.md5[slot] = e;
-    t.tag[slot] = TAG_PRESENT;
-    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+    md5[slot] = e;
+    tag[slot] = TAG_PRESENT;
+    if (L1 == 1) { md5[0] = e; tag[0] = TAG_PRESENT; }
 }
 
-__global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, const TileInfo *__restrict__ tinfo,
-                                                              const uint32_t *__restrict__ tseg,
-                                                              const uint32_t *__restrict__ tnb,
-                                                              const uint4 *__restrict__ tiles, uint64_t ntiles) {
+// Persistent K1: wave w hashes global tiles w, w + nw, ...; GROUP: global
+// tile g is tile g % ntpt of tree g / ntpt (trees[]), else all tiles belong
+// to `one`.
+template <bool GROUP>
+__global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTiles one, const TreeTiles *__restrict__ trees,
+                                                              uint64_t ntpt, uint64_t ntiles) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * 4;
-    uint64_t tl = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tl >= ntiles) return;
-    TileInfo ti = tinfo[tl];
-    uint32_t seg = tseg[tl * 64 + lane], nb = tnb[tl * 64 + lane];
+    uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= ntiles) return;
+    TreeTiles cur = GROUP ? trees[g / ntpt] : one;
+    uint64_t tl = GROUP ? g % ntpt : g;
+    TileInfo ti = cur.tinfo[tl];
+    uint32_t seg = cur.tseg[tl * 64 + lane], nb = cur.tnb[tl * 64 + lane];
     uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
     if (ti.B) {
-        const uint4 *b = tiles + ti.base + lane;
+        const uint4 *b = cur.tiles + ti.base + lane;
         n0 = b[0]; n1 = b[64]; n2 = b[128]; n3 = b[192];
     }
     for (;;) {
-        const uint64_t nx = tl + nw;
+        const uint64_t gx = g + nw;
+        TreeTiles nxt = cur;
+        uint64_t tn_l = 0;
         TileInfo tn;
         tn.base = 0; tn.B = 0; tn.pad = 0;
         uint32_t segn = 0xffffffffu, nbn = 0;
-        if (nx < ntiles) {
-            tn = tinfo[nx];
-            segn = tseg[nx * 64 + lane];
-            nbn = tnb[nx * 64 + lane];
+        if (gx < ntiles) {
+            if (GROUP) nxt = trees[gx / ntpt];
+            tn_l = GROUP ? gx % ntpt : gx;
+            tn = nxt.tinfo[tn_l];
+            segn = nxt.tseg[tn_l * 64 + lane];
+            nbn = nxt.tnb[tn_l * 64 + lane];
         }
         uint32_t st[4];
         stmd5::init(st);
-        const uint4 *b = tiles + ti.base + lane;
+        const uint4 *b = cur.tiles + ti.base + lane;
         for (uint32_t k = 0; k < ti.B; k++) {
             uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
             if (k + 1 < ti.B) {
                 const uint4 *q = b + 256 * (k + 1);
                 n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
             } else if (tn.B) {
-                const uint4 *q = tiles + tn.base + lane;
+                const uint4 *q = nxt.tiles + tn.base + lane;
                 n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
             }
             if (k < nb) stmd5::compress(st, m);
         }
-        tile_store(t, seg, nb, st);
-        if (nx >= ntiles) break;
+        tile_store(t, cur.md5, cur.tag, seg, nb, st);
+        if (gx >= ntiles) break;
         if (ti.B == 0 && tn.B) {
-            const uint4 *q = tiles + tn.base + lane;
+            const uint4 *q = nxt.tiles + tn.base + lane;
             n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
         }
-        tl = nx;
+        g = gx;
+        cur = nxt;
         ti = tn;
         seg = segn;
         nb = nbn;
@@ -2009,6 +2031,22 @@ __global__ void __launch_bounds__(64) k_segment_hash_tiled_x2(DevTree t, const T
 #pragma unroll
         for (int i = 0; i < 4; i++) { st0[i] = g0 ? u0[i] : st0[i]; st1[i] = g1 ? u1[i] : st1[i]; }
     }
-    tile_store(t, s0, b0, st0);
-    tile_store(t, s1, b1, st1);
+    tile_store(t, t.md5, t.tag, s0, b0, st0);
+    tile_store(t, t.md5, t.tag, s1, b1, st1);
+}
+
+// One inner level of a batch of trees (W == 16): node i is node i % per of
+// tree i / per.  Throughput form for many trees: every lane hashes one node
+// from global memory at full occupancy (st_rehash_group).
+__global__ void __launch_bounds__(64) k_level16_group(DevTree g, const TreeTiles *__restrict__ trees, uint32_t l,
+                                                      uint64_t per, uint64_t total) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
+    for (uint64_t i = gtid(); i < total; i += gstride()) {
+        DevTree t = g;
+        const TreeTiles &tt = trees[i / per];
+        t.md5 = tt.md5;
+        t.tag = tt.tag;
+        hash_node16(t, l, i % per, reg);
+    }
 }

@@ -444,6 +444,25 @@ static int ensure_tiles(st_tree *t) {
     return ST_OK;
 }
 
+static TreeTiles tree_tiles(const st_tree *t) {
+    TreeTiles x;
+    x.md5 = t->md5;
+    x.tag = t->tag;
+    x.cnt = t->lvl_cnt;
+    x.tinfo = t->tinfo;
+    x.tseg = t->tseg;
+    x.tnb = t->tnb;
+    x.tiles = t->tiles;
+    return x;
+}
+
+static int ensure_lvl_cnt(st_tree *t) {
+    if (t->lvl_cnt || t->H < 3) return ST_OK;
+    CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
+    HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
+    return ST_OK;
+}
+
 // Full rehash, default strategy: K1 k_segment_hash_tiled over the global
 // block-count tiles, then (W == 16, H >= 3) every inner level and the top hash
 // in ONE launch of k_levels_flow16 (levels H..H-2 per workgroup, the rest by
@@ -458,8 +477,8 @@ static int rehash_tiled(st_tree *t) {
     static const uint32_t k1wgs = getenv("ST_K1_WGS") ? (uint32_t)atoi(getenv("ST_K1_WGS")) : 1024u;
     const uint64_t ntl = num_tiles(t);
     if (k1t == 1)
-        LAUNCH(t, "segment_hash", k_segment_hash_tiled_p, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, k1wgs), 256, 0, d,
-               (const TileInfo *)t->tinfo, (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles, ntl);
+        LAUNCH(t, "segment_hash", k_segment_hash_tiled_p<false>, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, k1wgs), 256, 0, d,
+               tree_tiles(t), (const TreeTiles *)nullptr, ntl, ntl);
     else if (k1t == 2)
         LAUNCH(t, "segment_hash", k_segment_hash_tiled_x2, (uint32_t)((ntl + 1) / 2), 64, 0, d, (const TileInfo *)t->tinfo,
                (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles, ntl);
@@ -468,10 +487,7 @@ static int rehash_tiled(st_tree *t) {
                (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
-        if (!t->lvl_cnt) {
-            CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
-            HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
-        }
+        CHK(ensure_lvl_cnt(t));
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         // a partition hashes only its own level-(H-2) subtrees (4096 segments
         // each) and stops at level 2; st_combine_upper finishes level 1 + top
@@ -1054,6 +1070,58 @@ extern "C" int st_rehash(st_tree *t, int upper) {
     else CHK(rehash_all(t, nullptr));
     t->fresh = false;
     return ST_OK;
+}
+
+// rehash/1 of n trees of one geometry (W == 16, H >= 3) as one batch: K1
+// over every tree's tiles (persistent waves, global tile index = tree x
+// tiles-per-tree + tile), then one k_level16_group launch per level over
+// every tree's nodes at full occupancy.  The latency-bound level chain is
+// paid once per batch instead of once per tree, and the level work runs as
+// throughput (many ensembles per GPU).
+extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
+    if (n == 0) return ST_OK;
+    st_tree *t = trees[0];
+    CHK(use_device(t));
+    for (uint32_t i = 0; i < n; i++) {
+        st_tree *u = trees[i];
+        if (u->W != 16 || u->H < 3 || u->S != t->S || u->device != t->device || u->partitioned || rehash_mode() != 2) {
+            g_err = "group rehash needs unpartitioned width-16 trees of one geometry (height >= 3) on one device";
+            return ST_EINVAL;
+        }
+        for (uint32_t j = 0; j < i; j++)
+            if (trees[j] == u) { g_err = "a tree appears twice in the group"; return ST_EINVAL; }
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        CHK(ensure_tiles(trees[i]));
+        HIPCHK(hipStreamSynchronize(trees[i]->stream));
+    }
+    std::vector<TreeTiles> h(n);
+    for (uint32_t i = 0; i < n; i++) h[i] = tree_tiles(trees[i]);
+    TreeTiles *dtt = nullptr;
+    CHK(dalloc_t(t, &dtt, n));
+    HIPCHK(hipMemcpyAsync(dtt, h.data(), n * sizeof(TreeTiles), hipMemcpyHostToDevice, t->stream));
+    DevTree d = view(t);
+    const uint64_t ntpt = num_tiles(t);
+    int r = ST_OK;
+    do {
+        // 7 waves per SIMD (1792 x 4 waves): small trees have mostly 1-block
+        // tiles, so the per-tile load chain, not MD5, bounds the batch
+        hipLaunchKernelGGL((k_segment_hash_tiled_p<true>), dim3((uint32_t)std::min<uint64_t>((ntpt * n + 3) / 4, 1792)),
+                           dim3(256), 0, t->stream, d, h[0], (const TreeTiles *)dtt, ntpt, ntpt * n);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) { g_err = std::string("launch segment_hash group: ") + hipGetErrorString(e); r = ST_EDEVICE; break; }
+        for (uint32_t l = t->H; l >= 1 && r == ST_OK; l--) {
+            const uint64_t per = t->base[l + 1] - t->base[l];
+            hipLaunchKernelGGL(k_level16_group, dim3(grid_for(per * n, 64, 65536)), dim3(64),
+                               (size_t)64 * lane_region_bytes(16), t->stream, d, (const TreeTiles *)dtt, l, per, per * n);
+            e = hipGetLastError();
+            if (e != hipSuccess) { g_err = std::string("launch level_rehash group: ") + hipGetErrorString(e); r = ST_EDEVICE; }
+        }
+    } while (0);
+    dfree(t, dtt);
+    HIPCHK(hipStreamSynchronize(t->stream));
+    for (uint32_t i = 0; i < n; i++) trees[i]->fresh = false;
+    return r;
 }
 
 extern "C" int st_verify(st_tree *t, int upper, int *ok) {

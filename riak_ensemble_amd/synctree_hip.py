@@ -323,3 +323,13 @@ def store_batch(updates, state):
         if u[0] == 'delete':
             state.delete_node(u[1][0], u[1][1])
     return state
+
+
+def rehash_group(trees):
+    """rehash/1 of every tree in `trees` (one geometry, one device) as one
+    device batch (st_rehash_group): ensembles sharded onto one GPU."""
+    if not trees:
+        return
+    L = trees[0].L
+    arr = (ctypes.c_void_p * len(trees))(*[t.h.value for t in trees])
+    _lib.check(L.st_rehash_group(arr, len(trees)), 'st_rehash_group')

@@ -217,3 +217,43 @@ def test_partition_rejects_bad_ranges():
     t.set_partition(0, 1 << 19)
     with pytest.raises(Exception):
         t.rehash(upper=True)
+
+
+@pytest.mark.gpu
+def test_group_rehash_parity():
+    """Ensemble sharding on one GPU: st_rehash_group over trees of different
+    sizes (incl. an empty one and a corrupted-then-rehashed one) == per-tree
+    rehash == the oracle."""
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip
+    sizes = [0, 1, 1000, 50_000, 200_000, 7]
+    trees, oracles = [], []
+    for e, n in enumerate(sizes):
+        keys = workload.keys_int63(n, workload.SEED ^ e) if n else np.zeros(0, np.int64)
+        vals = workload.obj_hash_values(n)
+        t = synctree_hip.DeviceTree()
+        if n:
+            t.insert_int64(keys, vals)
+        trees.append(t)
+        oracles.append(C.OTree().bulk_load_int64(keys, vals) if n else C.OTree())
+    # stale inner state in one tree: a raw segment store without rehash
+    seg = int(np.nonzero(oracles[3].level_entries(6)[0])[0][5])
+    node = oracles[3].node(6, seg)
+    bad = [(node[0][0], b'\x00' + bytes(16))] + node[1:]
+    trees[3].store_node(6, seg, bad)
+    oracles[3].store_segment(seg, bad)
+    oracles[3].rehash()
+    synctree_hip.rehash_group(trees)
+    for t, o in zip(trees, oracles):
+        assert t.top_hash() == o.top_hash()
+        for lvl in (2, 5, 6):
+            pa, ha = t.level_entries(lvl)
+            pb, hb = o.level_entries(lvl)
+            assert (pa == pb).all() and (ha == hb).all()
+        assert t.verify()
+    # twice in a row (self-resetting counters) and against the single-tree path
+    synctree_hip.rehash_group(trees[::-1])
+    tops = [t.top_hash() for t in trees]
+    for t in trees:
+        t.rehash()
+    assert [t.top_hash() for t in trees] == tops
