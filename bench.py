@@ -40,12 +40,13 @@ HBM_PEAK_GBS = 8000.0
 SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9
 MD5_SIMD_CYCLES_PER_BLOCK = 916.0 / 64
-# HBM bytes of one K1 launch from rocprofv3 PMC (profiles/r01_pmc_k1_session2.txt):
-# (FETCH_SIZE + WRITE_SIZE) x 1 KiB, averaged over 12 launches.  No x2
-# correction: K1's reads are per-lane 16-B loads of scattered segments (not the
-# wide coalesced stream the gfx950 1/2-count applies to), and the raw count
-# already equals the algorithmic read bytes.
-K1_PMC_TRAFFIC_BYTES = None   # re-collected for k_segment_hash_tiled (tools/profile_round.sh)
+# HBM bytes of one K1 launch (k_segment_hash_tiled_p) from rocprofv3 PMC,
+# separate FETCH_SIZE / WRITE_SIZE passes (profiles/r01_session5_pmc_summary.txt):
+# FETCH_SIZE x 2 (gfx950 counts half of a wide coalesced 16-B/lane stream,
+# MI355X_MICROARCH.md; the doubled 220.1 MB = 211.1 MB tiles + 8.4 MB tile
+# metadata) + WRITE_SIZE (37.1 MB: 19 MB of entries stored as scattered
+# 16-B + 2-B writes), KiB -> bytes.
+K1_PMC_TRAFFIC_BYTES = int((2 * 107486.5 + 36233.6) * 1024)
 METRIC = 'synctree keys rehashed/sec + exchange tree-diffs/sec at 10M keys, 1–8 GPUs'
 
 
