@@ -68,6 +68,9 @@ def main():
     ap.add_argument('--no-extras', action='store_true', help='skip build/compare/ensemble legs')
     ap.add_argument('--ensembles', type=int, default=32, help='config-4 leg: ensembles (trees) per GPU')
     ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
+    ap.add_argument('--part-keys', type=int, default=100_000_000, help='config-5 leg: keys in the partitioned tree')
+    ap.add_argument('--part-batches', type=int, default=5, help='config-5 leg: timed write batches')
+    ap.add_argument('--part-batch-keys', type=int, default=1_000_000, help='config-5 leg: keys per write batch')
     args = ap.parse_args()
 
     import torch
@@ -200,9 +203,16 @@ def main():
         if not args.no_extras:
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, local, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_h, vals_h, keys_d, vals_d, n, local, torch)
-            del keys_d, vals_d
-            tree.close()
+    tree.close()
+    del keys_d, vals_d
+    if not args.no_extras:
+        # config 5 runs on every rank (one tree partitioned by segment range)
+        part = _bench_partition(synctree_hip, dist, args, local, torch)
+        if rank == 0:
+            out['partition'] = part
             out['ensembles'] = _bench_ensembles(synctree_hip, workload, args.ensembles, args.ensemble_keys, local, torch)
+            out['config1'] = _bench_config1(synctree_hip, workload, local, torch, cpu=not args.no_cpu)
+    if rank == 0:
         if not args.no_cpu:
             out['cpu_baseline'] = _cpu_baseline(keys_h, vals_h, top0)
     if dist:
@@ -328,6 +338,149 @@ def _bench_ensembles(synctree_hip, workload, E, nk, local, torch, reps=10):
             'per_tree_rehash_keys_per_s': round(E * nk / dt_s, 1), 'ensembles': E, 'keys_per_ensemble': nk,
             'what': 'config4 shape per GPU: %d ensembles x %d keys rehashed as one st_rehash_group batch '
                     '(K1 over all trees\' tiles + one level-dataflow launch), vs st_rehash per tree' % (E, nk)}
+
+
+def _dev_keys(seed, start, n, dev, torch):
+    """splitmix64(seed + i), i = start+1 .. start+n, masked to 63 bits, on the
+    device (a bijection before the mask: distinct keys with overwhelming
+    probability; inserts are last-writer-wins anyway)."""
+    return _dev_keys_at(seed, torch.arange(start, start + n, dtype=torch.int64, device=dev), dev, torch)
+
+
+def _dev_values(seq, dev, torch, epoch=1):
+    """<<0, Epoch:64, Seq:64>> rows for an int64 seq tensor (device)."""
+    v = torch.zeros((seq.numel(), 17), dtype=torch.uint8, device=dev)
+    v[:, 8] = epoch
+    for b in range(8):
+        v[:, 9 + b] = ((seq >> (56 - 8 * b)) & 0xFF).to(torch.uint8)
+    return v
+
+
+def _bench_partition(synctree_hip, dist, args, local, torch):
+    """Config 5: one tree of part_keys keys partitioned by segment range over
+    the ranks (st_set_partition); timed: part_batches write batches of
+    part_batch_keys keys (50 % overwrites with Seq + 1, 50 % new keys), each an
+    insert/3 batch with dirty-path rehash on every rank + the all-gather of the
+    level-2 entries and level 1 + top (parallel.PartitionedTree.combine)."""
+    from riak_ensemble_amd import parallel
+    import numpy as np
+    dev = torch.device('cuda', local)
+    world = dist.get_world_size() if dist else 1
+    grp = dist if dist else _SoloGroup()
+    pt = parallel.PartitionedTree(synctree_hip.DeviceTree(device=local), grp, device=dev)
+    N, B, K = args.part_keys, args.part_batch_keys, args.part_batches
+    seed = 0x5EED0005
+    chunk = 10_000_000
+    t0 = time.perf_counter()
+    for a in range(0, N, chunk):
+        m = min(chunk, N - a)
+        k = _dev_keys(seed, a, m, dev, torch)
+        v = _dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
+        pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
+        del k, v
+    pt.combine()
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    rng = np.random.default_rng(5)
+    batches = []
+    for j in range(K + 1):
+        old = torch.from_numpy(rng.integers(0, N, B // 2)).to(dev)          # overwrites: Seq + 1 of a loaded key
+        k = torch.cat([_dev_keys_at(seed, old, dev, torch), _dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
+        seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
+        batches.append((k.contiguous(), _dev_values(seq, dev, torch).contiguous()))
+    # one warm-up batch, then K timed
+    k, v = batches[0]
+    pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
+    pt.combine()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(1, K + 1):
+        k, v = batches[j]
+        pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
+        pt.combine()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    top = pt.top_hash()
+    same = True
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        tops = parallel.gather_tops(dist, [top], device=dev)
+        same = all(x == top for x in tops)
+    entries = pt.tree.num_entries()
+    pt.tree.close()
+    return {'batch_keys_per_s': round(K * B / el, 1), 'ms_per_batch': round(el * 1e3 / K, 4), 'batches': K,
+            'batch_keys': B, 'tree_keys': N, 'ranks': world, 'entries_on_rank0': entries,
+            'tops_agree_across_ranks': same, 'load_s': round(load_s, 3),
+            'what': 'config5: %d-key tree partitioned by segment range over %d rank(s); per batch: insert/3 of %d keys '
+                    '(50%% overwrites Seq+1, 50%% new; verify + dirty-path rehash) on every rank, all-gather of the '
+                    'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits)'
+                    % (N, world, B)}
+
+
+def _dev_keys_at(seed, idx, dev, torch):
+    """Keys at arbitrary generation indices idx (0-based) of _dev_keys."""
+    def c(x):
+        return x - (1 << 64) if x >= 1 << 63 else x
+
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+    z = c(seed) + (idx + 1) * c(0x9E3779B97F4A7C15)
+    z = (z ^ lsr(z, 30)) * c(0xBF58476D1CE4E5B9)
+    z = (z ^ lsr(z, 27)) * c(0x94D049BB133111EB)
+    z = z ^ lsr(z, 31)
+    return z & 0x7FFFFFFFFFFFFFFF
+
+
+class _SoloGroup:
+    @staticmethod
+    def get_rank(group=None):
+        return 0
+
+    @staticmethod
+    def get_world_size(group=None):
+        return 1
+
+
+def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
+    """Config 1: a 100k-key tree, full build (n inserts) + rehash + top hash.
+    GPU: one st_insert_int64 batch + st_rehash.  CPU: the C restatement in
+    reference-faithful mode (one verified insert per key, DFS rehash over all
+    2^20 slots), one thread -- the reference Erlang cannot run here."""
+    keys = workload.keys_int63(n, workload.SEED ^ 0x100)
+    vals = workload.obj_hash_values(n)
+    best = 1e9
+    for _ in range(4):
+        t = synctree_hip.DeviceTree(device=local)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        t.insert_int64(keys, vals)
+        t.rehash()
+        top = t.top_hash()
+        best = min(best, time.perf_counter() - t0)
+        t.close()
+    out = {'gpu_keys_per_s': round(n / best, 1), 'gpu_ms': round(best * 1e3, 3),
+           'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)'}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+        import oracle_c
+        ot = oracle_c.OTree()
+        t0 = time.perf_counter()
+        for k, v in zip(keys.tolist(), vals):
+            ot.insert(int(k), bytes(v))
+        ot.rehash()
+        ctop = ot.top_hash()
+        dt = time.perf_counter() - t0
+        assert ctop == top, 'config1: CPU restatement and GPU disagree'
+        out['cpu'] = {'keys_per_s': round(n / dt, 1), 'seconds': round(dt, 3), 'cores': 1, 'kind': 'port',
+                      'sample': 'oracle/synctree_oracle.c: 100k verified inserts (ctypes per key) + rehash + top_hash'}
+    return out
 
 
 def _cpu_baseline(keys_h, vals_h, top0, reps=2):

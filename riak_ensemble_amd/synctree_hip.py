@@ -27,6 +27,19 @@ def _bytes(p, o0, o1):
     return ctypes.string_at(ctypes.addressof(p.contents) + int(o0), n)
 
 
+class _Closed:
+    """Handle of a closed DeviceTree: passing it to the library raises."""
+
+    @property
+    def _as_parameter_(self):
+        raise ValueError('DeviceTree is closed')
+
+    value = None
+
+    def __bool__(self):
+        return False
+
+
 class DeviceTree:
     """One device-resident tree (a C-ABI st_tree handle)."""
 
@@ -43,9 +56,10 @@ class DeviceTree:
         self.shift = self.width.bit_length() - 1
 
     def close(self):
+        """Free the device tree; any later call raises (the handle is gone)."""
         if getattr(self, 'h', None):
             self.L.st_destroy(self.h)
-            self.h = None
+            self.h = _Closed()
 
     def __del__(self):
         try:
