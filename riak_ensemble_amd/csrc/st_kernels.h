@@ -501,6 +501,102 @@ __global__ void k_merge(MergeArgs a, uint64_t *cnt_or_off, uint64_t *src, uint8_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Parallel merge.  k_merge walks every segment's old entries serially (one
+// thread per segment, ~100 entries per segment in a 100M-key tree) and writes
+// src[] with uncoalesced stores; for batches much smaller than the tree that
+// walk is the whole ingest.  Here only the batch runs are walked: every kept
+// batch record r of segment s gets pos_r = lower_bound(old keys of s, key_r),
+// eq_r (key present) and ne_r (not an ERASE).  With exclusive scans ceq/cne
+// of those flags over the sorted batch, the merged order is closed-form:
+//   old entry li (dropped iff some eq_r has pos_r == li):
+//     new = li - #{r: eq_r, pos_r < li} + #{r: ne_r, pos_r <= li}
+//   batch record r with ne_r:
+//     new = pos_r - #{r' < r: eq_r'} + #{r' < r: ne_r'}
+// so old entries are placed by a coalesced pass (k_merge_old) and batch
+// records by one thread each (k_merge_new).  Same result as k_merge<true>.
+__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, uint64_t *feq, uint64_t *fne, uint64_t *cnt, uint8_t *dirty) {
+    for (uint64_t s = gtid(); s < a.S; s += gstride()) {
+        const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+        uint64_t nold = a.seg_off ? a.seg_off[s + 1] - i0 : 0;
+        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
+        const bool rej = a.seg_reject && a.seg_reject[s];
+        if (a.seg_replace && a.seg_replace[s]) nold = 0;
+        uint64_t lo = 0, neq = 0, nne = 0;
+        bool changed = false;
+        for (uint64_t j = j0; j < je; j++) {
+            if (rej) { pos[j] = 0; feq[j] = fne[j] = 0; continue; }
+            const uint32_t bi = a.perm[j];
+            const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
+            const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
+            uint64_t hi = nold;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
+                if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
+            }
+            const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[i0 + lo], a.koff[i0 + lo + 1] - a.koff[i0 + lo], kb, kl) == 0;
+            pos[j] = (uint32_t)lo;
+            const bool kept = a.keep[j] != 0;
+            const bool ne = kept && !(a.bop && a.bop[bi]);
+            feq[j] = kept && eq ? 1 : 0;
+            fne[j] = ne ? 1 : 0;
+            changed |= kept;
+            neq += kept && eq;
+            nne += ne;
+        }
+        cnt[s] = nold - neq + nne;
+        if (dirty) dirty[s] = changed ? 1 : 0;
+    }
+}
+
+// Old entries: a workgroup per 256 consecutive segments walks their old
+// entries with consecutive threads on consecutive entries.
+__device__ __forceinline__ uint64_t bound_pos(const uint32_t *pos, uint64_t lo, uint64_t hi, uint64_t li, bool upper) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const bool go = upper ? pos[mid] <= li : pos[mid] < li;
+        if (go) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *pos, const uint64_t *ceq, const uint64_t *cne,
+                                                   const uint64_t *noff, uint64_t *src) {
+    __shared__ uint64_t so[257];
+    const uint64_t s0 = (uint64_t)blockIdx.x * 256;
+    const uint64_t ns = a.S - s0 < 256 ? a.S - s0 : 256;
+    for (uint32_t i = threadIdx.x; i <= ns; i += 256) so[i] = a.seg_off[s0 + i];
+    __syncthreads();
+    const uint64_t e0 = so[0], e1 = so[ns];
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        uint32_t lo = 0, hi = (uint32_t)ns;   // local segment: so[k] <= e < so[k+1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (so[mid] <= e) lo = mid; else hi = mid;
+        }
+        const uint64_t s = s0 + lo, li = e - so[lo];
+        if (a.seg_replace && a.seg_replace[s]) continue;
+        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
+        uint64_t nw = noff[s] + li;
+        if (j0 != je && !(a.seg_reject && a.seg_reject[s])) {
+            const uint64_t k = bound_pos(pos, j0, je, li, true), k2 = bound_pos(pos, j0, je, li, false);
+            if (ceq[k] != ceq[k2]) continue;   // overwritten or erased by the batch
+            nw = noff[s] + li - (ceq[k2] - ceq[j0]) + (cne[k] - cne[j0]);
+        }
+        src[nw] = e;
+    }
+}
+
+// Batch records that produce an entry (kept, not ERASE, run not rejected).
+__global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const uint32_t *pos, const uint64_t *ceq,
+                            const uint64_t *cne, const uint64_t *noff, uint64_t *src) {
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        if (cne[j + 1] == cne[j]) continue;
+        const uint64_t s = sseg[j], j0 = a.bseg_off[s];
+        src[noff[s] + pos[j] - (ceq[j] - ceq[j0]) + (cne[j] - cne[j0])] = (1ull << 63) | a.perm[j];
+    }
+}
+
 // Per new entry: key/value byte lengths (for the offset scans).
 __global__ void k_src_lengths(const uint64_t *src, uint64_t n, const uint64_t *okoff, const uint64_t *ovoff,
                               const uint64_t *bkoff, const uint64_t *bvoff, uint64_t *klen, uint64_t *vlen) {

@@ -742,13 +742,39 @@ static int ingest(st_tree *t, IngestIn &in) {
     ICHK(dalloc_t(t, &cnt, S + 1));
     ICHK(dalloc_t(t, &dirty, S));
     HIPCHK(hipMemsetAsync(cnt + S, 0, 8, t->stream));
-    LAUNCH(t, "merge_count", (k_merge<false>), grid_for(S), 256, 0, ma, cnt, (uint64_t *)nullptr, dirty);
+    // merge strategy (env ST_MERGE, A/B knob): 1 = parallel (k_merge_pos /
+    // k_merge_old / k_merge_new, default), 0 = per-segment serial walk
+    static const int pmerge = getenv("ST_MERGE") ? atoi(getenv("ST_MERGE")) : 1;
+    uint32_t *mpos = nullptr;
+    uint64_t *feq = nullptr, *fne = nullptr, *ceq = nullptr, *cne = nullptr;
+    auto mfree = [&]() { dfree(t, mpos); dfree(t, feq); dfree(t, fne); dfree(t, ceq); dfree(t, cne); };
+    if (pmerge) {
+        if ((r = dalloc_t(t, &mpos, n)) || (r = dalloc_t(t, &feq, n + 1)) || (r = dalloc_t(t, &fne, n + 1)) ||
+            (r = dalloc_t(t, &ceq, n + 1)) || (r = dalloc_t(t, &cne, n + 1))) { mfree(); cleanup(); return r; }
+        // records outside every run (a partition's clamped runs) keep flags 0
+        HIPCHK(hipMemsetAsync(feq, 0, (n + 1) * 8, t->stream));
+        HIPCHK(hipMemsetAsync(fne, 0, (n + 1) * 8, t->stream));
+        LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, feq, fne, cnt, dirty);
+        if ((r = exclusive_scan<uint64_t>(t, feq, ceq, n + 1)) || (r = exclusive_scan<uint64_t>(t, fne, cne, n + 1))) {
+            mfree(); cleanup(); return r;
+        }
+    } else {
+        LAUNCH(t, "merge_count", (k_merge<false>), grid_for(S), 256, 0, ma, cnt, (uint64_t *)nullptr, dirty);
+    }
     ICHK(dalloc_t(t, &nseg_off, S + 1));
     ICHK(exclusive_scan<uint64_t>(t, cnt, nseg_off, S + 1));
     uint64_t n_new = 0;
     ICHK(d2h(t, &n_new, nseg_off + S, 8));
     ICHK(dalloc_t(t, &src, n_new + 1));
-    LAUNCH(t, "merge_write", (k_merge<true>), grid_for(S), 256, 0, ma, nseg_off, src, (uint8_t *)nullptr);
+    if (pmerge) {
+        LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
+               (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
+        LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
+               (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
+        mfree();
+    } else {
+        LAUNCH(t, "merge_write", (k_merge<true>), grid_for(S), 256, 0, ma, nseg_off, src, (uint8_t *)nullptr);
+    }
     ICHK(dalloc_t(t, &klen, n_new + 1));
     ICHK(dalloc_t(t, &vlen, n_new + 1));
     LAUNCH(t, "src_lengths", k_src_lengths, grid_for(n_new + 1), 256, 0, (const uint64_t *)src, n_new,
