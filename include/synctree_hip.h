@@ -239,6 +239,45 @@ int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uin
 int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
                       uint64_t *cbucket, int *cside);
 
+/* ---- synctree_leveldb on-disk format ---------------
+ * The records src/synctree_leveldb.erl writes for this tree: one per stored
+ * node {Level, Bucket}, key <<0, TreeId/binary, Level:8,
+ * (binary:encode_unsigned(Bucket))/binary>> (synctree_leveldb.erl:104-109),
+ * value term_to_binary(Node) (:134-152): the 17-byte top hash at {0,0},
+ * [{ChildId, Hash17}] for inner nodes, [{Key, Value}] for segments.  Nodes
+ * the device holds as empty are not written (rehash/1 deletes them,
+ * synctree.erl:529-531).  Records are in (Level, Bucket) order.  Atoms are
+ * written in the UTF-8 forms (SMALL_)ATOM_UTF8_EXT of term_to_binary. */
+typedef struct st_kv {
+    uint64_t n;          /* records */
+    uint64_t *koff;      /* n+1 */
+    uint8_t *kheap;
+    uint64_t *voff;      /* n+1 */
+    uint8_t *vheap;
+} st_kv;
+void st_free_kv(st_kv *kv);
+
+/* Encode the whole tree on the device and copy the records to the host. */
+int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, st_kv **out);
+/* The same encode with the records left in (then freed from) device memory:
+ * the bench path; reports the record count and key/value byte totals. */
+int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t *n_records,
+                               uint64_t *key_bytes, uint64_t *value_bytes);
+/* Replace the tree's content with the nodes stored in n LevelDB records (any
+ * order; for a repeated key the later record wins, as in one write batch) and
+ * set #tree.top_hash from {0,0} (new/5 + reload_top_hash, synctree.erl:
+ * 151-175).  Records of other tree ids, or keys db_key/3 never produces for
+ * this geometry, are ignored (a shared DB, synctree_leveldb.erl:66-83).  A
+ * value binary_to_term cannot decode (malformed, truncated, trailing bytes)
+ * leaves that node absent, as fetch/3 answers Default for it
+ * (synctree_leveldb.erl:111-123), and counts in *n_skipped.  A decodable node
+ * the device cannot hold (non-17-byte hashes, child ids outside the node,
+ * keys outside the int64/atom/binary domain, non-binary values, unsorted
+ * orddicts, compressed terms) returns ST_EINVAL and changes nothing. */
+int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t n, const uint8_t *kheap,
+                       const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff, uint64_t *n_loaded,
+                       uint64_t *n_skipped);
+
 /* ---- diagnostics ---------------------------------------------------- */
 
 /* Key -> segment (get_segment/2, synctree.erl:251-253) on the device. */

@@ -29,6 +29,10 @@ class StResult(ctypes.Structure):
                 ('seg', u64p)]
 
 
+class StKv(ctypes.Structure):
+    _fields_ = [('n', ctypes.c_uint64), ('koff', u64p), ('kheap', u8p), ('voff', u64p), ('vheap', u8p)]
+
+
 class DeviceError(RuntimeError):
     pass
 
@@ -80,6 +84,14 @@ _SIGS = {
                                          ctypes.POINTER(ctypes.c_int)]),
     'st_segment_of_batch': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    'st_free_kv': (None, [ctypes.POINTER(StKv)]),
+    'st_snapshot_leveldb': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.POINTER(StKv))]),
+    'st_snapshot_leveldb_device': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, u64p, u64p,
+                                                  u64p]),
+    'st_restore_leveldb': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p,
+                                          u64p]),
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
 }

@@ -18,6 +18,7 @@
 
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
+#include "leveldb_fmt.h"
 
 static thread_local std::string g_err;
 static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past a range
@@ -1824,5 +1825,367 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
     done();
     records_to_keys(res, n);
     *out = res;
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ synctree_leveldb format
+// device tree <-> the LevelDB records synctree_leveldb
+// writes (src/synctree_leveldb.erl:104-109, 134-152).  Encoding runs on the
+// device (leveldb_fmt.h); decoding parses the caller's host records once
+// (they arrive from LevelDB on the host) and uploads the node arrays and the
+// segment CSR in one pass.
+
+extern "C" void st_free_kv(st_kv *kv) {
+    if (!kv) return;
+    free(kv->koff); free(kv->kheap); free(kv->voff); free(kv->vheap);
+    free(kv);
+}
+
+static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t *n_out, uint64_t **okoff,
+                           uint8_t **kout, uint64_t **ovoff, uint8_t **vout, uint64_t tot[3]) {
+    const uint64_t R = t->nslots;
+    DevTree d = view(t);
+    uint64_t *pres = nullptr, *kl = nullptr, *vl = nullptr, *rank = nullptr, *ko = nullptr, *vo = nullptr;
+    uint8_t *did = nullptr;
+    int r = ST_OK;
+    auto done = [&]() { dfree(t, pres); dfree(t, kl); dfree(t, vl); dfree(t, rank); dfree(t, ko); dfree(t, vo); dfree(t, did); };
+    if ((r = dalloc_t(t, &pres, R + 1)) || (r = dalloc_t(t, &kl, R + 1)) || (r = dalloc_t(t, &vl, R + 1)) ||
+        (r = dalloc_t(t, &rank, R + 1)) || (r = dalloc_t(t, &ko, R + 1)) || (r = dalloc_t(t, &vo, R + 1)) ||
+        (r = dalloc(t, (void **)&did, id_len + 1)) || (r = h2d(t, did, tree_id, id_len))) { done(); return r; }
+    LAUNCH(t, "snap_sizes", k_snap_sizes, grid_for(R + 1), 256, 0, d, id_len, R, pres, kl, vl);
+    if ((r = exclusive_scan<uint64_t>(t, pres, rank, R + 1)) || (r = exclusive_scan<uint64_t>(t, kl, ko, R + 1)) ||
+        (r = exclusive_scan<uint64_t>(t, vl, vo, R + 1))) { done(); return r; }
+    HIPCHK(hipMemcpyAsync(&tot[0], rank + R, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[1], ko + R, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[2], vo + R, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    const uint64_t n = tot[0];
+    if ((r = dalloc_t(t, okoff, n + 1)) || (r = dalloc_t(t, ovoff, n + 1)) || (r = dalloc(t, (void **)kout, tot[1] + 16)) ||
+        (r = dalloc(t, (void **)vout, tot[2] + 16))) { done(); return r; }
+    LAUNCH(t, "snap_write", k_snap_write, grid_for(R), 256, 0, d, (const uint8_t *)did, id_len, R, (const uint64_t *)rank,
+           (const uint64_t *)ko, (const uint64_t *)vo, *kout, *vout, *okoff, *ovoff);
+    HIPCHK(hipMemcpyAsync(*okoff + n, &tot[1], 8, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(hipMemcpyAsync(*ovoff + n, &tot[2], 8, hipMemcpyHostToDevice, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    done();
+    *n_out = n;
+    return ST_OK;
+}
+
+extern "C" int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, st_kv **out) {
+    *out = nullptr;
+    CHK(use_device(t));
+    if (t->partitioned) { g_err = "snapshot of a partitioned tree (one partition is not a synctree)"; return ST_EINVAL; }
+    if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
+    uint64_t n = 0, tot[3] = {0, 0, 0}, *okoff = nullptr, *ovoff = nullptr;
+    uint8_t *kout = nullptr, *vout = nullptr;
+    int r = snapshot_device(t, tree_id, id_len, &n, &okoff, &kout, &ovoff, &vout, tot);
+    st_kv *kv = nullptr;
+    if (!r) {
+        kv = (st_kv *)calloc(1, sizeof(st_kv));
+        kv->n = n;
+        kv->koff = (uint64_t *)malloc((n + 1) * 8);
+        kv->voff = (uint64_t *)malloc((n + 1) * 8);
+        kv->kheap = (uint8_t *)malloc(tot[1] + 1);
+        kv->vheap = (uint8_t *)malloc(tot[2] + 1);
+        if (!kv->koff || !kv->voff || !kv->kheap || !kv->vheap) { g_err = "host allocation"; r = ST_ENOMEM; }
+        if (!r) r = d2h(t, kv->koff, okoff, (n + 1) * 8);
+        if (!r) r = d2h(t, kv->voff, ovoff, (n + 1) * 8);
+        if (!r) r = d2h(t, kv->kheap, kout, tot[1]);
+        if (!r) r = d2h(t, kv->vheap, vout, tot[2]);
+    }
+    dfree(t, okoff); dfree(t, ovoff); dfree(t, kout); dfree(t, vout);
+    if (r) { st_free_kv(kv); return r; }
+    *out = kv;
+    return ST_OK;
+}
+
+extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t *n_records,
+                                          uint64_t *key_bytes, uint64_t *value_bytes) {
+    CHK(use_device(t));
+    if (t->partitioned) { g_err = "snapshot of a partitioned tree"; return ST_EINVAL; }
+    if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
+    uint64_t n = 0, tot[3] = {0, 0, 0}, *okoff = nullptr, *ovoff = nullptr;
+    uint8_t *kout = nullptr, *vout = nullptr;
+    int r = snapshot_device(t, tree_id, id_len, &n, &okoff, &kout, &ovoff, &vout, tot);
+    dfree(t, okoff); dfree(t, ovoff); dfree(t, kout); dfree(t, vout);
+    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (n_records) *n_records = n;
+    if (key_bytes) *key_bytes = tot[1];
+    if (value_bytes) *value_bytes = tot[2];
+    return r;
+}
+
+namespace {
+// binary_to_term reader over one record value.  bad: malformed bytes (the
+// reference's binary_to_term raises and fetch/3 answers Default); dom: a
+// well-formed term the device tree cannot hold.
+struct Etf {
+    const uint8_t *p, *e;
+    bool bad = false, dom = false;
+    bool need(uint64_t n) {
+        if (bad || (uint64_t)(e - p) < n) bad = true;
+        return !bad;
+    }
+    uint8_t u8() { return need(1) ? *p++ : 0; }
+    uint32_t u16() {
+        if (!need(2)) return 0;
+        uint32_t v = ((uint32_t)p[0] << 8) | p[1];
+        p += 2;
+        return v;
+    }
+    uint32_t u32() {
+        if (!need(4)) return 0;
+        uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        p += 4;
+        return v;
+    }
+    // a tag that is standard ETF but outside the node domain
+    void other(uint8_t tg) {
+        static const uint8_t known[] = {70, 77, 80, 88, 90, 97, 98, 99, 100, 101, 102, 103, 104, 105,
+                                        106, 107, 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, 119};
+        bool k = false;
+        for (uint8_t x : known) k |= x == tg;
+        if (k) dom = true; else bad = true;
+    }
+    bool integer(int64_t &v) {
+        const uint8_t tg = u8();
+        if (bad) return false;
+        if (tg == 97) { v = u8(); return !bad; }
+        if (tg == 98) { v = (int32_t)u32(); return !bad; }
+        if (tg == 110) {
+            const uint32_t n = u8();
+            const uint8_t sign = u8();
+            if (!need(n)) return false;
+            uint64_t m = 0;
+            bool big = false;
+            for (uint32_t i = 0; i < n; i++) {
+                if (i < 8) m |= (uint64_t)p[i] << (8 * i);
+                else big |= p[i] != 0;
+            }
+            p += n;
+            if (big || (!sign && m > 0x7FFFFFFFFFFFFFFFull) || (sign && m > 0x8000000000000000ull)) { dom = true; return false; }
+            v = sign ? (int64_t)(0 - m) : (int64_t)m;
+            return true;
+        }
+        other(tg);
+        return false;
+    }
+    bool binary(const uint8_t *&b, uint32_t &len) {
+        const uint8_t tg = u8();
+        if (bad) return false;
+        if (tg != 109) { other(tg); return false; }
+        len = u32();
+        if (!need(len)) return false;
+        b = p;
+        p += len;
+        return true;
+    }
+    // list header: count (106 alone = [])
+    bool list(uint32_t &n) {
+        const uint8_t tg = u8();
+        if (bad) return false;
+        if (tg == 106) { n = 0; return true; }
+        if (tg != 108) { other(tg); return false; }
+        n = u32();
+        return !bad;
+    }
+    bool tuple2() {
+        const uint8_t tg = u8();
+        if (bad) return false;
+        if (tg != 104) { other(tg); return false; }
+        if (u8() != 2) { dom = !bad; return false; }
+        return true;
+    }
+    bool nil() {
+        const uint8_t tg = u8();
+        if (bad) return false;
+        if (tg != 106) { dom = true; return false; }   // an improper list
+        return true;
+    }
+    // key term -> device key record (tag + payload, synctree_hip.hip pack_records)
+    bool key(std::vector<uint8_t> &rec) {
+        if (!need(1)) return false;
+        const uint8_t tg = *p;
+        rec.clear();
+        if (tg == 97 || tg == 98 || tg == 110) {
+            int64_t v;
+            if (!integer(v)) return false;
+            const uint64_t u = (uint64_t)v ^ 0x8000000000000000ull;
+            rec.push_back(KEYTAG_INT);
+            for (int i = 7; i >= 0; i--) rec.push_back((uint8_t)(u >> (8 * i)));
+            return true;
+        }
+        if (tg == 100 || tg == 115 || tg == 118 || tg == 119) {
+            p++;
+            const uint32_t len = (tg == 100 || tg == 118) ? u16() : u8();
+            if (!need(len)) return false;
+            rec.push_back(KEYTAG_ATOM);
+            for (uint32_t i = 0; i < len; i++) {
+                const uint8_t c = p[i];
+                if ((tg == 100 || tg == 115) && c >= 0x80) {   // Latin-1 -> UTF-8
+                    rec.push_back((uint8_t)(0xC0 | (c >> 6)));
+                    rec.push_back((uint8_t)(0x80 | (c & 0x3F)));
+                } else {
+                    rec.push_back(c);
+                }
+            }
+            p += len;
+            return true;
+        }
+        const uint8_t *b;
+        uint32_t len;
+        if (!binary(b, len)) return false;
+        rec.push_back(KEYTAG_BINARY);
+        rec.insert(rec.end(), b, b + len);
+        return true;
+    }
+    bool version() {
+        const uint8_t v = u8();
+        if (!bad && v != 131) bad = true;
+        if (!bad && p < e && *p == 80) { dom = true; return false; }   // compressed term
+        return !bad;
+    }
+    bool end() {
+        if (!bad && p != e) bad = true;   // trailing bytes: binary_to_term/1 raises badarg
+        return !bad;
+    }
+};
+}  // namespace
+
+extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t n,
+                                  const uint8_t *kheap, const uint64_t *koff, const uint8_t *vheap,
+                                  const uint64_t *voff, uint64_t *n_loaded, uint64_t *n_skipped) {
+    CHK(use_device(t));
+    if (t->partitioned) { g_err = "restore into a partitioned tree"; return ST_EINVAL; }
+    if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
+    const uint64_t R = t->nslots, W = t->W, H = t->H;
+    // 1. keys -> record slot r (last write of a key wins, as in one write batch)
+    std::vector<int64_t> rec(R, -1);
+    uint64_t foreign = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *k = kheap + koff[i];
+        const uint64_t kl = koff[i + 1] - koff[i];
+        if (kl < 3 + (uint64_t)id_len || k[0] != 0 || (id_len && memcmp(k + 1, tree_id, id_len))) { foreign++; continue; }
+        const uint32_t L = k[1 + id_len];
+        const uint8_t *bb = k + 2 + id_len;
+        const uint64_t bl = kl - 2 - id_len;
+        // only keys db_key/3 produces are ever fetched: minimal encode_unsigned
+        if (bl > 8 || (bl > 1 && bb[0] == 0) || L > H + 1) { foreign++; continue; }
+        uint64_t b = 0;
+        for (uint64_t q = 0; q < bl; q++) b = (b << 8) | bb[q];
+        if (b >= t->base[L + 1] - t->base[L] && L > 0) { foreign++; continue; }
+        if (L == 0 && b != 0) { foreign++; continue; }
+        rec[L == 0 ? 0 : t->base[L] + b] = (int64_t)i;
+    }
+    // 2. decode values into the slot arrays and the segment CSR
+    std::vector<uint16_t> tags(R, 0);
+    std::vector<uint4> md(R, make_uint4(0, 0, 0, 0));
+    const uint64_t S = t->S, sb = t->base[H + 1];
+    std::vector<uint64_t> seg_off(S + 1, 0), seg_voff(S + 1, 0), ko(1, 0), vo(1, 0);
+    std::vector<uint8_t> kh, vh, krec, prev;
+    uint64_t loaded = 0, skipped = 0;
+    (void)foreign;   // other trees' records in a shared DB (synctree_leveldb.erl:66-83)
+    for (uint64_t r = 0; r < R; r++) {
+        if (r >= sb) seg_off[r - sb] = ko.size() - 1;
+        if (rec[r] < 0) continue;
+        const uint64_t i = (uint64_t)rec[r];
+        Etf in{vheap + voff[i], vheap + voff[i + 1]};
+        bool good = in.version();
+        if (r == 0) {
+            const uint8_t *h;
+            uint32_t len;
+            good = good && in.binary(h, len) && in.end();
+            if (good && len != 17) in.dom = true;
+            if (in.dom) { g_err = "{0,0} is not a 17-byte hash"; return ST_EINVAL; }
+            if (!good) { skipped++; continue; }
+            set_entry_host(tags[1], md[1], h);
+            set_entry_host(tags[0], md[0], h);   // reload_top_hash (synctree.erl:172-175)
+            loaded++;
+            continue;
+        }
+        if (r < sb) {
+            uint32_t L = 1;
+            while (L <= H && r >= t->base[L + 1]) L++;
+            const uint64_t b = r - t->base[L], c0 = t->base[L + 1] + b * W;
+            uint32_t cnt = 0;
+            good = good && in.list(cnt);
+            std::vector<std::pair<uint64_t, const uint8_t *>> ch;
+            int64_t prevc = -1;
+            for (uint32_t j = 0; good && j < cnt; j++) {
+                int64_t c;
+                const uint8_t *h;
+                uint32_t len;
+                good = in.tuple2() && in.integer(c) && in.binary(h, len);
+                if (good && (len != 17 || c < (int64_t)(b * W) || c >= (int64_t)((b + 1) * W) || c <= prevc)) in.dom = true;
+                if (in.dom) break;
+                prevc = c;
+                ch.push_back({(uint64_t)c, h});
+            }
+            if (good && !in.dom && cnt) good = in.nil();
+            good = good && !in.dom && in.end();
+            if (in.dom) { g_err = "inner node {" + std::to_string(L) + "," + std::to_string(b) + "} outside the device node domain"; return ST_EINVAL; }
+            if (!good) { skipped++; continue; }
+            for (auto &c : ch) set_entry_host(tags[c0 + (c.first - b * W)], md[c0 + (c.first - b * W)], c.second);
+            loaded++;
+            continue;
+        }
+        // segment: [{Key, Value}] strictly ascending (an orddict)
+        const uint64_t k_mark = kh.size(), v_mark = vh.size(), n_mark = ko.size();
+        uint32_t cnt = 0;
+        good = good && in.list(cnt);
+        prev.clear();
+        for (uint32_t j = 0; good && j < cnt; j++) {
+            const uint8_t *v;
+            uint32_t len;
+            good = in.tuple2() && in.key(krec);
+            if (good && j && host_rec_cmp(prev.data(), prev.size(), krec.data(), krec.size()) >= 0) in.dom = true;
+            good = good && !in.dom && in.binary(v, len);
+            if (in.dom) break;
+            if (!good) break;
+            kh.insert(kh.end(), krec.begin(), krec.end());
+            vh.insert(vh.end(), v, v + len);
+            ko.push_back(kh.size());
+            vo.push_back(vh.size());
+            prev.swap(krec);
+        }
+        if (good && !in.dom && cnt) good = in.nil();
+        good = good && !in.dom && in.end();
+        if (in.dom) { g_err = "segment " + std::to_string(r - sb) + " outside the device key/value domain"; return ST_EINVAL; }
+        if (!good) {   // undecodable: fetch/3 answers [] (synctree_leveldb.erl:116-120)
+            kh.resize(k_mark); vh.resize(v_mark); ko.resize(n_mark); vo.resize(n_mark);
+            skipped++;
+            continue;
+        }
+        loaded++;
+    }
+    const uint64_t ne = ko.size() - 1;
+    seg_off[S] = ne;
+    for (uint64_t s = 0; s <= S; s++) seg_voff[s] = vo[seg_off[s]];
+    const uint64_t kb = kh.size(), vb = vh.size();
+    kh.resize(kb + HEAP_SLACK, 0);
+    vh.resize(vb + HEAP_SLACK, 0);
+    // 3. upload: node arrays and a fresh CSR
+    uint64_t *dso = nullptr, *dsvo = nullptr, *dko = nullptr, *dvo = nullptr;
+    uint8_t *dkh = nullptr, *dvh = nullptr;
+    int r = ST_OK;
+    if ((r = dalloc_t(t, &dso, S + 1)) || (r = dalloc_t(t, &dsvo, S + 1)) || (r = dalloc_t(t, &dko, ne + 1)) ||
+        (r = dalloc_t(t, &dvo, ne + 1)) || (r = dalloc(t, (void **)&dkh, kh.size())) || (r = dalloc(t, (void **)&dvh, vh.size())) ||
+        (r = h2d(t, dso, seg_off.data(), (S + 1) * 8)) || (r = h2d(t, dsvo, seg_voff.data(), (S + 1) * 8)) ||
+        (r = h2d(t, dko, ko.data(), (ne + 1) * 8)) || (r = h2d(t, dvo, vo.data(), (ne + 1) * 8)) ||
+        (r = h2d(t, dkh, kh.data(), kh.size())) || (r = h2d(t, dvh, vh.data(), vh.size())) ||
+        (r = h2d(t, t->tag, tags.data(), R * 2)) || (r = h2d(t, t->md5, md.data(), R * 16))) {
+        dfree(t, dso); dfree(t, dsvo); dfree(t, dko); dfree(t, dvo); dfree(t, dkh); dfree(t, dvh);
+        return r;
+    }
+    HIPCHK(hipStreamSynchronize(t->stream));   // host vectors die at return
+    dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
+    t->seg_off = dso; t->seg_voff = dsvo; t->koff = dko; t->voff = dvo; t->kheap = dkh; t->vheap = dvh;
+    t->n = ne; t->kbytes = kb; t->vbytes = vb;
+    t->perm_valid = false;
+    t->tiles_valid = false;
+    t->fresh = false;
+    if (n_loaded) *n_loaded = loaded;
+    if (n_skipped) *n_skipped = skipped;
     return ST_OK;
 }

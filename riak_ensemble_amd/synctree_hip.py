@@ -288,6 +288,45 @@ class DeviceTree:
         info = {'diffs': int(nd.value), 'applied': int(na.value), 'rejected': int(nr.value)}
         return ('exchange_failed' if cr.value else 'ok', info)
 
+    # ------------------------------------------------------------ LevelDB format
+    def snapshot_leveldb(self, tree_id=b''):
+        """The synctree_leveldb records of this tree (src/synctree_leveldb.erl:
+        104-109, 134-152), encoded on the device: list of (key, value) bytes
+        in (Level, Bucket) order."""
+        rp = ctypes.POINTER(_lib.StKv)()
+        tid = bytes(tree_id)
+        _lib.check(self.L.st_snapshot_leveldb(self.h, tid, len(tid), ctypes.byref(rp)), 'st_snapshot_leveldb')
+        try:
+            kv = rp.contents
+            n = int(kv.n)
+            ko = np.ctypeslib.as_array(kv.koff, (n + 1,)).copy()
+            vo = np.ctypeslib.as_array(kv.voff, (n + 1,)).copy()
+            kh = _bytes(kv.kheap, 0, ko[n])
+            vh = _bytes(kv.vheap, 0, vo[n])
+        finally:
+            self.L.st_free_kv(rp)
+        return [(kh[ko[i]:ko[i + 1]], vh[vo[i]:vo[i + 1]]) for i in range(n)]
+
+    def snapshot_leveldb_device(self, tree_id=b''):
+        """Device-only encode (bench): (records, key bytes, value bytes)."""
+        n, kb, vb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        tid = bytes(tree_id)
+        _lib.check(self.L.st_snapshot_leveldb_device(self.h, tid, len(tid), ctypes.byref(n), ctypes.byref(kb),
+                                                     ctypes.byref(vb)), 'st_snapshot_leveldb_device')
+        return int(n.value), int(kb.value), int(vb.value)
+
+    def restore_leveldb(self, records, tree_id=b''):
+        """Replace the tree with the nodes in LevelDB records [(key, value)]
+        and reload #tree.top_hash from {0,0} (synctree.erl:151-175).
+        Returns (nodes loaded, undecodable nodes skipped)."""
+        kh, ko = terms.pack_blobs([k for k, _ in records])
+        vh, vo = terms.pack_blobs([v for _, v in records])
+        nl, ns = ctypes.c_uint64(), ctypes.c_uint64()
+        tid = bytes(tree_id)
+        _lib.check(self.L.st_restore_leveldb(self.h, tid, len(tid), len(records), _ptr(kh), _ptr(ko), _ptr(vh),
+                                             _ptr(vo), ctypes.byref(nl), ctypes.byref(ns)), 'st_restore_leveldb')
+        return int(nl.value), int(ns.value)
+
     # ------------------------------------------------------------ timing
     def set_timing(self, on=True):
         _lib.check(self.L.st_set_timing(self.h, 1 if on else 0), 'st_set_timing')

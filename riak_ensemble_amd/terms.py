@@ -72,6 +72,14 @@ def pack_keys(keys):
     return kt, kh, koff
 
 
+def pack_blobs(blobs):
+    """Byte strings -> (heap u8[], off u64[n+1])."""
+    off = np.zeros(len(blobs) + 1, np.uint64)
+    if blobs:
+        off[1:] = np.cumsum([len(b) for b in blobs])
+    return np.frombuffer(b''.join(bytes(b) for b in blobs) + b'\0' * 8, np.uint8).copy(), off
+
+
 def pack_values(values):
     n = len(values)
     voff = np.zeros(n + 1, np.uint64)
