@@ -203,6 +203,7 @@ def main():
         if not args.no_extras:
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, local, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_h, vals_h, keys_d, vals_d, n, local, torch)
+            out['leveldb'] = _bench_leveldb(synctree_hip, tree, local, torch)
     tree.close()
     del keys_d, vals_d
     if not args.no_extras:
@@ -220,6 +221,65 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
+    """synctree_leveldb format of the 10M-key tree:
+    device encode of every node record (k_snap_sizes + 3 scans + k_snap_write),
+    the host-inclusive snapshot (D2H of the records), and restore into a fresh
+    tree from those host records (host ETF decode + upload)."""
+    import ctypes
+    from riak_ensemble_amd import _lib
+    L = _lib.load()
+    tid = b'ens-1'
+    tree.snapshot_leveldb_device(tid)   # warm-up
+    tree.set_timing(True)
+    kn = ('snap_entry_sizes', 'snap_sizes', 'snap_write', 'snap_entries')
+    k0 = [tree.kernel_stats(k) for k in kn]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        n, kb, vb = tree.snapshot_leveldb_device(tid)
+    dt = (time.perf_counter() - t0) / reps
+    k1 = [tree.kernel_stats(k) for k in kn]
+    tree.set_timing(False)
+    kms = [(b[1] - a[1]) / max(1, b[0] - a[0]) for a, b in zip(k0, k1)]
+    rp = ctypes.POINTER(_lib.StKv)()
+    t0 = time.perf_counter()
+    _lib.check(L.st_snapshot_leveldb(tree.h, tid, len(tid), ctypes.byref(rp)), 'snapshot')
+    host_s = time.perf_counter() - t0
+    kv = rp.contents
+    fresh = synctree_hip.DeviceTree(device=local)
+    nl, ns = ctypes.c_uint64(), ctypes.c_uint64()
+    t0 = time.perf_counter()
+    _lib.check(L.st_restore_leveldb(fresh.h, tid, len(tid), kv.n, kv.kheap, kv.koff, kv.vheap, kv.voff,
+                                    ctypes.byref(nl), ctypes.byref(ns)), 'restore')
+    restore_s = time.perf_counter() - t0
+    L.st_free_kv(rp)
+    same = fresh.top_hash() == tree.top_hash() and int(nl.value) == n and int(ns.value) == 0
+    fresh.close()
+    return {'records': n, 'key_bytes': kb, 'value_bytes': vb,
+            'device_encode_ms': round(dt * 1e3, 3),
+            'kernel_ms': {k: round(m, 4) for k, m in zip(kn, kms)},
+            # k_snap_entries per entry: koff 8 + key record 9 + voff 8 + value 17
+            # + entry offset 8 read, the entry's ETF bytes written (the values
+            # heap minus list headers/NILs and inner-node records)
+            'entries_roofline': _entries_roof(tree, vb, kms[3]),
+            'encode_GB_per_s_written': round((kb + vb) / dt / 1e9, 1),
+            'snapshot_to_host_ms': round(host_s * 1e3, 1),
+            'restore_from_host_ms': round(restore_s * 1e3, 1),
+            'restore_same_top_hash': bool(same),
+            'what': 'config2 tree (10M keys): every node as <<0,Id,Level,encode_unsigned(Bucket)>> => '
+                    'term_to_binary(Node) (synctree_leveldb.erl:104-152); restore = new/5 + reload_top_hash'}
+
+
+def _entries_roof(tree, vb, ms):
+    ne = tree.num_entries()
+    written = vb - 23 - 7 * ne   # upper bound of entry bytes; headers are O(records)
+    algo = ne * (8 + 9 + 8 + 17 + 8) + written
+    gbs = algo / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': int(algo)}
 
 
 def _segment_histogram(tree, keys_h):

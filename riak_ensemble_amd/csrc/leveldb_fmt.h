@@ -29,10 +29,14 @@
 // out in that (Level, Bucket) order; a LevelDB write batch of distinct keys
 // does not depend on it.
 //
-// Both kernels are HBM-bound byte formatting (no MD5): k_snap_sizes reads the
-// tags (inner) or the CSR offsets + key tags (segments) and writes three
-// lengths per record; k_snap_write reads the node content once and writes the
-// record bytes once.
+// All kernels are HBM-bound byte formatting (no MD5):
+//   k_snap_entry_sizes  one lane per segment entry: its ETF length
+//   k_snap_sizes        one lane per record: present flag, key and value length
+//   k_snap_write        one lane per record: key, list header / NIL, inner
+//                       nodes' children, the {0,0} hash
+//   k_snap_entries      one lane per segment entry: {Key, Value} bytes
+// (three rocPRIM scans between them give the offsets).  Node content is read
+// once and every output byte written once.
 #pragma once
 #include "st_kernels.h"
 
@@ -111,8 +115,19 @@ __device__ inline uint32_t snap_level(const DevTree &t, uint64_t r) {
     return L;
 }
 
-// Per record: present flag, key length, value length.
-__global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, uint64_t *pres, uint64_t *klen, uint64_t *vlen) {
+// ETF bytes of every segment entry {Key, Value}: 2 + key + 5 + |Value|
+__global__ void k_snap_entry_sizes(DevTree t, uint64_t n, uint64_t *es) {
+    for (uint64_t e = gtid(); e <= n; e += gstride()) {
+        if (e == n) { es[e] = 0; break; }
+        const uint64_t k0 = t.koff[e];
+        es[e] = 2 + etf_key_size(t.kheap + k0, t.koff[e + 1] - k0) + 5 + (t.voff[e + 1] - t.voff[e]);
+    }
+}
+
+// Per record: present flag, key length, value length.  eo: exclusive scan of
+// k_snap_entry_sizes (n + 1 entries).
+__global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64_t *eo, uint64_t *pres, uint64_t *klen,
+                             uint64_t *vlen) {
     for (uint64_t r = gtid(); r <= R; r += gstride()) {
         uint64_t p = 0, kl = 0, vl = 0;
         if (r == 0) {
@@ -131,14 +146,7 @@ __global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, uint64_t *pr
                 if (cnt) { p = 1; vl = 7 + body; }
             } else {
                 const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
-                if (e1 > e0) {
-                    uint64_t body = 0;
-                    for (uint64_t e = e0; e < e1; e++) {
-                        const uint64_t k0 = t.koff[e];
-                        body += 2 + etf_key_size(t.kheap + k0, t.koff[e + 1] - k0) + 5 + (t.voff[e + 1] - t.voff[e]);
-                    }
-                    p = 1; vl = 7 + body;
-                }
+                if (e1 > e0) { p = 1; vl = 7 + eo[e1] - eo[e0]; }
             }
             if (p) kl = 2 + idlen + enc_unsigned_len(b);
         }
@@ -147,10 +155,11 @@ __global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, uint64_t *pr
 }
 
 // Write every present record at its scanned offsets; rank[r] numbers the
-// present records (output koff/voff entries).
+// present records (output koff/voff entries).  Segment records get their
+// list header and NIL here; k_snap_entries writes their entries.
 __global__ void k_snap_write(DevTree t, const uint8_t *id, uint32_t idlen, uint64_t R, const uint64_t *rank,
-                             const uint64_t *ko, const uint64_t *vo, uint8_t *kout, uint8_t *vout, uint64_t *okoff,
-                             uint64_t *ovoff) {
+                             const uint64_t *ko, const uint64_t *vo, const uint64_t *eo, uint8_t *kout, uint8_t *vout,
+                             uint64_t *okoff, uint64_t *ovoff) {
     for (uint64_t r = gtid(); r < R; r += gstride()) {
         if (rank[r + 1] == rank[r]) continue;
         const uint64_t n = rank[r];
@@ -197,15 +206,29 @@ __global__ void k_snap_write(DevTree t, const uint8_t *id, uint32_t idlen, uint6
         }
         const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
         v[1] = 108; v = etf_u32be(v + 2, (uint32_t)(e1 - e0));
-        for (uint64_t e = e0; e < e1; e++) {
-            v[0] = 104; v[1] = 2;
-            const uint64_t k0 = t.koff[e];
-            v = etf_key_write(v + 2, t.kheap + k0, t.koff[e + 1] - k0);
-            const uint64_t v0 = t.voff[e], vl = t.voff[e + 1] - v0;
-            v[0] = 109; v = etf_u32be(v + 1, (uint32_t)vl);
-            for (uint64_t i = 0; i < vl; i++) v[i] = t.vheap[v0 + i];
-            v += vl;
+        v[eo[e1] - eo[e0]] = 106;
+    }
+}
+
+// One lane per segment entry: {Key, Value} at the record's value offset +
+// 6 (list header) + the entry's offset within its segment.  Consecutive
+// entries land in consecutive output bytes, so a wave's stores stay within
+// a few cache lines.
+__global__ void k_snap_entries(DevTree t, uint64_t n, uint64_t sb, const uint64_t *vo, const uint64_t *eo,
+                               uint8_t *vout) {
+    for (uint64_t e = gtid(); e < n; e += gstride()) {
+        // segment of entry e: last s with seg_off[s] <= e (segments are non-empty here)
+        uint64_t lo = 0, hi = t.S;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (t.seg_off[mid] <= e) lo = mid; else hi = mid;
         }
-        v[0] = 106;
+        uint8_t *v = vout + vo[sb + lo] + 6 + (eo[e] - eo[t.seg_off[lo]]);
+        v[0] = 104; v[1] = 2;
+        const uint64_t k0 = t.koff[e];
+        v = etf_key_write(v + 2, t.kheap + k0, t.koff[e + 1] - k0);
+        const uint64_t v0 = t.voff[e], vl = t.voff[e + 1] - v0;
+        v[0] = 109; v = etf_u32be(v + 1, (uint32_t)vl);
+        for (uint64_t i = 0; i < vl; i++) v[i] = t.vheap[v0 + i];
     }
 }

@@ -1845,14 +1845,21 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
                            uint8_t **kout, uint64_t **ovoff, uint8_t **vout, uint64_t tot[3]) {
     const uint64_t R = t->nslots;
     DevTree d = view(t);
+    const uint64_t ne = t->n;
     uint64_t *pres = nullptr, *kl = nullptr, *vl = nullptr, *rank = nullptr, *ko = nullptr, *vo = nullptr;
+    uint64_t *es = nullptr, *eo = nullptr;
     uint8_t *did = nullptr;
     int r = ST_OK;
-    auto done = [&]() { dfree(t, pres); dfree(t, kl); dfree(t, vl); dfree(t, rank); dfree(t, ko); dfree(t, vo); dfree(t, did); };
-    if ((r = dalloc_t(t, &pres, R + 1)) || (r = dalloc_t(t, &kl, R + 1)) || (r = dalloc_t(t, &vl, R + 1)) ||
+    auto done = [&]() {
+        dfree(t, pres); dfree(t, kl); dfree(t, vl); dfree(t, rank); dfree(t, ko); dfree(t, vo); dfree(t, did);
+        dfree(t, es); dfree(t, eo);
+    };
+    if ((r = dalloc_t(t, &es, ne + 1)) || (r = dalloc_t(t, &eo, ne + 1)) || (r = dalloc_t(t, &pres, R + 1)) || (r = dalloc_t(t, &kl, R + 1)) || (r = dalloc_t(t, &vl, R + 1)) ||
         (r = dalloc_t(t, &rank, R + 1)) || (r = dalloc_t(t, &ko, R + 1)) || (r = dalloc_t(t, &vo, R + 1)) ||
         (r = dalloc(t, (void **)&did, id_len + 1)) || (r = h2d(t, did, tree_id, id_len))) { done(); return r; }
-    LAUNCH(t, "snap_sizes", k_snap_sizes, grid_for(R + 1), 256, 0, d, id_len, R, pres, kl, vl);
+    LAUNCH(t, "snap_entry_sizes", k_snap_entry_sizes, grid_for(ne + 1), 256, 0, d, ne, es);
+    if ((r = exclusive_scan<uint64_t>(t, es, eo, ne + 1))) { done(); return r; }
+    LAUNCH(t, "snap_sizes", k_snap_sizes, grid_for(R + 1), 256, 0, d, id_len, R, (const uint64_t *)eo, pres, kl, vl);
     if ((r = exclusive_scan<uint64_t>(t, pres, rank, R + 1)) || (r = exclusive_scan<uint64_t>(t, kl, ko, R + 1)) ||
         (r = exclusive_scan<uint64_t>(t, vl, vo, R + 1))) { done(); return r; }
     HIPCHK(hipMemcpyAsync(&tot[0], rank + R, 8, hipMemcpyDeviceToHost, t->stream));
@@ -1863,7 +1870,9 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
     if ((r = dalloc_t(t, okoff, n + 1)) || (r = dalloc_t(t, ovoff, n + 1)) || (r = dalloc(t, (void **)kout, tot[1] + 16)) ||
         (r = dalloc(t, (void **)vout, tot[2] + 16))) { done(); return r; }
     LAUNCH(t, "snap_write", k_snap_write, grid_for(R), 256, 0, d, (const uint8_t *)did, id_len, R, (const uint64_t *)rank,
-           (const uint64_t *)ko, (const uint64_t *)vo, *kout, *vout, *okoff, *ovoff);
+           (const uint64_t *)ko, (const uint64_t *)vo, (const uint64_t *)eo, *kout, *vout, *okoff, *ovoff);
+    if (ne) LAUNCH(t, "snap_entries", k_snap_entries, grid_for(ne), 256, 0, d, ne, t->base[t->H + 1], (const uint64_t *)vo,
+                   (const uint64_t *)eo, *vout);
     HIPCHK(hipMemcpyAsync(*okoff + n, &tot[1], 8, hipMemcpyHostToDevice, t->stream));
     HIPCHK(hipMemcpyAsync(*ovoff + n, &tot[2], 8, hipMemcpyHostToDevice, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
