@@ -275,7 +275,15 @@ def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
 
 def _entries_roof(tree, vb, ms):
     ne = tree.num_entries()
-    written = vb - 23 - 7 * ne   # upper bound of entry bytes; headers are O(records)
+    # entry bytes = value bytes - {0,0} record - inner-node records - segment
+    # list headers/NILs (7 B per non-empty segment)
+    inner = 0
+    for L in range(2, tree.height + 2):
+        p = tree.level_entries(L)[0]
+        ids = np.nonzero(p)[0]
+        inner += 7 * int(p.reshape(-1, tree.width).any(1).sum()) + int((24 + np.where(ids < 256, 2, 5)).sum())
+    nseg = int(tree.level_entries(tree.height + 1)[0].sum())
+    written = vb - 23 - inner - 7 * nseg
     algo = ne * (8 + 9 + 8 + 17 + 8) + written
     gbs = algo / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     return {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
