@@ -232,3 +232,311 @@ __global__ void k_snap_entries(DevTree t, uint64_t n, uint64_t sb, const uint64_
         for (uint64_t i = 0; i < vl; i++) v[i] = t.vheap[v0 + i];
     }
 }
+
+// ---------------------------------------------------------------------------
+// Restore: binary_to_term of the records on the device.
+//
+// bad = malformed bytes (the reference's binary_to_term raises and fetch/3
+// answers Default: the node is absent); dom = a well-formed term the device
+// tree cannot hold (the whole restore fails with ST_EINVAL).
+struct DEtf {
+    const uint8_t *p, *e;
+    bool bad, dom;
+    __device__ DEtf(const uint8_t *a, const uint8_t *b) : p(a), e(b), bad(false), dom(false) {}
+    __device__ bool need(uint64_t n) {
+        if (bad || (uint64_t)(e - p) < n) bad = true;
+        return !bad;
+    }
+    __device__ uint32_t u8() { return need(1) ? *p++ : 0; }
+    __device__ uint32_t u16() {
+        if (!need(2)) return 0;
+        const uint32_t v = ((uint32_t)p[0] << 8) | p[1];
+        p += 2;
+        return v;
+    }
+    __device__ uint32_t u32() {
+        if (!need(4)) return 0;
+        const uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+        p += 4;
+        return v;
+    }
+    // a standard ETF tag outside the node domain, or garbage
+    __device__ void other(uint32_t tg) {
+        if (tg == 70 || tg == 77 || tg == 80 || tg == 88 || tg == 90 || (tg >= 97 && tg <= 119)) dom = true;
+        else bad = true;
+    }
+    __device__ bool integer(int64_t &v) {
+        const uint32_t tg = u8();
+        if (bad) return false;
+        if (tg == 97) { v = u8(); return !bad; }
+        if (tg == 98) { v = (int32_t)u32(); return !bad; }
+        if (tg == 110) {
+            const uint32_t n = u8(), sign = u8();
+            if (!need(n)) return false;
+            uint64_t m = 0;
+            bool big = false;
+            for (uint32_t i = 0; i < n; i++) {
+                if (i < 8) m |= (uint64_t)p[i] << (8 * i);
+                else big |= p[i] != 0;
+            }
+            p += n;
+            if (big || (!sign && m > 0x7FFFFFFFFFFFFFFFull) || (sign && m > 0x8000000000000000ull)) { dom = true; return false; }
+            v = sign ? (int64_t)(0 - m) : (int64_t)m;
+            return true;
+        }
+        other(tg);
+        return false;
+    }
+    __device__ bool binary(const uint8_t *&b, uint32_t &len) {
+        const uint32_t tg = u8();
+        if (bad) return false;
+        if (tg != 109) { other(tg); return false; }
+        len = u32();
+        if (!need(len)) return false;
+        b = p;
+        p += len;
+        return true;
+    }
+    __device__ bool list(uint32_t &n) {
+        const uint32_t tg = u8();
+        if (bad) return false;
+        if (tg == 106) { n = 0; return true; }
+        if (tg != 108) { other(tg); return false; }
+        n = u32();
+        return !bad;
+    }
+    __device__ bool tuple2() {
+        const uint32_t tg = u8();
+        if (bad) return false;
+        if (tg != 104) { other(tg); return false; }
+        if (u8() != 2) { dom = !bad; return false; }
+        return true;
+    }
+    __device__ bool nil() {
+        const uint32_t tg = u8();
+        if (bad) return false;
+        if (tg != 106) { dom = true; return false; }   // an improper list
+        return true;
+    }
+    __device__ bool version() {
+        const uint32_t v = u8();
+        if (!bad && v != 131) bad = true;
+        if (!bad && p < e && *p == 80) { dom = true; return false; }   // compressed term
+        return !bad;
+    }
+    __device__ bool end() {
+        if (!bad && p != e) bad = true;   // trailing bytes: binary_to_term/1 raises badarg
+        return !bad;
+    }
+    // Key term -> device key record (tag byte + payload; integers as
+    // sign-flipped big-endian, Latin-1 atoms converted to UTF-8).  dst NULL:
+    // only the record length.
+    __device__ bool key(uint8_t *dst, uint32_t &rlen) {
+        if (!need(1)) return false;
+        const uint32_t tg = *p;
+        if (tg == 97 || tg == 98 || tg == 110) {
+            int64_t v;
+            if (!integer(v)) return false;
+            if (dst) {
+                const uint64_t u = (uint64_t)v ^ 0x8000000000000000ull;
+                dst[0] = KEYTAG_INT;
+                for (int i = 0; i < 8; i++) dst[1 + i] = (uint8_t)(u >> (8 * (7 - i)));
+            }
+            rlen = 9;
+            return true;
+        }
+        if (tg == 100 || tg == 115 || tg == 118 || tg == 119) {
+            p++;
+            const uint32_t len = (tg == 100 || tg == 118) ? u16() : u8();
+            if (!need(len)) return false;
+            const bool latin = tg == 100 || tg == 115;
+            uint32_t o = 1;
+            for (uint32_t i = 0; i < len; i++) {
+                const uint8_t c = p[i];
+                if (latin && c >= 0x80) {
+                    if (dst) { dst[o] = (uint8_t)(0xC0 | (c >> 6)); dst[o + 1] = (uint8_t)(0x80 | (c & 0x3F)); }
+                    o += 2;
+                } else {
+                    if (dst) dst[o] = c;
+                    o++;
+                }
+            }
+            if (dst) dst[0] = KEYTAG_ATOM;
+            p += len;
+            rlen = o;
+            return true;
+        }
+        const uint8_t *b;
+        uint32_t len;
+        if (!binary(b, len)) return false;
+        if (dst) {
+            dst[0] = KEYTAG_BINARY;
+            for (uint32_t i = 0; i < len; i++) dst[1 + i] = b[i];
+        }
+        rlen = 1 + len;
+        return true;
+    }
+};
+
+// Counters of one restore: [0] nodes loaded, [1] undecodable nodes skipped,
+// [2] domain error flag, [3] lowest record slot with a domain error.
+#define RST_LOADED 0
+#define RST_SKIPPED 1
+#define RST_DOM 2
+#define RST_DOMSLOT 3
+
+__device__ inline void rst_dom(unsigned long long *ctr, uint64_t r) {
+    atomicOr(&ctr[RST_DOM], 1ull);
+    atomicMin(&ctr[RST_DOMSLOT], (unsigned long long)r);
+}
+
+__device__ inline void set_entry_dev(uint16_t &tag, uint4 &m, const uint8_t *h17) {
+    tag = (uint16_t)(TAG_PRESENT | h17[0]);
+    uint32_t w[4];
+    for (int k = 0; k < 4; k++)
+        w[k] = (uint32_t)h17[1 + 4 * k] | ((uint32_t)h17[2 + 4 * k] << 8) | ((uint32_t)h17[3 + 4 * k] << 16) |
+               ((uint32_t)h17[4 + 4 * k] << 24);
+    m = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// One lane per record: its node slot r (db_key/3 inverted for this tree id
+// and geometry); the last record of a key wins (atomicMax of index + 1).
+// Other trees' records and keys db_key/3 never produces are ignored.
+__global__ void k_rest_keys(DevTree t, const uint8_t *id, uint32_t idlen, uint64_t n, const uint8_t *kh,
+                            const uint64_t *ko, unsigned long long *recof) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint8_t *k = kh + ko[i];
+        const uint64_t kl = ko[i + 1] - ko[i];
+        if (kl < 3 + (uint64_t)idlen || k[0] != 0) continue;
+        bool same = true;
+        for (uint32_t q = 0; q < idlen; q++) same &= k[1 + q] == id[q];
+        if (!same) continue;
+        const uint32_t L = k[1 + idlen];
+        const uint8_t *bb = k + 2 + idlen;
+        const uint64_t bl = kl - 2 - idlen;
+        if (bl > 8 || (bl > 1 && bb[0] == 0) || L > t.H + 1) continue;
+        uint64_t b = 0;
+        for (uint64_t q = 0; q < bl; q++) b = (b << 8) | bb[q];
+        if (L == 0 ? b != 0 : b >= t.base[L + 1] - t.base[L]) continue;
+        atomicMax(&recof[L == 0 ? 0 : t.base[L] + b], (unsigned long long)(i + 1));
+    }
+}
+
+// One lane per node slot r: decode its record (if any).  {0,0} and inner
+// nodes go straight into the staging slot arrays (stag/smd, zeroed); a
+// segment is validated and sized (entries, key-record bytes, value bytes).
+__global__ void k_rest_nodes(DevTree t, uint64_t R, const unsigned long long *recof, const uint8_t *vh,
+                             const uint64_t *vo, uint16_t *stag, uint4 *smd, uint64_t *ecnt, uint64_t *kcnt,
+                             uint64_t *vcnt, uint8_t *segok, unsigned long long *ctr) {
+    const uint64_t sb = t.base[t.H + 1];
+    for (uint64_t r = gtid(); r < R; r += gstride()) {
+        const bool seg = r >= sb;
+        if (seg) { ecnt[r - sb] = 0; kcnt[r - sb] = 0; vcnt[r - sb] = 0; segok[r - sb] = 0; }
+        const unsigned long long i1 = recof[r];
+        if (!i1) continue;
+        const uint64_t i = i1 - 1;
+        DEtf in(vh + vo[i], vh + vo[i + 1]);
+        bool good = in.version();
+        if (r == 0) {
+            const uint8_t *h = nullptr;
+            uint32_t len = 0;
+            good = good && in.binary(h, len) && in.end();
+            if (good && len != 17) in.dom = true;
+            if (in.dom) { rst_dom(ctr, r); continue; }
+            if (!good) { atomicAdd(&ctr[RST_SKIPPED], 1ull); continue; }
+            set_entry_dev(stag[1], smd[1], h);
+            set_entry_dev(stag[0], smd[0], h);   // reload_top_hash (synctree.erl:172-175)
+            atomicAdd(&ctr[RST_LOADED], 1ull);
+            continue;
+        }
+        if (!seg) {
+            const uint32_t L = snap_level(t, r);
+            const uint64_t b = r - t.base[L], c0 = t.base[L + 1] + b * t.W;
+            uint32_t cnt = 0;
+            good = good && in.list(cnt);
+            const uint8_t *first = in.p;
+            int64_t prevc = -1;
+            for (uint32_t j = 0; good && j < cnt; j++) {
+                int64_t c = 0;
+                const uint8_t *h;
+                uint32_t len = 0;
+                good = in.tuple2() && in.integer(c) && in.binary(h, len);
+                if (good && (len != 17 || c < (int64_t)(b * t.W) || c >= (int64_t)((b + 1) * t.W) || c <= prevc)) in.dom = true;
+                if (in.dom) break;
+                prevc = c;
+            }
+            if (good && !in.dom && cnt) good = in.nil();
+            good = good && !in.dom && in.end();
+            if (in.dom) { rst_dom(ctr, r); continue; }
+            if (!good) { atomicAdd(&ctr[RST_SKIPPED], 1ull); continue; }
+            DEtf w(first, vh + vo[i + 1]);   // second pass: store the validated children
+            for (uint32_t j = 0; j < cnt; j++) {
+                int64_t c = 0;
+                const uint8_t *h;
+                uint32_t len;
+                w.tuple2(); w.integer(c); w.binary(h, len);
+                const uint64_t s = c0 + ((uint64_t)c - b * t.W);
+                set_entry_dev(stag[s], smd[s], h);
+            }
+            atomicAdd(&ctr[RST_LOADED], 1ull);
+            continue;
+        }
+        uint32_t cnt = 0;
+        uint64_t kb = 0, vb = 0;
+        good = good && in.list(cnt);
+        for (uint32_t j = 0; good && j < cnt; j++) {
+            uint32_t kl = 0, len = 0;
+            const uint8_t *v;
+            good = in.tuple2() && in.key(nullptr, kl) && in.binary(v, len);
+            if (in.dom) break;
+            kb += kl;
+            vb += len;
+        }
+        if (good && !in.dom && cnt) good = in.nil();
+        good = good && !in.dom && in.end();
+        if (in.dom) { rst_dom(ctr, r); continue; }
+        if (!good) { atomicAdd(&ctr[RST_SKIPPED], 1ull); continue; }   // fetch/3 answers []
+        ecnt[r - sb] = cnt; kcnt[r - sb] = kb; vcnt[r - sb] = vb;
+        segok[r - sb] = 1;
+        atomicAdd(&ctr[RST_LOADED], 1ull);
+    }
+}
+
+// One lane per validated segment: its entries' key records and values into
+// the new CSR at the scanned offsets; keys must be strictly ascending (an
+// orddict), else a domain error.
+__global__ void k_rest_segments(DevTree t, const unsigned long long *recof, const uint8_t *vh, const uint64_t *vo,
+                                const uint8_t *segok, const uint64_t *seg_off, const uint64_t *kbase,
+                                const uint64_t *vbase, uint64_t *koff, uint8_t *kheap, uint64_t *voff, uint8_t *vheap,
+                                unsigned long long *ctr) {
+    const uint64_t sb = t.base[t.H + 1];
+    for (uint64_t s = gtid(); s < t.S; s += gstride()) {
+        if (!segok[s]) continue;
+        const uint64_t i = recof[sb + s] - 1;
+        DEtf in(vh + vo[i], vh + vo[i + 1]);
+        uint32_t cnt = 0;
+        in.version();
+        in.list(cnt);
+        uint64_t e = seg_off[s], kp = kbase[s], vp = vbase[s];
+        uint64_t pk = 0, pl = 0;
+        for (uint32_t j = 0; j < cnt; j++, e++) {
+            uint32_t kl = 0, len = 0;
+            const uint8_t *v;
+            in.tuple2();
+            in.key(kheap + kp, kl);
+            in.binary(v, len);
+            if (j) {   // strictly ascending in term order (memcmp, then length)
+                const uint64_t m = pl < kl ? pl : kl;
+                int c = 0;
+                for (uint64_t q = 0; q < m && !c; q++) c = (int)kheap[pk + q] - (int)kheap[kp + q];
+                if (c > 0 || (c == 0 && pl >= kl)) rst_dom(ctr, sb + s);
+            }
+            koff[e] = kp;
+            voff[e] = vp;
+            for (uint32_t q = 0; q < len; q++) vheap[vp + q] = v[q];
+            pk = kp; pl = kl;
+            kp += kl;
+            vp += len;
+        }
+    }
+}

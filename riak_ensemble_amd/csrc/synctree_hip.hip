@@ -1925,276 +1925,103 @@ extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, ui
     return r;
 }
 
-namespace {
-// binary_to_term reader over one record value.  bad: malformed bytes (the
-// reference's binary_to_term raises and fetch/3 answers Default); dom: a
-// well-formed term the device tree cannot hold.
-struct Etf {
-    const uint8_t *p, *e;
-    bool bad = false, dom = false;
-    bool need(uint64_t n) {
-        if (bad || (uint64_t)(e - p) < n) bad = true;
-        return !bad;
-    }
-    uint8_t u8() { return need(1) ? *p++ : 0; }
-    uint32_t u16() {
-        if (!need(2)) return 0;
-        uint32_t v = ((uint32_t)p[0] << 8) | p[1];
-        p += 2;
-        return v;
-    }
-    uint32_t u32() {
-        if (!need(4)) return 0;
-        uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-        p += 4;
-        return v;
-    }
-    // a tag that is standard ETF but outside the node domain
-    void other(uint8_t tg) {
-        static const uint8_t known[] = {70, 77, 80, 88, 90, 97, 98, 99, 100, 101, 102, 103, 104, 105,
-                                        106, 107, 108, 109, 110, 111, 112, 113, 114, 115, 116, 117, 118, 119};
-        bool k = false;
-        for (uint8_t x : known) k |= x == tg;
-        if (k) dom = true; else bad = true;
-    }
-    bool integer(int64_t &v) {
-        const uint8_t tg = u8();
-        if (bad) return false;
-        if (tg == 97) { v = u8(); return !bad; }
-        if (tg == 98) { v = (int32_t)u32(); return !bad; }
-        if (tg == 110) {
-            const uint32_t n = u8();
-            const uint8_t sign = u8();
-            if (!need(n)) return false;
-            uint64_t m = 0;
-            bool big = false;
-            for (uint32_t i = 0; i < n; i++) {
-                if (i < 8) m |= (uint64_t)p[i] << (8 * i);
-                else big |= p[i] != 0;
-            }
-            p += n;
-            if (big || (!sign && m > 0x7FFFFFFFFFFFFFFFull) || (sign && m > 0x8000000000000000ull)) { dom = true; return false; }
-            v = sign ? (int64_t)(0 - m) : (int64_t)m;
-            return true;
-        }
-        other(tg);
-        return false;
-    }
-    bool binary(const uint8_t *&b, uint32_t &len) {
-        const uint8_t tg = u8();
-        if (bad) return false;
-        if (tg != 109) { other(tg); return false; }
-        len = u32();
-        if (!need(len)) return false;
-        b = p;
-        p += len;
-        return true;
-    }
-    // list header: count (106 alone = [])
-    bool list(uint32_t &n) {
-        const uint8_t tg = u8();
-        if (bad) return false;
-        if (tg == 106) { n = 0; return true; }
-        if (tg != 108) { other(tg); return false; }
-        n = u32();
-        return !bad;
-    }
-    bool tuple2() {
-        const uint8_t tg = u8();
-        if (bad) return false;
-        if (tg != 104) { other(tg); return false; }
-        if (u8() != 2) { dom = !bad; return false; }
-        return true;
-    }
-    bool nil() {
-        const uint8_t tg = u8();
-        if (bad) return false;
-        if (tg != 106) { dom = true; return false; }   // an improper list
-        return true;
-    }
-    // key term -> device key record (tag + payload, synctree_hip.hip pack_records)
-    bool key(std::vector<uint8_t> &rec) {
-        if (!need(1)) return false;
-        const uint8_t tg = *p;
-        rec.clear();
-        if (tg == 97 || tg == 98 || tg == 110) {
-            int64_t v;
-            if (!integer(v)) return false;
-            const uint64_t u = (uint64_t)v ^ 0x8000000000000000ull;
-            rec.push_back(KEYTAG_INT);
-            for (int i = 7; i >= 0; i--) rec.push_back((uint8_t)(u >> (8 * i)));
-            return true;
-        }
-        if (tg == 100 || tg == 115 || tg == 118 || tg == 119) {
-            p++;
-            const uint32_t len = (tg == 100 || tg == 118) ? u16() : u8();
-            if (!need(len)) return false;
-            rec.push_back(KEYTAG_ATOM);
-            for (uint32_t i = 0; i < len; i++) {
-                const uint8_t c = p[i];
-                if ((tg == 100 || tg == 115) && c >= 0x80) {   // Latin-1 -> UTF-8
-                    rec.push_back((uint8_t)(0xC0 | (c >> 6)));
-                    rec.push_back((uint8_t)(0x80 | (c & 0x3F)));
-                } else {
-                    rec.push_back(c);
-                }
-            }
-            p += len;
-            return true;
-        }
-        const uint8_t *b;
-        uint32_t len;
-        if (!binary(b, len)) return false;
-        rec.push_back(KEYTAG_BINARY);
-        rec.insert(rec.end(), b, b + len);
-        return true;
-    }
-    bool version() {
-        const uint8_t v = u8();
-        if (!bad && v != 131) bad = true;
-        if (!bad && p < e && *p == 80) { dom = true; return false; }   // compressed term
-        return !bad;
-    }
-    bool end() {
-        if (!bad && p != e) bad = true;   // trailing bytes: binary_to_term/1 raises badarg
-        return !bad;
-    }
-};
-}  // namespace
-
 extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t n,
                                   const uint8_t *kheap, const uint64_t *koff, const uint8_t *vheap,
                                   const uint64_t *voff, uint64_t *n_loaded, uint64_t *n_skipped) {
     CHK(use_device(t));
     if (t->partitioned) { g_err = "restore into a partitioned tree"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
-    const uint64_t R = t->nslots, W = t->W, H = t->H;
-    // 1. keys -> record slot r (last write of a key wins, as in one write batch)
-    std::vector<int64_t> rec(R, -1);
-    uint64_t foreign = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        const uint8_t *k = kheap + koff[i];
-        const uint64_t kl = koff[i + 1] - koff[i];
-        if (kl < 3 + (uint64_t)id_len || k[0] != 0 || (id_len && memcmp(k + 1, tree_id, id_len))) { foreign++; continue; }
-        const uint32_t L = k[1 + id_len];
-        const uint8_t *bb = k + 2 + id_len;
-        const uint64_t bl = kl - 2 - id_len;
-        // only keys db_key/3 produces are ever fetched: minimal encode_unsigned
-        if (bl > 8 || (bl > 1 && bb[0] == 0) || L > H + 1) { foreign++; continue; }
-        uint64_t b = 0;
-        for (uint64_t q = 0; q < bl; q++) b = (b << 8) | bb[q];
-        if (b >= t->base[L + 1] - t->base[L] && L > 0) { foreign++; continue; }
-        if (L == 0 && b != 0) { foreign++; continue; }
-        rec[L == 0 ? 0 : t->base[L] + b] = (int64_t)i;
-    }
-    // 2. decode values into the slot arrays and the segment CSR
-    std::vector<uint16_t> tags(R, 0);
-    std::vector<uint4> md(R, make_uint4(0, 0, 0, 0));
-    const uint64_t S = t->S, sb = t->base[H + 1];
-    std::vector<uint64_t> seg_off(S + 1, 0), seg_voff(S + 1, 0), ko(1, 0), vo(1, 0);
-    std::vector<uint8_t> kh, vh, krec, prev;
-    uint64_t loaded = 0, skipped = 0;
-    (void)foreign;   // other trees' records in a shared DB (synctree_leveldb.erl:66-83)
-    for (uint64_t r = 0; r < R; r++) {
-        if (r >= sb) seg_off[r - sb] = ko.size() - 1;
-        if (rec[r] < 0) continue;
-        const uint64_t i = (uint64_t)rec[r];
-        Etf in{vheap + voff[i], vheap + voff[i + 1]};
-        bool good = in.version();
-        if (r == 0) {
-            const uint8_t *h;
-            uint32_t len;
-            good = good && in.binary(h, len) && in.end();
-            if (good && len != 17) in.dom = true;
-            if (in.dom) { g_err = "{0,0} is not a 17-byte hash"; return ST_EINVAL; }
-            if (!good) { skipped++; continue; }
-            set_entry_host(tags[1], md[1], h);
-            set_entry_host(tags[0], md[0], h);   // reload_top_hash (synctree.erl:172-175)
-            loaded++;
-            continue;
-        }
-        if (r < sb) {
-            uint32_t L = 1;
-            while (L <= H && r >= t->base[L + 1]) L++;
-            const uint64_t b = r - t->base[L], c0 = t->base[L + 1] + b * W;
-            uint32_t cnt = 0;
-            good = good && in.list(cnt);
-            std::vector<std::pair<uint64_t, const uint8_t *>> ch;
-            int64_t prevc = -1;
-            for (uint32_t j = 0; good && j < cnt; j++) {
-                int64_t c;
-                const uint8_t *h;
-                uint32_t len;
-                good = in.tuple2() && in.integer(c) && in.binary(h, len);
-                if (good && (len != 17 || c < (int64_t)(b * W) || c >= (int64_t)((b + 1) * W) || c <= prevc)) in.dom = true;
-                if (in.dom) break;
-                prevc = c;
-                ch.push_back({(uint64_t)c, h});
-            }
-            if (good && !in.dom && cnt) good = in.nil();
-            good = good && !in.dom && in.end();
-            if (in.dom) { g_err = "inner node {" + std::to_string(L) + "," + std::to_string(b) + "} outside the device node domain"; return ST_EINVAL; }
-            if (!good) { skipped++; continue; }
-            for (auto &c : ch) set_entry_host(tags[c0 + (c.first - b * W)], md[c0 + (c.first - b * W)], c.second);
-            loaded++;
-            continue;
-        }
-        // segment: [{Key, Value}] strictly ascending (an orddict)
-        const uint64_t k_mark = kh.size(), v_mark = vh.size(), n_mark = ko.size();
-        uint32_t cnt = 0;
-        good = good && in.list(cnt);
-        prev.clear();
-        for (uint32_t j = 0; good && j < cnt; j++) {
-            const uint8_t *v;
-            uint32_t len;
-            good = in.tuple2() && in.key(krec);
-            if (good && j && host_rec_cmp(prev.data(), prev.size(), krec.data(), krec.size()) >= 0) in.dom = true;
-            good = good && !in.dom && in.binary(v, len);
-            if (in.dom) break;
-            if (!good) break;
-            kh.insert(kh.end(), krec.begin(), krec.end());
-            vh.insert(vh.end(), v, v + len);
-            ko.push_back(kh.size());
-            vo.push_back(vh.size());
-            prev.swap(krec);
-        }
-        if (good && !in.dom && cnt) good = in.nil();
-        good = good && !in.dom && in.end();
-        if (in.dom) { g_err = "segment " + std::to_string(r - sb) + " outside the device key/value domain"; return ST_EINVAL; }
-        if (!good) {   // undecodable: fetch/3 answers [] (synctree_leveldb.erl:116-120)
-            kh.resize(k_mark); vh.resize(v_mark); ko.resize(n_mark); vo.resize(n_mark);
-            skipped++;
-            continue;
-        }
-        loaded++;
-    }
-    const uint64_t ne = ko.size() - 1;
-    seg_off[S] = ne;
-    for (uint64_t s = 0; s <= S; s++) seg_voff[s] = vo[seg_off[s]];
-    const uint64_t kb = kh.size(), vb = vh.size();
-    kh.resize(kb + HEAP_SLACK, 0);
-    vh.resize(vb + HEAP_SLACK, 0);
-    // 3. upload: node arrays and a fresh CSR
-    uint64_t *dso = nullptr, *dsvo = nullptr, *dko = nullptr, *dvo = nullptr;
-    uint8_t *dkh = nullptr, *dvh = nullptr;
-    int r = ST_OK;
-    if ((r = dalloc_t(t, &dso, S + 1)) || (r = dalloc_t(t, &dsvo, S + 1)) || (r = dalloc_t(t, &dko, ne + 1)) ||
-        (r = dalloc_t(t, &dvo, ne + 1)) || (r = dalloc(t, (void **)&dkh, kh.size())) || (r = dalloc(t, (void **)&dvh, vh.size())) ||
-        (r = h2d(t, dso, seg_off.data(), (S + 1) * 8)) || (r = h2d(t, dsvo, seg_voff.data(), (S + 1) * 8)) ||
-        (r = h2d(t, dko, ko.data(), (ne + 1) * 8)) || (r = h2d(t, dvo, vo.data(), (ne + 1) * 8)) ||
-        (r = h2d(t, dkh, kh.data(), kh.size())) || (r = h2d(t, dvh, vh.data(), vh.size())) ||
-        (r = h2d(t, t->tag, tags.data(), R * 2)) || (r = h2d(t, t->md5, md.data(), R * 16))) {
-        dfree(t, dso); dfree(t, dsvo); dfree(t, dko); dfree(t, dvo); dfree(t, dkh); dfree(t, dvh);
-        return r;
-    }
-    HIPCHK(hipStreamSynchronize(t->stream));   // host vectors die at return
+    const uint64_t R = t->nslots, S = t->S;
+    const uint64_t kin = n ? koff[n] - koff[0] : 0, vin = n ? voff[n] - voff[0] : 0;
+    DevTree d = view(t);
+    // staging: nothing of the tree changes until every record has decoded
+    uint8_t *dkh = nullptr, *dvh = nullptr, *did = nullptr, *segok = nullptr;
+    uint64_t *dko = nullptr, *dvo = nullptr, *ec = nullptr, *kc = nullptr, *vc = nullptr;
+    uint64_t *nso = nullptr, *kbase = nullptr, *vbase = nullptr, *nsvo = nullptr, *nko = nullptr, *nvo = nullptr;
+    uint8_t *nkh = nullptr, *nvh = nullptr;
+    unsigned long long *recof = nullptr, *ctr = nullptr;
+    uint16_t *stag = nullptr;
+    uint4 *smd = nullptr;
+    auto done = [&](bool keep_new) {
+        void *ps[] = {dkh, dvh, did, segok, dko, dvo, ec, kc, vc, kbase, vbase, recof, ctr, stag, smd};
+        for (void *p : ps) dfree(t, p);
+        if (!keep_new) { dfree(t, nso); dfree(t, nsvo); dfree(t, nko); dfree(t, nvo); dfree(t, nkh); dfree(t, nvh); }
+    };
+#define RCHK(x)                               \
+    do {                                      \
+        int r_ = (x);                         \
+        if (r_ != ST_OK) { done(false); return r_; } \
+    } while (0)
+    // records as they lie in the caller's buffers (offsets rebased to 0)
+    std::vector<uint64_t> ko0(n + 1), vo0(n + 1);
+    for (uint64_t i = 0; i <= n; i++) { ko0[i] = koff[i] - koff[0]; vo0[i] = voff[i] - voff[0]; }
+    RCHK(dalloc(t, (void **)&dkh, kin + 16)); RCHK(dalloc(t, (void **)&dvh, vin + 16));
+    RCHK(dalloc_t(t, &dko, n + 1)); RCHK(dalloc_t(t, &dvo, n + 1)); RCHK(dalloc(t, (void **)&did, id_len + 1));
+    RCHK(h2d(t, dkh, kheap + (n ? koff[0] : 0), kin)); RCHK(h2d(t, dvh, vheap + (n ? voff[0] : 0), vin));
+    RCHK(h2d(t, dko, ko0.data(), (n + 1) * 8)); RCHK(h2d(t, dvo, vo0.data(), (n + 1) * 8));
+    RCHK(h2d(t, did, tree_id, id_len));
+    RCHK(dalloc_t(t, &recof, R)); RCHK(dalloc_t(t, &ctr, 4)); RCHK(dalloc_t(t, &stag, R)); RCHK(dalloc_t(t, &smd, R));
+    RCHK(dalloc_t(t, &ec, S + 1)); RCHK(dalloc_t(t, &kc, S + 1)); RCHK(dalloc_t(t, &vc, S + 1)); RCHK(dalloc_t(t, &segok, S));
+    HIPCHK(hipMemsetAsync(recof, 0, R * 8, t->stream));
+    HIPCHK(hipMemsetAsync(ctr, 0, 3 * 8, t->stream));
+    HIPCHK(hipMemsetAsync(ctr + RST_DOMSLOT, 0xFF, 8, t->stream));
+    HIPCHK(hipMemsetAsync(stag, 0, R * 2, t->stream));
+    HIPCHK(hipMemsetAsync(smd, 0, R * 16, t->stream));
+    HIPCHK(hipMemsetAsync(ec + S, 0, 8, t->stream));
+    HIPCHK(hipMemsetAsync(kc + S, 0, 8, t->stream));
+    HIPCHK(hipMemsetAsync(vc + S, 0, 8, t->stream));
+    if (n) LAUNCH(t, "rest_keys", k_rest_keys, grid_for(n), 256, 0, d, (const uint8_t *)did, id_len, n,
+                  (const uint8_t *)dkh, (const uint64_t *)dko, recof);
+    LAUNCH(t, "rest_nodes", k_rest_nodes, grid_for(R), 256, 0, d, R, (const unsigned long long *)recof,
+           (const uint8_t *)dvh, (const uint64_t *)dvo, stag, smd, ec, kc, vc, segok, ctr);
+    unsigned long long hc[4] = {0, 0, 0, 0};
+    auto domain_error = [&]() {
+        const uint64_t r = hc[RST_DOMSLOT];
+        uint32_t L = 0;
+        while (L <= t->H && r >= t->base[L + 1]) L++;
+        const uint64_t b = r == 0 ? 0 : r - t->base[L];
+        g_err = "node {" + std::to_string(L) + "," + std::to_string(b) +
+                "} decodes to a term outside the device node domain (hash size, child id, key/value type or order)";
+        done(false);
+        return ST_EINVAL;
+    };
+    RCHK(d2h(t, hc, ctr, sizeof(hc)));
+    if (hc[RST_DOM]) return domain_error();
+    RCHK(dalloc_t(t, &nso, S + 1)); RCHK(dalloc_t(t, &kbase, S + 1)); RCHK(dalloc_t(t, &vbase, S + 1));
+    RCHK(exclusive_scan<uint64_t>(t, ec, nso, S + 1));
+    RCHK(exclusive_scan<uint64_t>(t, kc, kbase, S + 1));
+    RCHK(exclusive_scan<uint64_t>(t, vc, vbase, S + 1));
+    uint64_t tot[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(&tot[0], nso + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[1], kbase + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(&tot[2], vbase + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    const uint64_t ne = tot[0], kb = tot[1], vb = tot[2];
+    RCHK(dalloc_t(t, &nko, ne + 1)); RCHK(dalloc_t(t, &nvo, ne + 1)); RCHK(dalloc_t(t, &nsvo, S + 1));
+    RCHK(dalloc(t, (void **)&nkh, kb + HEAP_SLACK)); RCHK(dalloc(t, (void **)&nvh, vb + HEAP_SLACK));
+    HIPCHK(hipMemsetAsync(nkh + kb, 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(nvh + vb, 0, HEAP_SLACK, t->stream));
+    RCHK(h2d(t, nko + ne, &tot[1], 8));
+    RCHK(h2d(t, nvo + ne, &tot[2], 8));
+    LAUNCH(t, "rest_segments", k_rest_segments, grid_for(S), 256, 0, d, (const unsigned long long *)recof,
+           (const uint8_t *)dvh, (const uint64_t *)dvo, (const uint8_t *)segok, (const uint64_t *)nso,
+           (const uint64_t *)kbase, (const uint64_t *)vbase, nko, nkh, nvo, nvh, ctr);
+    LAUNCH(t, "seg_voff", k_seg_voff, grid_for(S + 1), 256, 0, (const uint64_t *)nso, (const uint64_t *)nvo, S, nsvo);
+    RCHK(d2h(t, hc, ctr, sizeof(hc)));
+    if (hc[RST_DOM]) return domain_error();
+    // commit: node arrays and the new CSR
+    HIPCHK(hipMemcpyAsync(t->tag, stag, R * 2, hipMemcpyDeviceToDevice, t->stream));
+    HIPCHK(hipMemcpyAsync(t->md5, smd, R * 16, hipMemcpyDeviceToDevice, t->stream));
     dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
-    t->seg_off = dso; t->seg_voff = dsvo; t->koff = dko; t->voff = dvo; t->kheap = dkh; t->vheap = dvh;
+    t->seg_off = nso; t->seg_voff = nsvo; t->koff = nko; t->voff = nvo; t->kheap = nkh; t->vheap = nvh;
     t->n = ne; t->kbytes = kb; t->vbytes = vb;
     t->perm_valid = false;
     t->tiles_valid = false;
     t->fresh = false;
-    if (n_loaded) *n_loaded = loaded;
-    if (n_skipped) *n_skipped = skipped;
+    done(true);
+    HIPCHK(hipStreamSynchronize(t->stream));   // the caller's buffers may go after return
+#undef RCHK
+    if (n_loaded) *n_loaded = hc[RST_LOADED];
+    if (n_skipped) *n_skipped = hc[RST_SKIPPED];
     return ST_OK;
 }
