@@ -1830,10 +1830,10 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
 
 // ------------------------------------------------------------------ synctree_leveldb format
 // device tree <-> the LevelDB records synctree_leveldb
-// writes (src/synctree_leveldb.erl:104-109, 134-152).  Encoding runs on the
-// device (leveldb_fmt.h); decoding parses the caller's host records once
-// (they arrive from LevelDB on the host) and uploads the node arrays and the
-// segment CSR in one pass.
+// writes (src/synctree_leveldb.erl:104-109, 134-152).  Encoding and decoding
+// both run on the device (leveldb_fmt.h): restore copies the caller's host
+// records to HBM once and commits the decoded slot arrays and CSR only when
+// every record decoded.
 
 extern "C" void st_free_kv(st_kv *kv) {
     if (!kv) return;
