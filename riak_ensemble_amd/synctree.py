@@ -75,9 +75,18 @@ def _after_top_change(t):
 # ---------------------------------------------------------------- construction
 def newdb(id_, opts=()):
     """synctree.erl:127-133 — the persistent-backend constructor.  The device
-    tree replaces synctree_leveldb on this path (the on-disk format is a
-    SURVEY §8f 'next' row)."""
+    tree stands in for synctree_leveldb; with opts ``leveldb`` (the DB's
+    records: a dict or (key, value) pairs) and ``tree_id`` (binary) it opens
+    the tree those records hold, as synctree_leveldb:new/1 + reload_top_hash
+    would (synctree_leveldb.erl:59-64, synctree.erl:172-175)."""
     return new(id_, 'default', 'default', synctree_hip, opts)
+
+
+def checkpoint(t, tree_id=b''):
+    """The synctree_leveldb records of tree t (src/synctree_leveldb.erl:104-152),
+    encoded on the device: [(DbKey, term_to_binary(Node))] to write into the
+    peer's LevelDB."""
+    return _device_state(t).snapshot_leveldb(tree_id)
 
 
 def new(id_=None, width='default', segments='default', mod=synctree_hip, opts=()):
@@ -89,11 +98,17 @@ def new(id_=None, width='default', segments='default', mod=synctree_hip, opts=()
     if mod is not synctree_hip:
         raise ValueError('backend %r is not a device backend' % (mod,))
     o = dict(opts) if opts else {}
+    records = o.pop('leveldb', None)
+    tree_id = o.pop('tree_id', b'')
     o.update(width=width, segments=segments)
     try:
         state = mod.new(o)
     except ValueError as e:
         raise SynctreeCrash('case_clause in compute_height/compute_shift: %s' % e)
+    if records is not None:
+        if isinstance(records, dict):
+            records = list(records.items())
+        state.restore_leveldb(records, tree_id)
     t = Tree()
     t.id = id_
     t.width = state.width
