@@ -163,6 +163,20 @@ __global__ void k_run_bounds(const uint32_t *sseg, uint64_t n, uint64_t S, uint6
     }
 }
 
+// Same result for batches much smaller than S (a single-key insert/3): one
+// lane per segment, lower_bound of s in the sorted segment ids (the loop
+// form above would walk all S + 1 bounds in one lane).
+__global__ void k_run_bounds_search(const uint32_t *sseg, uint64_t n, uint64_t S, uint64_t *bseg_off) {
+    for (uint64_t s = gtid(); s <= S; s += gstride()) {
+        uint64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (sseg[mid] < s) lo = mid + 1; else hi = mid;
+        }
+        bseg_off[s] = lo;
+    }
+}
+
 struct BatchView {
     const uint8_t *kheap;
     const uint64_t *koff;

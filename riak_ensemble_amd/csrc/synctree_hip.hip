@@ -705,7 +705,10 @@ static int ingest(st_tree *t, IngestIn &in) {
         HIPCHK(hipMemcpyAsync(sseg, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
         HIPCHK(hipMemcpyAsync(perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
     }
-    LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
+    if (n < S)
+        LAUNCH(t, "run_bounds", k_run_bounds_search, grid_for(S + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
+    else
+        LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
     if (t->partitioned) LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bseg_off, S, t->part_lo, t->part_hi);
     BatchView bv{in.krec, in.koff};
     LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, perm, (const uint64_t *)bseg_off, S, keep);
