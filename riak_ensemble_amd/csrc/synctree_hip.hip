@@ -1279,14 +1279,21 @@ static int fetch_entries(st_tree *t, const uint64_t *d_idx, uint64_t n, st_resul
     if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, vl, vo, n + 1))) { done(); return r; }
     res->koff = (uint64_t *)calloc(n + 1, 8);
     res->aoff = (uint64_t *)calloc(n + 1, 8);
-    if ((r = d2h(t, res->koff, ko, (n + 1) * 8)) || (r = d2h(t, res->aoff, vo, (n + 1) * 8))) { done(); return r; }
+    if (hipMemcpyAsync(res->koff, ko, (n + 1) * 8, hipMemcpyDeviceToHost, t->stream) != hipSuccess) {
+        done(); g_err = "hipMemcpyAsync"; return ST_EDEVICE;
+    }
+    if ((r = d2h(t, res->aoff, vo, (n + 1) * 8))) { done(); return r; }
     const uint64_t kb = res->koff[n], vb = res->aoff[n];
     if ((r = dalloc(t, (void **)&kh, kb + 16)) || (r = dalloc(t, (void **)&vh, vb + 16))) { done(); return r; }
     LAUNCH(t, "entry_gather", k_entry_gather, grid_for(n), 256, 0, d, d_idx, n, (const uint64_t *)ko, kh,
            (const uint64_t *)vo, vh);
     res->kheap = (uint8_t *)malloc(kb + 1);
     res->aheap = (uint8_t *)malloc(vb + 1);
-    if ((r = d2h(t, res->kheap, kh, kb)) || (r = d2h(t, res->aheap, vh, vb))) { done(); return r; }
+    if (kb && hipMemcpyAsync(res->kheap, kh, kb, hipMemcpyDeviceToHost, t->stream) != hipSuccess) {
+        done(); g_err = "hipMemcpyAsync"; return ST_EDEVICE;
+    }
+    if ((r = d2h(t, res->aheap, vh, vb))) { done(); return r; }
+    if (!vb) HIPCHK(hipStreamSynchronize(t->stream));
     done();
     (void)keys;
     return ST_OK;
@@ -1368,8 +1375,10 @@ extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const 
         hipLaunchKernelGGL(k_lookup, dim3(grid_for(n)), dim3(256), 0, t->stream, d, bv, seg, n, found);
         std::vector<uint32_t> ps(n), sg(n);
         std::vector<uint64_t> fd(n);
-        r = d2h(t, ps.data(), pst, n * 4);
-        if (!r) r = d2h(t, sg.data(), seg, n * 4);
+        // one sync for the three per-key outputs
+        if (hipMemcpyAsync(ps.data(), pst, n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess ||
+            hipMemcpyAsync(sg.data(), seg, n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess)
+            r = ST_EDEVICE;
         if (!r) r = d2h(t, fd.data(), found, n * 8);
         if (!r) {
             for (uint64_t i = 0; i < n; i++) {
