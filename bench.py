@@ -532,9 +532,24 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
         t.rehash()
         top = t.top_hash()
         best = min(best, time.perf_counter() - t0)
-        t.close()
+    # the per-key verified-path calls (get/2, insert/3,
+    # synctree.erl:189-227) one at a time through the C-ABI (ctypes), i.e. the
+    # low-batch latency path; the tree is the 100k-key one just built
+    kl = [int(k) for k in keys[:200]]
+    t0 = time.perf_counter()
+    for k in kl:
+        t.get_batch([k])
+    gpu_get_us = (time.perf_counter() - t0) / len(kl) * 1e6
+    t0 = time.perf_counter()
+    for k in kl:
+        t.insert_batch([k], [b'\x00' * 17])
+    gpu_ins_us = (time.perf_counter() - t0) / len(kl) * 1e6
+    t.close()
     out = {'gpu_keys_per_s': round(n / best, 1), 'gpu_ms': round(best * 1e3, 3),
-           'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)'}
+           'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)',
+           'per_key_latency_us': {'gpu_get': round(gpu_get_us, 1), 'gpu_insert': round(gpu_ins_us, 1),
+                                  'what': 'one get/2 or insert/3 per C-ABI call (verified path + dirty-path '
+                                          'rehash on the device), 200 calls, ctypes overhead included'}}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle_c
@@ -545,6 +560,14 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
         ot.rehash()
         ctop = ot.top_hash()
         dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for k in kl:
+            ot.get(k)
+        out['per_key_latency_us']['cpu_get'] = round((time.perf_counter() - t0) / len(kl) * 1e6, 1)
+        t0 = time.perf_counter()
+        for k in kl:
+            ot.insert(k, b'\x00' * 17)
+        out['per_key_latency_us']['cpu_insert'] = round((time.perf_counter() - t0) / len(kl) * 1e6, 1)
         assert ctop == top, 'config1: CPU restatement and GPU disagree'
         out['cpu'] = {'keys_per_s': round(n / dt, 1), 'seconds': round(dt, 3), 'cores': 1, 'kind': 'port',
                       'sample': 'oracle/synctree_oracle.c: 100k verified inserts (ctypes per key) + rehash + top_hash'}
