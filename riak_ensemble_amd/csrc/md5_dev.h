@@ -213,68 +213,6 @@ __device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
 
-// Two independent messages in one lane, compressed interleaved (ILP 2 on
-// the ~6-cycle dependent-latency MD5 chain).  Blocks past a message's end
-// are computed and discarded (callers pair messages of equal block count).
-__device__ __forceinline__ void md5_global_x2(const uint8_t *p1, uint64_t len1, const uint8_t *p2, uint64_t len2,
-                                              uint32_t o1[4], uint32_t o2[4]) {
-    uint32_t s1[4], s2[4];
-    init(s1);
-    init(s2);
-    const uint64_t n1 = (len1 + 8) / 64 + 1, n2 = (len2 + 8) / 64 + 1;
-    const uint64_t nb = n1 > n2 ? n1 : n2;
-    uint32_t x1[16], x2[16];
-#pragma unroll
-    for (int w = 0; w < 16; w++) { x1[w] = 0u; x2[w] = 0u; }
-    if (len1 > 0) load_block_global(p1, x1);
-    if (len2 > 0) load_block_global(p2, x2);
-    for (uint64_t k = 0; k < nb; k++) {
-        uint32_t m1[16], m2[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) { m1[w] = x1[w]; m2[w] = x2[w]; }
-        const int64_t r1 = (int64_t)len1 - (int64_t)(64 * k), r2 = (int64_t)len2 - (int64_t)(64 * k);
-        if (r1 - 64 > 0) load_block_global(p1 + 64 * (k + 1), x1);
-        if (r2 - 64 > 0) load_block_global(p2 + 64 * (k + 1), x2);
-        if (r1 < 64) pad_block(m1, r1, k + 1 == n1, len1);
-        if (r2 < 64) pad_block(m2, r2, k + 1 == n2, len2);
-        uint32_t t1[4] = {s1[0], s1[1], s1[2], s1[3]}, t2[4] = {s2[0], s2[1], s2[2], s2[3]};
-        compress(t1, m1);
-        compress(t2, m2);
-        const bool u1 = k < n1, u2 = k < n2;
-#pragma unroll
-        for (int i = 0; i < 4; i++) { s1[i] = u1 ? t1[i] : s1[i]; s2[i] = u2 ? t2[i] : s2[i]; }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) { o1[i] = s1[i]; o2[i] = s2[i]; }
-}
-
-// MD5 of len bytes at byte offset `off` of an LDS buffer (any alignment):
-// 17 aligned dword reads + alignbit per block, next block read ahead.  The
-// buffer must be readable 68 bytes past off+len.
-__device__ __forceinline__ void md5_lds_at(const uint32_t *buf, uint32_t off, uint32_t len, uint32_t out[4]) {
-    uint32_t st[4];
-    init(st);
-    const uint32_t nblk = (len + 8) / 64 + 1;
-    const uint32_t *pw = buf + (off >> 2);
-    const uint32_t sh = (off & 3) * 8;
-    uint32_t nx[17];
-#pragma unroll
-    for (int w = 0; w < 17; w++) nx[w] = pw[w];
-    for (uint32_t k = 0; k < nblk; k++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) m[w] = __builtin_amdgcn_alignbit(nx[w + 1], nx[w], sh);
-        const int32_t rem = (int32_t)len - (int32_t)(64 * k);
-        if (k + 1 < nblk) {
-#pragma unroll
-            for (int w = 0; w < 17; w++) nx[w] = pw[16 * (k + 1) + w];
-        }
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        compress(st, m);
-    }
-    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
-}
-
 // MD5 of a FULL W=16 inner node: 16 present children, message = 16 x
 // (prefix byte ‖ 16 md5 bytes) = 272 bytes = 5 blocks, assembled in
 // registers.  Chunk j starts at byte 17j, so the byte alignment cycles every
@@ -359,31 +297,6 @@ __device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[
     for (int k = 0; k < 5; k++) {
         uint32_t m[16];
         node16_block(k, pf, h, m);
-        compress(st, m);
-    }
-    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
-}
-
-// md5_lds for a 16-byte aligned message whose region spans whole 64-byte
-// blocks (ds_read_b128 reads, next block read ahead).
-__device__ __forceinline__ void md5_lds_a16(const uint8_t *p, uint32_t len, uint32_t out[4]) {
-    uint32_t st[4];
-    init(st);
-    const uint32_t nblk = (len + 8) / 64 + 1;
-    const uint4 *pq = reinterpret_cast<const uint4 *>(p);
-    uint4 nx[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) nx[q] = pq[q];
-    for (uint32_t k = 0; k < nblk; k++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) { m[4 * q] = nx[q].x; m[4 * q + 1] = nx[q].y; m[4 * q + 2] = nx[q].z; m[4 * q + 3] = nx[q].w; }
-        const int32_t rem = (int32_t)len - (int32_t)(64 * k);
-        if (k + 1 < nblk) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) nx[q] = pq[4 * (k + 1) + q];
-        }
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
         compress(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];

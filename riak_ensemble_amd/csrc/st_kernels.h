@@ -473,48 +473,6 @@ struct MergeArgs {
     uint64_t S;
 };
 
-template <bool WRITE>
-__global__ void k_merge(MergeArgs a, uint64_t *cnt_or_off, uint64_t *src, uint8_t *dirty) {
-    for (uint64_t s = gtid(); s < a.S; s += gstride()) {
-        uint64_t i = a.seg_off ? a.seg_off[s] : 0, ie = a.seg_off ? a.seg_off[s + 1] : 0;
-        uint64_t j = a.bseg_off[s], je = a.bseg_off[s + 1];
-        if (a.seg_reject && a.seg_reject[s]) j = je;
-        if (a.seg_replace && a.seg_replace[s]) i = ie;
-        uint64_t out = WRITE ? cnt_or_off[s] : 0;
-        bool changed = false;
-        while (i < ie || j < je) {
-            if (j < je && !a.keep[j]) { j++; continue; }
-            int c;
-            uint32_t bi = 0;
-            if (j < je) bi = a.perm[j];
-            if (i < ie && j < je) {
-                c = rec_cmp(a.kheap + a.koff[i], a.koff[i + 1] - a.koff[i], a.bv.kheap + a.bv.koff[bi],
-                            a.bv.koff[bi + 1] - a.bv.koff[bi]);
-            } else {
-                c = (i < ie) ? -1 : 1;
-            }
-            if (c < 0) {
-                if (WRITE) src[out] = i;
-                out++;
-                i++;
-            } else {
-                const bool erase = a.bop && a.bop[bi];
-                if (!erase) {
-                    if (WRITE) src[out] = (1ull << 63) | bi;
-                    out++;
-                }
-                changed = true;
-                if (c == 0) i++;
-                j++;
-            }
-        }
-        if (!WRITE) {
-            cnt_or_off[s] = out;
-            if (dirty) dirty[s] = changed ? 1 : 0;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Parallel merge.  k_merge walks every segment's old entries serially (one
 // thread per segment, ~100 entries per segment in a 100M-key tree) and writes
@@ -656,12 +614,6 @@ __global__ void k_seg_voff(const uint64_t *seg_off, const uint64_t *voff, uint64
 // Per batch key: insert status from its segment's path status.
 __global__ void k_key_status(const uint32_t *seg, uint64_t n, const uint8_t *seg_reject, uint32_t *clevel) {
     for (uint64_t i = gtid(); i < n; i += gstride()) clevel[i] = seg_reject[seg[i]];
-}
-
-__global__ void k_count_nonzero(const uint8_t *flags, uint64_t n, unsigned long long *cnt) {
-    uint32_t c = 0;
-    for (uint64_t i = gtid(); i < n; i += gstride()) c += flags[i] ? 1u : 0u;
-    if (c) atomicAdd(cnt, (unsigned long long)c);
 }
 
 // ---------------------------------------------------------------------------
@@ -1001,346 +953,6 @@ __global__ void k_entry_gather(DevTree t, const uint64_t *idx, uint64_t n, const
 }
 
 // ---------------------------------------------------------------------------
-// Fused rehash (K1 + the first d levels of K2 in one launch).
-//
-// One workgroup per subtree of SEGS = W^d consecutive segments (W^d <= 256,
-// d <= H): every lane hashes one segment (the lanes are assigned segments in
-// order of their MD5 block count, so the 64 lanes of a wave run loops of
-// (nearly) equal length), the entries stay in LDS, and the workgroup then
-// reduces the d levels above them (rehash/4, synctree.erl:515-535) with one
-// lane per node.  With a mask (dirty-path rehash after inserts) only marked
-// nodes are recomputed; unmarked ones keep their stored entry, exactly like
-// update_path leaves untouched siblings alone.
-
-struct SubtreeLds {
-    uint4 *md5;      // SEGS entries of the current level (then SEGS/W, ...)
-    uint32_t *tag;
-    uint4 *md5b;     // next level
-    uint32_t *tagb;
-    uint32_t *hist;  // 64 bins
-    uint32_t *perm;  // SEGS
-    uint8_t *stage;  // per-lane inner-node staging
-};
-
-__host__ __device__ __forceinline__ uint32_t subtree_lds_bytes(uint32_t W, uint32_t segs) {
-    uint32_t b = segs * 16 * 2 + segs * 4 * 2 + 64 * 4 + segs * 4;
-    const uint32_t inner_lanes = segs / W > 0 ? segs / W : 1;
-    b = (b + 15) & ~15u;
-    return b + inner_lanes * lane_region_bytes(W);
-}
-
-__device__ __forceinline__ uint32_t stage_entries(uint32_t W, const uint4 *md5, const uint32_t *tag, uint32_t c0,
-                                                  uint8_t *reg) {
-    MsgWriter mw;
-    mw.init(reg);
-    for (uint32_t j = 0; j < W; j++) {
-        const uint32_t ct = tag[c0 + j];
-        if (ct & TAG_PRESENT) mw.entry(ct, md5[c0 + j]);
-    }
-    return mw.finish();
-}
-
-__global__ void __launch_bounds__(256) k_rehash_subtree(DevTree t, uint32_t dseg, uint32_t segs, uint32_t d,
-                                                        const uint8_t *mask, uint32_t ilp2) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    SubtreeLds L;
-    L.md5 = reinterpret_cast<uint4 *>(lds);
-    L.md5b = L.md5 + segs;
-    L.tag = reinterpret_cast<uint32_t *>(L.md5b + segs);
-    L.tagb = L.tag + segs;
-    L.hist = L.tagb + segs;
-    L.perm = L.hist + 64;
-    L.stage = lds + ((segs * 16 * 2 + segs * 4 * 2 + 64 * 4 + segs * 4 + 15) & ~15u);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t H1 = t.H + 1;
-    const uint64_t s0 = (uint64_t)blockIdx.x * segs;
-    // subtree root (level H1-d, bucket blockIdx.x): nothing to do when unmarked
-    if (mask && !mask[t.base[H1 - dseg] + blockIdx.x]) return;
-
-    // ---- lane -> segment assignment by MD5 block count (LDS counting sort)
-    if (tid < 64) L.hist[tid] = 0;
-    __syncthreads();
-    uint32_t mybin[2] = {0, 0};
-    for (uint32_t q = 0, i = tid; q < 2 && i < segs; q++, i += blockDim.x) {
-        const uint64_t s = s0 + i;
-        const uint64_t bytes = t.seg_voff[s + 1] - t.seg_voff[s];
-        uint64_t blocks = (bytes + 8) / 64 + 1;
-        mybin[q] = 63 - (blocks > 63 ? 63u : (uint32_t)blocks);   // longest first
-        atomicAdd(&L.hist[mybin[q]], 1u);
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < 64; b++) { const uint32_t c = L.hist[b]; L.hist[b] = acc; acc += c; }
-    }
-    __syncthreads();
-    for (uint32_t q = 0, i = tid; q < 2 && i < segs; q++, i += blockDim.x) L.perm[atomicAdd(&L.hist[mybin[q]], 1u)] = i;
-    __syncthreads();
-
-    // ---- K1: segment hashes.  ilp2: a lane takes two neighbouring positions
-    // of the block-count order (two equally long messages, interleaved).
-    const uint32_t per = ilp2 ? 2 : 1;
-    for (uint32_t pos = tid * per; pos < segs && pos < (tid + 1) * per; pos += per) {
-        uint32_t li[2] = {L.perm[pos], per == 2 && pos + 1 < segs ? L.perm[pos + 1] : L.perm[pos]};
-        const uint32_t cnt = (per == 2 && pos + 1 < segs) ? 2 : 1;
-        uint64_t s_[2], slot[2];
-        bool work[2];
-        for (uint32_t q = 0; q < 2; q++) {
-            s_[q] = s0 + li[q];
-            slot[q] = t.base[H1] + s_[q];
-            work[q] = q < cnt && !(mask && !mask[slot[q]]) && t.seg_off[s_[q]] != t.seg_off[s_[q] + 1];
-        }
-        uint32_t d1[4] = {0, 0, 0, 0}, d2[4] = {0, 0, 0, 0};
-        if (cnt == 2 && work[0] && work[1]) {
-            const uint64_t a0 = t.seg_voff[s_[0]], b0 = t.seg_voff[s_[1]];
-            stmd5::md5_global_x2(t.vheap + a0, t.seg_voff[s_[0] + 1] - a0, t.vheap + b0, t.seg_voff[s_[1] + 1] - b0,
-                                 d1, d2);
-        } else {
-            if (work[0]) {
-                const uint64_t a0 = t.seg_voff[s_[0]];
-                stmd5::md5_global_pf(t.vheap + a0, t.seg_voff[s_[0] + 1] - a0, d1);
-            }
-            if (cnt == 2 && work[1]) {
-                const uint64_t b0 = t.seg_voff[s_[1]];
-                stmd5::md5_global_pf(t.vheap + b0, t.seg_voff[s_[1] + 1] - b0, d2);
-            }
-        }
-        for (uint32_t q = 0; q < cnt; q++) {
-            const uint32_t *dg = q == 0 ? d1 : d2;
-            uint4 e;
-            uint32_t tg;
-            if (mask && !mask[slot[q]]) {
-                e = t.md5[slot[q]];
-                tg = t.tag[slot[q]];
-            } else if (!work[q]) {
-                e = make_uint4(0, 0, 0, 0);
-                tg = 0;
-                t.tag[slot[q]] = 0;
-                if (H1 == 1) t.tag[0] = 0;
-            } else {
-                e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-                tg = TAG_PRESENT;
-                t.md5[slot[q]] = e;
-                t.tag[slot[q]] = TAG_PRESENT;
-                if (H1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
-            }
-            L.md5[li[q]] = e;
-            L.tag[li[q]] = tg;
-        }
-    }
-    __syncthreads();
-
-    // ---- the d levels above, one lane per node.  Only wave 0 stays (the
-    // widest of these levels has segs/W <= 64 nodes when W >= 4); the other
-    // waves leave so their slots go to other workgroups' segment hashing.
-    if (d == 0) return;
-    const bool one_wave = (segs / t.W) <= 64;
-    if (one_wave && tid >= 64) return;
-    uint32_t nodes = segs;
-    uint4 *cm = L.md5, *nm = L.md5b;
-    uint32_t *ct = L.tag, *nt = L.tagb;
-    for (uint32_t q = 1; q <= d; q++) {
-        nodes /= t.W;
-        const uint32_t lvl = H1 - q;
-        if (tid < nodes) {
-            const uint64_t b = ((uint64_t)blockIdx.x * nodes) + tid;
-            const uint64_t slot = t.base[lvl] + b;
-            uint4 e;
-            uint32_t tg;
-            if (mask && !mask[slot]) {
-                e = t.md5[slot];
-                tg = t.tag[slot];
-            } else {
-                uint8_t *reg = L.stage + tid * lane_region_bytes(t.W);
-                const uint32_t len = stage_entries(t.W, cm, ct, tid * t.W, reg);
-                if (len == 0) {
-                    e = make_uint4(0, 0, 0, 0);
-                    tg = 0;
-                } else {
-                    uint32_t dg[4];
-                    stmd5::md5_lds(reg, len, dg);
-                    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-                    tg = TAG_PRESENT;
-                    t.md5[slot] = e;
-                }
-                t.tag[slot] = (uint16_t)tg;
-                if (lvl == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
-            }
-            nm[tid] = e;
-            nt[tid] = tg;
-        }
-        if (one_wave) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            __syncthreads();
-        }
-        uint4 *xm = cm; cm = nm; nm = xm;
-        uint32_t *xt = ct; ct = nt; nt = xt;
-    }
-}
-
-// The remaining upper levels [lmin, lmax] (at most 256 nodes each) in ONE
-// workgroup, level by level (entries of level lmax+1 come from the previous
-// launch).  Dynamic LDS: 256 lane regions.
-__global__ void __launch_bounds__(256) k_rehash_upper_levels(DevTree t, uint32_t lmin, uint32_t lmax,
-                                                             const uint8_t *mask) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(t.W);
-    for (uint32_t l = lmax; l >= lmin; l--) {
-        const uint64_t nodes = t.base[l + 1] - t.base[l];
-        for (uint64_t b = threadIdx.x; b < nodes; b += blockDim.x) {
-            const uint64_t slot = t.base[l] + b;
-            if (mask && !mask[slot]) continue;
-            const uint32_t len = stage_inner(t, l, b, reg);
-            uint32_t tg = 0;
-            uint4 e = make_uint4(0, 0, 0, 0);
-            if (len) {
-                uint32_t dg[4];
-                stmd5::md5_lds(reg, len, dg);
-                e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-                tg = TAG_PRESENT;
-                t.md5[slot] = e;
-            }
-            t.tag[slot] = (uint16_t)tg;
-            if (l == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
-        }
-        __syncthreads();
-        if (l == lmin) break;
-    }
-}
-
-// Levels [H+1-dl, H] in one launch: one single-wave workgroup per subtree of
-// W^(dl-1) <= 64 level-H nodes.  Lanes stage their node's W child entries from
-// global memory, hash, keep the result in LDS for the next level up; the
-// wave reduces dl levels with wave-level syncs only.  Serial-MD5 latency per
-// level is what bounds this, so every workgroup is one short wave.
-__global__ void __launch_bounds__(64) k_rehash_levels_wave(DevTree t, uint32_t dl, const uint8_t *mask) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x;
-    uint32_t nodes = 1;
-    for (uint32_t q = 1; q < dl; q++) nodes *= t.W;      // level-H nodes of this subtree
-    uint4 *em = reinterpret_cast<uint4 *>(lds);           // 64 entries (current level)
-    uint32_t *et = reinterpret_cast<uint32_t *>(em + 64);
-    uint8_t *reg = lds + 64 * 20 + lane * lane_region_bytes(t.W);
-    const uint32_t H = t.H;
-    for (uint32_t q = 0; q < dl; q++) {
-        const uint32_t lvl = H - q;
-        uint4 e = make_uint4(0, 0, 0, 0);
-        uint32_t tg = 0;
-        const bool act = lane < nodes;
-        const uint64_t b = (uint64_t)blockIdx.x * nodes + lane;
-        const uint64_t slot = t.base[lvl] + b;
-        if (act) {
-            if (mask && !mask[slot]) {
-                e = t.md5[slot];
-                tg = t.tag[slot];
-            } else {
-                const uint32_t len = (q == 0) ? stage_inner(t, lvl, b, reg)
-                                              : stage_entries(t.W, em, et, lane * t.W, reg);
-                if (len) {
-                    uint32_t dg[4];
-                    stmd5::md5_lds(reg, len, dg);
-                    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-                    tg = TAG_PRESENT;
-                    t.md5[slot] = e;
-                }
-                t.tag[slot] = (uint16_t)tg;
-                if (lvl == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (act) { em[lane] = e; et[lane] = tg; }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        nodes /= t.W;
-        if (nodes == 0) break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K1 segment_hash, LDS-staged (the rehash hot loop).
-//
-// One wave per 64 consecutive segments.  Their values are ONE contiguous byte
-// range of the value heap (CSR order), so the wave first copies that range
-// into its LDS slice with coalesced 16-byte loads (every HBM byte read once,
-// full lines, many bytes in flight), then each lane hashes one segment out of
-// LDS.  Lanes take segments in order of MD5 block count (wave bitonic sort)
-// so a wave's 64 loops have (nearly) equal trip counts.  A wave whose range
-// does not fit its slice hashes straight from global memory instead.
-#define K1_WAVES 4
-#define K1_SLICE 13312   // bytes of LDS per wave (the 64-segment range + 80 B)
-
-__device__ __forceinline__ uint32_t wave_sort_key(uint32_t key) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t o = __shfl_xor(key, j, 64);
-            const bool up = ((lane & k) == 0);
-            const bool lower = (lane & j) == 0;
-            const uint32_t mn = key < o ? key : o, mx = key < o ? o : key;
-            key = (lower == up) ? mn : mx;
-        }
-    }
-    return key;
-}
-
-__global__ void __launch_bounds__(64 * K1_WAVES) k_segment_hash_lds(DevTree t, const uint8_t *mask) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint8_t *slice = lds + wave * K1_SLICE;
-    const uint32_t L1 = t.H + 1;
-    const uint64_t s0 = ((uint64_t)blockIdx.x * K1_WAVES + wave) * 64;
-    if (s0 >= t.S) return;
-    const uint64_t nseg = (t.S - s0) < 64 ? (t.S - s0) : 64;
-    // this lane's own segment (natural order) -> sort key = (255 - blocks) << 6 | lane
-    const uint64_t my = s0 + (lane < nseg ? lane : 0);
-    const uint64_t mv0 = t.seg_voff[my], mv1 = t.seg_voff[my + 1];
-    uint32_t blocks = (uint32_t)((mv1 - mv0 + 8) / 64 + 1);
-    blocks = blocks > 255 ? 255 : blocks;
-    uint32_t key = lane < nseg ? (((255u - blocks) << 6) | lane) : (0xffffffu);
-    key = wave_sort_key(key);
-    const uint32_t src = key & 63;                       // lane whose segment I hash
-    const bool act = key != 0xffffffu;
-    const uint64_t v0 = __shfl(mv0, 0, 64);
-    const uint64_t vend = __shfl(mv1, (int)(nseg - 1), 64);
-    const uint64_t a0 = v0 & ~15ull;
-    const uint64_t need = vend - a0 + 80;
-    const bool staged = need <= K1_SLICE;
-    if (staged) {
-        const uint4 *g = reinterpret_cast<const uint4 *>(t.vheap + a0);
-        uint4 *l = reinterpret_cast<uint4 *>(slice);
-        const uint32_t chunks = (uint32_t)((need + 15) / 16);
-        for (uint32_t c = lane; c < chunks; c += 64) l[c] = g[c];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    const uint64_t s = s0 + src;
-    const uint64_t sv0 = __shfl(mv0, (int)src, 64), sv1 = __shfl(mv1, (int)src, 64);
-    if (!act) return;
-    const uint64_t slot = t.base[L1] + s;
-    if (mask && !mask[slot]) return;
-    if (t.seg_off[s] == t.seg_off[s + 1]) {
-        t.tag[slot] = 0;
-        if (L1 == 1) t.tag[0] = 0;
-        return;
-    }
-    uint32_t dg[4];
-    if (staged) stmd5::md5_lds_at(reinterpret_cast<const uint32_t *>(slice), (uint32_t)(sv0 - a0), (uint32_t)(sv1 - sv0), dg);
-    else stmd5::md5_global_pf(t.vheap + sv0, sv1 - sv0, dg);
-    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-    t.md5[slot] = e;
-    t.tag[slot] = TAG_PRESENT;
-    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
-}
-
-// ---------------------------------------------------------------------------
 // Rehash v3 kernels.
 //
 // k_seg_perm_*: order segments by MD5 block count (descending; empty last),
@@ -1492,125 +1104,6 @@ __global__ void __launch_bounds__(256) k_upper16(DevTree t, uint32_t lmin, uint3
         __syncthreads();
         if (l == lmin) break;
     }
-}
-
-// K1 segment_hash v4: block-count order + coalesced gather into LDS.
-// One wave per 64 consecutive positions of the block-count order (so its 64
-// segments need (nearly) the same number of MD5 blocks B).  Each segment gets
-// an aligned LDS slot of 64*B bytes; the wave copies all slots with
-// consecutive lanes on consecutive 16-byte chunks of a segment (a few cache
-// lines per instruction instead of 64), then every lane hashes its segment out
-// of its slot.  Waves whose slots exceed the slice hash from global memory.
-#define K1G_SLICE 20480
-
-__global__ void __launch_bounds__(64) k_segment_hash_gather(DevTree t, const uint32_t *perm, const uint8_t *mask) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint32_t *pre = reinterpret_cast<uint32_t *>(lds + K1G_SLICE);        // 65 words after the slots
-    uint64_t *src = reinterpret_cast<uint64_t *>(lds + K1G_SLICE + 272);  // 64 source offsets
-    const uint32_t lane = threadIdx.x;
-    const uint32_t L1 = t.H + 1;
-    const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
-    const bool inr = p < t.S;
-    const uint64_t s = inr ? perm[p] : 0;
-    const uint64_t slot = t.base[L1] + s;
-    const bool nonempty = inr && t.seg_off[s] != t.seg_off[s + 1];
-    const bool work = nonempty && !(mask && !mask[slot]);
-    const uint64_t v0 = t.seg_voff[s];
-    const uint32_t len = work ? (uint32_t)(t.seg_voff[s + 1] - v0) : 0u;
-    const uint32_t nblk = work ? (len + 8) / 64 + 1 : 0u;
-    // wave-inclusive scan of chunk counts (4 chunks of 16 B per 64 B block)
-    uint32_t c = nblk * 4, x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    const uint32_t total = __shfl(x, 63, 64);
-    pre[lane + 1] = x;
-    src[lane] = v0;
-    if (lane == 0) pre[0] = 0;
-    uint32_t dg[4];
-    const bool staged = total * 16 <= K1G_SLICE;
-    __syncthreads();
-    if (staged) {
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (uint32_t q = lane; q < total; q += 64) {
-            uint32_t lo = 0, hi = 64;   // segment j with pre[j] <= q < pre[j+1]
-#pragma unroll
-            for (int it = 0; it < 6; it++) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (pre[mid] <= q) lo = mid; else hi = mid;
-            }
-            const uint64_t vj = src[lo];   // (a shuffle here would read inactive lanes as 0)
-            uint4 v;
-            __builtin_memcpy(&v, t.vheap + vj + 16ull * (q - pre[lo]), 16);
-            dst[q] = v;
-        }
-        __syncthreads();
-        if (work) stmd5::md5_lds(lds + 16u * (x - c), len, dg);
-    } else if (work) {
-        stmd5::md5_global_pf(t.vheap + v0, len, dg);
-    }
-    if (!inr || (mask && !mask[slot])) return;
-    if (!nonempty) {
-        t.tag[slot] = 0;
-        if (L1 == 1) t.tag[0] = 0;
-        return;
-    }
-    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-    t.md5[slot] = e;
-    t.tag[slot] = TAG_PRESENT;
-    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
-}
-
-// K1 segment_hash v5: block-count order; a wave whose 64 segments all need
-// the same B <= 4 blocks (the common case in that order) gathers them into
-// 64-byte-aligned LDS slots with fully coalesced loads (consecutive lanes on
-// consecutive 16 B of a segment) and hashes from LDS; any other wave loads
-// directly from global memory.
-#define K1U_MAXB 4
-__global__ void __launch_bounds__(64) k_segment_hash_v5(DevTree t, const uint32_t *perm, const uint8_t *mask) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t L1 = t.H + 1;
-    const uint64_t p = (uint64_t)blockIdx.x * 64 + lane;
-    const bool inr = p < t.S;
-    const uint64_t s = inr ? perm[p] : 0;
-    const uint64_t slot = t.base[L1] + s;
-    const bool nonempty = inr && t.seg_off[s] != t.seg_off[s + 1];
-    const bool work = nonempty && !(mask && !mask[slot]);
-    const uint64_t v0 = t.seg_voff[s];
-    const uint32_t len = work ? (uint32_t)(t.seg_voff[s + 1] - v0) : 0u;
-    const uint32_t nblk = work ? (len + 8) / 64 + 1 : 0u;
-    const uint32_t B = __shfl(nblk, 0, 64);
-    const bool uniform = (__ballot(nblk == B) == ~0ull) && B >= 1 && B <= K1U_MAXB;
-    uint32_t dg[4];
-    if (uniform) {
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        const uint32_t per = 4 * B;            // 16-byte chunks per segment
-        for (uint32_t it = 0; it < per; it++) {
-            const uint32_t q = it * 64 + lane;
-            const uint32_t j = q / per, k = q - j * per;
-            const uint64_t vj = __shfl(v0, (int)j, 64);   // every lane active here
-            uint4 v;
-            __builtin_memcpy(&v, t.vheap + vj + 16ull * k, 16);
-            dst[q] = v;
-        }
-        __syncthreads();
-        stmd5::md5_lds_a16(lds + 64u * B * lane, len, dg);
-    } else if (work) {
-        stmd5::md5_global_pf(t.vheap + v0, len, dg);
-    }
-    if (!inr || (mask && !mask[slot])) return;
-    if (!nonempty) {
-        t.tag[slot] = 0;
-        if (L1 == 1) t.tag[0] = 0;
-        return;
-    }
-    const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-    t.md5[slot] = e;
-    t.tag[slot] = TAG_PRESENT;
-    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
 }
 
 // ---------------------------------------------------------------------------
@@ -1839,45 +1332,6 @@ __global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint
     if ((threadIdx.x & 63) == 0 && tl < ntiles) tsize[tl] = (uint64_t)m * 256;
 }
 
-// One wave per tile.  Writes every segment's entry (absent segments: tag 0).
-__global__ void __launch_bounds__(64) k_segment_hash_tiled(DevTree t, const TileInfo *__restrict__ tinfo,
-                                                           const uint32_t *__restrict__ tseg,
-                                                           const uint32_t *__restrict__ tnb,
-                                                           const uint4 *__restrict__ tiles) {
-    const uint32_t lane = threadIdx.x;
-    const uint64_t tl = blockIdx.x;
-    const TileInfo ti = tinfo[tl];
-    const uint32_t seg = tseg[tl * 64 + lane];
-    const uint32_t nb = tnb[tl * 64 + lane];
-    const uint32_t B = ti.B;
-    uint32_t st[4];
-    stmd5::init(st);
-    if (B) {
-        const uint4 *b = tiles + ti.base + lane;
-        uint4 n0 = b[0], n1 = b[64], n2 = b[128], n3 = b[192];
-        for (uint32_t k = 0; k < B; k++) {
-            uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
-            if (k + 1 < B) {
-                const uint4 *q = b + 256 * (k + 1);
-                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
-            }
-            if (k < nb) stmd5::compress(st, m);
-        }
-    }
-    if (seg == 0xffffffffu) return;
-    const uint32_t L1 = t.H + 1;
-    const uint64_t slot = t.base[L1] + seg;
-    if (!nb) {
-        t.tag[slot] = 0;
-        if (L1 == 1) t.tag[0] = 0;
-        return;
-    }
-    const uint4 e = make_uint4(st[0], st[1], st[2], st[3]);
-    t.md5[slot] = e;
-    t.tag[slot] = TAG_PRESENT;
-    if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
-}
-
 // ---------------------------------------------------------------------------
 // K2 full level rehash (W == 16, H >= 3) in ONE launch with ONE inlined copy
 // of the node-hash code.  A workgroup per level-(H-2) subtree stages its 4096
@@ -2025,11 +1479,9 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
 #undef FLOW_STAMP
 }
 
-// K1 variants over the same tiles (A/B, env ST_K1T):
-//  1: persistent waves, grid-stride over tiles; the next tile's info and first
-//     block are fetched while the current tile's last block is hashed.
-//  2: two adjacent tiles per wave (2 x 64 segments), their MD5 chains
-//     interleaved in every lane (ILP 2).
+// K1 over the tiles: persistent waves, grid-stride over tiles; the next
+// tile's info and first block are fetched while the current tile's last
+// block is hashed.
 __device__ __forceinline__ void tile_store(const DevTree &t, uint4 *md5, uint16_t *tag, uint32_t seg, uint32_t nb,
                                            const uint32_t st[4]) {
     if (seg == 0xffffffffu) return;
@@ -2105,44 +1557,6 @@ __global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTil
         seg = segn;
         nb = nbn;
     }
-}
-
-__global__ void __launch_bounds__(64) k_segment_hash_tiled_x2(DevTree t, const TileInfo *__restrict__ tinfo,
-                                                              const uint32_t *__restrict__ tseg,
-                                                              const uint32_t *__restrict__ tnb,
-                                                              const uint4 *__restrict__ tiles, uint64_t ntiles) {
-    const uint32_t lane = threadIdx.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * 2, t1 = t0 + 1;
-    const bool has1 = t1 < ntiles;
-    const TileInfo i0 = tinfo[t0];
-    TileInfo i1;
-    i1.base = 0; i1.B = 0; i1.pad = 0;
-    if (has1) i1 = tinfo[t1];
-    const uint32_t s0 = tseg[t0 * 64 + lane], b0 = tnb[t0 * 64 + lane];
-    const uint32_t s1 = has1 ? tseg[t1 * 64 + lane] : 0xffffffffu, b1 = has1 ? tnb[t1 * 64 + lane] : 0u;
-    const uint32_t B = i0.B > i1.B ? i0.B : i1.B;
-    uint32_t st0[4], st1[4];
-    stmd5::init(st0);
-    stmd5::init(st1);
-    const uint4 *p0 = tiles + i0.base + lane, *p1 = tiles + i1.base + lane;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    uint4 a0 = z, a1 = z, a2 = z, a3 = z, c0 = z, c1 = z, c2 = z, c3 = z;
-    if (i0.B) { a0 = p0[0]; a1 = p0[64]; a2 = p0[128]; a3 = p0[192]; }
-    if (i1.B) { c0 = p1[0]; c1 = p1[64]; c2 = p1[128]; c3 = p1[192]; }
-    for (uint32_t k = 0; k < B; k++) {
-        uint32_t m0[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-        uint32_t m1[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        if (k + 1 < i0.B) { const uint4 *q = p0 + 256 * (k + 1); a0 = q[0]; a1 = q[64]; a2 = q[128]; a3 = q[192]; }
-        if (k + 1 < i1.B) { const uint4 *q = p1 + 256 * (k + 1); c0 = q[0]; c1 = q[64]; c2 = q[128]; c3 = q[192]; }
-        uint32_t u0[4] = {st0[0], st0[1], st0[2], st0[3]}, u1[4] = {st1[0], st1[1], st1[2], st1[3]};
-        stmd5::compress(u0, m0);
-        stmd5::compress(u1, m1);
-        const bool g0 = k < b0, g1 = k < b1;
-#pragma unroll
-        for (int i = 0; i < 4; i++) { st0[i] = g0 ? u0[i] : st0[i]; st1[i] = g1 ? u1[i] : st1[i]; }
-    }
-    tile_store(t, t.md5, t.tag, s0, b0, st0);
-    tile_store(t, t.md5, t.tag, s1, b1, st1);
 }
 
 // One inner level of a batch of trees (W == 16): node i is node i % per of

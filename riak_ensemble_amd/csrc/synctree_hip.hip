@@ -97,6 +97,30 @@ static void dfree(st_tree *t, void *p) {
     if (p) (void)hipFreeAsync(p, t->stream);
 }
 
+// Stream-ordered scratch buffers freed when the scope ends, on every return
+// path (error returns from LAUNCH / HIPCHK / CHK included).  release() hands a
+// buffer over to the caller (e.g. a new CSR swapped into the tree).
+struct Scratch {
+    st_tree *t;
+    std::vector<void *> ps;
+    explicit Scratch(st_tree *t_) : t(t_) {}
+    Scratch(const Scratch &) = delete;
+    ~Scratch() {
+        for (void *p : ps) dfree(t, p);
+    }
+    template <typename T>
+    int alloc(T **p, uint64_t count) {
+        int r = dalloc(t, (void **)p, count * sizeof(T));
+        if (r == ST_OK) ps.push_back((void *)*p);
+        return r;
+    }
+    int bytes(uint8_t **p, uint64_t n) { return alloc(p, n); }
+    void release(void *p) {
+        for (auto &q : ps)
+            if (q == p) q = nullptr;
+    }
+};
+
 static DevTree view(const st_tree *t) {
     DevTree d;
     memset(&d, 0, sizeof(d));
@@ -374,32 +398,20 @@ static int rehash_levels(st_tree *t, uint32_t top_level, const uint8_t *mask) {
     return ST_OK;
 }
 
-// Full or dirty (mask) rehash of segments + every inner level:
-// k_rehash_subtree covers the segments and the d levels above them (W^d <= 256
-// segments per workgroup), per-level kernels any level still wider than 256
-// nodes, and k_rehash_upper_levels the rest in one workgroup.
+// seg_perm: segments by MD5 block count (descending), the K1 order.
 static int ensure_perm(st_tree *t) {
     if (t->perm_valid) return ST_OK;
     DevTree d = view(t);
+    Scratch sc(t);
     uint32_t *cnt = nullptr;
-    CHK(dalloc_t(t, &cnt, PERM_BINS));
+    CHK(sc.alloc(&cnt, PERM_BINS));
     HIPCHK(hipMemsetAsync(cnt, 0, PERM_BINS * 4, t->stream));
     LAUNCH(t, "seg_perm", k_seg_perm_count, grid_for(t->S, 256, 1024), 256, 0, d, cnt);
     LAUNCH(t, "seg_perm", k_seg_perm_scan, 1, 256, 0, cnt);
     LAUNCH(t, "seg_perm", k_seg_perm_scatter, grid_for(t->S, 256, 1024), 256, 0, d, cnt, t->seg_perm);
-    dfree(t, cnt);
     t->perm_valid = true;
     return ST_OK;
 }
-
-// Full-rehash strategy (env ST_REHASH, A/B knob): 2 = tiled K1 in global
-// block-count order + level dataflow (default), 0 = K1 over seg_perm straight
-// from the CSR + per-level kernels.
-static int rehash_mode() {
-    static const int m = getenv("ST_REHASH") ? atoi(getenv("ST_REHASH")) : 2;
-    return m;
-}
-static int ensure_perm(st_tree *t);
 
 // Build the hash-ready tiled messages from the CSR (k_tile_order, scan,
 // k_tile_fill).  Called at the end of every ingest and lazily by rehash.
@@ -409,7 +421,7 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // (k_tile_order_global, scan, k_tile_fill).  Called at the end of every bulk
 // ingest and lazily by rehash.
 static int ensure_tiles(st_tree *t) {
-    if (rehash_mode() != 2 || t->tiles_valid) return ST_OK;
+    if (t->tiles_valid) return ST_OK;
     CHK(ensure_perm(t));
     const uint64_t ntiles = num_tiles(t);
     if (!t->tseg) {
@@ -417,14 +429,14 @@ static int ensure_tiles(st_tree *t) {
         CHK(dalloc_t(t, &t->tnb, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
+    Scratch sc(t);
     uint64_t *tsize = nullptr, *tbase = nullptr;
-    int r = ST_OK;
-    auto done = [&]() { dfree(t, tsize); dfree(t, tbase); };
-    if ((r = dalloc_t(t, &tsize, ntiles + 1)) || (r = dalloc_t(t, &tbase, ntiles + 1))) { done(); return r; }
+    CHK(sc.alloc(&tsize, ntiles + 1));
+    CHK(sc.alloc(&tbase, ntiles + 1));
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
     LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
            (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
-    if ((r = exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1))) { done(); return r; }
+    CHK(exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1));
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
@@ -433,14 +445,13 @@ static int ensure_tiles(st_tree *t) {
         t->tiles = nullptr;
         t->tiles_cap = 0;
         const uint64_t cap = total + total / 8 + 1;
-        if ((r = dalloc_t(t, &t->tiles, cap))) { done(); return r; }
+        CHK(dalloc_t(t, &t->tiles, cap));
         t->tiles_cap = cap;
     }
     LAUNCH(t, "tile_build", k_tile_fill, (uint32_t)ntiles, 256, 0, (const uint64_t *)t->seg_voff, (const uint8_t *)t->vheap,
            (const uint32_t *)t->tseg, (const uint64_t *)tbase, (const uint64_t *)tsize, t->tiles);
     LAUNCH(t, "tile_build", k_tile_info, grid_for(ntiles), 256, 0, (const uint64_t *)tbase, (const uint64_t *)tsize, ntiles,
            t->tinfo);
-    done();
     t->tiles_valid = true;
     return ST_OK;
 }
@@ -464,28 +475,30 @@ static int ensure_lvl_cnt(st_tree *t) {
     return ST_OK;
 }
 
-// Full rehash, default strategy: K1 k_segment_hash_tiled over the global
-// block-count tiles, then (W == 16, H >= 3) every inner level and the top hash
-// in ONE launch of k_levels_flow16 (levels H..H-2 per workgroup, the rest by
-// last-arriving workgroups).  Other geometries use the per-level kernels.
+// Inner levels of a W == 16 tree from level `top` down to 1 (dirty path:
+// only marked nodes) with the per-level kernels: k_level16 while a level is
+// wider than 256 nodes, then k_upper16 for the rest in one workgroup.
+static int levels16(st_tree *t, uint32_t top, const uint8_t *mask) {
+    DevTree d = view(t);
+    uint32_t l = top;
+    for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
+        LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
+               (size_t)64 * lane_region_bytes(16), d, l, mask);
+    if (l >= 1)
+        LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, mask);
+    return ST_OK;
+}
+
+// Full rehash: K1 k_segment_hash_tiled_p over the global block-count tiles,
+// then (W == 16, H >= 3) every inner level and the top hash in ONE launch of
+// k_levels_flow16 (levels H..H-2 per workgroup, the rest by last-arriving
+// workgroups).  Other geometries use the per-level kernels.
 static int rehash_tiled(st_tree *t) {
     CHK(ensure_tiles(t));
     DevTree d = view(t);
-    // K1 variant (env ST_K1T, A/B knob): 1 = persistent waves with cross-tile
-    // prefetch (default; 1024 workgroups x 4 waves), 0 = one wave per tile,
-    // 2 = two tiles per wave interleaved (ILP 2).
-    static const int k1t = getenv("ST_K1T") ? atoi(getenv("ST_K1T")) : 1;
-    static const uint32_t k1wgs = getenv("ST_K1_WGS") ? (uint32_t)atoi(getenv("ST_K1_WGS")) : 1024u;
     const uint64_t ntl = num_tiles(t);
-    if (k1t == 1)
-        LAUNCH(t, "segment_hash", k_segment_hash_tiled_p<false>, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, k1wgs), 256, 0, d,
-               tree_tiles(t), (const TreeTiles *)nullptr, ntl, ntl);
-    else if (k1t == 2)
-        LAUNCH(t, "segment_hash", k_segment_hash_tiled_x2, (uint32_t)((ntl + 1) / 2), 64, 0, d, (const TileInfo *)t->tinfo,
-               (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles, ntl);
-    else
-        LAUNCH(t, "segment_hash", k_segment_hash_tiled, (uint32_t)ntl, 64, 0, d, (const TileInfo *)t->tinfo,
-               (const uint32_t *)t->tseg, (const uint32_t *)t->tnb, (const uint4 *)t->tiles);
+    LAUNCH(t, "segment_hash", k_segment_hash_tiled_p<false>, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, 1024u), 256, 0, d,
+           tree_tiles(t), (const TreeTiles *)nullptr, ntl, ntl);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         CHK(ensure_lvl_cnt(t));
@@ -498,123 +511,55 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t nwg = t->partitioned ? (uint32_t)((t->part_hi - t->part_lo) / sub) : (uint32_t)nroots;
         if (root0 + nwg > nroots || nwg == 0) { g_err = "level rehash range out of bounds"; return ST_EINVAL; }
         const uint32_t lmin = t->partitioned ? 2u : 1u;
-        if (!stamp)
+        if (!stamp) {
             LAUNCH(t, "level_rehash", k_levels_flow16<false>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt,
                    (uint64_t *)nullptr, root0, lmin);
-        else {   // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
-            uint64_t *st = nullptr;
-            CHK(dalloc_t(t, &st, (uint64_t)nwg * 16));
-            HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
-            LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st, root0,
-                   lmin);
-            std::vector<uint64_t> h((uint64_t)nwg * 16);
-            HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
-            HIPCHK(hipStreamSynchronize(t->stream));
-            dfree(t, st);
-            uint64_t t0 = ~0ull;
-            for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
-            for (int k = 0; k < 12; k++) {
-                std::vector<double> v;
-                for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
-                if (v.empty()) continue;
-                std::sort(v.begin(), v.end());
-                fprintf(stderr, "flow stamp %2d: n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, v.size(), v[0], v[v.size() / 2],
-                        v.back());
-            }
+            return ST_OK;
+        }
+        // diagnostic (ST_LEVEL_STAMPS=1): per-phase wall-clock stamps (100 MHz) to stderr
+        uint64_t *st = nullptr;
+        CHK(dalloc_t(t, &st, (uint64_t)nwg * 16));
+        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
+        LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st, root0, lmin);
+        std::vector<uint64_t> h((uint64_t)nwg * 16);
+        HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        dfree(t, st);
+        uint64_t t0 = ~0ull;
+        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
+        for (int k = 0; k < 12; k++) {
+            std::vector<double> v;
+            for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, "flow stamp %2d: n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, v.size(), v[0], v[v.size() / 2],
+                    v.back());
         }
         return ST_OK;
     }
-    if (t->W == 16) {
-        uint32_t l = t->H;
-        for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
-            LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
-                   (size_t)64 * lane_region_bytes(16), d, l, (const uint8_t *)nullptr);
-        if (l >= 1)
-            LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, (const uint8_t *)nullptr);
-        return ST_OK;
-    }
+    if (t->W == 16) return levels16(t, t->H, nullptr);
     return rehash_levels(t, t->H, nullptr);
 }
 
+// Full (mask == NULL) or dirty-path (mask: marked segments + ancestors) rehash.
+// The dirty path hashes the marked segments straight from the CSR in
+// block-count order (k_segment_hash_perm), then the marked inner nodes:
+// W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the per-level
+// kernels above; other geometries: one k_level_hash launch per level.
 static int rehash_all(st_tree *t, const uint8_t *mask) {
-    if (!mask && rehash_mode() == 2) return rehash_tiled(t);
+    if (!mask) return rehash_tiled(t);
     DevTree d = view(t);
-    uint32_t depth = 0;
-    uint64_t segs = 1;
-    while (depth < t->H && segs * t->W <= 256) { segs *= t->W; depth++; }
-    // K1 variant (env ST_K1: A/B knob): 3 = block-count order (default),
-    // 2 = LDS-staged waves, 1 = subtree kernel (optional in-kernel levels)
-    static const int k1 = getenv("ST_K1") ? atoi(getenv("ST_K1")) : 3;
-    static const int knob = getenv("ST_FUSED_LEVELS") ? atoi(getenv("ST_FUSED_LEVELS")) : 0;
-    uint32_t dlev = 0;
-    if (k1 == 3 || k1 == 4 || k1 == 5) {
-        CHK(ensure_perm(t));
-        if (k1 == 5)
-            LAUNCH(t, "segment_hash", k_segment_hash_v5, (uint32_t)((t->S + 63) / 64), 64, 64 * 64 * K1U_MAXB, d,
-                   (const uint32_t *)t->seg_perm, mask);
-        else if (k1 == 4)
-            LAUNCH(t, "segment_hash", k_segment_hash_gather, (uint32_t)((t->S + 63) / 64), 64, K1G_SLICE + 272 + 512, d,
-                   (const uint32_t *)t->seg_perm, mask);
-        else
-            LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
-        static const int k2 = getenv("ST_K2") ? atoi(getenv("ST_K2")) : 2;
-        if (k2 == 2 && t->W == 16 && t->H >= 3) {
-            LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256,
-                   levels3_16_lds_bytes(), d, mask);
-            uint32_t l = t->H - 3;
-            for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
-                LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
-                       (size_t)64 * lane_region_bytes(16), d, l, mask);
-            if (l >= 1)
-                LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, mask);
-            return ST_OK;
-        }
-        if (t->W == 16 && t->H >= 1) {
-            uint32_t l = t->H;
-            for (; l >= 1 && t->base[l + 1] - t->base[l] > 256; l--)
-                LAUNCH(t, "level_rehash", k_level16, grid_for(t->base[l + 1] - t->base[l], 64), 64,
-                       (size_t)64 * lane_region_bytes(16), d, l, mask);
-            if (l >= 1)
-                LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, l, mask);
-            return ST_OK;
-        }
-    } else if (k1 == 2) {
-        const uint64_t waves = (t->S + 63) / 64;
-        LAUNCH(t, "segment_hash", k_segment_hash_lds, (uint32_t)((waves + K1_WAVES - 1) / K1_WAVES), 64 * K1_WAVES,
-               (size_t)K1_WAVES * K1_SLICE, d, mask);
-    } else {
-        dlev = (int)depth < knob ? depth : (uint32_t)(knob < 0 ? 0 : knob);
-        static const int ilp_knob = getenv("ST_K1_ILP") ? atoi(getenv("ST_K1_ILP")) : 1;
-        const uint32_t ilp2 = (ilp_knob == 2 && segs >= 128 && dlev == 0) ? 1 : 0;
-        uint32_t block = segs < 64 ? 64 : (uint32_t)segs;
-        if (ilp2) block = (uint32_t)segs / 2;
-        LAUNCH(t, "segment_hash", k_rehash_subtree, (uint32_t)(t->S / segs), block,
-               subtree_lds_bytes((uint32_t)t->W, (uint32_t)segs), d, depth, (uint32_t)segs, dlev, mask, ilp2);
+    CHK(ensure_perm(t));
+    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
+    if (t->H == 0) return ST_OK;
+    if (t->W == 16 && t->H >= 3) {
+        LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
+               d, mask);
+        if (t->H - 3 >= 1) CHK(levels16(t, t->H - 3, mask));
+        return ST_OK;
     }
-    if (t->H <= dlev) return ST_OK;
-    uint32_t l = t->H - dlev;   // highest level not yet recomputed
-    if (l == t->H && t->H >= 1) {
-        // levels H .. H+1-dl in single-wave subtrees of <= 64 level-H nodes
-        uint32_t dl = 1;
-        uint64_t nh = 1;
-        while (dl < t->H && nh * t->W <= 64) { nh *= t->W; dl++; }
-        const uint64_t wgs = (t->base[t->H + 1] - t->base[t->H]) / nh;
-        LAUNCH(t, "level_rehash", k_rehash_levels_wave, (uint32_t)wgs, 64, 64 * 20 + nh * lane_region_bytes((uint32_t)t->W),
-               d, dl, mask);
-        l = t->H - dl;
-        if (l == 0) return ST_OK;
-    }
-    while (l >= 1 && t->base[l + 1] - t->base[l] > 256) {
-        const uint64_t nodes = t->base[l + 1] - t->base[l];
-        LAUNCH(t, "level_rehash", (k_level_hash<MODE_STORE>), grid_for(nodes, inner_block(t)), inner_block(t),
-               inner_shmem(t), d, l, l, mask, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr,
-               (uint32_t *)nullptr);
-        l--;
-    }
-    if (l >= 1)
-        LAUNCH(t, "level_rehash", k_rehash_upper_levels, 1, 256, (size_t)256 * lane_region_bytes((uint32_t)t->W), d, 1u, l,
-               mask);
-    return ST_OK;
+    if (t->W == 16) return levels16(t, t->H, mask);
+    return rehash_levels(t, t->H, mask);
 }
 
 // Verify every node marked in t->mark (levels 1..L); results in t->ok.
@@ -661,26 +606,18 @@ static int ingest(st_tree *t, IngestIn &in) {
     in.n_rejected = 0;
     if (n == 0) return ST_OK;
     DevTree d = view(t);
-    uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr;
+    Scratch sc(t);
+    uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr, *mpos = nullptr;
     uint64_t *bseg_off = nullptr, *cnt = nullptr, *nseg_off = nullptr, *src = nullptr, *klen = nullptr, *vlen = nullptr;
-    uint64_t *nkoff = nullptr, *nvoff = nullptr, *nseg_voff = nullptr;
+    uint64_t *nkoff = nullptr, *nvoff = nullptr, *nseg_voff = nullptr, *feq = nullptr, *fne = nullptr, *ceq = nullptr,
+             *cne = nullptr;
     uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr, *nkheap = nullptr, *nvheap = nullptr;
-    int r = ST_OK;
-    auto cleanup = [&]() {
-        void *ps[] = {seg, sseg, idx, perm, bseg_off, cnt, src, klen, vlen, keep, reject, dirty};
-        for (void *p : ps) dfree(t, p);
-    };
-#define ICHK(x)                        \
-    do {                               \
-        r = (x);                       \
-        if (r != ST_OK) { cleanup(); return r; } \
-    } while (0)
-    ICHK(dalloc_t(t, &seg, n));
-    ICHK(dalloc_t(t, &sseg, n));
-    ICHK(dalloc_t(t, &idx, n));
-    ICHK(dalloc_t(t, &perm, n));
-    ICHK(dalloc_t(t, &bseg_off, S + 1));
-    ICHK(dalloc_t(t, &keep, n));
+    CHK(sc.alloc(&seg, n));
+    CHK(sc.alloc(&sseg, n));
+    CHK(sc.alloc(&idx, n));
+    CHK(sc.alloc(&perm, n));
+    CHK(sc.alloc(&bseg_off, S + 1));
+    CHK(sc.alloc(&keep, n));
     if (in.seg_given) {
         HIPCHK(hipMemcpyAsync(seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
     } else {
@@ -693,14 +630,10 @@ static int ingest(st_tree *t, IngestIn &in) {
         while ((1ull << end_bit) < S) end_bit++;
         size_t bytes = 0;
         HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream));
-        void *tmp;
-        ICHK(dalloc(t, &tmp, bytes));
-        {
-            TimedLaunch tl(t, "radix_sort");
-            hipError_t e = rocprim::radix_sort_pairs(tmp, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream);
-            if (e != hipSuccess) { dfree(t, tmp); cleanup(); g_err = "radix_sort_pairs failed"; return ST_EDEVICE; }
-        }
-        dfree(t, tmp);
+        uint8_t *tmp = nullptr;
+        CHK(sc.bytes(&tmp, bytes));
+        TimedLaunch tl(t, "radix_sort");
+        HIPCHK(rocprim::radix_sort_pairs(tmp, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream));
     } else {
         HIPCHK(hipMemcpyAsync(sseg, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
         HIPCHK(hipMemcpyAsync(perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
@@ -715,14 +648,14 @@ static int ingest(st_tree *t, IngestIn &in) {
 
     // path verification of touched segments (insert semantics)
     if (in.verify_rehash) {
-        ICHK(dalloc_t(t, &reject, S));
+        CHK(sc.alloc(&reject, S));
         if (t->fresh) {
             HIPCHK(hipMemsetAsync(reject, 0, S, t->stream));
         } else {
             HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
             LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
                    (const uint64_t *)nullptr, S, t->mark);
-            ICHK(verify_marked(t, t->H + 1));
+            CHK(verify_marked(t, t->H + 1));
             LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
                    (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
         }
@@ -730,7 +663,7 @@ static int ingest(st_tree *t, IngestIn &in) {
                                   (const uint8_t *)reject, in.clevel_out);
     }
 
-    // merge: count, scan, write
+    // merge (k_merge_pos / k_merge_old / k_merge_new): count, scan, write
     MergeArgs ma;
     ma.seg_off = t->seg_off;
     ma.koff = t->koff;
@@ -743,69 +676,60 @@ static int ingest(st_tree *t, IngestIn &in) {
     ma.seg_replace = in.seg_replace;
     ma.bv = bv;
     ma.S = S;
-    ICHK(dalloc_t(t, &cnt, S + 1));
-    ICHK(dalloc_t(t, &dirty, S));
+    CHK(sc.alloc(&cnt, S + 1));
+    CHK(sc.alloc(&dirty, S));
+    CHK(sc.alloc(&mpos, n));
+    CHK(sc.alloc(&feq, n + 1));
+    CHK(sc.alloc(&fne, n + 1));
+    CHK(sc.alloc(&ceq, n + 1));
+    CHK(sc.alloc(&cne, n + 1));
     HIPCHK(hipMemsetAsync(cnt + S, 0, 8, t->stream));
-    // merge strategy (env ST_MERGE, A/B knob): 1 = parallel (k_merge_pos /
-    // k_merge_old / k_merge_new, default), 0 = per-segment serial walk
-    static const int pmerge = getenv("ST_MERGE") ? atoi(getenv("ST_MERGE")) : 1;
-    uint32_t *mpos = nullptr;
-    uint64_t *feq = nullptr, *fne = nullptr, *ceq = nullptr, *cne = nullptr;
-    auto mfree = [&]() { dfree(t, mpos); dfree(t, feq); dfree(t, fne); dfree(t, ceq); dfree(t, cne); };
-    if (pmerge) {
-        if ((r = dalloc_t(t, &mpos, n)) || (r = dalloc_t(t, &feq, n + 1)) || (r = dalloc_t(t, &fne, n + 1)) ||
-            (r = dalloc_t(t, &ceq, n + 1)) || (r = dalloc_t(t, &cne, n + 1))) { mfree(); cleanup(); return r; }
-        // records outside every run (a partition's clamped runs) keep flags 0
-        HIPCHK(hipMemsetAsync(feq, 0, (n + 1) * 8, t->stream));
-        HIPCHK(hipMemsetAsync(fne, 0, (n + 1) * 8, t->stream));
-        LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, feq, fne, cnt, dirty);
-        if ((r = exclusive_scan<uint64_t>(t, feq, ceq, n + 1)) || (r = exclusive_scan<uint64_t>(t, fne, cne, n + 1))) {
-            mfree(); cleanup(); return r;
-        }
-    } else {
-        LAUNCH(t, "merge_count", (k_merge<false>), grid_for(S), 256, 0, ma, cnt, (uint64_t *)nullptr, dirty);
-    }
-    ICHK(dalloc_t(t, &nseg_off, S + 1));
-    ICHK(exclusive_scan<uint64_t>(t, cnt, nseg_off, S + 1));
+    // records outside every run (a partition's clamped runs) keep flags 0
+    HIPCHK(hipMemsetAsync(feq, 0, (n + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(fne, 0, (n + 1) * 8, t->stream));
+    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, feq, fne, cnt, dirty);
+    CHK(exclusive_scan<uint64_t>(t, feq, ceq, n + 1));
+    CHK(exclusive_scan<uint64_t>(t, fne, cne, n + 1));
+    CHK(sc.alloc(&nseg_off, S + 1));
+    CHK(exclusive_scan<uint64_t>(t, cnt, nseg_off, S + 1));
     uint64_t n_new = 0;
-    ICHK(d2h(t, &n_new, nseg_off + S, 8));
-    ICHK(dalloc_t(t, &src, n_new + 1));
-    if (pmerge) {
-        LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
-               (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
-        LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
-               (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
-        mfree();
-    } else {
-        LAUNCH(t, "merge_write", (k_merge<true>), grid_for(S), 256, 0, ma, nseg_off, src, (uint8_t *)nullptr);
-    }
-    ICHK(dalloc_t(t, &klen, n_new + 1));
-    ICHK(dalloc_t(t, &vlen, n_new + 1));
+    CHK(d2h(t, &n_new, nseg_off + S, 8));
+    CHK(sc.alloc(&src, n_new + 1));
+    LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
+           (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
+    LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
+           (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
+    CHK(sc.alloc(&klen, n_new + 1));
+    CHK(sc.alloc(&vlen, n_new + 1));
     LAUNCH(t, "src_lengths", k_src_lengths, grid_for(n_new + 1), 256, 0, (const uint64_t *)src, n_new,
            (const uint64_t *)t->koff, (const uint64_t *)t->voff, in.koff, in.voff, klen, vlen);
-    ICHK(dalloc_t(t, &nkoff, n_new + 1));
-    ICHK(dalloc_t(t, &nvoff, n_new + 1));
-    ICHK(exclusive_scan<uint64_t>(t, klen, nkoff, n_new + 1));
-    ICHK(exclusive_scan<uint64_t>(t, vlen, nvoff, n_new + 1));
+    CHK(sc.alloc(&nkoff, n_new + 1));
+    CHK(sc.alloc(&nvoff, n_new + 1));
+    CHK(exclusive_scan<uint64_t>(t, klen, nkoff, n_new + 1));
+    CHK(exclusive_scan<uint64_t>(t, vlen, nvoff, n_new + 1));
     uint64_t tot[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(&tot[0], nkoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&tot[1], nvoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
-    ICHK(dalloc(t, (void **)&nkheap, tot[0] + HEAP_SLACK));
-    ICHK(dalloc(t, (void **)&nvheap, tot[1] + HEAP_SLACK));
+    CHK(sc.bytes(&nkheap, tot[0] + HEAP_SLACK));
+    CHK(sc.bytes(&nvheap, tot[1] + HEAP_SLACK));
     HIPCHK(hipMemsetAsync(nkheap + tot[0], 0, HEAP_SLACK, t->stream));
     HIPCHK(hipMemsetAsync(nvheap + tot[1], 0, HEAP_SLACK, t->stream));
     LAUNCH(t, "gather_entries", k_gather_entries, grid_for(n_new), 256, 0, (const uint64_t *)src, n_new,
            (const uint64_t *)t->koff, (const uint8_t *)t->kheap, (const uint64_t *)t->voff, (const uint8_t *)t->vheap,
            in.koff, in.krec, in.voff, in.vheap, (const uint64_t *)nkoff, nkheap, (const uint64_t *)nvoff, nvheap);
-    ICHK(dalloc_t(t, &nseg_voff, S + 1));
+    CHK(sc.alloc(&nseg_voff, S + 1));
     LAUNCH(t, "seg_voff", k_seg_voff, grid_for(S + 1), 256, 0, (const uint64_t *)nseg_off, (const uint64_t *)nvoff, S,
            nseg_voff);
-    // swap in the new CSR
+    // swap in the new CSR (the old one is freed in stream order)
     dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
     t->seg_off = nseg_off; t->seg_voff = nseg_voff; t->koff = nkoff; t->voff = nvoff; t->kheap = nkheap; t->vheap = nvheap;
+    for (void *p : {(void *)nseg_off, (void *)nseg_voff, (void *)nkoff, (void *)nvoff, (void *)nkheap, (void *)nvheap})
+        sc.release(p);
     t->n = n_new; t->kbytes = tot[0]; t->vbytes = tot[1];
     t->perm_valid = false;
+    // the hash-ready tiles are stale now; the next full rehash rebuilds them
+    // (streaming batches never pay for a tile rebuild they do not use)
     t->tiles_valid = false;
 
     if (in.verify_rehash) {
@@ -813,14 +737,9 @@ static int ingest(st_tree *t, IngestIn &in) {
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         d = view(t);
         LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
-        ICHK(rehash_all(t, t->mark));
+        CHK(rehash_all(t, t->mark));
     }
     t->fresh = false;
-    // bulk batches rebuild the hash-ready tiles now (the build pays for the
-    // layout); small ones leave it to the next full rehash
-    if (n >= 65536) ICHK(ensure_tiles(t));
-    cleanup();
-#undef ICHK
     return ST_OK;
 }
 
@@ -1092,7 +1011,7 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 extern "C" int st_rehash(st_tree *t, int upper) {
     CHK(use_device(t));
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
-    if (t->partitioned && (upper || rehash_mode() != 2)) {
+    if (t->partitioned && upper) {
         g_err = "a segment-range partition supports the full rehash (st_rehash upper = 0) only";
         return ST_EINVAL;
     }
@@ -1114,7 +1033,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     CHK(use_device(t));
     for (uint32_t i = 0; i < n; i++) {
         st_tree *u = trees[i];
-        if (u->W != 16 || u->H < 3 || u->S != t->S || u->device != t->device || u->partitioned || rehash_mode() != 2) {
+        if (u->W != 16 || u->H < 3 || u->S != t->S || u->device != t->device || u->partitioned) {
             g_err = "group rehash needs unpartitioned width-16 trees of one geometry (height >= 3) on one device";
             return ST_EINVAL;
         }
