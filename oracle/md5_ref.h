@@ -74,14 +74,17 @@ static inline void md5r_update(md5r_ctx *c, const uint8_t *p, size_t n) {
 }
 
 static inline void md5r_final(md5r_ctx *c, uint8_t out[16]) {
+    /* RFC 1321 §3.1-3.2: 0x80, zeros to 56 mod 64, 64-bit little-endian bit length */
     uint64_t bits = c->len * 8;
-    uint8_t pad = 0x80;
-    md5r_update(c, &pad, 1);
-    uint8_t z = 0;
-    while (c->fill != 56) md5r_update(c, &z, 1);
-    uint8_t lb[8];
-    for (int i = 0; i < 8; i++) lb[i] = (uint8_t)(bits >> (8 * i));
-    md5r_update(c, lb, 8);
+    c->buf[c->fill++] = 0x80;
+    if (c->fill > 56) {
+        memset(c->buf + c->fill, 0, 64 - c->fill);
+        md5r_block(c->s, c->buf);
+        c->fill = 0;
+    }
+    memset(c->buf + c->fill, 0, 56 - c->fill);
+    for (int i = 0; i < 8; i++) c->buf[56 + i] = (uint8_t)(bits >> (8 * i));
+    md5r_block(c->s, c->buf);
     for (int i = 0; i < 4; i++) {
         out[4 * i] = (uint8_t)c->s[i]; out[4 * i + 1] = (uint8_t)(c->s[i] >> 8);
         out[4 * i + 2] = (uint8_t)(c->s[i] >> 16); out[4 * i + 3] = (uint8_t)(c->s[i] >> 24);

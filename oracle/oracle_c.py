@@ -75,6 +75,8 @@ def lib():
         L.ot_bulk_load_int64.restype = ctypes.c_int
         L.ot_bulk_load_int64.argtypes = [vp, u64, vp, vp, u32]
         L.ot_md5.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p]
+        L.ot_insert_int64_seq.restype = u64
+        L.ot_insert_int64_seq.argtypes = [vp, u64, vp, vp, u32]
         _lib = L
     return _lib
 
@@ -245,6 +247,12 @@ class OTree:
         if r != 0:
             raise ValueError('bulk_load needs a fresh tree')
         return self
+
+    def insert_int64_seq(self, keys, values):
+        """len(keys) sequential insert/3 calls in C; returns #rejected."""
+        keys = np.ascontiguousarray(keys, np.int64)
+        values = np.ascontiguousarray(values, np.uint8)
+        return int(lib().ot_insert_int64_seq(self.h, len(keys), keys.ctypes.data, values.ctypes.data, values.shape[1]))
 
     def bulk_load_int64(self, keys, values):
         """keys: int64 ndarray [n]; values: uint8 ndarray [n, vlen]."""

@@ -26,6 +26,7 @@
  * 2 = binary.  Term order: integer < atom < binary; atoms/binaries compare
  * bytewise with a proper prefix first (ERTS order).
  */
+#define _GNU_SOURCE
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -586,16 +587,19 @@ void ot_diff_free(ot_diff *d) {
 }
 
 /* ------------------------------------------------------------------ */
-/* Bulk load into a FRESH tree: sequential-insert semantics, then rehash. */
-static ot_tree *g_sort_tree;
-static const uint8_t *g_kt;
-static const uint8_t *g_kh;
-static const uint64_t *g_ko;
+/* Bulk load into a FRESH tree: sequential-insert semantics, then rehash.
+ * (qsort_r with the key arrays as context: several trees may load in
+ * parallel threads.) */
+typedef struct {
+    const uint8_t *kt, *kh;
+    const uint64_t *ko;
+} sort_ctx;
 
-static int cmp_idx(const void *x, const void *y) {
+static int cmp_idx(const void *x, const void *y, void *arg) {
+    const sort_ctx *s = (const sort_ctx *)arg;
     uint64_t i = *(const uint64_t *)x, j = *(const uint64_t *)y;
-    int c = key_cmp(g_kt[i], g_kh + g_ko[i], (uint32_t)(g_ko[i + 1] - g_ko[i]), g_kt[j], g_kh + g_ko[j],
-                    (uint32_t)(g_ko[j + 1] - g_ko[j]));
+    int c = key_cmp(s->kt[i], s->kh + s->ko[i], (uint32_t)(s->ko[i + 1] - s->ko[i]), s->kt[j], s->kh + s->ko[j],
+                    (uint32_t)(s->ko[j + 1] - s->ko[j]));
     if (c) return c;
     return i < j ? -1 : (i > j ? 1 : 0);
 }
@@ -620,11 +624,11 @@ int ot_bulk_load(ot_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kh
     /* copy payloads into the tree arena once */
     uint8_t *kh = arena_put(t, kheap, koff[n]);
     uint8_t *vh = arena_put(t, vheap, voff[n]);
-    g_sort_tree = t; g_kt = ktype; g_kh = kheap; g_ko = koff;
+    sort_ctx sc = {ktype, kheap, koff};
     for (uint64_t s = 0; s < S; s++) {
         uint64_t a = cnt[s], b = cnt[s + 1];
         if (a == b) continue;
-        qsort(order + a, b - a, sizeof(uint64_t), cmp_idx);
+        qsort_r(order + a, b - a, sizeof(uint64_t), cmp_idx, &sc);
         onode *nd = node_at(t, H1, s);
         node_reserve_seg(nd, (uint32_t)(b - a));
         uint32_t m = 0;
@@ -668,33 +672,81 @@ int ot_bulk_load_int64(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_
 }
 
 /* ------------------------------------------------------------------ */
-/* Throughput-mode rehash for the CPU baseline: same result as ot_rehash(t,0)
- * on a tree, with segment hashing spread over `threads` OpenMP threads. */
+/* Throughput-mode rehash for the CPU baseline: the same result as
+ * ot_rehash(t, 0) on a tree, level by level over flat entry arrays with every
+ * level's nodes spread over `threads` OpenMP threads (0 = all).  Segments
+ * hash their values in key order (synctree.erl:255-259), inner nodes their
+ * present children's 17-byte entries; empty nodes are dropped
+ * (delete_existing_batch, synctree.erl:537-543). */
 #ifdef _OPENMP
 #include <omp.h>
 #endif
 void ot_rehash_par(ot_tree *t, int threads) {
     uint64_t H1 = t->height + 1;
-    uint64_t S = t->lvsize[H1];
     if (t->height == 0 || t->width > 64) { ot_rehash(t, 0); return; }
-    /* level H entries from segments, in parallel over level-H parents */
-    uint64_t P = t->lvsize[H1 - 1];
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 64)
 #endif
-    for (int64_t p = 0; p < (int64_t)P; p++) {
-        onode *me = node_at(t, H1 - 1, (uint64_t)p);
-        ochild ch[64];
-        uint32_t nc = 0;
-        for (uint64_t x = (uint64_t)p * t->width; x < ((uint64_t)p + 1) * t->width && x < S; x++) {
-            onode *cn = node_at(t, H1, x);
-            if (cn->n) { ch[nc].child = x; hash_seg(cn, ch[nc].h); nc++; }
-        }
-        if (!nc) node_clear(me);
-        else { node_reserve_inner(me, nc); memcpy(me->c, ch, nc * sizeof(ochild)); me->n = nc; }
+    /* entry arrays of the level below the one being built */
+    uint64_t n = t->lvsize[H1];
+    uint8_t *pres = (uint8_t *)malloc(n);
+    uint8_t *hash = (uint8_t *)malloc(n * 17);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 4096)
+#endif
+    for (int64_t s = 0; s < (int64_t)n; s++) {
+        onode *cn = node_at(t, H1, (uint64_t)s);
+        pres[s] = cn->n != 0;
+        if (cn->n) hash_seg(cn, hash + 17 * s);
     }
-    ot_rehash(t, 1);   /* levels 1..H-1 from the stored level-H nodes */
+    for (uint64_t l = t->height; l >= 1; l--) {
+        uint64_t m = t->lvsize[l];
+        uint8_t *p2 = (uint8_t *)malloc(m);
+        uint8_t *h2 = (uint8_t *)malloc(m * 17);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 256)
+#endif
+        for (int64_t b = 0; b < (int64_t)m; b++) {
+            onode *me = node_at(t, l, (uint64_t)b);
+            ochild ch[64];
+            uint32_t nc = 0;
+            for (uint64_t x = (uint64_t)b * t->width; x < ((uint64_t)b + 1) * t->width; x++)
+                if (pres[x]) { ch[nc].child = x; memcpy(ch[nc].h, hash + 17 * x, 17); nc++; }
+            if (!nc) { node_clear(me); p2[b] = 0; continue; }
+            node_reserve_inner(me, nc);
+            memcpy(me->c, ch, nc * sizeof(ochild));
+            me->n = nc;
+            hash_inner(me, h2 + 17 * b);
+            p2[b] = 1;
+        }
+        free(pres); free(hash);
+        pres = p2; hash = h2;
+        if (l == 1) break;
+    }
+    /* level 1 holds one node: its hash is the top hash */
+    if (pres[0]) {
+        memcpy(t->st_top, hash, 17); memcpy(t->rec_top, hash, 17);
+        t->st_top_def = 1; t->rec_top_def = 1;
+    } else {
+        t->st_top_def = 0; t->rec_top_def = 0;
+    }
+    free(pres); free(hash);
+}
+
+/* N sequential insert/3 calls (synctree.erl:189-209) with 8-byte integer
+ * keys and fixed-width values, in one C loop (the oracle side of streaming
+ * write batches).  Returns the number of keys rejected as corrupted. */
+uint64_t ot_insert_int64_seq(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen) {
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint8_t kb[8];
+        uint64_t x = (uint64_t)keys[i];
+        for (int j = 0; j < 8; j++) kb[j] = (uint8_t)(x >> (56 - 8 * j));
+        uint32_t cl;
+        uint64_t cb;
+        if (ot_insert(t, 0, kb, 8, vals + (uint64_t)vlen * i, vlen, &cl, &cb) != OT_OK) bad++;
+    }
+    return bad;
 }
 
 /* exported for the RFC 1321 known-answer tests */

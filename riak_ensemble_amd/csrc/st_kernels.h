@@ -638,12 +638,25 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 }
 
 // ---------------------------------------------------------------------------
-// K3 tree_compare: level-synchronous diff (exchange/exchange_level,
-// synctree.erl:386-406) of two trees of the same geometry.  One lane per
-// frontier node: verify the node on both sides against its parent's entry
-// (exchange_get's verified path; ancestors were verified at earlier levels),
-// then diff the W child entries (orddict_delta, riak_ensemble_util.erl:115-141)
-// under the filter and set the differing children in the next frontier bitmap.
+// K3 tree_compare: the level-synchronous diff of compare/3 (exchange,
+// exchange_level, exchange_final: synctree.erl:372-417) of two trees of the
+// same geometry, in three device passes with no host round trip in between:
+//
+//  1. k_cmp_frontier (one workgroup): the frontier of every level.  Level 0
+//     compares the two top hashes (exchange_get(0,0) is not verified); at
+//     level L the children of the frontier nodes whose entries differ under
+//     the filter (orddict_delta, riak_ensemble_util.erl:115-141, plus
+//     filter/2, synctree.erl:434-449) form the next frontier, in ascending
+//     bucket order.  Only stored child entries are compared: no hashing.
+//  2. k_cmp_visit<false> (whole grid): every visited node is verified on both
+//     sides against its parent's entry (exchange_get's verified_hashes,
+//     synctree.erl:288-298: the ancestors are visited nodes too), and every
+//     final-level segment pair is merge-joined (exchange_final) by one wave,
+//     counting its diff records.
+//  3. device-side scan of the counts, then k_cmp_visit<true> writes the
+//     records in reference order: AccFun = Keys ++ Acc over ascending
+//     segments (synctree.erl:373-375) => the LAST frontier segment first,
+//     ascending keys within a segment.
 // err: min over (level, bucket, side) of a failed verification — the
 // reference's first crash in visiting order (local before remote).
 
@@ -676,132 +689,246 @@ __device__ __forceinline__ uint64_t err_code(uint32_t level, uint64_t bucket, ui
     return ((uint64_t)level << 56) | (bucket << 1) | side;
 }
 
-// level 0: [{0,TopA}] vs [{0,TopB}] (exchange_get(0,0) is not verified)
-__global__ void k_cmp_top(DevTree A, DevTree B, uint32_t *list, uint32_t *cnt) {
-    if (gtid() != 0) return;
-    const uint16_t ta = A.tag[0], tb = B.tag[0];
-    bool same = (ta == tb);
-    if (same && (ta & TAG_PRESENT)) {
-        const uint4 x = A.md5[0], y = B.md5[0];
-        same = x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
-    }
-    list[0] = 0;
-    *cnt = same ? 0u : 1u;
-}
-
-__global__ void k_cmp_inner(DevTree A, DevTree B, uint32_t level, const uint32_t *list, const uint32_t *cnt,
-                            unsigned long long *bitmap, int filter, unsigned long long *err) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(A.W);
-    if (*err != ~0ull) return;
-    const uint64_t n = *cnt;
-    for (uint64_t i = gtid(); i < n; i += gstride()) {
-        const uint64_t b = list[i];
-        if (!verify_inner_node(A, level, b, reg)) { atomicMin(err, err_code(level, b, 0)); continue; }
-        if (!verify_inner_node(B, level, b, reg)) { atomicMin(err, err_code(level, b, 1)); continue; }
-        const uint64_t c0 = A.base[level + 1] + b * A.W;
-        unsigned long long word = 0;
-        uint64_t cur_w = ~0ull;
-        for (uint32_t j = 0; j < A.W; j++) {
-            const uint16_t ta = A.tag[c0 + j], tb = B.tag[c0 + j];
-            const bool pa = ta & TAG_PRESENT, pb = tb & TAG_PRESENT;
-            bool d = false;
-            if (pa && pb) {
-                const uint4 x = A.md5[c0 + j], y = B.md5[c0 + j];
-                d = ta != tb || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
-            } else if (pa) {
-                d = filter != 1;   // {C,{H,'$none'}} dropped by local_only
-            } else if (pb) {
-                d = filter != 2;   // {C,{'$none',H}} dropped by remote_only
-            }
-            if (!d) continue;
-            const uint64_t child = b * A.W + j;
-            const uint64_t w = child >> 6;
-            if (w != cur_w) {
-                if (word) atomicOr(bitmap + cur_w, word);
-                word = 0;
-                cur_w = w;
-            }
-            word |= 1ull << (child & 63);
-        }
-        if (word) atomicOr(bitmap + cur_w, word);
-    }
-}
-
-// bitmap (nwords 64-bit words) -> ascending list of set bit indices; clears
-// the bitmap.  One workgroup of 1024 threads.
-__global__ void __launch_bounds__(1024) k_bitmap_to_list(unsigned long long *bitmap, uint64_t nwords, uint32_t *list,
-                                                         uint32_t *cnt) {
-    __shared__ uint32_t part[1024];
-    __shared__ uint32_t carry;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    const uint64_t per = 16;
-    for (uint64_t base = 0; base < nwords; base += 1024 * per) {
-        const uint64_t w0 = base + tid * per;
-        uint32_t c = 0;
-        for (uint64_t w = w0; w < w0 + per && w < nwords; w++) c += __popcll(bitmap[w]);
-        part[tid] = c;
-        __syncthreads();
-        for (uint32_t off = 1; off < 1024; off <<= 1) {
-            uint32_t v = tid >= off ? part[tid - off] : 0;
-            __syncthreads();
-            part[tid] += v;
-            __syncthreads();
-        }
-        uint32_t pos = carry + part[tid] - c;
-        for (uint64_t w = w0; w < w0 + per && w < nwords; w++) {
-            unsigned long long x = bitmap[w];
-            if (!x) continue;
-            bitmap[w] = 0;
-            while (x) {
-                const int bit = __ffsll((long long)x) - 1;
-                list[pos++] = (uint32_t)(w * 64 + bit);
-                x &= x - 1;
-            }
-        }
-        __syncthreads();
-        if (tid == 1023) carry += part[1023];
-        __syncthreads();
-    }
-    if (tid == 0) *cnt = carry;
-}
-
-// Final level (exchange_final, synctree.erl:408-417): verify both segments,
-// merge-join their key lists, count (WRITE=false) or emit (WRITE=true) the
-// diff records.  Output order: AccFun = Keys ++ Acc over ascending segments
-// => records of the LAST frontier segment first.
+// One diff record: entry indices into the two trees' CSR (~0 = '$none').
 struct DiffRec {
-    uint64_t a, b, seg;   // entry indices (~0 = '$none')
+    uint64_t a, b, seg;
     uint32_t kind, pad;
 };
 
-template <bool WRITE>
-__global__ void k_cmp_segments(DevTree A, DevTree B, const uint32_t *list, uint64_t n, int filter,
-                               uint64_t *dcnt, const uint64_t *doff, uint64_t total, DiffRec *out,
-                               unsigned long long *err) {
-    for (uint64_t i = gtid(); i < n; i += gstride()) {
-        const uint64_t s = list[i];
-        if (!WRITE) {
-            if (!verify_segment(A, s)) { atomicMin(err, err_code(A.H + 1, s, 0)); dcnt[i] = 0; continue; }
-            if (!verify_segment(B, s)) { atomicMin(err, err_code(A.H + 1, s, 1)); dcnt[i] = 0; continue; }
+// Does child entry `slot` differ between the trees under the filter?
+// (1 = local_only drops {C,{H,'$none'}}, 2 = remote_only drops {C,{'$none',H}})
+__device__ __forceinline__ bool entry_differs(uint16_t ta, uint16_t tb, const uint4 &x, const uint4 &y, int filter) {
+    const bool pa = ta & TAG_PRESENT, pb = tb & TAG_PRESENT;
+    if (pa && pb) return ta != tb || x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+    if (pa) return filter != 1;
+    if (pb) return filter != 2;
+    return false;
+}
+
+// Exclusive scan of one u32 per thread over a workgroup of up to 1024
+// threads; returns the prefix, sets *total.  wsum: 17 words of LDS.
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t w = 0; w < nw; w++) { const uint32_t c = wsum[w]; wsum[w] = acc; acc += c; }
+        wsum[16] = acc;
+    }
+    __syncthreads();
+    const uint32_t r = wsum[wave] + x - v;
+    *total = wsum[16];
+    __syncthreads();
+    return r;
+}
+
+// Pass 1.  flist: level L's frontier at flist[base[L] - 1 ..], fcnt[L] its
+// length (levels 1..H+1).  [lo2, hi2): level-2 buckets a segment-range
+// partition owns (its level-1 frontier is cut to them); err is reset here.
+__global__ void __launch_bounds__(1024) k_cmp_frontier(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2,
+                                                       uint32_t *flist, uint32_t *fcnt, unsigned long long *err,
+                                                       uint64_t *nfinal) {
+    __shared__ uint32_t wsum[17];
+    __shared__ uint32_t n0;
+    const uint32_t tid = threadIdx.x;
+    if (tid < ST_MAXLEV + 2) fcnt[tid] = 0;
+    if (tid == 0) {
+        *err = ~0ull;
+        const uint16_t ta = A.tag[0], tb = B.tag[0];
+        bool same = (ta == tb);
+        if (same && (ta & TAG_PRESENT)) {
+            const uint4 x = A.md5[0], y = B.md5[0];
+            same = x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
         }
-        uint64_t x = A.seg_off[s], xe = A.seg_off[s + 1];
-        uint64_t y = B.seg_off[s], ye = B.seg_off[s + 1];
-        uint64_t c = 0;
-        uint64_t pos = WRITE ? (total - doff[i] - dcnt[i]) : 0;
-        while (x < xe || y < ye) {
+        n0 = same ? 0u : 1u;
+        flist[0] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) fcnt[1] = n0;
+    uint32_t n = n0;
+    const uint32_t W = A.W;
+    for (uint32_t L = 1; L <= A.H && n; L++) {
+        const uint32_t *cur = flist + (A.base[L] - 1);
+        uint32_t *nxt = flist + (A.base[L + 1] - 1);
+        const uint64_t cb = A.base[L + 1];
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
+            const uint32_t f = c0 + tid;
+            uint64_t mask = 0, b = 0;
+            if (f < n) {
+                b = cur[f];
+                const uint64_t s0 = cb + b * W;
+#pragma unroll 16
+                for (uint32_t j = 0; j < W; j++) {
+                    const uint16_t ta = A.tag[s0 + j], tb = B.tag[s0 + j];
+                    uint4 x = make_uint4(0, 0, 0, 0), y = x;
+                    if ((ta & tb & TAG_PRESENT) && ta == tb) { x = A.md5[s0 + j]; y = B.md5[s0 + j]; }
+                    const uint64_t c = b * W + j;
+                    const bool keep = L != 1 || (c >= lo2 && c < hi2);
+                    if (keep && entry_differs(ta, tb, x, y, filter)) mask |= 1ull << j;
+                }
+            }
+            uint32_t tot;
+            const uint32_t pos = carry + block_scan_u32((uint32_t)__popcll(mask), wsum, &tot);
+            uint32_t q = 0;
+            while (mask) {
+                const uint32_t j = (uint32_t)(__ffsll((long long)mask) - 1);
+                nxt[pos + q++] = (uint32_t)(b * W + j);
+                mask &= mask - 1;
+            }
+            carry += tot;
+        }
+        n = carry;
+        if (tid == 0) fcnt[L + 1] = n;
+        __syncthreads();   // this level's list is the next level's input
+    }
+    if (tid == 0) *nfinal = fcnt[A.H + 1];
+}
+
+// Per-wave LDS of the segment merge-join: key offsets and key bytes of both
+// segments, and one packed record per slot of the merged key sequence.
+#define CMP_CAP 256     // entries per side handled from LDS (larger: lane 0 walks them)
+#define CMP_KB 4096     // key bytes per side
+__host__ __device__ __forceinline__ uint32_t cmp_merge_lds_bytes() { return (CMP_CAP + 1) * 4 * 2 + CMP_KB * 2 + 2 * CMP_CAP * 4; }
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Erlang term order of two key records staged in LDS at arbitrary byte
+// offsets (byte reads: no unaligned wide LDS access).
+__device__ __forceinline__ int lds_rec_cmp(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+    const uint32_t m = la < lb ? la : lb;
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t x = a[i], y = b[i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// lower_bound of key k in the n staged keys (LDS); *eq: equal key found
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *off, const uint8_t *kb, uint32_t n, const uint8_t *k,
+                                                    uint32_t kl, bool *eq) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (lds_rec_cmp(kb + off[m], off[m + 1] - off[m], k, kl) < 0) lo = m + 1; else hi = m;
+    }
+    *eq = lo < n && lds_rec_cmp(kb + off[lo], off[lo + 1] - off[lo], k, kl) == 0;
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
+    const uint64_t bal = __ballot(f);
+    return (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+}
+
+// exchange_final for one segment pair (orddict_delta + filter), one wave.
+// WRITE=false: returns the record count; WRITE=true: writes the records in
+// ascending key order at out[pos0 ..].  Record kinds: 0 = {K,{A,B}},
+// 1 = {K,{A,'$none'}}, 2 = {K,{'$none',B}}.
+template <bool WRITE>
+__device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint8_t *lds,
+                                   DiffRec *out, uint64_t pos0, uint64_t cap) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t a0 = A.seg_off[s], a1 = A.seg_off[s + 1], b0 = B.seg_off[s], b1 = B.seg_off[s + 1];
+    const uint64_t nA = a1 - a0, nB = b1 - b0;
+    const uint64_t ka0 = A.koff[a0], kb0 = B.koff[b0];
+    const uint64_t bytesA = A.koff[a1] - ka0, bytesB = B.koff[b1] - kb0;
+    if (nA <= CMP_CAP && nB <= CMP_CAP && bytesA <= CMP_KB && bytesB <= CMP_KB) {
+        uint32_t *ao = reinterpret_cast<uint32_t *>(lds);
+        uint32_t *bo = ao + CMP_CAP + 1;
+        uint8_t *ak = reinterpret_cast<uint8_t *>(bo + CMP_CAP + 1);
+        uint8_t *bk = ak + CMP_KB;
+        uint32_t *ur = reinterpret_cast<uint32_t *>(bk + CMP_KB);
+        for (uint64_t i = lane; i <= nA; i += 64) ao[i] = (uint32_t)(A.koff[a0 + i] - ka0);
+        for (uint64_t i = lane; i <= nB; i += 64) bo[i] = (uint32_t)(B.koff[b0 + i] - kb0);
+        for (uint64_t q = lane; q < bytesA; q += 64) ak[q] = A.kheap[ka0 + q];
+        for (uint64_t q = lane; q < bytesB; q += 64) bk[q] = B.kheap[kb0 + q];
+        const uint32_t nu_max = (uint32_t)(nA + nB);
+        if (WRITE)
+            for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+        wave_sync_lds();
+        uint64_t cnt = 0;
+        uint32_t mcarry = 0;
+        for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
+            const uint32_t i = c + lane;
+            bool eq = false, emit = false;
+            uint32_t rb = 0;
+            if (i < nA) {
+                rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
+                if (eq) {
+                    const uint64_t x = a0 + i, y = b0 + rb;
+                    emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
+                                     B.voff[y + 1] - B.voff[y]);
+                } else {
+                    emit = filter != 1;
+                }
+            }
+            const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+            mcarry += (uint32_t)__popcll(__ballot(eq));
+            cnt += (uint32_t)__popcll(__ballot(emit));
+            if (WRITE && emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
+        }
+        mcarry = 0;
+        for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
+            const uint32_t j = c + lane;
+            bool eq = false, emit = false;
+            uint32_t ra = 0;
+            if (j < nB) {
+                ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
+                emit = !eq && filter != 2;
+            }
+            const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+            mcarry += (uint32_t)__popcll(__ballot(eq));
+            cnt += (uint32_t)__popcll(__ballot(emit));
+            if (WRITE && emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
+        }
+        if (!WRITE) return cnt;
+        wave_sync_lds();
+        uint64_t pos = pos0;
+        for (uint32_t c = 0; c < nu_max; c += 64) {   // union slots in key order -> records
+            const uint32_t u = c + lane;
+            const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
+            const bool e = r != 0xffffffffu;
+            const uint64_t p = pos + wave_prefix_count(e, lane);
+            if (e && p < cap) {
+                DiffRec d;
+                const uint32_t kind = r >> 30, x = (r >> 15) & 0x7fffu, y = r & 0x7fffu;
+                d.kind = kind;
+                d.pad = 0;
+                d.seg = s;
+                d.a = kind == 2 ? ~0ull : a0 + x;
+                d.b = kind == 1 ? ~0ull : b0 + y;
+                out[p] = d;
+            }
+            pos += (uint32_t)__popcll(__ballot(e));
+        }
+        return pos - pos0;
+    }
+    // oversized segments: lane 0 walks the two key lists
+    uint64_t c = 0;
+    if (lane == 0) {
+        uint64_t x = a0, y = b0, pos = pos0;
+        while (x < a1 || y < b1) {
             int cmp;
-            if (x < xe && y < ye)
-                cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y],
-                              B.koff[y + 1] - B.koff[y]);
+            if (x < a1 && y < b1)
+                cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y], B.koff[y + 1] - B.koff[y]);
             else
-                cmp = x < xe ? -1 : 1;
+                cmp = x < a1 ? -1 : 1;
             DiffRec r;
             r.seg = s;
             r.pad = 0;
-            bool emit = false;
+            bool emit;
             if (cmp < 0) {
                 r.a = x; r.b = ~0ull; r.kind = 1;
                 emit = filter != 1;
@@ -811,18 +938,138 @@ __global__ void k_cmp_segments(DevTree A, DevTree B, const uint32_t *list, uint6
                 emit = filter != 2;
                 y++;
             } else {
-                const uint64_t la = A.voff[x + 1] - A.voff[x], lb = B.voff[y + 1] - B.voff[y];
-                emit = !bytes_eq(A.vheap + A.voff[x], la, B.vheap + B.voff[y], lb);
+                emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y], B.voff[y + 1] - B.voff[y]);
                 r.a = x; r.b = y; r.kind = 0;
                 x++; y++;
             }
             if (emit) {
-                if (WRITE) out[pos] = r;
+                if (WRITE && pos < cap) out[pos] = r;
                 pos++;
                 c++;
             }
         }
-        if (!WRITE) dcnt[i] = c;
+    }
+    return __shfl(c, 0, 64);
+}
+
+// Passes 2 and 3.  WRITE=false: verify every visited node (lane per node and
+// side, all levels), then count each final segment's records (wave per
+// segment) into dcnt.  WRITE=true: write the records at their reference
+// positions (doff: exclusive scan of dcnt, *total its sum).
+template <bool WRITE>
+__global__ void __launch_bounds__(256) k_cmp_visit(DevTree A, DevTree B, int filter, const uint32_t *flist,
+                                                  const uint32_t *fcnt, uint64_t *dcnt, const uint64_t *doff,
+                                                  const uint64_t *total, DiffRec *out, uint64_t cap,
+                                                  unsigned long long *err, uint32_t slice) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *wl = lds + (uint64_t)wave * slice;
+    const uint32_t L1 = A.H + 1;
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave, nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    if (!WRITE) {
+        uint64_t nv = 0;
+        for (uint32_t L = 1; L <= L1; L++) nv += fcnt[L];
+        uint8_t *reg = wl + lane * lane_region_bytes(A.W);
+        for (uint64_t g = gwave * 64 + lane; g < 2 * nv; g += nwaves * 64) {
+            uint64_t k = g >> 1;
+            const uint32_t side = (uint32_t)(g & 1);
+            uint32_t L = 1;
+            while (k >= fcnt[L]) { k -= fcnt[L]; L++; }
+            const uint64_t b = flist[A.base[L] - 1 + k];
+            const DevTree &T = side ? B : A;
+            const bool good = L == L1 ? verify_segment(T, b) : verify_inner_node(T, L, b, reg);
+            if (!good) atomicMin(err, err_code(L, b, side));
+        }
+        wave_sync_lds();
+    }
+    const uint64_t nf = fcnt[L1];
+    const uint32_t *seg = flist + (A.base[L1] - 1);
+    const uint64_t tot = WRITE ? *total : 0;
+    for (uint64_t i = gwave; i < nf; i += nwaves) {
+        const uint64_t s = seg[i];
+        if (!WRITE) {
+            const uint64_t c = seg_merge_wave<false>(A, B, s, filter, wl, nullptr, 0, 0);
+            if (lane == 0) dcnt[i] = c;
+        } else {
+            (void)seg_merge_wave<true>(A, B, s, filter, wl, out, tot - doff[i] - dcnt[i], cap);
+        }
+        wave_sync_lds();
+    }
+}
+
+// Exclusive scan of n (read on the device) uint64 values, NA arrays at once,
+// in three launches that need no host round trip: per-workgroup range sums,
+// a one-workgroup scan of those, then each workgroup rescans its range.
+#define DSCAN_WGS 256
+template <int NA>
+struct DScanArgs {
+    const uint64_t *in[NA];
+    uint64_t *out[NA];
+};
+
+template <int NA>
+__global__ void __launch_bounds__(256) k_dscan_sums(DScanArgs<NA> a, const uint64_t *n_ptr, uint64_t *part) {
+    __shared__ uint64_t red[NA][4];
+    const uint64_t n = *n_ptr;
+    const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint64_t s[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) s[k] = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+#pragma unroll
+        for (int k = 0; k < NA; k++) s[k] += a.in[k][i];
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+        uint64_t v = s[k];
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NA) {
+        const int k = threadIdx.x;
+        part[(uint64_t)k * (gridDim.x + 1) + blockIdx.x] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
+    }
+}
+
+template <int NA>
+__global__ void __launch_bounds__(256) k_dscan_top(uint64_t *part, uint32_t nparts, uint64_t *totals) {
+    if (threadIdx.x >= NA) return;
+    uint64_t *p = part + (uint64_t)threadIdx.x * (nparts + 1);
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < nparts; i++) { const uint64_t c = p[i]; p[i] = acc; acc += c; }
+    p[nparts] = acc;
+    totals[threadIdx.x] = acc;
+}
+
+template <int NA>
+__global__ void __launch_bounds__(256) k_dscan_apply(DScanArgs<NA> a, const uint64_t *n_ptr, const uint64_t *part) {
+    __shared__ uint64_t ws[NA][4];
+    const uint64_t n = *n_ptr;
+    const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t carry[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) carry[k] = part[(uint64_t)k * (gridDim.x + 1) + blockIdx.x];
+    for (uint64_t c0 = lo; c0 < hi; c0 += blockDim.x) {
+        const uint64_t i = c0 + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < NA; k++) {
+            const uint64_t v = i < hi ? a.in[k][i] : 0;
+            uint64_t x = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint64_t y = __shfl_up(x, o, 64);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            if (lane == 63) ws[k][wave] = x;
+            __syncthreads();
+            uint64_t before = 0;
+            for (uint32_t w = 0; w < wave; w++) before += ws[k][w];
+            if (i < hi) a.out[k][i] = carry[k] + before + x - v;
+            carry[k] += ws[k][0] + ws[k][1] + ws[k][2] + ws[k][3];
+            __syncthreads();
+        }
     }
 }
 

@@ -38,6 +38,14 @@ static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past 
         if (r_ != ST_OK) return r_;                \
     } while (0)
 
+struct CmpWork {
+    uint32_t *flist = nullptr, *fcnt = nullptr;
+    unsigned long long *err = nullptr;
+    uint64_t *dcnt = nullptr, *doff = nullptr, *part = nullptr, *tot = nullptr;
+    DiffRec *rec = nullptr;
+    uint64_t cap = 0;
+};
+
 struct Pending {
     std::string name;
     hipEvent_t a, b;
@@ -72,6 +80,10 @@ struct st_tree {
     // segment-range partition (st_set_partition): owned segments [part_lo, part_hi)
     bool partitioned = false;
     uint64_t part_lo = 0, part_hi = 0;
+    // compare (K3) workspace, grown on demand
+    CmpWork cw;
+    // small pinned host buffer for scalar results (one D2H per call)
+    uint64_t *pin = nullptr;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -255,6 +267,12 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
         return ST_EDEVICE;
     }
     t->stream = t->own_stream;
+    if (hipHostMalloc((void **)&t->pin, 64 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
+        g_err = "hipHostMalloc failed";
+        t->pin = nullptr;
+        st_destroy(t);
+        return ST_EDEVICE;
+    }
     {
         // keep freed pool memory cached (no release to the OS at every sync)
         hipMemPool_t pool;
@@ -293,8 +311,10 @@ extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt};
+                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.flist, t->cw.fcnt, t->cw.err,
+                  t->cw.dcnt, t->cw.doff, t->cw.part, t->cw.tot, t->cw.rec};
     for (void *p : ps) dfree(t, p);
+    if (t->pin) (void)hipHostFree(t->pin);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -1480,86 +1500,111 @@ extern "C" int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype,
 }
 
 // ------------------------------------------------------------------ compare (K3)
+// Device-side scan of NA uint64 arrays over n_ptr[0] elements (no host round
+// trip); totals[k] receives the sum of array k.
+template <int NA>
+static int dscan(st_tree *t, const DScanArgs<NA> &a, const uint64_t *n_ptr, uint64_t *part, uint64_t *totals) {
+    LAUNCH(t, "dscan", k_dscan_sums<NA>, DSCAN_WGS, 256, 0, a, n_ptr, part);
+    LAUNCH(t, "dscan", k_dscan_top<NA>, 1, 64, 0, part, (uint32_t)DSCAN_WGS, totals);
+    LAUNCH(t, "dscan", k_dscan_apply<NA>, DSCAN_WGS, 256, 0, a, n_ptr, (const uint64_t *)part);
+    return ST_OK;
+}
+
+static int ensure_cmp_work(st_tree *t) {
+    CmpWork &w = t->cw;
+    if (w.flist) return ST_OK;
+    CHK(dalloc_t(t, &w.flist, t->nslots));
+    CHK(dalloc_t(t, &w.fcnt, ST_MAXLEV + 2));
+    CHK(dalloc_t(t, &w.err, 1));
+    CHK(dalloc_t(t, &w.dcnt, t->S + 1));
+    CHK(dalloc_t(t, &w.doff, t->S + 1));
+    CHK(dalloc_t(t, &w.part, 4 * (DSCAN_WGS + 1)));
+    CHK(dalloc_t(t, &w.tot, 8));
+    return ST_OK;
+}
+
+static int grow_records(st_tree *t, uint64_t need) {
+    CmpWork &w = t->cw;
+    if (need <= w.cap) return ST_OK;
+    dfree(t, w.rec);
+    w.rec = nullptr;
+    w.cap = 0;
+    const uint64_t cap = need + need / 4 + 1024;
+    CHK(dalloc_t(t, &w.rec, cap));
+    w.cap = cap;
+    return ST_OK;
+}
+
 struct CompareOut {
     uint64_t n = 0;
-    DiffRec *rec = nullptr;   // device
+    const DiffRec *rec = nullptr;   // device, in the local tree's compare workspace
 };
 
+static uint32_t cmp_slice(const st_tree *t) {
+    uint32_t s = std::max<uint32_t>(64 * lane_region_bytes((uint32_t)t->W), cmp_merge_lds_bytes());
+    return (s + 15) & ~15u;
+}
+
+// K3: frontier, verify + count, device scan, write; ONE host round trip
+// (two when the record buffer has to grow).  A partitioned pair compares its
+// own segment range only (same partition on both sides).
 static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint32_t *clevel, uint64_t *cbucket,
                         int *cside, int *status) {
     *status = ST_OK;
+    co = CompareOut();
     if (A->W != B->W || A->S != B->S) { g_err = "trees of different shape"; return ST_EINVAL; }
     if (filter < 0 || filter > 2) { g_err = "both local_only and remote_only (case_clause)"; return ST_EINVAL; }
     if (A->device != B->device) { g_err = "trees on different devices"; return ST_EINVAL; }
+    if (A->partitioned != B->partitioned || (A->partitioned && (A->part_lo != B->part_lo || A->part_hi != B->part_hi))) {
+        g_err = "compare needs both trees partitioned alike";
+        return ST_EINVAL;
+    }
     st_tree *t = A;   // work is enqueued on the local tree's stream
     if (B->stream != A->stream) HIPCHK(hipStreamSynchronize(B->stream));
+    CHK(ensure_cmp_work(t));
+    CmpWork &w = t->cw;
     DevTree da = view(A), db = view(B);
-    const uint64_t S = A->S;
-    uint32_t *list[2] = {nullptr, nullptr}, *cnt = nullptr;
-    unsigned long long *bitmap = nullptr, *err = nullptr;
-    uint64_t *dcnt = nullptr, *doff = nullptr;
-    const uint64_t nwords = (S + 63) / 64;
-    int r = ST_OK;
-    auto done = [&]() {
-        dfree(t, list[0]); dfree(t, list[1]); dfree(t, cnt); dfree(t, bitmap); dfree(t, err); dfree(t, dcnt); dfree(t, doff);
-    };
-#define CCHK(x)                               \
-    do {                                      \
-        r = (x);                              \
-        if (r != ST_OK) { done(); return r; } \
-    } while (0)
-    CCHK(dalloc_t(t, &list[0], S + 1));
-    CCHK(dalloc_t(t, &list[1], S + 1));
-    CCHK(dalloc_t(t, &cnt, 2));
-    CCHK(dalloc_t(t, &bitmap, nwords + 1));
-    CCHK(dalloc_t(t, &err, 1));
-    HIPCHK(hipMemsetAsync(bitmap, 0, (nwords + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(err, 0xff, 8, t->stream));
-    LAUNCH(t, "tree_compare", k_cmp_top, 1, 64, 0, da, db, list[0], cnt);
-    int cur = 0;
-    for (uint32_t l = 1; l <= A->H; l++) {
-        const uint64_t lsize = A->base[l + 1] - A->base[l];
-        const uint64_t nsize = A->base[l + 2] - A->base[l + 1];
-        LAUNCH(t, "tree_compare", k_cmp_inner, grid_for(lsize, inner_block(t)), inner_block(t), inner_shmem(t), da, db, l,
-               (const uint32_t *)list[cur], (const uint32_t *)(cnt + cur), bitmap, filter, err);
-        LAUNCH(t, "tree_compare_list", k_bitmap_to_list, 1, 1024, 0, bitmap, (nsize + 63) / 64, list[cur ^ 1],
-               cnt + (cur ^ 1));
-        cur ^= 1;
+    const uint32_t L1 = A->H + 1;
+    uint64_t lo2 = 0, hi2 = ~0ull;
+    if (A->partitioned) {
+        const uint64_t per2 = A->S / A->W;   // segments under one level-2 bucket
+        lo2 = A->part_lo / per2;
+        hi2 = A->part_hi / per2;
     }
-    uint32_t nf = 0;
-    unsigned long long e = ~0ull;
-    HIPCHK(hipMemcpyAsync(&nf, cnt + cur, 4, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(&e, err, 8, hipMemcpyDeviceToHost, t->stream));
+    uint64_t *nfinal = w.tot + 1, *total = w.tot;
+    LAUNCH(t, "cmp_frontier", k_cmp_frontier, 1, 1024, 0, da, db, filter, lo2, hi2, w.flist, w.fcnt, w.err, nfinal);
+    const uint32_t slice = cmp_slice(t);
+    const uint32_t wpg = std::max<uint32_t>(1, std::min<uint32_t>(4, (160 * 1024) / slice));
+    LAUNCH(t, "cmp_visit", k_cmp_visit<false>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
+           (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)nullptr, (const uint64_t *)nullptr, (DiffRec *)nullptr,
+           (uint64_t)0, w.err, slice);
+    DScanArgs<1> sa;
+    sa.in[0] = w.dcnt;
+    sa.out[0] = w.doff;
+    CHK(dscan<1>(t, sa, nfinal, w.part, total));
+    LAUNCH(t, "cmp_write", k_cmp_visit<true>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
+           (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)w.doff, (const uint64_t *)total, w.rec, w.cap, w.err, slice);
+    HIPCHK(hipMemcpyAsync(t->pin, w.tot, 16, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 2, w.err, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
-    if (e == ~0ull && nf > 0) {
-        CCHK(dalloc_t(t, &dcnt, (uint64_t)nf + 1));
-        CCHK(dalloc_t(t, &doff, (uint64_t)nf + 1));
-        HIPCHK(hipMemsetAsync(dcnt + nf, 0, 8, t->stream));
-        LAUNCH(t, "tree_compare", (k_cmp_segments<false>), grid_for(nf), 256, 0, da, db, (const uint32_t *)list[cur],
-               (uint64_t)nf, filter, dcnt, (const uint64_t *)nullptr, (uint64_t)0, (DiffRec *)nullptr, err);
-        CCHK(exclusive_scan<uint64_t>(t, dcnt, doff, (uint64_t)nf + 1));
-        uint64_t total = 0;
-        HIPCHK(hipMemcpyAsync(&total, doff + nf, 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipMemcpyAsync(&e, err, 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipStreamSynchronize(t->stream));
-        if (e == ~0ull && total > 0) {
-            CCHK(dalloc_t(t, &co.rec, total));
-            LAUNCH(t, "tree_compare", (k_cmp_segments<true>), grid_for(nf), 256, 0, da, db, (const uint32_t *)list[cur],
-                   (uint64_t)nf, filter, dcnt, (const uint64_t *)doff, total, co.rec, err);
-            co.n = total;
-        }
-    }
+    const uint64_t ntot = t->pin[0], e = t->pin[2];
     if (e != ~0ull) {
         *status = ST_CORRUPTED;
         *clevel = (uint32_t)(e >> 56);
         *cbucket = (e & ((1ull << 56) - 1)) >> 1;
         *cside = (int)(e & 1);
-        dfree(t, co.rec);
-        co.rec = nullptr;
-        co.n = 0;
+        return ST_OK;
     }
-    done();
-#undef CCHK
+    (void)L1;
+    if (ntot > w.cap) {   // first compare with this many records: grow and write again
+        CHK(grow_records(t, ntot));
+        LAUNCH(t, "cmp_write", k_cmp_visit<true>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter,
+               (const uint32_t *)w.flist, (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)w.doff,
+               (const uint64_t *)total, w.rec, w.cap, w.err, slice);
+        HIPCHK(hipStreamSynchronize(t->stream));
+    }
+    co.n = ntot;
+    co.rec = w.rec;
     return ST_OK;
 }
 
@@ -1570,38 +1615,6 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
     int status = ST_OK;
     CHK(compare_core(local, remote, filter, co, clevel, cbucket, cside, &status));
     *n_diffs = co.n;
-    if (co.rec) {
-        // materialise the diff records' keys/values on the device, as st_compare does
-        st_tree *t = local;
-        DevTree da = view(local), db = view(remote);
-        uint64_t *kl, *al, *bl, *ko, *ao, *bo;
-        uint8_t *kind;
-        uint64_t *seg;
-        int r = ST_OK;
-        if ((r = dalloc_t(t, &kl, co.n + 1)) || (r = dalloc_t(t, &al, co.n + 1)) || (r = dalloc_t(t, &bl, co.n + 1)) ||
-            (r = dalloc_t(t, &ko, co.n + 1)) || (r = dalloc_t(t, &ao, co.n + 1)) || (r = dalloc_t(t, &bo, co.n + 1)) ||
-            (r = dalloc_t(t, &kind, co.n)) || (r = dalloc_t(t, &seg, co.n)))
-            return r;
-        LAUNCH(t, "diff_lengths", k_diff_lengths, grid_for(co.n + 1), 256, 0, da, db, (const DiffRec *)co.rec, co.n, kl, al, bl);
-        CHK(exclusive_scan<uint64_t>(t, kl, ko, co.n + 1));
-        CHK(exclusive_scan<uint64_t>(t, al, ao, co.n + 1));
-        CHK(exclusive_scan<uint64_t>(t, bl, bo, co.n + 1));
-        uint64_t tot[3];
-        HIPCHK(hipMemcpyAsync(&tot[0], ko + co.n, 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipMemcpyAsync(&tot[1], ao + co.n, 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipMemcpyAsync(&tot[2], bo + co.n, 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipStreamSynchronize(t->stream));
-        uint8_t *kh, *ah, *bh;
-        CHK(dalloc(t, (void **)&kh, tot[0] + 16));
-        CHK(dalloc(t, (void **)&ah, tot[1] + 16));
-        CHK(dalloc(t, (void **)&bh, tot[2] + 16));
-        LAUNCH(t, "diff_gather", k_diff_gather, grid_for(co.n), 256, 0, da, db, (const DiffRec *)co.rec, co.n,
-               (const uint64_t *)ko, kh, (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
-        HIPCHK(hipStreamSynchronize(t->stream));
-        void *ps[] = {kl, al, bl, ko, ao, bo, kind, seg, kh, ah, bh, co.rec};
-        for (void *p : ps) dfree(t, p);
-    }
-    HIPCHK(hipStreamSynchronize(local->stream));
     return status;
 }
 
@@ -1621,74 +1634,57 @@ extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_di
     int status = ST_OK;
     CHK(compare_core(local, remote, ST_FILTER_ALL, co, clevel, cbucket, cside, &status));
     *n_diffs = co.n;
-    if (status != ST_OK || !co.rec || co.n == 0) {
-        if (co.rec) dfree(local, co.rec);
-        HIPCHK(hipStreamSynchronize(local->stream));
-        return status;
-    }
+    if (status != ST_OK || co.n == 0) return status;
     st_tree *t = local;
     const uint64_t n = co.n;
     DevTree da = view(local), db = view(remote);
+    Scratch sc(t);
     uint8_t *take = nullptr, *kh = nullptr, *vh = nullptr;
     unsigned long long *fb = nullptr;
     uint64_t *one = nullptr, *kl = nullptr, *vl = nullptr, *pos = nullptr, *ko = nullptr, *vo = nullptr, *bko = nullptr,
              *bvo = nullptr;
     uint32_t *dcl = nullptr;
-    int r = ST_OK;
-    auto done = [&]() {
-        void *ps[] = {take, kh, vh, fb, one, kl, vl, pos, ko, vo, bko, bvo, dcl, co.rec};
-        for (void *p : ps) dfree(t, p);
-    };
-#define XCHK(x)                               \
-    do {                                      \
-        r = (x);                              \
-        if (r != ST_OK) { done(); return r; } \
-    } while (0)
-    XCHK(dalloc_t(t, &take, n));
-    XCHK(dalloc_t(t, &fb, 1));
-    XCHK(dalloc_t(t, &one, n + 1));
-    XCHK(dalloc_t(t, &kl, n + 1));
-    XCHK(dalloc_t(t, &vl, n + 1));
-    XCHK(dalloc_t(t, &pos, n + 1));
-    XCHK(dalloc_t(t, &ko, n + 1));
-    XCHK(dalloc_t(t, &vo, n + 1));
+    CHK(sc.alloc(&take, n));
+    CHK(sc.alloc(&fb, 1));
+    CHK(sc.alloc(&one, n + 1));
+    CHK(sc.alloc(&kl, n + 1));
+    CHK(sc.alloc(&vl, n + 1));
+    CHK(sc.alloc(&pos, n + 1));
+    CHK(sc.alloc(&ko, n + 1));
+    CHK(sc.alloc(&vo, n + 1));
     HIPCHK(hipMemsetAsync(fb, 0xff, 8, t->stream));
-    LAUNCH(t, "diff_apply", k_diff_apply_select, grid_for(n), 256, 0, da, db, (const DiffRec *)co.rec, n, take, fb);
-    LAUNCH(t, "diff_apply", k_diff_apply_lengths, grid_for(n + 1), 256, 0, db, (const DiffRec *)co.rec, n,
-           (const uint8_t *)take, (const unsigned long long *)fb, one, kl, vl);
-    XCHK(exclusive_scan<uint64_t>(t, one, pos, n + 1));
-    XCHK(exclusive_scan<uint64_t>(t, kl, ko, n + 1));
-    XCHK(exclusive_scan<uint64_t>(t, vl, vo, n + 1));
-    uint64_t tot[3] = {0, 0, 0};
-    unsigned long long hfb = 0;
-    HIPCHK(hipMemcpyAsync(&tot[0], pos + n, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(&tot[1], ko + n, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(&tot[2], vo + n, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(&hfb, fb, 8, hipMemcpyDeviceToHost, t->stream));
+    LAUNCH(t, "diff_apply", k_diff_apply_select, grid_for(n), 256, 0, da, db, co.rec, n, take, fb);
+    LAUNCH(t, "diff_apply", k_diff_apply_lengths, grid_for(n + 1), 256, 0, db, co.rec, n, (const uint8_t *)take,
+           (const unsigned long long *)fb, one, kl, vl);
+    CHK(exclusive_scan<uint64_t>(t, one, pos, n + 1));
+    CHK(exclusive_scan<uint64_t>(t, kl, ko, n + 1));
+    CHK(exclusive_scan<uint64_t>(t, vl, vo, n + 1));
+    HIPCHK(hipMemcpyAsync(t->pin, pos + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 1, ko + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 2, vo + n, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 3, fb, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
-    *crashed = hfb != ~0ull ? 1 : 0;
-    const uint64_t m = tot[0];
+    const uint64_t m = t->pin[0], kb = t->pin[1], vb = t->pin[2];
+    *crashed = t->pin[3] != ~0ull ? 1 : 0;
     if (m) {
-        XCHK(dalloc(t, (void **)&kh, tot[1] + HEAP_SLACK));
-        XCHK(dalloc(t, (void **)&vh, tot[2] + HEAP_SLACK));
-        XCHK(dalloc_t(t, &bko, m + 1));
-        XCHK(dalloc_t(t, &bvo, m + 1));
-        XCHK(dalloc_t(t, &dcl, m));
-        LAUNCH(t, "diff_apply", k_diff_apply_gather, grid_for(n + 1), 256, 0, db, (const DiffRec *)co.rec, n,
-               (const uint64_t *)pos, (const uint64_t *)ko, (const uint64_t *)vo, kh, bko, vh, bvo);
+        CHK(sc.bytes(&kh, kb + HEAP_SLACK));
+        CHK(sc.bytes(&vh, vb + HEAP_SLACK));
+        CHK(sc.alloc(&bko, m + 1));
+        CHK(sc.alloc(&bvo, m + 1));
+        CHK(sc.alloc(&dcl, m));
+        LAUNCH(t, "diff_apply", k_diff_apply_gather, grid_for(n + 1), 256, 0, db, co.rec, n, (const uint64_t *)pos,
+               (const uint64_t *)ko, (const uint64_t *)vo, kh, bko, vh, bvo);
         IngestIn in{};
         in.n = m; in.krec = kh; in.koff = bko; in.vheap = vh; in.voff = bvo;
         in.verify_rehash = true; in.clevel_out = dcl;
-        XCHK(ingest(t, in));
+        CHK(ingest(t, in));
         std::vector<uint32_t> cl(m);
-        XCHK(d2h(t, cl.data(), dcl, m * 4));
+        CHK(d2h(t, cl.data(), dcl, m * 4));
         uint64_t rej = 0;
         for (uint64_t i = 0; i < m; i++) rej += cl[i] != 0;
         *n_rejected = rej;
         *n_applied = m - rej;
     }
-    done();
-#undef XCHK
     HIPCHK(hipStreamSynchronize(t->stream));
     return ST_OK;
 }
@@ -1708,52 +1704,46 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
     res->eoff[0] = 0;
     res->eoff[1] = n;
     res->n_entries = n;
+    res->koff = (uint64_t *)calloc(n + 1, 8);
+    res->aoff = (uint64_t *)calloc(n + 1, 8);
+    res->boff = (uint64_t *)calloc(n + 1, 8);
+    res->kind = (uint8_t *)calloc(n + 1, 1);
+    res->seg = (uint64_t *)calloc(n + 1, 8);
     if (n == 0) {
         res->ktype = (uint8_t *)calloc(1, 1);
-        res->koff = (uint64_t *)calloc(1, 8);
-        res->aoff = (uint64_t *)calloc(1, 8);
-        res->boff = (uint64_t *)calloc(1, 8);
         res->kheap = (uint8_t *)malloc(1);
         res->aheap = (uint8_t *)malloc(1);
         res->bheap = (uint8_t *)malloc(1);
-        res->kind = (uint8_t *)calloc(1, 1);
-        res->seg = (uint64_t *)calloc(1, 8);
         *out = res;
         return ST_OK;
     }
     DevTree da = view(local), db = view(remote);
+    Scratch sc(t);
     uint64_t *kl = nullptr, *al = nullptr, *bl = nullptr, *ko = nullptr, *ao = nullptr, *bo = nullptr, *seg = nullptr;
     uint8_t *kind = nullptr, *kh = nullptr, *ah = nullptr, *bh = nullptr;
     int r = ST_OK;
-    auto done = [&]() {
-        void *ps[] = {kl, al, bl, ko, ao, bo, seg, kind, kh, ah, bh, co.rec};
-        for (void *p : ps) dfree(t, p);
-    };
-    if ((r = dalloc_t(t, &kl, n + 1)) || (r = dalloc_t(t, &al, n + 1)) || (r = dalloc_t(t, &bl, n + 1)) ||
-        (r = dalloc_t(t, &ko, n + 1)) || (r = dalloc_t(t, &ao, n + 1)) || (r = dalloc_t(t, &bo, n + 1)) ||
-        (r = dalloc_t(t, &kind, n)) || (r = dalloc_t(t, &seg, n))) { done(); st_free_result(res); return r; }
-    hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, da, db, (const DiffRec *)co.rec, n, kl, al, bl);
+    auto fail = [&](int rc) { st_free_result(res); return rc; };
+    if ((r = sc.alloc(&kl, n + 1)) || (r = sc.alloc(&al, n + 1)) || (r = sc.alloc(&bl, n + 1)) || (r = sc.alloc(&ko, n + 1)) ||
+        (r = sc.alloc(&ao, n + 1)) || (r = sc.alloc(&bo, n + 1)) || (r = sc.alloc(&kind, n)) || (r = sc.alloc(&seg, n)))
+        return fail(r);
+    hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, da, db, co.rec, n, kl, al, bl);
     if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, al, ao, n + 1)) ||
-        (r = exclusive_scan<uint64_t>(t, bl, bo, n + 1))) { done(); st_free_result(res); return r; }
-    res->koff = (uint64_t *)calloc(n + 1, 8);
-    res->aoff = (uint64_t *)calloc(n + 1, 8);
-    res->boff = (uint64_t *)calloc(n + 1, 8);
+        (r = exclusive_scan<uint64_t>(t, bl, bo, n + 1)))
+        return fail(r);
     if ((r = d2h(t, res->koff, ko, (n + 1) * 8)) || (r = d2h(t, res->aoff, ao, (n + 1) * 8)) ||
-        (r = d2h(t, res->boff, bo, (n + 1) * 8))) { done(); st_free_result(res); return r; }
+        (r = d2h(t, res->boff, bo, (n + 1) * 8)))
+        return fail(r);
     const uint64_t kb = res->koff[n], ab = res->aoff[n], bb = res->boff[n];
-    if ((r = dalloc(t, (void **)&kh, kb + 16)) || (r = dalloc(t, (void **)&ah, ab + 16)) || (r = dalloc(t, (void **)&bh, bb + 16))) {
-        done(); st_free_result(res); return r;
-    }
-    hipLaunchKernelGGL(k_diff_gather, dim3(grid_for(n)), dim3(256), 0, t->stream, da, db, (const DiffRec *)co.rec, n,
-                       (const uint64_t *)ko, kh, (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
+    if ((r = sc.bytes(&kh, kb + 16)) || (r = sc.bytes(&ah, ab + 16)) || (r = sc.bytes(&bh, bb + 16))) return fail(r);
+    hipLaunchKernelGGL(k_diff_gather, dim3(grid_for(n)), dim3(256), 0, t->stream, da, db, co.rec, n, (const uint64_t *)ko, kh,
+                       (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
+    if (hipGetLastError() != hipSuccess) { g_err = "launch diff_gather"; return fail(ST_EDEVICE); }
     res->kheap = (uint8_t *)malloc(kb + 1);
     res->aheap = (uint8_t *)malloc(ab + 1);
     res->bheap = (uint8_t *)malloc(bb + 1);
-    res->kind = (uint8_t *)malloc(n);
-    res->seg = (uint64_t *)malloc(n * 8);
     if ((r = d2h(t, res->kheap, kh, kb)) || (r = d2h(t, res->aheap, ah, ab)) || (r = d2h(t, res->bheap, bh, bb)) ||
-        (r = d2h(t, res->kind, kind, n)) || (r = d2h(t, res->seg, seg, n * 8))) { done(); st_free_result(res); return r; }
-    done();
+        (r = d2h(t, res->kind, kind, n)) || (r = d2h(t, res->seg, seg, n * 8)))
+        return fail(r);
     records_to_keys(res, n);
     *out = res;
     return ST_OK;
