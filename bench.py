@@ -1,27 +1,42 @@
-"""bench.py — synctree keys rehashed/s (+ build and exchange tree-diff rates)
-on MI355X, per BASELINE.json.
+"""bench.py — synctree keys rehashed/s (+ build, exchange tree-diffs/s and the
+other BASELINE configs) on MI355X, per BASELINE.json.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--keys 10000000]
 
 A step is one full ``synctree:rehash/1`` (src/synctree.erl:493-509) of a
-device-resident 10M-key tree: K1 segment_hash over all 2^20 segments + K2
-level_rehash for levels 5..1 + the top hash (BASELINE config 2).  With N GPUs
-(torchrun, one rank per GPU) every rank owns its own ensemble's tree (keys
-seeded SEED ^ rank): ensemble sharding, weak scaling, no collective in the
-timed region.  An RCCL all-gather of the per-ensemble top hashes
-runs once after timing to show the cross-GPU combine.
+device-resident 10M-key tree: K1 segment_hash over all 2^20 segments + the
+inner levels 5..1 + the top hash (BASELINE config 2).  ``--gpus N`` with no
+torchrun environment starts N ranks itself (``torch.distributed.run``, one
+process per GPU) before any GPU call; every rank owns its own ensemble's tree
+(keys seeded SEED ^ rank): ensemble sharding, weak scaling, no collective in
+the timed region.  ``value`` = all ranks' keys / the slowest
+rank's time.
 
-Also reported (rank 0): build = st_insert_int64 of the 10M keys from HBM into
-an empty tree (key->segment, sort, merge, dirty rehash); compare = config 3
-(two 10M-key trees, 0.1% of non-empty segments with a bumped first value,
-rehashed) through the device K3 compare; the per-kernel roofline of K1 from
-HIP events on the library's stream; the CPU baseline (oracle/ C port, one
-host thread) rehashing the same 10M-key tree.
+Also reported (rank 0 unless noted):
+  build      st_insert_int64 of the 10M keys from HBM into an empty tree
+  compare    config 3: two 10M-key trees, every 1000th non-empty segment's
+             first value bumped; K3 with the ordered diff records on the
+             device (tree-diffs/s) and copied to the host; + compare roofline
+  ensembles  config 4 per GPU (every rank): --ensembles trees x 1M keys, one
+             st_rehash_group batch + the RCCL all-gather of every ensemble's
+             top hash (st_tops_to_device -> all_gather_into_tensor)
+  partition  config 5 (every rank): a 100M-key tree partitioned by segment
+             range over the ranks, 1M-key write batches
+  config1    100k keys build + rehash + top hash; per-key get/insert latency
+  cold_l3    K1 with the 256 MiB Infinity Cache flushed before every launch
+  cpu_baseline  the C port (oracle/) rehashing the same 10M-key tree on the
+             host: 1 thread and every host core
+The K1 roofline's ``traffic`` comes from rocprofv3 PMC passes (FETCH_SIZE,
+WRITE_SIZE) run by this script on a K1-only child process (N = 1).
 """
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -32,21 +47,14 @@ sys.path.insert(0, ROOT)
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): HBM3E 8.0 TB/s spec.
 # Integer VALU, measured on gfx950 (tools/microbench/valu_peak.cpp,
 # profiles/r01_valu_peak.txt): v_add_u32 / v_bitop3_b32 issue a wave64 in 2
-# SIMD cycles, v_add3_u32 / v_alignbit_b32 in 4.  The MD5 block loop of
-# k_segment_hash_tiled (ISA count) is 130 add + 64 bitop3
-# (2 cyc) and 65 add3 + 64 alignbit (4 cyc) = 916 SIMD cycles per wave =
-# 14.3 SIMD-cycles per 64-B block.
+# SIMD cycles, v_add3_u32 / v_alignbit_b32 in 4.  The MD5 block loop (ISA
+# count) is 130 add + 64 bitop3 (2 cyc) and 65 add3 + 64
+# alignbit (4 cyc) = 916 SIMD cycles per wave = 14.3 SIMD-cycles per block.
 HBM_PEAK_GBS = 8000.0
 SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9
 MD5_SIMD_CYCLES_PER_BLOCK = 916.0 / 64
-# HBM bytes of one K1 launch (k_segment_hash_tiled_p) from rocprofv3 PMC,
-# separate FETCH_SIZE / WRITE_SIZE passes (profiles/r01_session5_pmc_summary.txt):
-# FETCH_SIZE x 2 (gfx950 counts half of a wide coalesced 16-B/lane stream,
-# MI355X_MICROARCH.md; the doubled 220.1 MB = 211.1 MB tiles + 8.4 MB tile
-# metadata) + WRITE_SIZE (37.1 MB: 19 MB of entries stored as scattered
-# 16-B + 2-B writes), KiB -> bytes.
-K1_PMC_TRAFFIC_BYTES = int((2 * 107486.5 + 36233.6) * 1024)
+K1_KERNEL = 'k_rehash_fused'   # K1 segment_hash + the inner levels, one launch
 METRIC = 'synctree keys rehashed/sec + exchange tree-diffs/sec at 10M keys, 1–8 GPUs'
 
 
@@ -58,33 +66,64 @@ def md5_blocks(nbytes):
     return (np.asarray(nbytes, np.int64) + 8) // 64 + 1
 
 
-def main():
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--keys', type=int, default=10_000_000)
-    ap.add_argument('--no-cpu', action='store_true', help='skip the CPU baseline leg')
-    ap.add_argument('--no-extras', action='store_true', help='skip build/compare/ensemble legs')
-    ap.add_argument('--ensembles', type=int, default=32, help='config-4 leg: ensembles (trees) per GPU')
+    ap.add_argument('--no-cpu', action='store_true', help='skip the CPU baseline legs')
+    ap.add_argument('--no-extras', action='store_true', help='skip every leg but the headline rehash')
+    ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
+    ap.add_argument('--ensembles', type=int, default=512,
+                    help='config-4 leg: ensembles (trees) per GPU (4096 over 8 GPUs = 512)')
     ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
     ap.add_argument('--part-keys', type=int, default=100_000_000, help='config-5 leg: keys in the partitioned tree')
     ap.add_argument('--part-batches', type=int, default=5, help='config-5 leg: timed write batches')
     ap.add_argument('--part-batch-keys', type=int, default=1_000_000, help='config-5 leg: keys per write batch')
-    args = ap.parse_args()
+    ap.add_argument('--pmc-probe', action='store_true', help=argparse.SUPPRESS)
+    return ap.parse_args()
 
-    import torch
+
+def main():
+    args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # one process per GPU, started before this process touches the GPU
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args.gpus),
+               '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    if args.pmc_probe:
+        return pmc_probe(args)
+
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    pmc = None
+    if rank == 0 and world == 1 and not args.no_pmc:
+        pmc = k1_pmc_traffic(args)          # child processes, before this one touches the GPU
+
+    import torch
+    ndev = torch.cuda.device_count()
+    dev_index = local % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device('cuda', dev_index)
+    dist = None
+    coll_dev = dev
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        dist = None
-        torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+        if ndev >= world:
+            dist.init_process_group('nccl', device_id=dev)
+        else:   # more ranks than GPUs (a rehearsal on a small box): host collectives
+            dist.init_process_group('gloo')
+            coll_dev = torch.device('cpu')
 
     from riak_ensemble_amd import synctree_hip, workload
 
@@ -96,11 +135,8 @@ def main():
     vals_d = torch.from_numpy(vals_h).to(dev)
     torch.cuda.synchronize()
 
-    tree = synctree_hip.DeviceTree(device=local)
-    t0 = time.perf_counter()
+    tree = synctree_hip.DeviceTree(device=dev_index)
     nc = tree.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
-    torch.cuda.synchronize()
-    build_s = time.perf_counter() - t0
     assert nc == 0 and tree.num_entries() == n
     top0 = tree.top_hash()
 
@@ -120,7 +156,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     assert tree.top_hash() == top0, 'rehash changed the top hash of a consistent tree'
@@ -130,15 +166,14 @@ def main():
     tree.kernel_stats('*reset*')
     for _ in range(args.steps):
         tree.rehash()
-    k1_n, k1_ms = tree.kernel_stats('segment_hash')
-    k2_n, k2_ms = tree.kernel_stats('level_rehash')
+    k1_n, k1_ms = tree.kernel_stats('rehash_fused')
     tree.set_timing(False)
 
-    # cross-GPU combine of the ensembles' top hashes (RCCL all-gather, untimed)
+    # cross-GPU combine of the ensembles' top hashes (all-gather, untimed)
     tops_ok = True
     if dist:
         from riak_ensemble_amd import parallel
-        tops = parallel.gather_tops(dist, [top0], device=dev)
+        tops = parallel.gather_tops(dist, [top0], device=coll_dev)
         tops_ok = len(tops) == world and tops[rank] == top0
 
     ms_per_step = el * 1000.0 / args.steps
@@ -146,48 +181,35 @@ def main():
 
     out = None
     if rank == 0:
-        # algorithmic bytes / ops of K1 per launch
         S = 1 << 20
-        counts = None
-        pres, _ = tree.level_entries(6)
-        nseg = int(pres.sum())
-        # segment sizes from the level-5 images are not needed: values are fixed
-        # 17 B, so bytes per segment = 17 * keys in segment.  Use the oracle-free
-        # count from the device CSR through exchange_get is costly; instead the
-        # block count follows from the per-segment key histogram computed on host.
-        seg_of = None
-        try:
-            seg_of = _segment_histogram(tree, keys_h)
-        except Exception as e:  # pragma: no cover
-            log('histogram failed', e)
-        # Algorithmic work of one K1 launch (k_segment_hash_tiled): the hash
-        # input of every segment (its values, 17 B per key: MD5 padding is
-        # computed, not data), the tile metadata (segment id + block count,
-        # 2 x 4 B per segment; 16 B per 64-segment tile) and the 18-B entry
-        # (md5 + tag) written per segment.  The tiles K1 actually streams hold
-        # each message padded to whole 64-B blocks (64 B x blocks, reported
-        # as tile_bytes); the PMC traffic shows what HBM really served.
-        if seg_of is not None:
-            seg_blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
-        else:
-            seg_blocks = int(n * 17 / 64 + nseg)
-        blocks = seg_blocks
-        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S * 18
+        seg_of = _segment_histogram(tree, keys_h)
+        seg_blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
+        # Algorithmic bytes of one rehash launch (k_rehash_fused = K1 + the
+        # inner levels): every segment's hash input (its values, 17 B per key;
+        # MD5 padding is computed, not data), the tile metadata (segment id +
+        # block count, 2 x 4 B per segment; 16 B per 64-segment tile), the
+        # 18-B entry (md5 + tag) written per segment and per inner node
+        # (69,905 for W=16, H=5; their inputs stay in LDS, except the 16
+        # children read by each of the 17 climbing nodes).
+        inner_nodes = sum(16 ** l for l in range(5))
+        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
+        seg_blocks += 349525   # inner-node MD5 blocks (full nodes: 5 each)
         k1_avg_ms = max(k1_ms / max(k1_n, 1), 1e-9)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
-        t_valu = blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
-        roof = {'bound': 'hbm' if t_hbm >= t_valu else 'valu', 'achieved': round(achieved_gbs, 1),
-                'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
-                'traffic': K1_PMC_TRAFFIC_BYTES,
-                'kernel': 'k_segment_hash_tiled_p (K1 segment_hash)', 'kernel_avg_ms': round(k1_avg_ms, 4),
-                'bytes_per_launch': k1_bytes, 'tile_bytes_per_launch': 64 * seg_blocks, 'md5_blocks_per_launch': blocks,
-                't_min_hbm_us': round(t_hbm * 1e6, 2),
+        t_valu = seg_blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
+        roof = {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
+                'traffic': pmc['traffic_bytes'] if pmc and pmc.get('traffic_bytes') else None,
+                'kernel': K1_KERNEL + ' (K1 segment_hash + levels 5..1 + top, one launch)',
+                'kernel_avg_ms': round(k1_avg_ms, 4),
+                'kernel_time_source': 'HIP events on the library stream around every launch (%d launches)' % k1_n,
+                'bytes_per_launch': k1_bytes, 'tile_bytes_per_launch': 64 * seg_blocks,
+                'md5_blocks_per_launch': seg_blocks, 't_min_hbm_us': round(t_hbm * 1e6, 2),
                 'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),
                          'simd_cycles_per_block': round(MD5_SIMD_CYCLES_PER_BLOCK, 2),
                          'peak': '1024 SIMDs x 2.4 GHz'},
-                'level_rehash_avg_ms_per_step': round(k2_ms / max(args.steps, 1), 4),
-                'level_rehash_kernel': 'k_levels_flow16 (levels 5..1 + top, one launch)'}
+                'pmc': pmc}
         out = {'metric': METRIC, 'value': round(value, 1), 'unit': 'keys/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32',
@@ -197,25 +219,24 @@ def main():
                           'keys_per_gpu': n, 'width': 16, 'segments': S,
                           'parallelism': 'ensemble-sharded: one tree per GPU, no collective in the timed region'},
                'roofline': roof,
-               'rehash_top_hash': top0.hex(), 'tops_allgather_ok': tops_ok,
-               'build': {'keys_per_s': round(n / build_s, 1), 'seconds': round(build_s, 4),
-                         'note': 'first st_insert_int64 from HBM into an empty tree (includes allocator warm-up)'}}
+               'rehash_top_hash': top0.hex(), 'tops_allgather_ok': tops_ok}
         if not args.no_extras:
-            out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, local, torch)
-            out['compare'] = _bench_compare(synctree_hip, tree, keys_h, vals_h, keys_d, vals_d, n, local, torch)
-            out['leveldb'] = _bench_leveldb(synctree_hip, tree, local, torch)
+            out['cold_l3'] = _bench_cold_l3(tree, torch, dev, k1_bytes, k1_avg_ms)
+            out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, dev_index, torch)
+            out['compare'] = _bench_compare(synctree_hip, tree, keys_d, vals_d, n, dev_index, torch)
+            out['leveldb'] = _bench_leveldb(synctree_hip, tree, dev_index, torch)
     tree.close()
     del keys_d, vals_d
     if not args.no_extras:
-        # config 5 runs on every rank (one tree partitioned by segment range)
-        part = _bench_partition(synctree_hip, dist, args, local, torch)
+        # configs 4 and 5 run on every rank
+        ens = _bench_ensembles(synctree_hip, dist, coll_dev, args, dev_index, torch)
+        part = _bench_partition(synctree_hip, dist, coll_dev, args, dev_index, torch)
         if rank == 0:
+            out['ensembles'] = ens
             out['partition'] = part
-            out['ensembles'] = _bench_ensembles(synctree_hip, workload, args.ensembles, args.ensemble_keys, local, torch)
-            out['config1'] = _bench_config1(synctree_hip, workload, local, torch, cpu=not args.no_cpu)
-    if rank == 0:
-        if not args.no_cpu:
-            out['cpu_baseline'] = _cpu_baseline(keys_h, vals_h, top0)
+            out['config1'] = _bench_config1(synctree_hip, workload, dev_index, torch, cpu=not args.no_cpu)
+    if rank == 0 and not args.no_cpu:
+        out['cpu_baseline'] = _cpu_baseline(keys_h, vals_h, top0)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -223,11 +244,207 @@ def main():
         print(json.dumps(out), flush=True)
 
 
+# ---------------------------------------------------------------- PMC traffic of K1
+def pmc_probe(args):
+    """Child of k1_pmc_traffic (run under rocprofv3 --pmc): build the tree and
+    rehash it a few times; only K1 launches are counted (kernel regex)."""
+    import torch
+    from riak_ensemble_amd import synctree_hip, workload
+    n = args.keys
+    keys = torch.from_numpy(workload.keys_int63(n, workload.SEED)).cuda()
+    vals = torch.from_numpy(workload.obj_hash_values(n)).cuda()
+    t = synctree_hip.DeviceTree()
+    t.insert_int64_device(keys.data_ptr(), vals.data_ptr(), n, 17)
+    for _ in range(6):
+        t.rehash()
+    t.sync()
+    t.close()
+
+
+def k1_pmc_traffic(args):
+    """HBM bytes per K1 launch from rocprofv3 PMC, one counter group per pass
+    (FETCH_SIZE, then WRITE_SIZE), corrected as MI355X_MICROARCH.md §HBM
+    prescribes: FETCH_SIZE counts half the bytes of a wide coalesced 16-B/lane
+    stream on gfx950 (x2); WRITE_SIZE is exact for 16-B stores.  Both are KiB.
+    Infinity-Cache hits are counted too (the tile array may stay resident
+    between back-to-back launches)."""
+    prof = shutil.which('rocprofv3')
+    if not prof:
+        return {'error': 'rocprofv3 not found'}
+    res = {}
+    env = dict(os.environ, TMPDIR=tempfile.gettempdir())
+    for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
+        d = tempfile.mkdtemp(prefix='pmc_')
+        cmd = ['timeout', '-s', 'KILL', '150', prof, '--pmc', ctr, '--kernel-include-regex', K1_KERNEL, '-f', 'csv',
+               '-d', d, '-o', 'pmc', '--', sys.executable, os.path.abspath(__file__), '--pmc-probe', '--keys',
+               str(args.keys)]
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
+        vals = []
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith('counter_collection.csv'):
+                    import csv
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        if row.get('Counter_Name') == ctr and K1_KERNEL in row.get('Kernel_Name', ''):
+                            vals.append(float(row['Counter_Value']))
+        shutil.rmtree(d, ignore_errors=True)
+        if r.returncode != 0 or not vals:
+            res[ctr] = {'error': 'rc=%d, %d samples: %s' % (r.returncode, len(vals), r.stderr.decode()[-300:])}
+            continue
+        # the first launch follows the tile build; report the steady state (launches 2..)
+        steady = vals[1:] if len(vals) > 1 else vals
+        res[ctr] = {'kib_per_launch_mean': round(sum(steady) / len(steady), 1), 'launches': len(vals),
+                    'pass_s': round(time.perf_counter() - t0, 1)}
+    try:
+        fetch = res['FETCH_SIZE']['kib_per_launch_mean'] * 1024 * 2
+        write = res['WRITE_SIZE']['kib_per_launch_mean'] * 1024
+        res['traffic_bytes'] = int(fetch + write)
+        res['read_bytes'] = int(fetch)
+        res['write_bytes'] = int(write)
+        res['formula'] = 'FETCH_SIZE[KiB] x 1024 x 2 (gfx950 half-count of 16-B/lane streams) + WRITE_SIZE[KiB] x 1024'
+    except (KeyError, TypeError):
+        pass
+    return res
+
+
+# ---------------------------------------------------------------- legs
+def _bench_cold_l3(tree, torch, dev, k1_bytes, hot_ms, reps=5):
+    """The rehash kernel with a cold Infinity Cache: a 1 GiB read (4x the
+    256 MiB L3) before every rehash, so the tiles come from HBM (as they
+    always do for trees whose tiles exceed the L3, e.g. config 5's 1.8 GB).
+    Kernel time from HIP events on the library stream."""
+    flush = torch.ones(1 << 30, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    tree.set_timing(True)
+    tree.kernel_stats('*reset*')
+    for i in range(reps):
+        int(flush.sum())          # 1 GiB read: the L3 now holds clean lines of `flush`
+        torch.cuda.synchronize()
+        tree.rehash()
+        tree.sync()
+    n, ms = tree.kernel_stats('rehash_fused')
+    tree.set_timing(False)
+    del flush
+    avg = ms / max(n, 1)
+    gbs = k1_bytes / (avg / 1e3) / 1e9
+    return {'kernel_avg_ms': round(avg, 4), 'achieved_GBps': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 4),
+            'hot_kernel_avg_ms': round(hot_ms, 4), 'launches': n,
+            'what': 'rehash kernel after a 1 GiB read per launch (Infinity Cache flushed): tiles read from HBM'}
+
+
+def _segment_histogram(tree, keys_h):
+    """Keys per segment via the device key->segment map (st_segment_of_batch)."""
+    step = 1 << 21
+    parts = []
+    for i in range(0, len(keys_h), step):
+        parts.append(np.array(tree.segments_of(keys_h[i:i + step].tolist()), np.int64))
+    segs = np.concatenate(parts)
+    return np.bincount(segs, minlength=1 << 20)
+
+
+def _bench_build(synctree_hip, keys_d, vals_d, n, local, torch, reps=3):
+    """Full build (insert of N keys from HBM into an empty tree)."""
+    times = []
+    for _ in range(reps + 1):
+        t = synctree_hip.DeviceTree(device=local)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        t.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        t.close()
+    best = min(times[1:])
+    return {'keys_per_s': round(n / best, 1), 'seconds': round(best, 4),
+            'what': 'st_insert_int64: key->segment MD5, radix sort, run sort, merge, gather, dirty rehash (all levels)'}
+
+
+def _compare_roofline(tree_a, ms):
+    """Algorithmic bytes of one compare: per visited inner node and
+    side, its W child entries + the parent's entry (18 B each: md5 + tag),
+    read to verify it and diff its children; per visited segment pair the
+    offsets, key records, values and entries of both sides (counted on the
+    device); plus the 32-B diff records written."""
+    vis, seg_bytes = tree_a.compare_stats()
+    H = tree_a.height
+    inner = sum(vis[1:H + 1])
+    W = tree_a.width
+    inner_bytes = 2 * inner * (W + 1) * 18
+    return vis, inner_bytes + seg_bytes
+
+
+def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=20):
+    """Config 3: B = A with the first value of every 1000th non-empty segment
+    bumped (test/synctree_intercepts.erl:96-104) and rehashed."""
+    pres, _ = tree_a.level_entries(6)
+    segs = np.nonzero(pres)[0][::1000].tolist()
+    imgs = tree_a.exchange_get_batch(6, segs)
+    mut = [(img[0][0], bytes([(img[0][1][0] + 1) % 256]) + img[0][1][1:]) for img in imgs]
+    tb = synctree_hip.DeviceTree(device=local)
+    tb.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    tb.insert_batch([k for k, _ in mut], [v for _, v in mut])
+    nd = tree_a.compare_device(tb)
+    assert nd == len(segs), (nd, len(segs))
+    tree_a.set_timing(True)
+    tree_a.kernel_stats('*reset*')
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tree_a.compare_device(tb)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    kern = {k: round(tree_a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_frontier', 'cmp_visit', 'cmp_scan', 'cmp_reorder')}
+    tree_a.set_timing(False)
+    vis, algo = _compare_roofline(tree_a, dt * 1e3)
+    t0 = time.perf_counter()
+    res = tree_a.compare(tb)
+    dt_host = time.perf_counter() - t0
+    assert res[0] == 'ok' and len(res[1]) == len(segs)
+    # (B's bumped FIRST byte is the ?H_OBJ_NONE prefix: the reference exchange
+    # would crash in valid_obj_hash on these diffs, and so does ours)
+    assert tree_a.exchange_apply(tb)[0] == 'exchange_failed'
+    tb.close()
+    # riak_ensemble_exchange.erl:71-97 as one device batch: B2 = A with the
+    # same keys' Seq advanced (last byte + 1, so B2 > A: valid_obj_hash holds);
+    # compare + apply into a fresh copy of A, which then equals B2
+    mut2 = [(k, v[:-1] + bytes([v[-1] + 1])) for k, v in
+            ((img[0][0], img[0][1]) for img in imgs) if v[-1] < 255]
+    tb2 = synctree_hip.DeviceTree(device=local)
+    tb2.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    tb2.insert_batch([k for k, _ in mut2], [v for _, v in mut2])
+    ta = synctree_hip.DeviceTree(device=local)
+    ta.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res_apply = ta.exchange_apply(tb2)
+    torch.cuda.synchronize()
+    dt_apply = time.perf_counter() - t0
+    assert res_apply[0] == 'ok' and res_apply[1]['applied'] == len(mut2), res_apply
+    assert ta.top_hash() == tb2.top_hash(), 'exchange did not converge the trees'
+    ta.close()
+    tb2.close()
+    gbs = algo / dt / 1e9
+    return {'tree_compares_per_s': round(1.0 / dt, 1), 'ms_per_compare': round(dt * 1e3, 4),
+            'diff_keys': nd, 'diff_keys_per_s': round(nd / dt, 1),
+            'kernel_ms_per_compare': kern,
+            'visited_per_level': vis[1:tree_a.height + 2],
+            'roofline': {'bound': 'hbm', 'achieved': round(gbs, 2), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(gbs / HBM_PEAK_GBS, 6), 'bytes_per_compare': int(algo),
+                         'note': 'latency-bound: ~1 MB of algorithmic traffic per compare; the bound that binds is '
+                                 'the dependent chain frontier -> verify/merge -> scan -> write'},
+            'ms_per_compare_incl_d2h_records': round(dt_host * 1e3, 4),
+            'exchange_apply_ms': round(dt_apply * 1e3, 4),
+            'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
+                              'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),
+            'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 (frontier, verify + '
+                    'merge-join, device scan, reorder) with the ordered diff records left on the device; one host '
+                    'round trip per compare'}
+
+
 def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
     """synctree_leveldb format of the 10M-key tree:
-    device encode of every node record (k_snap_sizes + 3 scans + k_snap_write),
-    the host-inclusive snapshot (D2H of the records), and restore into a fresh
-    tree from those host records (host ETF decode + upload)."""
+    device encode of every node record, the host-inclusive snapshot (D2H of
+    the records), and restore into a fresh tree from those host records."""
     import ctypes
     from riak_ensemble_amd import _lib
     L = _lib.load()
@@ -261,9 +478,6 @@ def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
     return {'records': n, 'key_bytes': kb, 'value_bytes': vb,
             'device_encode_ms': round(dt * 1e3, 3),
             'kernel_ms': {k: round(m, 4) for k, m in zip(kn, kms)},
-            # k_snap_entries per entry: koff 8 + key record 9 + voff 8 + value 17
-            # + entry offset 8 read, the entry's ETF bytes written (the values
-            # heap minus list headers/NILs and inner-node records)
             'entries_roofline': _entries_roof(tree, vb, kms[3]),
             'encode_GB_per_s_written': round((kb + vb) / dt / 1e9, 1),
             'snapshot_to_host_ms': round(host_s * 1e3, 1),
@@ -274,9 +488,9 @@ def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
 
 
 def _entries_roof(tree, vb, ms):
+    """k_snap_entries per entry: koff 8 + key record 9 + voff 8 + value 17 +
+    entry offset 8 read, the entry's ETF bytes written."""
     ne = tree.num_entries()
-    # entry bytes = value bytes - {0,0} record - inner-node records - segment
-    # list headers/NILs (7 B per non-empty segment)
     inner = 0
     for L in range(2, tree.height + 2):
         p = tree.level_entries(L)[0]
@@ -290,129 +504,25 @@ def _entries_roof(tree, vb, ms):
             'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': int(algo)}
 
 
-def _segment_histogram(tree, keys_h):
-    """Keys per segment via the device key->segment map (st_segment_of_batch)."""
-    segs = np.zeros(0, np.uint64)
-    step = 1 << 21
-    parts = []
-    for i in range(0, len(keys_h), step):
-        parts.append(np.array(tree.segments_of(keys_h[i:i + step].tolist()), np.int64))
-    segs = np.concatenate(parts)
-    return np.bincount(segs, minlength=1 << 20)
-
-
-def _bench_build(synctree_hip, keys_d, vals_d, n, local, torch, reps=3):
-    """Full build (insert of N keys from HBM into an empty tree)."""
-    times = []
-    for _ in range(reps + 1):
-        t = synctree_hip.DeviceTree(device=local)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        t.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-        t.close()
-    best = min(times[1:])
-    return {'keys_per_s': round(n / best, 1), 'seconds': round(best, 4),
-            'what': 'st_insert_int64: key->segment MD5, radix sort, run sort, merge, gather, dirty rehash (all levels)'}
-
-
-def _bench_compare(synctree_hip, tree_a, keys_h, vals_h, keys_d, vals_d, n, local, torch, reps=10):
-    """Config 3: B = A with the first value of every 1000th non-empty segment
-    bumped (test/synctree_intercepts.erl:96-104) and rehashed."""
-    pres, _ = tree_a.level_entries(6)
-    segs = np.nonzero(pres)[0][::1000].tolist()
-    imgs = tree_a.exchange_get_batch(6, segs)
-    mut = [(img[0][0], bytes([(img[0][1][0] + 1) % 256]) + img[0][1][1:]) for img in imgs]
-    tb = synctree_hip.DeviceTree(device=local)
-    tb.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
-    tb.insert_batch([k for k, _ in mut], [v for _, v in mut])
-    nd = tree_a.compare_device(tb)
-    assert nd == len(segs), (nd, len(segs))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        tree_a.compare_device(tb)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    t0 = time.perf_counter()
-    res = tree_a.compare(tb)
-    dt_host = time.perf_counter() - t0
-    assert res[0] == 'ok' and len(res[1]) == len(segs)
-    # (B's bumped FIRST byte is the ?H_OBJ_NONE prefix: the reference exchange
-    # would crash in valid_obj_hash on these diffs, and so does ours)
-    assert tree_a.exchange_apply(tb)[0] == 'exchange_failed'
-    tb.close()
-    # riak_ensemble_exchange.erl:71-97 as one device batch: B2 = A with the
-    # same keys' Seq advanced (last byte + 1, so B2 > A: valid_obj_hash holds);
-    # compare + apply into a fresh copy of A, which then equals B2
-    mut2 = [(k, v[:-1] + bytes([v[-1] + 1])) for k, v in
-            ((img[0][0], img[0][1]) for img in imgs) if v[-1] < 255]
-    tb2 = synctree_hip.DeviceTree(device=local)
-    tb2.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
-    tb2.insert_batch([k for k, _ in mut2], [v for _, v in mut2])
-    ta = synctree_hip.DeviceTree(device=local)
-    ta.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res_apply = ta.exchange_apply(tb2)
-    torch.cuda.synchronize()
-    dt_apply = time.perf_counter() - t0
-    assert res_apply[0] == 'ok' and res_apply[1]['applied'] == len(mut2), res_apply
-    assert ta.top_hash() == tb2.top_hash(), 'exchange did not converge the trees'
-    ta.close()
-    tb2.close()
-    return {'tree_compares_per_s': round(1.0 / dt, 1), 'ms_per_compare': round(dt * 1e3, 4),
-            'diff_keys': nd, 'diff_keys_per_s': round(nd / dt, 1),
-            'ms_per_compare_incl_d2h_records': round(dt_host * 1e3, 4),
-            'exchange_apply_ms': round(dt_apply * 1e3, 4),
-            'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
-                              'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),
-            'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 with per-node '
-                    'self-verification, diff records materialised on device'}
-
-
-def _bench_ensembles(synctree_hip, workload, E, nk, local, torch, reps=10):
-    """Config 4 shape on one GPU: E independent ensembles x nk keys (keys
-    seeded SEED ^ e), all rehashed as ONE batch (st_rehash_group) vs one
-    st_rehash per tree."""
-    trees = []
-    for e in range(E):
-        k = torch.from_numpy(workload.keys_int63(nk, workload.SEED ^ (e + 1))).to(torch.device('cuda', local))
-        v = torch.from_numpy(workload.obj_hash_values(nk)).to(k.device)
-        t = synctree_hip.DeviceTree(device=local)
-        t.insert_int64_device(k.data_ptr(), v.data_ptr(), nk, 17)
-        trees.append(t)
-    torch.cuda.synchronize()
-    tops = [t.top_hash() for t in trees]
-    synctree_hip.rehash_group(trees)
-    assert [t.top_hash() for t in trees] == tops
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        synctree_hip.rehash_group(trees)
-    torch.cuda.synchronize()
-    dt_g = (time.perf_counter() - t0) / reps
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        for t in trees:
-            t.rehash()
-    for t in trees:
-        t.sync()
-    dt_s = (time.perf_counter() - t0) / reps
-    assert [t.top_hash() for t in trees] == tops
-    for t in trees:
-        t.close()
-    return {'keys_per_s': round(E * nk / dt_g, 1), 'ms_per_batch': round(dt_g * 1e3, 4),
-            'per_tree_rehash_keys_per_s': round(E * nk / dt_s, 1), 'ensembles': E, 'keys_per_ensemble': nk,
-            'what': 'config4 shape per GPU: %d ensembles x %d keys rehashed as one st_rehash_group batch '
-                    '(K1 over all trees\' tiles + one level-dataflow launch), vs st_rehash per tree' % (E, nk)}
-
-
 def _dev_keys(seed, start, n, dev, torch):
     """splitmix64(seed + i), i = start+1 .. start+n, masked to 63 bits, on the
     device (a bijection before the mask: distinct keys with overwhelming
     probability; inserts are last-writer-wins anyway)."""
     return _dev_keys_at(seed, torch.arange(start, start + n, dtype=torch.int64, device=dev), dev, torch)
+
+
+def _dev_keys_at(seed, idx, dev, torch):
+    """Keys at arbitrary generation indices idx (0-based) of _dev_keys."""
+    def c(x):
+        return x - (1 << 64) if x >= 1 << 63 else x
+
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+    z = c(seed) + (idx + 1) * c(0x9E3779B97F4A7C15)
+    z = (z ^ lsr(z, 30)) * c(0xBF58476D1CE4E5B9)
+    z = (z ^ lsr(z, 27)) * c(0x94D049BB133111EB)
+    z = z ^ lsr(z, 31)
+    return z & 0x7FFFFFFFFFFFFFFF
 
 
 def _dev_values(seq, dev, torch, epoch=1):
@@ -424,18 +534,85 @@ def _dev_values(seq, dev, torch, epoch=1):
     return v
 
 
-def _bench_partition(synctree_hip, dist, args, local, torch):
+def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
+    """Config 4 on every rank: E ensembles x nk keys per GPU (ensemble e of rank
+    r seeded SEED ^ (r * E + e + 1)), rehashed as ONE st_rehash_group batch,
+    then every ensemble's top hash all-gathered across the ranks (RCCL
+    all_gather_into_tensor of the 18-B records st_tops_to_device writes).
+    Timed: batch rehash + tops + all-gather, max over ranks."""
+    from riak_ensemble_amd import workload
+    rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    E, nk = args.ensembles, args.ensemble_keys
+    dev = torch.device('cuda', local)
+    trees = []
+    t0 = time.perf_counter()
+    vals = _dev_values(torch.arange(nk, dtype=torch.int64, device=dev), dev, torch)
+    for e in range(E):
+        k = _dev_keys(workload.SEED ^ (rank * E + e + 1), 0, nk, dev, torch)
+        t = synctree_hip.DeviceTree(device=local)
+        t.insert_int64_device(k.data_ptr(), vals.data_ptr(), nk, 17)
+        trees.append(t)
+        del k
+    torch.cuda.synchronize()
+    load_s = time.perf_counter() - t0
+    mine = torch.empty(E * 18, dtype=torch.uint8, device=dev)
+    allt = torch.empty(world * E * 18, dtype=torch.uint8, device=coll_dev)
+
+    def step():
+        synctree_hip.rehash_group(trees)
+        synctree_hip.tops_to_device(trees, mine.data_ptr())
+        if dist:
+            dist.all_gather_into_tensor(allt, mine.to(coll_dev))
+        else:
+            allt.copy_(mine)
+
+    step()
+    before = allt.cpu().numpy().copy()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    stable = bool((allt.cpu().numpy() == before).all()) and int(before.reshape(-1, 18)[:, 0].sum()) == world * E
+    # per-tree rehash for comparison (rank-local, untimed for the headline)
+    t0 = time.perf_counter()
+    for t in trees[:32]:
+        t.rehash()
+    for t in trees[:32]:
+        t.sync()
+    per_tree = (time.perf_counter() - t0) / min(32, E)
+    for t in trees:
+        t.close()
+    return {'keys_per_s': round(world * E * nk * reps / el, 1), 'ms_per_batch': round(el * 1e3 / reps, 3),
+            'ensembles_per_gpu': E, 'ensembles_total': world * E, 'keys_per_ensemble': nk, 'ranks': world,
+            'tops_allgather_stable': stable, 'load_s': round(load_s, 2),
+            'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
+            'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '
+                    'the rank\'s trees + st_tops_to_device + all_gather_into_tensor of every ensemble\'s top hash '
+                    '(keys generated on device: splitmix64 masked to 63 bits)' % (E, nk, world, world * E)}
+
+
+def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     """Config 5: one tree of part_keys keys partitioned by segment range over
     the ranks (st_set_partition); timed: part_batches write batches of
     part_batch_keys keys (50 % overwrites with Seq + 1, 50 % new keys), each an
     insert/3 batch with dirty-path rehash on every rank + the all-gather of the
     level-2 entries and level 1 + top (parallel.PartitionedTree.combine)."""
     from riak_ensemble_amd import parallel
-    import numpy as np
     dev = torch.device('cuda', local)
     world = dist.get_world_size() if dist else 1
     grp = dist if dist else _SoloGroup()
-    pt = parallel.PartitionedTree(synctree_hip.DeviceTree(device=local), grp, device=dev)
+    pt = parallel.PartitionedTree(synctree_hip.DeviceTree(device=local), grp, device=coll_dev)
     N, B, K = args.part_keys, args.part_batch_keys, args.part_batches
     seed = 0x5EED0005
     chunk = 10_000_000
@@ -476,10 +653,10 @@ def _bench_partition(synctree_hip, dist, args, local, torch):
     top = pt.top_hash()
     same = True
     if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tops = parallel.gather_tops(dist, [top], device=dev)
+        tops = parallel.gather_tops(dist, [top], device=coll_dev)
         same = all(x == top for x in tops)
     entries = pt.tree.num_entries()
     pt.tree.close()
@@ -490,20 +667,6 @@ def _bench_partition(synctree_hip, dist, args, local, torch):
                     '(50%% overwrites Seq+1, 50%% new; verify + dirty-path rehash) on every rank, all-gather of the '
                     'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits)'
                     % (N, world, B)}
-
-
-def _dev_keys_at(seed, idx, dev, torch):
-    """Keys at arbitrary generation indices idx (0-based) of _dev_keys."""
-    def c(x):
-        return x - (1 << 64) if x >= 1 << 63 else x
-
-    def lsr(z, k):
-        return (z >> k) & ((1 << (64 - k)) - 1)
-    z = c(seed) + (idx + 1) * c(0x9E3779B97F4A7C15)
-    z = (z ^ lsr(z, 30)) * c(0xBF58476D1CE4E5B9)
-    z = (z ^ lsr(z, 27)) * c(0x94D049BB133111EB)
-    z = z ^ lsr(z, 31)
-    return z & 0x7FFFFFFFFFFFFFFF
 
 
 class _SoloGroup:
@@ -519,8 +682,9 @@ class _SoloGroup:
 def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
     """Config 1: a 100k-key tree, full build (n inserts) + rehash + top hash.
     GPU: one st_insert_int64 batch + st_rehash.  CPU: the C restatement in
-    reference-faithful mode (one verified insert per key, DFS rehash over all
-    2^20 slots), one thread -- the reference Erlang cannot run here."""
+    reference-faithful mode (n verified inserts in one C loop, then the DFS
+    rehash over all 2^20 slots), one thread -- the reference Erlang cannot run
+    here.  Plus the per-key get/insert latency."""
     keys = workload.keys_int63(n, workload.SEED ^ 0x100)
     vals = workload.obj_hash_values(n)
     best = 1e9
@@ -532,51 +696,62 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
         t.rehash()
         top = t.top_hash()
         best = min(best, time.perf_counter() - t0)
-    # the per-key verified-path calls (get/2, insert/3,
-    # synctree.erl:189-227) one at a time through the C-ABI (ctypes), i.e. the
-    # low-batch latency path; the tree is the 100k-key one just built
+    # per-key verified-path calls (get/2, insert/3, synctree.erl:189-227) one at
+    # a time through the C-ABI (ctypes), i.e. the low-batch latency path
     kl = [int(k) for k in keys[:200]]
+    t.get_batch([kl[0]])                                # untimed warm-up
+    t.insert_batch([kl[0]], [bytes(vals[0])])
     t0 = time.perf_counter()
-    for k in kl:
-        t.get_batch([k])
+    got = [t.get_batch([k])[0] for k in kl]
     gpu_get_us = (time.perf_counter() - t0) / len(kl) * 1e6
+    assert got == [bytes(vals[i]) for i in range(len(kl))], 'per-key get returned wrong values'
+    newv = bytes(17)
     t0 = time.perf_counter()
-    for k in kl:
-        t.insert_batch([k], [b'\x00' * 17])
+    st = [t.insert_batch([k], [newv])[0] for k in kl]
     gpu_ins_us = (time.perf_counter() - t0) / len(kl) * 1e6
+    assert all(s is None for s in st), 'per-key insert rejected'
     t.close()
     out = {'gpu_keys_per_s': round(n / best, 1), 'gpu_ms': round(best * 1e3, 3),
            'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)',
            'per_key_latency_us': {'gpu_get': round(gpu_get_us, 1), 'gpu_insert': round(gpu_ins_us, 1),
                                   'what': 'one get/2 or insert/3 per C-ABI call (verified path + dirty-path '
-                                          'rehash on the device), 200 calls, ctypes overhead included'}}
+                                          'rehash on the device), 200 calls after a warm-up, ctypes overhead '
+                                          'included; results checked'}}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle_c
         ot = oracle_c.OTree()
         t0 = time.perf_counter()
-        for k, v in zip(keys.tolist(), vals):
-            ot.insert(int(k), bytes(v))
+        assert ot.insert_int64_seq(keys, vals) == 0
         ot.rehash()
         ctop = ot.top_hash()
         dt = time.perf_counter() - t0
+        assert ctop == top, 'config1: CPU restatement and GPU disagree'
+        ka = np.array(kl, np.int64)
+        t0 = time.perf_counter()
+        ot.insert_int64_seq(ka, np.zeros((len(kl), 17), np.uint8))
+        cpu_ins = (time.perf_counter() - t0) / len(kl) * 1e6
         t0 = time.perf_counter()
         for k in kl:
             ot.get(k)
-        out['per_key_latency_us']['cpu_get'] = round((time.perf_counter() - t0) / len(kl) * 1e6, 1)
-        t0 = time.perf_counter()
-        for k in kl:
-            ot.insert(k, b'\x00' * 17)
-        out['per_key_latency_us']['cpu_insert'] = round((time.perf_counter() - t0) / len(kl) * 1e6, 1)
-        assert ctop == top, 'config1: CPU restatement and GPU disagree'
+        cpu_get = (time.perf_counter() - t0) / len(kl) * 1e6
+        out['per_key_latency_us']['cpu_insert_in_c'] = round(cpu_ins, 2)
+        out['per_key_latency_us']['cpu_get_via_ctypes'] = round(cpu_get, 2)
         out['cpu'] = {'keys_per_s': round(n / dt, 1), 'seconds': round(dt, 3), 'cores': 1, 'kind': 'port',
-                      'sample': 'oracle/synctree_oracle.c: 100k verified inserts (ctypes per key) + rehash + top_hash'}
+                      'sample': 'oracle/synctree_oracle.c: 100k verified insert/3 calls in one C loop + rehash + '
+                                'top_hash'}
     return out
 
 
-def _cpu_baseline(keys_h, vals_h, top0, reps=2):
+def _cpu_baseline(keys_h, vals_h, top0, reps=3):
+    """The C port (oracle/synctree_oracle.c) rehashing the same 10M-key tree:
+    (a) the reference-faithful DFS rehash (synctree.erl:497-543) on one host
+    thread, and (b) the throughput-mode rehash (ot_rehash_par: level by level,
+    every node of a level spread over OpenMP threads) on every host core.
+    About 10-20 s of CPU work in total."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle_c
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
     t0 = time.perf_counter()
     ot = oracle_c.OTree().bulk_load_int64(keys_h, vals_h)
     load_s = time.perf_counter() - t0
@@ -586,11 +761,25 @@ def _cpu_baseline(keys_h, vals_h, top0, reps=2):
         t0 = time.perf_counter()
         ot.rehash()
         ts.append(time.perf_counter() - t0)
-    best = min(ts)
-    return {'value': round(len(keys_h) / best, 1), 'unit': 'keys/s', 'cores': 1, 'kind': 'port',
+    best1 = min(ts)
+    ot.rehash_par(ncpu)   # warm-up (first-touch of the per-level arrays)
+    tp = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ot.rehash_par(ncpu)
+        tp.append(time.perf_counter() - t0)
+    bestp = min(tp)
+    assert ot.top_hash() == top0
+    n = len(keys_h)
+    return {'value': round(n / best1, 1), 'unit': 'keys/s', 'cores': 1, 'kind': 'port',
             'sample': 'full synctree:rehash/1 restatement (oracle/synctree_oracle.c, DFS over all 2^20 segment '
                       'slots) of the same 10M-key tree, best of %d; tree load %.1f s untimed' % (reps, load_s),
-            'seconds_per_rehash': round(best, 3)}
+            'seconds_per_rehash': round(best1, 3),
+            'all_cores': {'value': round(n / bestp, 1), 'unit': 'keys/s', 'cores': ncpu, 'kind': 'port',
+                          'seconds_per_rehash': round(bestp, 3),
+                          'sample': 'ot_rehash_par: the same rehash level by level over flat entry arrays, every '
+                                    'level\'s nodes spread over %d OpenMP threads (host cores available to this '
+                                    'process), best of %d' % (ncpu, reps)}}
 
 
 if __name__ == '__main__':

@@ -176,6 +176,12 @@ int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64
 int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi);
 int st_combine_upper(st_tree *t, const uint8_t *present16, const uint8_t *hashes17);
 
+/* Ensemble sharding (riak_ensemble_peer.erl:1845-1846: one tree per peer):
+ * the top-hash records of n trees on one device written to DEVICE memory
+ * `out` (18 bytes per tree: present byte, then the 17-byte hash), the payload
+ * of the cross-GPU all-gather of top hashes. */
+int st_tops_to_device(st_tree **trees, uint32_t n, void *out);
+
 /* ---- reads ---------------------------------------------------------- */
 
 /* Library-allocated result blocks; free with st_free_result(). */
@@ -233,11 +239,18 @@ int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *bucke
 int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
                uint64_t *cbucket, int *cside);
 
-/* The same compare with every result kept in device memory (bench path):
- * *n_diffs receives the number of diff records.  Records are built on the
- * device exactly as st_compare's; st_compare = this + the D2H copy. */
+/* The same compare with the ordered diff records kept in device memory (the
+ * local tree's compare workspace, valid until its next compare): each record
+ * names the key's entry in the local and/or remote tree, in reference order.
+ * *n_diffs receives the number of records.  st_compare = this + the record
+ * bytes gathered and copied to the host.  One host round trip per call. */
 int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
                       uint64_t *cbucket, int *cside);
+
+/* Diagnostics of the last compare on `local`: visited[l] = nodes visited at
+ * level l (l = 1..Height+1; visited[0] unused), and the algorithmic bytes of
+ * the final-level segment pairs (offsets, key records, values, entries). */
+int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_levels, uint64_t *seg_bytes);
 
 /* ---- synctree_leveldb on-disk format ---------------
  * The records src/synctree_leveldb.erl writes for this tree: one per stored

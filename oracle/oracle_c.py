@@ -75,6 +75,8 @@ def lib():
         L.ot_bulk_load_int64.restype = ctypes.c_int
         L.ot_bulk_load_int64.argtypes = [vp, u64, vp, vp, u32]
         L.ot_md5.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p]
+        L.ot_num_entries.restype = u64
+        L.ot_num_entries.argtypes = [vp]
         L.ot_insert_int64_seq.restype = u64
         L.ot_insert_int64_seq.argtypes = [vp, u64, vp, vp, u32]
         _lib = L
@@ -247,6 +249,9 @@ class OTree:
         if r != 0:
             raise ValueError('bulk_load needs a fresh tree')
         return self
+
+    def num_entries(self):
+        return int(lib().ot_num_entries(self.h))
 
     def insert_int64_seq(self, keys, values):
         """len(keys) sequential insert/3 calls in C; returns #rejected."""

@@ -749,5 +749,12 @@ uint64_t ot_insert_int64_seq(ot_tree *t, uint64_t n, const int64_t *keys, const 
     return bad;
 }
 
+/* number of {Key,Value} entries over all segments */
+uint64_t ot_num_entries(ot_tree *t) {
+    uint64_t H1 = t->height + 1, c = 0;
+    for (uint64_t s = 0; s < t->lvsize[H1]; s++) c += node_at(t, H1, s)->n;
+    return c;
+}
+
 /* exported for the RFC 1321 known-answer tests */
 void ot_md5(const uint8_t *p, uint64_t n, uint8_t out[16]) { md5r(p, (size_t)n, out); }

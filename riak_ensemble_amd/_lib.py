@@ -92,6 +92,8 @@ _SIGS = {
     'st_restore_leveldb': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64p,
                                           u64p]),
+    'st_compare_stats': (ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32, u64p]),
+    'st_tops_to_device': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
 }

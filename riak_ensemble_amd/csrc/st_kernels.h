@@ -648,15 +648,16 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 //     the filter (orddict_delta, riak_ensemble_util.erl:115-141, plus
 //     filter/2, synctree.erl:434-449) form the next frontier, in ascending
 //     bucket order.  Only stored child entries are compared: no hashing.
-//  2. k_cmp_visit<false> (whole grid): every visited node is verified on both
-//     sides against its parent's entry (exchange_get's verified_hashes,
+//  2. k_cmp_visit (whole grid): every visited node is verified on both sides
+//     against its parent's entry (exchange_get's verified_hashes,
 //     synctree.erl:288-298: the ancestors are visited nodes too), and every
 //     final-level segment pair is merge-joined (exchange_final) by one wave,
-//     counting its diff records.
-//  3. device-side scan of the counts, then k_cmp_visit<true> writes the
-//     records in reference order: AccFun = Keys ++ Acc over ascending
-//     segments (synctree.erl:373-375) => the LAST frontier segment first,
-//     ascending keys within a segment.
+//     which writes its records, ascending by key, to a scratch area it
+//     reserves with one atomic.
+//  3. k_dscan1 scans the per-segment counts on the device; k_cmp_reorder
+//     copies each segment's records to its reference position: AccFun =
+//     Keys ++ Acc over ascending segments (synctree.erl:373-375) => the LAST
+//     frontier segment first, ascending keys within a segment.
 // err: min over (level, bucket, side) of a failed verification — the
 // reference's first crash in visiting order (local before remote).
 
@@ -732,15 +733,40 @@ __device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t *wsum, u
 // Pass 1.  flist: level L's frontier at flist[base[L] - 1 ..], fcnt[L] its
 // length (levels 1..H+1).  [lo2, hi2): level-2 buckets a segment-range
 // partition owns (its level-1 frontier is cut to them); err is reset here.
+// W == 16: two threads per frontier node, 8 children each, every child entry
+// of both trees loaded before any is compared (one memory round trip per
+// level chunk); other widths loop over the children.
+__device__ __forceinline__ uint64_t child_mask8(const DevTree &A, const DevTree &B, uint64_t s0, uint64_t c0, int filter,
+                                                bool cut, uint64_t lo2, uint64_t hi2) {
+    uint16_t ta[8], tb[8];
+    uint4 x[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        ta[j] = A.tag[s0 + j];
+        tb[j] = B.tag[s0 + j];
+        x[j] = A.md5[s0 + j];
+        y[j] = B.md5[s0 + j];
+    }
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint64_t c = c0 + j;
+        const bool keep = !cut || (c >= lo2 && c < hi2);
+        if (keep && entry_differs(ta[j], tb[j], x[j], y[j], filter)) m |= 1ull << j;
+    }
+    return m;
+}
+
 __global__ void __launch_bounds__(1024) k_cmp_frontier(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2,
                                                        uint32_t *flist, uint32_t *fcnt, unsigned long long *err,
-                                                       uint64_t *nfinal) {
+                                                       uint64_t *nfinal, unsigned long long *seg_bytes) {
     __shared__ uint32_t wsum[17];
     __shared__ uint32_t n0;
     const uint32_t tid = threadIdx.x;
     if (tid < ST_MAXLEV + 2) fcnt[tid] = 0;
     if (tid == 0) {
         *err = ~0ull;
+        *seg_bytes = 0;
         const uint16_t ta = A.tag[0], tb = B.tag[0];
         bool same = (ta == tb);
         if (same && (ta & TAG_PRESENT)) {
@@ -754,25 +780,35 @@ __global__ void __launch_bounds__(1024) k_cmp_frontier(DevTree A, DevTree B, int
     if (tid == 0) fcnt[1] = n0;
     uint32_t n = n0;
     const uint32_t W = A.W;
+    const bool w16 = W == 16;
+    const uint32_t per_chunk = w16 ? blockDim.x / 2 : blockDim.x;   // frontier nodes per chunk
     for (uint32_t L = 1; L <= A.H && n; L++) {
         const uint32_t *cur = flist + (A.base[L] - 1);
         uint32_t *nxt = flist + (A.base[L + 1] - 1);
         const uint64_t cb = A.base[L + 1];
         uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
-            const uint32_t f = c0 + tid;
-            uint64_t mask = 0, b = 0;
-            if (f < n) {
-                b = cur[f];
-                const uint64_t s0 = cb + b * W;
-#pragma unroll 16
-                for (uint32_t j = 0; j < W; j++) {
-                    const uint16_t ta = A.tag[s0 + j], tb = B.tag[s0 + j];
-                    uint4 x = make_uint4(0, 0, 0, 0), y = x;
-                    if ((ta & tb & TAG_PRESENT) && ta == tb) { x = A.md5[s0 + j]; y = B.md5[s0 + j]; }
-                    const uint64_t c = b * W + j;
-                    const bool keep = L != 1 || (c >= lo2 && c < hi2);
-                    if (keep && entry_differs(ta, tb, x, y, filter)) mask |= 1ull << j;
+        for (uint32_t c0 = 0; c0 < n; c0 += per_chunk) {
+            uint64_t mask = 0, cbase = 0;
+            if (w16) {
+                const uint32_t f = c0 + (tid >> 1), h = tid & 1;
+                if (f < n) {
+                    const uint64_t b = cur[f];
+                    cbase = b * 16 + 8 * h;
+                    mask = child_mask8(A, B, cb + cbase, cbase, filter, L == 1, lo2, hi2);
+                }
+            } else {
+                const uint32_t f = c0 + tid;
+                if (f < n) {
+                    const uint64_t b = cur[f];
+                    cbase = b * W;
+                    for (uint32_t j = 0; j < W; j++) {
+                        const uint64_t sl = cb + cbase + j;
+                        const uint16_t ta = A.tag[sl], tb = B.tag[sl];
+                        const uint4 x = A.md5[sl], y = B.md5[sl];
+                        const uint64_t c = cbase + j;
+                        const bool keep = L != 1 || (c >= lo2 && c < hi2);
+                        if (keep && entry_differs(ta, tb, x, y, filter)) mask |= 1ull << j;
+                    }
                 }
             }
             uint32_t tot;
@@ -780,7 +816,7 @@ __global__ void __launch_bounds__(1024) k_cmp_frontier(DevTree A, DevTree B, int
             uint32_t q = 0;
             while (mask) {
                 const uint32_t j = (uint32_t)(__ffsll((long long)mask) - 1);
-                nxt[pos + q++] = (uint32_t)(b * W + j);
+                nxt[pos + q++] = (uint32_t)(cbase + j);
                 mask &= mask - 1;
             }
             carry += tot;
@@ -832,13 +868,14 @@ __device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
     return (uint32_t)__popcll(bal & ((1ull << lane) - 1));
 }
 
-// exchange_final for one segment pair (orddict_delta + filter), one wave.
-// WRITE=false: returns the record count; WRITE=true: writes the records in
-// ascending key order at out[pos0 ..].  Record kinds: 0 = {K,{A,B}},
-// 1 = {K,{A,'$none'}}, 2 = {K,{'$none',B}}.
-template <bool WRITE>
+// exchange_final for one segment pair (orddict_delta + filter), one wave:
+// writes the pair's records in ascending key order to scratch space it
+// reserves with one atomicAdd on *ctr (records past cap are counted, not
+// written: the host grows the buffer and runs the compare again) and returns
+// (count, scratch offset).  Record kinds: 0 = {K,{A,B}}, 1 = {K,{A,'$none'}},
+// 2 = {K,{'$none',B}}.
 __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint8_t *lds,
-                                   DiffRec *out, uint64_t pos0, uint64_t cap) {
+                                   DiffRec *out, uint64_t cap, unsigned long long *ctr, uint64_t *base_out) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t a0 = A.seg_off[s], a1 = A.seg_off[s + 1], b0 = B.seg_off[s], b1 = B.seg_off[s + 1];
     const uint64_t nA = a1 - a0, nB = b1 - b0;
@@ -855,8 +892,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
         for (uint64_t q = lane; q < bytesA; q += 64) ak[q] = A.kheap[ka0 + q];
         for (uint64_t q = lane; q < bytesB; q += 64) bk[q] = B.kheap[kb0 + q];
         const uint32_t nu_max = (uint32_t)(nA + nB);
-        if (WRITE)
-            for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+        for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
         wave_sync_lds();
         uint64_t cnt = 0;
         uint32_t mcarry = 0;
@@ -877,7 +913,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             const uint32_t m = mcarry + wave_prefix_count(eq, lane);
             mcarry += (uint32_t)__popcll(__ballot(eq));
             cnt += (uint32_t)__popcll(__ballot(emit));
-            if (WRITE && emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
+            if (emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
         }
         mcarry = 0;
         for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
@@ -891,12 +927,15 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             const uint32_t m = mcarry + wave_prefix_count(eq, lane);
             mcarry += (uint32_t)__popcll(__ballot(eq));
             cnt += (uint32_t)__popcll(__ballot(emit));
-            if (WRITE && emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
+            if (emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
         }
-        if (!WRITE) return cnt;
+        uint64_t base = 0;
+        if (lane == 0 && cnt) base = atomicAdd(ctr, (unsigned long long)cnt);
+        base = __shfl(base, 0, 64);
+        *base_out = base;
         wave_sync_lds();
-        uint64_t pos = pos0;
-        for (uint32_t c = 0; c < nu_max; c += 64) {   // union slots in key order -> records
+        uint64_t pos = base;
+        for (uint32_t c = 0; c < nu_max && cnt; c += 64) {   // union slots in key order -> records
             const uint32_t u = c + lane;
             const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
             const bool e = r != 0xffffffffu;
@@ -913,163 +952,152 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             }
             pos += (uint32_t)__popcll(__ballot(e));
         }
-        return pos - pos0;
+        return cnt;
     }
-    // oversized segments: lane 0 walks the two key lists
-    uint64_t c = 0;
+    // oversized segments: lane 0 walks the two key lists (count, reserve, write)
+    uint64_t c = 0, base = 0;
     if (lane == 0) {
-        uint64_t x = a0, y = b0, pos = pos0;
-        while (x < a1 || y < b1) {
-            int cmp;
-            if (x < a1 && y < b1)
-                cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y], B.koff[y + 1] - B.koff[y]);
-            else
-                cmp = x < a1 ? -1 : 1;
-            DiffRec r;
-            r.seg = s;
-            r.pad = 0;
-            bool emit;
-            if (cmp < 0) {
-                r.a = x; r.b = ~0ull; r.kind = 1;
-                emit = filter != 1;
-                x++;
-            } else if (cmp > 0) {
-                r.a = ~0ull; r.b = y; r.kind = 2;
-                emit = filter != 2;
-                y++;
-            } else {
-                emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y], B.voff[y + 1] - B.voff[y]);
-                r.a = x; r.b = y; r.kind = 0;
-                x++; y++;
+        for (int pass = 0; pass < 2; pass++) {
+            uint64_t x = a0, y = b0, pos = base;
+            while (x < a1 || y < b1) {
+                int cmp;
+                if (x < a1 && y < b1)
+                    cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y],
+                                  B.koff[y + 1] - B.koff[y]);
+                else
+                    cmp = x < a1 ? -1 : 1;
+                DiffRec r;
+                r.seg = s;
+                r.pad = 0;
+                bool emit;
+                if (cmp < 0) {
+                    r.a = x; r.b = ~0ull; r.kind = 1;
+                    emit = filter != 1;
+                    x++;
+                } else if (cmp > 0) {
+                    r.a = ~0ull; r.b = y; r.kind = 2;
+                    emit = filter != 2;
+                    y++;
+                } else {
+                    emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
+                                     B.voff[y + 1] - B.voff[y]);
+                    r.a = x; r.b = y; r.kind = 0;
+                    x++; y++;
+                }
+                if (emit) {
+                    if (pass == 1 && pos < cap) out[pos] = r;
+                    pos++;
+                    if (pass == 0) c++;
+                }
             }
-            if (emit) {
-                if (WRITE && pos < cap) out[pos] = r;
-                pos++;
-                c++;
-            }
+            if (pass == 0 && c) base = atomicAdd(ctr, (unsigned long long)c);
+            if (!c) break;
         }
     }
+    *base_out = __shfl(base, 0, 64);
     return __shfl(c, 0, 64);
 }
 
-// Passes 2 and 3.  WRITE=false: verify every visited node (lane per node and
-// side, all levels), then count each final segment's records (wave per
-// segment) into dcnt.  WRITE=true: write the records at their reference
-// positions (doff: exclusive scan of dcnt, *total its sum).
-template <bool WRITE>
+// Pass 2: verify every visited node (lane per node and side, all levels; the
+// first waves), then merge-join each final segment pair (wave per segment,
+// assigned from the last wave down so the verifying waves get none when
+// there are fewer segments than waves) into scratch + dcnt/soff.
 __global__ void __launch_bounds__(256) k_cmp_visit(DevTree A, DevTree B, int filter, const uint32_t *flist,
-                                                  const uint32_t *fcnt, uint64_t *dcnt, const uint64_t *doff,
-                                                  const uint64_t *total, DiffRec *out, uint64_t cap,
-                                                  unsigned long long *err, uint32_t slice) {
+                                                  const uint32_t *fcnt, uint64_t *dcnt, uint64_t *soff, DiffRec *scratch,
+                                                  uint64_t cap, unsigned long long *ctr, unsigned long long *err,
+                                                  uint32_t slice, unsigned long long *seg_bytes) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint8_t *wl = lds + (uint64_t)wave * slice;
     const uint32_t L1 = A.H + 1;
     const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave, nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    if (!WRITE) {
-        uint64_t nv = 0;
-        for (uint32_t L = 1; L <= L1; L++) nv += fcnt[L];
-        uint8_t *reg = wl + lane * lane_region_bytes(A.W);
-        for (uint64_t g = gwave * 64 + lane; g < 2 * nv; g += nwaves * 64) {
-            uint64_t k = g >> 1;
-            const uint32_t side = (uint32_t)(g & 1);
-            uint32_t L = 1;
-            while (k >= fcnt[L]) { k -= fcnt[L]; L++; }
-            const uint64_t b = flist[A.base[L] - 1 + k];
-            const DevTree &T = side ? B : A;
-            const bool good = L == L1 ? verify_segment(T, b) : verify_inner_node(T, L, b, reg);
-            if (!good) atomicMin(err, err_code(L, b, side));
-        }
-        wave_sync_lds();
+    uint64_t nv = 0;
+    for (uint32_t L = 1; L <= L1; L++) nv += fcnt[L];
+    uint8_t *reg = wl + lane * lane_region_bytes(A.W);
+    for (uint64_t g = gwave * 64 + lane; g < 2 * nv; g += nwaves * 64) {
+        uint64_t k = g >> 1;
+        const uint32_t side = (uint32_t)(g & 1);
+        uint32_t L = 1;
+        while (k >= fcnt[L]) { k -= fcnt[L]; L++; }
+        const uint64_t b = flist[A.base[L] - 1 + k];
+        bool good;
+        if (side) good = L == L1 ? verify_segment(B, b) : verify_inner_node(B, L, b, reg);
+        else good = L == L1 ? verify_segment(A, b) : verify_inner_node(A, L, b, reg);
+        if (!good) atomicMin(err, err_code(L, b, side));
     }
+    wave_sync_lds();
     const uint64_t nf = fcnt[L1];
     const uint32_t *seg = flist + (A.base[L1] - 1);
-    const uint64_t tot = WRITE ? *total : 0;
-    for (uint64_t i = gwave; i < nf; i += nwaves) {
+    for (uint64_t i = nwaves - 1 - gwave; i < nf; i += nwaves) {
         const uint64_t s = seg[i];
-        if (!WRITE) {
-            const uint64_t c = seg_merge_wave<false>(A, B, s, filter, wl, nullptr, 0, 0);
-            if (lane == 0) dcnt[i] = c;
-        } else {
-            (void)seg_merge_wave<true>(A, B, s, filter, wl, out, tot - doff[i] - dcnt[i], cap);
+        uint64_t base;
+        const uint64_t c = seg_merge_wave(A, B, s, filter, wl, scratch, cap, ctr, &base);
+        if (lane == 0) {
+            dcnt[i] = c;
+            soff[i] = base;
+            // algorithmic bytes of this segment pair (bench roofline): per side the
+            // offsets, key records, values and the parent's entry
+            const uint64_t na = A.seg_off[s + 1] - A.seg_off[s], nb = B.seg_off[s + 1] - B.seg_off[s];
+            const uint64_t by = 2 * (16 + 16 + 18) + 16 * (na + nb + 2) +
+                                (A.koff[A.seg_off[s + 1]] - A.koff[A.seg_off[s]]) +
+                                (B.koff[B.seg_off[s + 1]] - B.koff[B.seg_off[s]]) + (A.seg_voff[s + 1] - A.seg_voff[s]) +
+                                (B.seg_voff[s + 1] - B.seg_voff[s]);
+            atomicAdd(seg_bytes, (unsigned long long)by);
         }
         wave_sync_lds();
     }
 }
 
-// Exclusive scan of n (read on the device) uint64 values, NA arrays at once,
-// in three launches that need no host round trip: per-workgroup range sums,
-// a one-workgroup scan of those, then each workgroup rescans its range.
-#define DSCAN_WGS 256
-template <int NA>
-struct DScanArgs {
-    const uint64_t *in[NA];
-    uint64_t *out[NA];
-};
-
-template <int NA>
-__global__ void __launch_bounds__(256) k_dscan_sums(DScanArgs<NA> a, const uint64_t *n_ptr, uint64_t *part) {
-    __shared__ uint64_t red[NA][4];
-    const uint64_t n = *n_ptr;
-    const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x;
-    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    uint64_t s[NA];
+// Exclusive scan of n = *n_ptr (read on the device) uint64 values in ONE
+// workgroup: thread t scans its contiguous range; *total receives the sum.
+__device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t *wsum, uint64_t *total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint64_t x = v;
 #pragma unroll
-    for (int k = 0; k < NA; k++) s[k] = 0;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-#pragma unroll
-        for (int k = 0; k < NA; k++) s[k] += a.in[k][i];
-#pragma unroll
-    for (int k = 0; k < NA; k++) {
-        uint64_t v = s[k];
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < nw; w++) { const uint64_t c = wsum[w]; wsum[w] = acc; acc += c; }
+        wsum[16] = acc;
     }
     __syncthreads();
-    if (threadIdx.x < NA) {
-        const int k = threadIdx.x;
-        part[(uint64_t)k * (gridDim.x + 1) + blockIdx.x] = red[k][0] + red[k][1] + red[k][2] + red[k][3];
-    }
+    const uint64_t r = wsum[wave] + x - v;
+    *total = wsum[16];
+    __syncthreads();
+    return r;
 }
 
-template <int NA>
-__global__ void __launch_bounds__(256) k_dscan_top(uint64_t *part, uint32_t nparts, uint64_t *totals) {
-    if (threadIdx.x >= NA) return;
-    uint64_t *p = part + (uint64_t)threadIdx.x * (nparts + 1);
-    uint64_t acc = 0;
-    for (uint32_t i = 0; i < nparts; i++) { const uint64_t c = p[i]; p[i] = acc; acc += c; }
-    p[nparts] = acc;
-    totals[threadIdx.x] = acc;
-}
-
-template <int NA>
-__global__ void __launch_bounds__(256) k_dscan_apply(DScanArgs<NA> a, const uint64_t *n_ptr, const uint64_t *part) {
-    __shared__ uint64_t ws[NA][4];
+__global__ void __launch_bounds__(1024) k_dscan1(const uint64_t *in, uint64_t *out, const uint64_t *n_ptr, uint64_t *total) {
+    __shared__ uint64_t wsum[17];
     const uint64_t n = *n_ptr;
-    const uint64_t chunk = (n + gridDim.x - 1) / gridDim.x;
-    const uint64_t lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t carry[NA];
-#pragma unroll
-    for (int k = 0; k < NA; k++) carry[k] = part[(uint64_t)k * (gridDim.x + 1) + blockIdx.x];
-    for (uint64_t c0 = lo; c0 < hi; c0 += blockDim.x) {
-        const uint64_t i = c0 + threadIdx.x;
-#pragma unroll
-        for (int k = 0; k < NA; k++) {
-            const uint64_t v = i < hi ? a.in[k][i] : 0;
-            uint64_t x = v;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint64_t y = __shfl_up(x, o, 64);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            if (lane == 63) ws[k][wave] = x;
-            __syncthreads();
-            uint64_t before = 0;
-            for (uint32_t w = 0; w < wave; w++) before += ws[k][w];
-            if (i < hi) a.out[k][i] = carry[k] + before + x - v;
-            carry[k] += ws[k][0] + ws[k][1] + ws[k][2] + ws[k][3];
-            __syncthreads();
-        }
+    const uint64_t per = (n + blockDim.x - 1) / blockDim.x;
+    const uint64_t lo = (uint64_t)threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; i++) s += in[i];
+    uint64_t tot;
+    uint64_t acc = block_scan_u64(s, wsum, &tot);
+    for (uint64_t i = lo; i < hi; i++) { const uint64_t v = in[i]; out[i] = acc; acc += v; }
+    if (threadIdx.x == 0) *total = tot;
+}
+
+// Pass 3b: each final segment's records from scratch to their reference
+// position total - doff[i] - dcnt[i] (wave per segment, lane per record).
+__global__ void __launch_bounds__(256) k_cmp_reorder(const uint32_t *fcnt, uint32_t L1, const uint64_t *dcnt,
+                                                    const uint64_t *doff, const uint64_t *soff, const uint64_t *total,
+                                                    const DiffRec *scratch, DiffRec *out, uint64_t cap) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t nf = fcnt[L1], tot = *total;
+    if (tot > cap) return;
+    for (uint64_t i = gwave; i < nf; i += nwaves) {
+        const uint64_t c = dcnt[i], src = soff[i], dst = tot - doff[i] - c;
+        for (uint64_t k = lane; k < c; k += 64) out[dst + k] = scratch[src + k];
     }
 }
 
@@ -1580,25 +1608,33 @@ __global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint
 }
 
 // ---------------------------------------------------------------------------
-// K2 full level rehash (W == 16, H >= 3) in ONE launch with ONE inlined copy
-// of the node-hash code.  A workgroup per level-(H-2) subtree stages its 4096
-// segment entries in LDS (as k_levels3_16), then loops: phase 0 = 256 level-H
-// nodes (one per lane), phase 1 = 16 level-(H-1) nodes, phase 2 = the
-// level-(H-2) node; after that lane 0 climbs while it is the last of 16
-// siblings to finish (cnt[slot] counts the finished children of inner node
-// `slot`, levels 1..H-3; the last arriver resets it to 0), hashing the parent from
-// global memory, up to level 1 and the top hash.  Children come through
-// generic pointers (LDS for phases 0-2, global for the climb), so every level
-// runs the same instructions: the code a CU warms at level H stays in its
-// instruction cache for the latency-bound single-lane levels above it.
-// Release/acquire fences at agent scope around the counter make the
-// children's entries, written by workgroups on other XCDs (other L2s),
-// visible to the climbing lane.
+// Fused full rehash (W == 16, H >= 3): K1 and the inner levels in ONE launch.
+//
+// One workgroup of 1024 threads per WINDOW = level-(H-2) subtree (4096
+// segments, 64 tiles built in window-local block-count order by
+// k_tile_order_window).  Phase 1 (K1): wave w hashes tiles w, w+16, w+32 and
+// w+48 of its window as one flat stream of MD5 blocks with two blocks in
+// flight (the loads of block f+2 are issued before block f is compressed),
+// and leaves each segment's entry in LDS in the node-block layout of
+// k_levels3_16.  Phase 2: the 4096 entries are copied to the slot arrays with
+// coalesced 16-B stores (one line-sized write per 8 entries instead of a
+// scattered 16-B + 2-B pair per segment).  Phase 3: levels H, H-1, H-2 of the
+// window from LDS (rehash/4, synctree.erl:515-535), then lane 0 climbs while
+// it is the last of 16 siblings to finish (cnt[slot] counts finished children
+// of inner node `slot`, levels 1..H-3; the last arriver resets it), hashing
+// the parent from global memory up to level lmin (1: the top hash; 2: a
+// segment-range partition stops at its level-2 entries).
+// Children come through generic pointers (LDS for phases 0-2, global for the
+// climb), so every level runs the same instructions.  Release/acquire fences
+// at agent scope around the counter make entries written by workgroups on
+// other XCDs (other L2s) visible to the climbing lane.
+// ent / tags point at LDS: the entries are read where the message needs them
+// (no 64-VGPR register copy of the node); reg must not overlap ent.
 __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tags, uint8_t *reg, uint4 &e, uint32_t &tg) {
-    uint4 h[16];
+    const uint4 *h = ent;
     uint32_t t16[16];
 #pragma unroll
-    for (int j = 0; j < 16; j++) { h[j] = ent[j]; t16[j] = tags[j]; }
+    for (int j = 0; j < 16; j++) t16[j] = tags[j];
     uint32_t full = 1;
 #pragma unroll
     for (int j = 0; j < 16; j++) full &= (t16[j] >> 8) & 1u;
@@ -1610,9 +1646,10 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
     // between the two paths (that would run both, one after the other).
     if (__ballot(!full) == 0) {
         uint32_t pf[16];
+        uint4 hr[16];   // one LDS round trip for the whole node
 #pragma unroll
-        for (int j = 0; j < 16; j++) pf[j] = t16[j] & 0xffu;
-        stmd5::md5_node16(pf, h, dg);
+        for (int j = 0; j < 16; j++) { pf[j] = t16[j] & 0xffu; hr[j] = h[j]; }
+        stmd5::md5_node16(pf, hr, dg);
         tg = TAG_PRESENT;
         e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         return;
@@ -1630,14 +1667,50 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
     e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
 }
 
-// root0: first level-(H-2) bucket (a segment-range partition hashes only its
-// own subtrees); lmin: the climb stops once level lmin is hashed (1 = up to
-// the top hash; 2 = a partition stops at its level-2 entries).
+#define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
+
+__device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t lane, uint32_t k, uint4 &a,
+                                                uint4 &b, uint4 &c, uint4 &d) {
+    const uint4 *q = tiles + base + lane + 256ull * k;
+    a = q[0]; b = q[64]; c = q[128]; d = q[192];
+}
+
+// LDS of k_rehash_fused: the k_levels3_16 node blocks, then one 272-byte
+// message region per level-H node (a node's message may not be packed over its
+// own entries: they are read from LDS while the message is written).
+#define MSG16 272
+__host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return levels3_16_lds_bytes() + 256 * MSG16 + 64; }
+
+// STAMP (diagnostic, ST_LEVEL_STAMPS=1): wall-clock stamps (100 MHz) per
+// workgroup at phase boundaries into stamps[blockIdx.x * 8 + k].
+// Mailbox of one inner-node entry that a climbing lane of another workgroup
+// (possibly on another XCD, behind another L2) reads: written and read with
+// agent-scope atomics, which are coherent across XCDs without a write-back of
+// the writer's L2 or an invalidate of the reader's.
+struct MailEntry {
+    unsigned long long lo, hi;
+    uint32_t tag, pad0;
+    uint64_t pad1;
+};
+
+__device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg) {
+    __hip_atomic_store(&m->lo, ((unsigned long long)e.y << 32) | e.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&m->hi, ((unsigned long long)e.w << 32) | e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&m->tag, tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
+    const unsigned long long lo = __hip_atomic_load(&m->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long hi = __hip_atomic_load(&m->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tg = (uint16_t)__hip_atomic_load(&m->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    e = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
 template <bool STAMP>
-__global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt, uint64_t *stamps, uint64_t root0,
-                                                       uint32_t lmin) {
-#define FLOW_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-    FLOW_STAMP(0);
+__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, uint32_t *cnt, MailEntry *mail,
+                                                       uint64_t root0, uint32_t lmin, uint64_t *stamps) {
+#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    RF_STAMP(0);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *A = lds;
     uint8_t *At = A + 256 * NB16;
@@ -1645,32 +1718,98 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
     uint8_t *Bt = Bb + 16 * NB16;
     uint8_t *Cb = Bt + 16 * TB16;
     uint8_t *Ct = Cb + NB16;
-    const uint32_t tid = threadIdx.x;
+    uint8_t *M = lds + levels3_16_lds_bytes();   // message regions
+    // wave-uniform values in scalar registers: the tile bookkeeping of the
+    // block stream below then runs on the scalar unit with scalar branches
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t H = t.H;
     const uint64_t root = root0 + blockIdx.x;
-    const uint64_t c0 = t.base[H + 1] + root * 4096;
-#pragma unroll 4
-    for (uint32_t it = 0; it < 16; it++) {
-        const uint32_t e = it * 256 + tid;
-        *reinterpret_cast<uint4 *>(A + (e >> 4) * NB16 + (e & 15) * 16) = t.md5[c0 + e];
+    const uint64_t seg0 = root * 4096;
+
+    // ---- phase 1: K1 over this wave's tiles, one flat block stream
+    uint32_t Bq[RF_TILES], nbq[RF_TILES], liq[RF_TILES];
+    uint64_t bq[RF_TILES];
+    uint32_t P[RF_TILES + 1];
+    P[0] = 0;
+#pragma unroll
+    for (int q = 0; q < RF_TILES; q++) {
+        const uint64_t tl = root * 64 + wave + 16 * q;
+        const TileInfo ti = tt.tinfo[tl];
+        Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
+        const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ti.base),
+                       bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ti.base >> 32));
+        bq[q] = ((uint64_t)bhi << 32) | blo;
+        liq[q] = (uint32_t)(tt.tseg[tl * 64 + lane] - seg0);
+        nbq[q] = tt.tnb[tl * 64 + lane];
+        P[q + 1] = P[q] + Bq[q];
     }
+    const uint32_t T = P[RF_TILES];
+    auto locate = [&](uint32_t f, uint32_t &q, uint32_t &k) {
+        q = (f >= P[1]) + (f >= P[2]) + (f >= P[3]);
+        k = f - (q == 0 ? P[0] : q == 1 ? P[1] : q == 2 ? P[2] : P[3]);
+    };
+    auto pick = [&](const uint32_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
+    auto pick64 = [&](const uint64_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
+    auto put_entry = [&](uint32_t li, uint32_t nb, const uint32_t st[4]) {
+        uint4 e = make_uint4(0, 0, 0, 0);
+        uint16_t tg = 0;
+        if (nb) { e = make_uint4(st[0], st[1], st[2], st[3]); tg = (uint16_t)TAG_PRESENT; }
+        *reinterpret_cast<uint4 *>(A + (li >> 4) * NB16 + (li & 15) * 16) = e;
+        *reinterpret_cast<uint16_t *>(At + (li >> 4) * TB16 + (li & 15) * 2) = tg;
+    };
     {
-        const uint4 *tg = reinterpret_cast<const uint4 *>(t.tag + c0);
-        for (uint32_t it = 0; it < 2; it++) {
-            const uint32_t q = it * 256 + tid;
-            *reinterpret_cast<uint4 *>(At + (q >> 1) * TB16 + (q & 1) * 16) = tg[q];
+        uint4 r0a, r0b, r0c, r0d, r1a, r1b, r1c, r1d;
+        uint32_t q, k;
+        if (T > 0) { locate(0, q, k); tile_block_load(tt.tiles, pick64(bq, q), lane, k, r0a, r0b, r0c, r0d); }
+        if (T > 1) { locate(1, q, k); tile_block_load(tt.tiles, pick64(bq, q), lane, k, r1a, r1b, r1c, r1d); }
+        uint32_t st[4];
+        stmd5::init(st);
+        for (uint32_t f = 0; f < T; f++) {
+            uint32_t m[16] = {r0a.x, r0a.y, r0a.z, r0a.w, r0b.x, r0b.y, r0b.z, r0b.w,
+                              r0c.x, r0c.y, r0c.z, r0c.w, r0d.x, r0d.y, r0d.z, r0d.w};
+            r0a = r1a; r0b = r1b; r0c = r1c; r0d = r1d;
+            if (f + 2 < T) {
+                uint32_t q2, k2;
+                locate(f + 2, q2, k2);
+                tile_block_load(tt.tiles, pick64(bq, q2), lane, k2, r1a, r1b, r1c, r1d);
+            }
+            locate(f, q, k);
+            const uint32_t nb = pick(nbq, q);
+            if (k < nb) stmd5::compress(st, m);
+            if (k + 1 == pick(Bq, q)) {
+                put_entry(pick(liq, q), nb, st);
+                stmd5::init(st);
+            }
+        }
+#pragma unroll
+        for (int q0 = 0; q0 < RF_TILES; q0++)
+            if (Bq[q0] == 0) put_entry(liq[q0], 0, st);   // a tile of empty segments
+    }
+    __syncthreads();
+
+    RF_STAMP(1);
+    // ---- phase 2: the window's segment entries to the slot arrays, coalesced
+    {
+        const uint64_t c0 = t.base[H + 1] + seg0;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            const uint32_t i = it * 1024 + tid;
+            t.md5[c0 + i] = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
+            t.tag[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
         }
     }
     __syncthreads();
-    FLOW_STAMP(1);
+
+    RF_STAMP(2);
+    // ---- phase 3: levels H, H-1, H-2 from LDS, then the climb
     uint32_t l = H;
     uint64_t b = root * 256 + tid;
-    const uint4 *ent = reinterpret_cast<const uint4 *>(A + tid * NB16);
-    const uint16_t *tgs = reinterpret_cast<const uint16_t *>(At + tid * TB16);
-    uint8_t *reg = A + tid * NB16;
-    uint8_t *nxE = Bb + (tid >> 4) * NB16 + (tid & 15) * 16;
-    uint8_t *nxT = Bt + (tid >> 4) * TB16 + (tid & 15) * 2;
-    bool act = true;
+    const uint4 *ent = reinterpret_cast<const uint4 *>(A + (tid & 255) * NB16);
+    const uint16_t *tgs = reinterpret_cast<const uint16_t *>(At + (tid & 255) * TB16);
+    uint8_t *reg = M + (tid & 255) * MSG16;
+    uint8_t *nxE = Bb + ((tid & 255) >> 4) * NB16 + (tid & 15) * 16;
+    uint8_t *nxT = Bt + ((tid & 255) >> 4) * TB16 + (tid & 15) * 2;
+    bool act = tid < 256;
 #pragma unroll 1
     for (uint32_t phase = 0;; phase++) {
         if (act) {
@@ -1684,46 +1823,103 @@ __global__ void __launch_bounds__(256) k_levels_flow16(DevTree t, uint32_t *cnt,
             if (phase < 2) {
                 *reinterpret_cast<uint4 *>(nxE) = e;
                 *reinterpret_cast<uint16_t *>(nxT) = (uint16_t)tg;
+            } else if (l > lmin) {
+                mail_put(mail + slot, e, tg);   // read by the climbing lane of another workgroup
             }
         }
-        FLOW_STAMP(2 + 2 * phase);
         if (phase < 2) {
             __syncthreads();
+            RF_STAMP(3 + phase);
             l--;
             if (phase == 0) {
                 act = tid < 16;
                 b = root * 16 + tid;
-                ent = reinterpret_cast<const uint4 *>(Bb + tid * NB16);
-                tgs = reinterpret_cast<const uint16_t *>(Bt + tid * TB16);
-                reg = Bb + tid * NB16;
-                nxE = Cb + tid * 16;
-                nxT = Ct + tid * 2;
+                ent = reinterpret_cast<const uint4 *>(Bb + (tid & 15) * NB16);
+                tgs = reinterpret_cast<const uint16_t *>(Bt + (tid & 15) * TB16);
+                nxE = Cb + (tid & 15) * 16;
+                nxT = Ct + (tid & 15) * 2;
             } else {
                 act = tid == 0;
                 b = root;
                 ent = reinterpret_cast<const uint4 *>(Cb);
                 tgs = reinterpret_cast<const uint16_t *>(Ct);
-                reg = Cb;
             }
             continue;
         }
+        if (phase == 2) RF_STAMP(5);
         if (tid != 0 || l <= lmin) break;
         const uint64_t p = b >> 4;
         uint32_t *c = cnt + t.base[l - 1] + p;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const uint32_t old = atomicAdd(c, 1u);
+        // the mailbox stores above have completed (agent-coherent) before the
+        // counter moves; no L2 write-back / invalidate is needed
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old != 15u) break;
-        *c = 0u;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        FLOW_STAMP(3 + 2 * phase);
+        __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         l--;
         b = p;
+        // the parent's 16 child entries from their mailboxes: one round trip into LDS
         const uint64_t cc = t.base[l + 1] + p * 16;
-        ent = t.md5 + cc;
-        tgs = t.tag + cc;
-        reg = A;
+        uint4 h[16];
+        uint16_t g[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) mail_get(mail + cc + j, h[j], g[j]);
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            *reinterpret_cast<uint4 *>(Cb + j * 16) = h[j];
+            *reinterpret_cast<uint16_t *>(Ct + j * 2) = g[j];
+        }
+        ent = reinterpret_cast<const uint4 *>(Cb);
+        tgs = reinterpret_cast<const uint16_t *>(Ct);
+        RF_STAMP(6 + (l == 1));
     }
-#undef FLOW_STAMP
+#undef RF_STAMP
+}
+
+// Window-local tile order (fused rehash): one workgroup per window of 4096
+// segments sorts them by MD5 block count (descending; LDS counting sort) into
+// the window's 64 tiles: tseg/tnb[window*4096 + position], tsize[tile] = 256 x
+// the largest block count in the tile.
+__global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
+                                                           uint64_t *__restrict__ tsize) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t pnb[4096];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t seg0 = (uint64_t)blockIdx.x * 4096;
+    hist[tid] = 0;
+    __syncthreads();
+    uint32_t nb[16], bin[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint64_t s = seg0 + k * 256 + tid;
+        nb[k] = t.seg_off[s] != t.seg_off[s + 1] ? (uint32_t)((t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1) : 0u;
+        bin[k] = 255u - (nb[k] > 255u ? 255u : nb[k]);
+        atomicAdd(&hist[bin[k]], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int x = 0; x < 256; x++) { const uint32_t c = hist[x]; hist[x] = acc; acc += c; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t pos = atomicAdd(&hist[bin[k]], 1u);
+        tseg[seg0 + pos] = (uint32_t)(seg0 + k * 256 + tid);
+        tnb[seg0 + pos] = nb[k];
+        pnb[pos] = nb[k];
+    }
+    __syncthreads();
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    for (uint32_t j = wave; j < 64; j += 4) {
+        uint32_t m = pnb[j * 64 + lane];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t y = __shfl_xor(m, o, 64);
+            m = y > m ? y : m;
+        }
+        if (lane == 0) tsize[blockIdx.x * 64 + j] = (uint64_t)m * 256;
+    }
 }
 
 // K1 over the tiles: persistent waves, grid-stride over tiles; the next
@@ -1819,5 +2015,27 @@ __global__ void __launch_bounds__(64) k_level16_group(DevTree g, const TreeTiles
         t.md5 = tt.md5;
         t.tag = tt.tag;
         hash_node16(t, l, i % per, reg);
+    }
+}
+
+// Top-hash records of many trees into one device array, 18 bytes per tree
+// (present byte + the 17-byte hash): the payload of the cross-GPU all-gather
+// of ensemble top hashes, built without a host round trip.
+__global__ void k_tops_out(const TreeTiles *__restrict__ trees, uint32_t n, uint8_t *out) {
+    for (uint64_t i = gtid(); i < (uint64_t)n * 18; i += gstride()) {
+        const uint64_t t = i / 18, k = i % 18;
+        const uint16_t tg = trees[t].tag[0];
+        uint8_t b = 0;
+        if (tg & TAG_PRESENT) {
+            if (k == 0) b = 1;
+            else if (k == 1) b = (uint8_t)(tg & 0xffu);
+            else {
+                const uint4 m = trees[t].md5[0];
+                const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+                const uint32_t j = (uint32_t)k - 2;
+                b = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+            }
+        }
+        out[i] = b;
     }
 }

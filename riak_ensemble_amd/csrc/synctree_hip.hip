@@ -19,6 +19,7 @@
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
 #include "leveldb_fmt.h"
+#include "small_path.h"
 
 static thread_local std::string g_err;
 static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past a range
@@ -40,9 +41,9 @@ static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past 
 
 struct CmpWork {
     uint32_t *flist = nullptr, *fcnt = nullptr;
-    unsigned long long *err = nullptr;
-    uint64_t *dcnt = nullptr, *doff = nullptr, *part = nullptr, *tot = nullptr;
-    DiffRec *rec = nullptr;
+    unsigned long long *err = nullptr, *seg_bytes = nullptr, *ctr = nullptr;
+    uint64_t *dcnt = nullptr, *doff = nullptr, *soff = nullptr, *tot = nullptr;
+    DiffRec *rec = nullptr, *scratch = nullptr;
     uint64_t cap = 0;
 };
 
@@ -76,7 +77,8 @@ struct st_tree {
     uint32_t *tseg = nullptr, *tnb = nullptr;
     TileInfo *tinfo = nullptr;
     bool tiles_valid = false;
-    uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_levels_flow16)
+    uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
+    MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
     // segment-range partition (st_set_partition): owned segments [part_lo, part_hi)
     bool partitioned = false;
     uint64_t part_lo = 0, part_hi = 0;
@@ -84,6 +86,11 @@ struct st_tree {
     CmpWork cw;
     // small pinned host buffer for scalar results (one D2H per call)
     uint64_t *pin = nullptr;
+    // per-key latency path (small_path.h): overlay of segments changed by
+    // small inserts, and the mapped pinned result block of k_small
+    Overlay ov{nullptr, nullptr, nullptr, 0};
+    bool ov_pending = false;
+    SmallOut *sout = nullptr, *sout_dev = nullptr;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -312,9 +319,14 @@ extern "C" void st_destroy(st_tree *t) {
     (void)hipSetDevice(t->device);
     void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
                   t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.flist, t->cw.fcnt, t->cw.err,
-                  t->cw.dcnt, t->cw.doff, t->cw.part, t->cw.tot, t->cw.rec};
+                  t->cw.dcnt, t->cw.doff, t->cw.soff, t->cw.tot, t->cw.rec, t->cw.scratch, t->cw.seg_bytes,
+                  t->cw.ctr, t->mail};
     for (void *p : ps) dfree(t, p);
+    dfree(t, t->ov.idx);
+    dfree(t, t->ov.heap);
+    dfree(t, t->ov.used);
     if (t->pin) (void)hipHostFree(t->pin);
+    if (t->sout) (void)hipHostFree(t->sout);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -440,9 +452,11 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // Build the hash-ready tiled messages from the CSR in seg_perm order
 // (k_tile_order_global, scan, k_tile_fill).  Called at the end of every bulk
 // ingest and lazily by rehash.
+static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3; }
+
 static int ensure_tiles(st_tree *t) {
     if (t->tiles_valid) return ST_OK;
-    CHK(ensure_perm(t));
+    if (!fused_geometry(t)) CHK(ensure_perm(t));
     const uint64_t ntiles = num_tiles(t);
     if (!t->tseg) {
         CHK(dalloc_t(t, &t->tseg, ntiles * 64));
@@ -454,8 +468,11 @@ static int ensure_tiles(st_tree *t) {
     CHK(sc.alloc(&tsize, ntiles + 1));
     CHK(sc.alloc(&tbase, ntiles + 1));
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
-    LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
-           (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
+    if (fused_geometry(t))   // window-local order (k_rehash_fused)
+        LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tnb, tsize);
+    else
+        LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
+               (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
     CHK(exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1));
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
@@ -490,6 +507,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
 
 static int ensure_lvl_cnt(st_tree *t) {
     if (t->lvl_cnt || t->H < 3) return ST_OK;
+    CHK(dalloc_t(t, &t->mail, t->base[t->H - 1]));
     CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
     HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
     return ST_OK;
@@ -509,54 +527,57 @@ static int levels16(st_tree *t, uint32_t top, const uint8_t *mask) {
     return ST_OK;
 }
 
-// Full rehash: K1 k_segment_hash_tiled_p over the global block-count tiles,
-// then (W == 16, H >= 3) every inner level and the top hash in ONE launch of
-// k_levels_flow16 (levels H..H-2 per workgroup, the rest by last-arriving
-// workgroups).  Other geometries use the per-level kernels.
+// Full rehash.  W == 16, H >= 3: ONE launch of k_rehash_fused, a workgroup
+// per level-(H-2) window: K1 over the window's tiles, its levels H..H-2 from
+// LDS, the levels above by last-arriving workgroups.  Other geometries: K1
+// (k_segment_hash_tiled_p over globally ordered tiles), then the per-level
+// kernels.
 static int rehash_tiled(st_tree *t) {
     CHK(ensure_tiles(t));
     DevTree d = view(t);
+    if (fused_geometry(t)) {
+        CHK(ensure_lvl_cnt(t));
+        // a partition hashes only its own windows (4096 segments each) and
+        // stops at level 2; st_combine_upper finishes level 1 + top
+        const uint64_t nroots = t->S / 4096;
+        const uint64_t root0 = t->partitioned ? t->part_lo / 4096 : 0;
+        const uint32_t nwg = t->partitioned ? (uint32_t)((t->part_hi - t->part_lo) / 4096) : (uint32_t)nroots;
+        if (root0 + nwg > nroots || nwg == 0) { g_err = "rehash window range out of bounds"; return ST_EINVAL; }
+        const uint32_t lmin = t->partitioned ? 2u : 1u;
+        static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
+        if (!stamp) {
+            LAUNCH(t, "rehash_fused", k_rehash_fused<false>, nwg, 1024, fused_lds_bytes(), d, tree_tiles(t), t->lvl_cnt,
+                   t->mail, root0, lmin, (uint64_t *)nullptr);
+            return ST_OK;
+        }
+        // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
+        Scratch sc(t);
+        uint64_t *st = nullptr;
+        CHK(sc.alloc(&st, (uint64_t)nwg * 8));
+        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 8 * 8, t->stream));
+        LAUNCH(t, "rehash_fused", k_rehash_fused<true>, nwg, 1024, fused_lds_bytes(), d, tree_tiles(t), t->lvl_cnt, t->mail,
+               root0, lmin, st);
+        std::vector<uint64_t> h((uint64_t)nwg * 8);
+        HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipStreamSynchronize(t->stream));
+        uint64_t t0 = ~0ull;
+        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 8]);
+        static const char *names[8] = {"start", "K1 done", "entries stored", "level H", "level H-1", "level H-2",
+                                       "climb level", "level 1 + top"};
+        for (int k = 0; k < 8; k++) {
+            std::vector<double> v;
+            for (uint32_t w = 0; w < nwg; w++) if (h[w * 8 + k]) v.push_back((h[w * 8 + k] - t0) / 100.0);
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, "fused stamp %d %-15s n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, names[k], v.size(), v[0],
+                    v[v.size() / 2], v.back());
+        }
+        return ST_OK;
+    }
     const uint64_t ntl = num_tiles(t);
     LAUNCH(t, "segment_hash", k_segment_hash_tiled_p<false>, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, 1024u), 256, 0, d,
            tree_tiles(t), (const TreeTiles *)nullptr, ntl, ntl);
     if (t->H == 0) return ST_OK;
-    if (t->W == 16 && t->H >= 3) {
-        CHK(ensure_lvl_cnt(t));
-        static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
-        // a partition hashes only its own level-(H-2) subtrees (4096 segments
-        // each) and stops at level 2; st_combine_upper finishes level 1 + top
-        const uint64_t nroots = t->base[t->H - 1] - t->base[t->H - 2];   // 16^(H-3) level-(H-2) nodes
-        const uint64_t sub = t->S / nroots;                                // segments per subtree
-        const uint64_t root0 = t->partitioned ? t->part_lo / sub : 0;
-        const uint32_t nwg = t->partitioned ? (uint32_t)((t->part_hi - t->part_lo) / sub) : (uint32_t)nroots;
-        if (root0 + nwg > nroots || nwg == 0) { g_err = "level rehash range out of bounds"; return ST_EINVAL; }
-        const uint32_t lmin = t->partitioned ? 2u : 1u;
-        if (!stamp) {
-            LAUNCH(t, "level_rehash", k_levels_flow16<false>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt,
-                   (uint64_t *)nullptr, root0, lmin);
-            return ST_OK;
-        }
-        // diagnostic (ST_LEVEL_STAMPS=1): per-phase wall-clock stamps (100 MHz) to stderr
-        uint64_t *st = nullptr;
-        CHK(dalloc_t(t, &st, (uint64_t)nwg * 16));
-        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
-        LAUNCH(t, "level_rehash", k_levels_flow16<true>, nwg, 256, levels3_16_lds_bytes(), d, t->lvl_cnt, st, root0, lmin);
-        std::vector<uint64_t> h((uint64_t)nwg * 16);
-        HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipStreamSynchronize(t->stream));
-        dfree(t, st);
-        uint64_t t0 = ~0ull;
-        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
-        for (int k = 0; k < 12; k++) {
-            std::vector<double> v;
-            for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
-            if (v.empty()) continue;
-            std::sort(v.begin(), v.end());
-            fprintf(stderr, "flow stamp %2d: n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, v.size(), v[0], v[v.size() / 2],
-                    v.back());
-        }
-        return ST_OK;
-    }
     if (t->W == 16) return levels16(t, t->H, nullptr);
     return rehash_levels(t, t->H, nullptr);
 }
@@ -763,6 +784,122 @@ static int ingest(st_tree *t, IngestIn &in) {
     return ST_OK;
 }
 
+// ------------------------------------------------------------------ overlay (small_path.h)
+// Merge the segments small inserts left in the overlay into the CSR: their
+// records become one ingest batch with replace flags (their hashes are already
+// in the slot arrays, so nothing is rehashed).  Every entry point that reads
+// segments other than the small kernels calls this first.
+static int flush_overlay(st_tree *t) {
+    if (!t->ov_pending) return ST_OK;
+    const uint64_t S = t->S;
+    Scratch sc(t);
+    uint64_t *cnt = nullptr, *kbs = nullptr, *vbs = nullptr, *eoff = nullptr, *ko0 = nullptr, *vo0 = nullptr;
+    uint8_t *rep = nullptr;
+    CHK(sc.alloc(&cnt, S + 1));
+    CHK(sc.alloc(&kbs, S + 1));
+    CHK(sc.alloc(&vbs, S + 1));
+    CHK(sc.alloc(&eoff, S + 1));
+    CHK(sc.alloc(&ko0, S + 1));
+    CHK(sc.alloc(&vo0, S + 1));
+    CHK(sc.alloc(&rep, S));
+    LAUNCH(t, "ov_flush", k_ov_sizes, grid_for(S + 1), 256, 0, t->ov, S, cnt, kbs, vbs, rep);
+    CHK(exclusive_scan<uint64_t>(t, cnt, eoff, S + 1));
+    CHK(exclusive_scan<uint64_t>(t, kbs, ko0, S + 1));
+    CHK(exclusive_scan<uint64_t>(t, vbs, vo0, S + 1));
+    HIPCHK(hipMemcpyAsync(t->pin, eoff + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 1, ko0 + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipMemcpyAsync(t->pin + 2, vo0 + S, 8, hipMemcpyDeviceToHost, t->stream));
+    HIPCHK(hipStreamSynchronize(t->stream));
+    const uint64_t n = t->pin[0], kt = t->pin[1], vt = t->pin[2];
+    if (n) {
+        uint8_t *krec = nullptr, *vh = nullptr;
+        uint64_t *ko = nullptr, *vo = nullptr;
+        uint32_t *segs = nullptr;
+        CHK(sc.bytes(&krec, kt + HEAP_SLACK));
+        CHK(sc.bytes(&vh, vt + HEAP_SLACK));
+        CHK(sc.alloc(&ko, n + 1));
+        CHK(sc.alloc(&vo, n + 1));
+        CHK(sc.alloc(&segs, n));
+        HIPCHK(hipMemsetAsync(krec + kt, 0, HEAP_SLACK, t->stream));
+        HIPCHK(hipMemsetAsync(vh + vt, 0, HEAP_SLACK, t->stream));
+        LAUNCH(t, "ov_flush", k_ov_gather, grid_for(S), 256, 0, t->ov, S, (const uint64_t *)eoff, (const uint64_t *)ko0,
+               (const uint64_t *)vo0, krec, ko, vh, vo, segs);
+        LAUNCH(t, "ov_flush", k_ov_terminate, 1, 64, 0, n, (const uint64_t *)(ko0 + S), (const uint64_t *)(vo0 + S), ko, vo);
+        const uint64_t nbefore = t->n;
+        IngestIn in{};
+        in.n = n; in.krec = krec; in.koff = ko; in.vheap = vh; in.voff = vo;
+        in.seg_given = segs; in.seg_replace = rep; in.verify_rehash = false;
+        CHK(ingest(t, in));
+        (void)nbefore;
+    }
+    HIPCHK(hipMemsetAsync(t->ov.idx, 0xff, S * 8, t->stream));
+    HIPCHK(hipMemsetAsync(t->ov.used, 0, 8, t->stream));
+    t->ov_pending = false;
+    return ST_OK;
+}
+
+#define FLUSH(t) CHK(flush_overlay(t))
+
+static int ensure_small(st_tree *t) {
+    if (!t->ov.idx) {
+        const uint64_t cap = 64ull << 20;
+        CHK(dalloc_t(t, &t->ov.idx, t->S));
+        CHK(dalloc(t, (void **)&t->ov.heap, cap + HEAP_SLACK));
+        CHK(dalloc_t(t, &t->ov.used, 1));
+        HIPCHK(hipMemsetAsync(t->ov.idx, 0xff, t->S * 8, t->stream));
+        HIPCHK(hipMemsetAsync(t->ov.heap + cap, 0, HEAP_SLACK, t->stream));
+        HIPCHK(hipMemsetAsync(t->ov.used, 0, 8, t->stream));
+        t->ov.cap = cap;
+    }
+    if (!t->sout) {
+        if (hipHostMalloc((void **)&t->sout, sizeof(SmallOut), hipHostMallocMapped) != hipSuccess) {
+            t->sout = nullptr;
+            g_err = "hipHostMalloc (mapped) failed";
+            return ST_EDEVICE;
+        }
+        HIPCHK(hipHostGetDevicePointer((void **)&t->sout_dev, t->sout, 0));
+    }
+    return ST_OK;
+}
+
+// One get/2 (op 0) or insert/3 (op 1) batch through k_small when it fits:
+// returns ST_OK with *served = 1 and t->sout filled, or *served = 0 (the
+// caller takes the bulk path).  Host pointers, records packed by the caller.
+static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, const uint8_t *vheap, const uint64_t *voff,
+                      int *served) {
+    *served = 0;
+    const uint64_t kbytes = hr.off[n];
+    const uint64_t vbytes = op == 1 ? voff[n] - voff[0] : 0;
+    if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
+        small_lds_bytes((uint32_t)t->W) > 160 * 1024)
+        return ST_OK;
+    CHK(ensure_small(t));
+    SmallIn in;
+    memset(&in, 0, sizeof(in));
+    in.n = (uint32_t)n;
+    in.op = (uint32_t)op;
+    for (uint64_t i = 0; i <= n; i++) in.koff[i] = (uint32_t)hr.off[i];
+    memcpy(in.kb, hr.heap.data(), kbytes);
+    if (op == 1) {
+        for (uint64_t i = 0; i <= n; i++) in.voff[i] = (uint32_t)(voff[i] - voff[0]);
+        memcpy(in.vb, vheap + voff[0], vbytes);
+    }
+    t->sout->done = 0;
+    LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev);
+    HIPCHK(hipStreamSynchronize(t->stream));
+    if (!t->sout->done) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
+    if (t->sout->retry) return ST_OK;
+    *served = 1;
+    if (op == 1) {
+        t->n += t->sout->new_entries;
+        t->ov_pending = true;
+        t->fresh = false;
+        t->tiles_valid = false;
+        t->perm_valid = false;
+    }
+    return ST_OK;
+}
+
 // ------------------------------------------------------------------ writes
 static int upload_records(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                           uint8_t **d_krec, uint64_t **d_koff) {
@@ -795,6 +932,21 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
                                uint64_t *cbucket) {
     CHK(use_device(t));
     if (n == 0) return ST_OK;
+    if (n <= SB_MAX) {   // per-key latency path: one launch, one sync
+        HostRecords hr;
+        CHK(pack_records(n, ktype, kheap, koff, hr));
+        int served = 0;
+        CHK(small_call(t, 1, n, hr, vheap, voff, &served));
+        if (served) {
+            for (uint64_t i = 0; i < n; i++) {
+                if (status) status[i] = t->sout->status[i];
+                if (clevel) clevel[i] = t->sout->clevel[i];
+                if (cbucket) cbucket[i] = t->sout->cbucket[i];
+            }
+            return ST_OK;
+        }
+    }
+    FLUSH(t);
     uint8_t *krec = nullptr, *dv = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr;
     uint32_t *dcl = nullptr, *dseg = nullptr;
@@ -829,6 +981,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
 extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                                int on_device, uint64_t *n_corrupted) {
     CHK(use_device(t));
+    FLUSH(t);
     if (n_corrupted) *n_corrupted = 0;
     if (n == 0) return ST_OK;
     const int64_t *dkeys = keys;
@@ -877,6 +1030,7 @@ extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, cons
 
 extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen) {
     CHK(use_device(t));
+    FLUSH(t);
     uint64_t koff[2] = {0, klen};
     uint8_t *krec = nullptr, *dv = nullptr, *bop = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr;
@@ -900,6 +1054,7 @@ extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
 extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
                                 const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff) {
     CHK(use_device(t));
+    FLUSH(t);
     if (segment >= t->S) { g_err = "segment out of range"; return ST_EINVAL; }
     HostRecords hr;
     CHK(pack_records(n, ktype, kheap, koff, hr));
@@ -1030,6 +1185,7 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 // ------------------------------------------------------------------ rehash / verify
 extern "C" int st_rehash(st_tree *t, int upper) {
     CHK(use_device(t));
+    FLUSH(t);
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
     if (t->partitioned && upper) {
         g_err = "a segment-range partition supports the full rehash (st_rehash upper = 0) only";
@@ -1061,6 +1217,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
             if (trees[j] == u) { g_err = "a tree appears twice in the group"; return ST_EINVAL; }
     }
     for (uint32_t i = 0; i < n; i++) {
+        CHK(flush_overlay(trees[i]));
         CHK(ensure_tiles(trees[i]));
         HIPCHK(hipStreamSynchronize(trees[i]->stream));
     }
@@ -1095,6 +1252,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
 
 extern "C" int st_verify(st_tree *t, int upper, int *ok) {
     CHK(use_device(t));
+    FLUSH(t);
     const uint32_t maxd = upper ? t->H : t->H + 1;
     if (maxd == 0) { g_err = "verify_upper at Height 0 crashes in the reference"; return ST_EINVAL; }
     DevTree d = view(t);
@@ -1137,6 +1295,7 @@ extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
 
 extern "C" int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi) {
     CHK(use_device(t));
+    FLUSH(t);
     if (seg_lo == 0 && seg_hi == t->S) { t->partitioned = false; return ST_OK; }
     const uint64_t l2 = t->W == 16 && t->H >= 4 ? t->S / 16 : 0;
     if (!l2 || seg_lo >= seg_hi || seg_hi > t->S || seg_lo % l2 || seg_hi % l2) {
@@ -1281,6 +1440,33 @@ extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const 
                             st_result **out) {
     CHK(use_device(t));
     *out = nullptr;
+    if (n >= 1 && n <= SB_MAX) {   // per-key latency path: one launch, one sync
+        HostRecords hr;
+        CHK(pack_records(n, ktype, kheap, koff, hr));
+        int served = 0;
+        CHK(small_call(t, 0, n, hr, nullptr, nullptr, &served));
+        if (served) {
+            const SmallOut *so = t->sout;
+            st_result *res = new_result(n);
+            res->n_entries = n;
+            res->koff = (uint64_t *)calloc(n + 1, 8);
+            res->aoff = (uint64_t *)calloc(n + 1, 8);
+            res->ktype = (uint8_t *)calloc(n + 1, 1);
+            res->kheap = (uint8_t *)malloc(1);
+            res->aheap = (uint8_t *)malloc(so->voff[n] + 1);
+            for (uint64_t i = 0; i < n; i++) {
+                res->status[i] = so->status[i];
+                res->clevel[i] = so->clevel[i];
+                res->cbucket[i] = so->cbucket[i];
+                res->eoff[i + 1] = i + 1;
+                res->aoff[i + 1] = so->voff[i + 1];
+            }
+            memcpy(res->aheap, so->vbytes, so->voff[n]);
+            *out = res;
+            return ST_OK;
+        }
+    }
+    FLUSH(t);
     st_result *res = new_result(n);
     int present = 0;
     uint8_t top[17];
@@ -1454,11 +1640,13 @@ static int node_images(st_tree *t, uint32_t level, uint64_t n, const uint64_t *b
 
 extern "C" int st_exchange_get_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
     CHK(use_device(t));
+    FLUSH(t);
     return node_images(t, level, n, buckets, out, true);
 }
 
 extern "C" int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
     CHK(use_device(t));
+    FLUSH(t);
     if (level == 0) {
         st_result *res = new_result(n);
         uint16_t tg = 0;
@@ -1500,25 +1688,17 @@ extern "C" int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype,
 }
 
 // ------------------------------------------------------------------ compare (K3)
-// Device-side scan of NA uint64 arrays over n_ptr[0] elements (no host round
-// trip); totals[k] receives the sum of array k.
-template <int NA>
-static int dscan(st_tree *t, const DScanArgs<NA> &a, const uint64_t *n_ptr, uint64_t *part, uint64_t *totals) {
-    LAUNCH(t, "dscan", k_dscan_sums<NA>, DSCAN_WGS, 256, 0, a, n_ptr, part);
-    LAUNCH(t, "dscan", k_dscan_top<NA>, 1, 64, 0, part, (uint32_t)DSCAN_WGS, totals);
-    LAUNCH(t, "dscan", k_dscan_apply<NA>, DSCAN_WGS, 256, 0, a, n_ptr, (const uint64_t *)part);
-    return ST_OK;
-}
-
 static int ensure_cmp_work(st_tree *t) {
     CmpWork &w = t->cw;
     if (w.flist) return ST_OK;
     CHK(dalloc_t(t, &w.flist, t->nslots));
     CHK(dalloc_t(t, &w.fcnt, ST_MAXLEV + 2));
     CHK(dalloc_t(t, &w.err, 1));
+    CHK(dalloc_t(t, &w.seg_bytes, 1));
+    CHK(dalloc_t(t, &w.ctr, 1));
     CHK(dalloc_t(t, &w.dcnt, t->S + 1));
     CHK(dalloc_t(t, &w.doff, t->S + 1));
-    CHK(dalloc_t(t, &w.part, 4 * (DSCAN_WGS + 1)));
+    CHK(dalloc_t(t, &w.soff, t->S + 1));
     CHK(dalloc_t(t, &w.tot, 8));
     return ST_OK;
 }
@@ -1527,10 +1707,12 @@ static int grow_records(st_tree *t, uint64_t need) {
     CmpWork &w = t->cw;
     if (need <= w.cap) return ST_OK;
     dfree(t, w.rec);
-    w.rec = nullptr;
+    dfree(t, w.scratch);
+    w.rec = w.scratch = nullptr;
     w.cap = 0;
     const uint64_t cap = need + need / 4 + 1024;
     CHK(dalloc_t(t, &w.rec, cap));
+    CHK(dalloc_t(t, &w.scratch, cap));
     w.cap = cap;
     return ST_OK;
 }
@@ -1545,9 +1727,10 @@ static uint32_t cmp_slice(const st_tree *t) {
     return (s + 15) & ~15u;
 }
 
-// K3: frontier, verify + count, device scan, write; ONE host round trip
-// (two when the record buffer has to grow).  A partitioned pair compares its
-// own segment range only (same partition on both sides).
+// K3: frontier, verify + merge-join into scratch, device scan, reorder; ONE
+// host round trip (a second compare when the record buffers have to grow).
+// A partitioned pair compares its own segment range only (same partition on
+// both sides).
 static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint32_t *clevel, uint64_t *cbucket,
                         int *cside, int *status) {
     *status = ST_OK;
@@ -1562,6 +1745,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
     st_tree *t = A;   // work is enqueued on the local tree's stream
     if (B->stream != A->stream) HIPCHK(hipStreamSynchronize(B->stream));
     CHK(ensure_cmp_work(t));
+    CHK(grow_records(t, 4096));
     CmpWork &w = t->cw;
     DevTree da = view(A), db = view(B);
     const uint32_t L1 = A->H + 1;
@@ -1572,45 +1756,45 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         hi2 = A->part_hi / per2;
     }
     uint64_t *nfinal = w.tot + 1, *total = w.tot;
-    LAUNCH(t, "cmp_frontier", k_cmp_frontier, 1, 1024, 0, da, db, filter, lo2, hi2, w.flist, w.fcnt, w.err, nfinal);
     const uint32_t slice = cmp_slice(t);
     const uint32_t wpg = std::max<uint32_t>(1, std::min<uint32_t>(4, (160 * 1024) / slice));
-    LAUNCH(t, "cmp_visit", k_cmp_visit<false>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
-           (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)nullptr, (const uint64_t *)nullptr, (DiffRec *)nullptr,
-           (uint64_t)0, w.err, slice);
-    DScanArgs<1> sa;
-    sa.in[0] = w.dcnt;
-    sa.out[0] = w.doff;
-    CHK(dscan<1>(t, sa, nfinal, w.part, total));
-    LAUNCH(t, "cmp_write", k_cmp_visit<true>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
-           (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)w.doff, (const uint64_t *)total, w.rec, w.cap, w.err, slice);
-    HIPCHK(hipMemcpyAsync(t->pin, w.tot, 16, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(t->pin + 2, w.err, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
-    const uint64_t ntot = t->pin[0], e = t->pin[2];
-    if (e != ~0ull) {
-        *status = ST_CORRUPTED;
-        *clevel = (uint32_t)(e >> 56);
-        *cbucket = (e & ((1ull << 56) - 1)) >> 1;
-        *cside = (int)(e & 1);
-        return ST_OK;
-    }
-    (void)L1;
-    if (ntot > w.cap) {   // first compare with this many records: grow and write again
-        CHK(grow_records(t, ntot));
-        LAUNCH(t, "cmp_write", k_cmp_visit<true>, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter,
-               (const uint32_t *)w.flist, (const uint32_t *)w.fcnt, w.dcnt, (const uint64_t *)w.doff,
-               (const uint64_t *)total, w.rec, w.cap, w.err, slice);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        HIPCHK(hipMemsetAsync(w.ctr, 0, 8, t->stream));
+        LAUNCH(t, "cmp_frontier", k_cmp_frontier, 1, 1024, 0, da, db, filter, lo2, hi2, w.flist, w.fcnt, w.err, nfinal,
+               w.seg_bytes);
+        LAUNCH(t, "cmp_visit", k_cmp_visit, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
+               (const uint32_t *)w.fcnt, w.dcnt, w.soff, w.scratch, w.cap, w.ctr, w.err, slice, w.seg_bytes);
+        LAUNCH(t, "cmp_scan", k_dscan1, 1, 1024, 0, (const uint64_t *)w.dcnt, w.doff, (const uint64_t *)nfinal, total);
+        LAUNCH(t, "cmp_reorder", k_cmp_reorder, 256, 256, 0, (const uint32_t *)w.fcnt, L1, (const uint64_t *)w.dcnt,
+               (const uint64_t *)w.doff, (const uint64_t *)w.soff, (const uint64_t *)total, (const DiffRec *)w.scratch,
+               w.rec, w.cap);
+        HIPCHK(hipMemcpyAsync(t->pin, w.tot, 16, hipMemcpyDeviceToHost, t->stream));
+        HIPCHK(hipMemcpyAsync(t->pin + 2, w.err, 8, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipStreamSynchronize(t->stream));
+        const uint64_t ntot = t->pin[0], e = t->pin[2];
+        if (e != ~0ull) {
+            *status = ST_CORRUPTED;
+            *clevel = (uint32_t)(e >> 56);
+            *cbucket = (e & ((1ull << 56) - 1)) >> 1;
+            *cside = (int)(e & 1);
+            return ST_OK;
+        }
+        if (ntot <= w.cap) {
+            co.n = ntot;
+            co.rec = w.rec;
+            return ST_OK;
+        }
+        CHK(grow_records(t, ntot));   // first compare with this many records
     }
-    co.n = ntot;
-    co.rec = w.rec;
-    return ST_OK;
+    g_err = "compare record buffer did not converge";
+    return ST_EDEVICE;
 }
 
 extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
                                  uint64_t *cbucket, int *cside) {
     CHK(use_device(local));
+    CHK(flush_overlay(local));
+    CHK(flush_overlay(remote));
     CompareOut co;
     int status = ST_OK;
     CHK(compare_core(local, remote, filter, co, clevel, cbucket, cside, &status));
@@ -1626,6 +1810,8 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
 extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
                                  uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
     CHK(use_device(local));
+    CHK(flush_overlay(local));
+    CHK(flush_overlay(remote));
     *n_diffs = 0;
     *n_applied = 0;
     *n_rejected = 0;
@@ -1692,6 +1878,8 @@ extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_di
 extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
                           uint64_t *cbucket, int *cside) {
     CHK(use_device(local));
+    CHK(flush_overlay(local));
+    CHK(flush_overlay(remote));
     *out = nullptr;
     CompareOut co;
     int status = ST_OK;
@@ -1746,6 +1934,43 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
         return fail(r);
     records_to_keys(res, n);
     *out = res;
+    return ST_OK;
+}
+
+// The last compare's frontier: visited nodes per level (levels 1..H+1) and
+// the algorithmic bytes of its final-level segment pairs (bench roofline).
+extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_levels, uint64_t *seg_bytes) {
+    CHK(use_device(local));
+    CmpWork &w = local->cw;
+    if (!w.flist) { g_err = "no compare has run on this tree"; return ST_EINVAL; }
+    uint32_t f[ST_MAXLEV + 2];
+    unsigned long long b = 0;
+    HIPCHK(hipMemcpyAsync(f, w.fcnt, sizeof(f), hipMemcpyDeviceToHost, local->stream));
+    HIPCHK(hipMemcpyAsync(&b, w.seg_bytes, 8, hipMemcpyDeviceToHost, local->stream));
+    HIPCHK(hipStreamSynchronize(local->stream));
+    for (uint32_t l = 0; l < max_levels && l < ST_MAXLEV + 2; l++) visited[l] = f[l];
+    *seg_bytes = b;
+    return ST_OK;
+}
+
+// Top-hash records of n trees (one device) into device memory `out`
+// (18 bytes per tree: present, hash17), for an RCCL all-gather.
+extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
+    if (n == 0) return ST_OK;
+    st_tree *t = trees[0];
+    CHK(use_device(t));
+    std::vector<TreeTiles> h(n);
+    for (uint32_t i = 0; i < n; i++) {
+        if (trees[i]->device != t->device) { g_err = "trees on different devices"; return ST_EINVAL; }
+        if (trees[i]->stream != t->stream) HIPCHK(hipStreamSynchronize(trees[i]->stream));
+        h[i] = tree_tiles(trees[i]);
+    }
+    Scratch sc(t);
+    TreeTiles *dtt = nullptr;
+    CHK(sc.alloc(&dtt, n));
+    HIPCHK(hipMemcpyAsync(dtt, h.data(), n * sizeof(TreeTiles), hipMemcpyHostToDevice, t->stream));
+    LAUNCH(t, "tops_out", k_tops_out, grid_for((uint64_t)n * 18), 256, 0, (const TreeTiles *)dtt, n, (uint8_t *)out);
+    HIPCHK(hipStreamSynchronize(t->stream));
     return ST_OK;
 }
 
@@ -1805,6 +2030,7 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
 extern "C" int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, st_kv **out) {
     *out = nullptr;
     CHK(use_device(t));
+    FLUSH(t);
     if (t->partitioned) { g_err = "snapshot of a partitioned tree (one partition is not a synctree)"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
     uint64_t n = 0, tot[3] = {0, 0, 0}, *okoff = nullptr, *ovoff = nullptr;
@@ -1833,6 +2059,7 @@ extern "C" int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t 
 extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t *n_records,
                                           uint64_t *key_bytes, uint64_t *value_bytes) {
     CHK(use_device(t));
+    FLUSH(t);
     if (t->partitioned) { g_err = "snapshot of a partitioned tree"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
     uint64_t n = 0, tot[3] = {0, 0, 0}, *okoff = nullptr, *ovoff = nullptr;
@@ -1850,6 +2077,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
                                   const uint8_t *kheap, const uint64_t *koff, const uint8_t *vheap,
                                   const uint64_t *voff, uint64_t *n_loaded, uint64_t *n_skipped) {
     CHK(use_device(t));
+    FLUSH(t);
     if (t->partitioned) { g_err = "restore into a partitioned tree"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
     const uint64_t R = t->nslots, S = t->S;

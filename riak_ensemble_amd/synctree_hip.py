@@ -272,6 +272,15 @@ class DeviceTree:
             return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
         return int(nd.value)
 
+    def compare_stats(self):
+        """(visited nodes per level [0..H+1], final-level segment bytes) of the
+        last compare on this tree (st_compare_stats)."""
+        v = np.zeros(40, np.uint64)
+        b = ctypes.c_uint64()
+        _lib.check(self.L.st_compare_stats(self.h, v.ctypes.data_as(_lib.u64p), 40, ctypes.byref(b)),
+                   'st_compare_stats')
+        return [int(x) for x in v[:self.height + 2]], int(b.value)
+
     def exchange_apply(self, remote):
         """riak_ensemble_exchange.erl:71-97 against one remote tree, as one
         device batch (st_exchange_apply).  Returns ('ok', info),
@@ -386,3 +395,14 @@ def rehash_group(trees):
     L = trees[0].L
     arr = (ctypes.c_void_p * len(trees))(*[t.h.value for t in trees])
     _lib.check(L.st_rehash_group(arr, len(trees)), 'st_rehash_group')
+
+
+def tops_to_device(trees, dev_ptr):
+    """Top-hash records (18 B each: present, hash17) of `trees` into device
+    memory at dev_ptr (st_tops_to_device), e.g. a torch uint8 tensor to
+    all-gather across ranks."""
+    if not trees:
+        return
+    L = trees[0].L
+    arr = (ctypes.c_void_p * len(trees))(*[t.h.value for t in trees])
+    _lib.check(L.st_tops_to_device(arr, len(trees), ctypes.c_void_p(dev_ptr)), 'st_tops_to_device')

@@ -1,0 +1,133 @@
+"""The per-key latency path: insert/3 and get/2 batches of
+up to 16 keys served by one fused kernel (k_small) with an overlay of changed
+segments that every other entry point merges into the CSR first.  Checked
+against the C restatement (oracle/, the checker only) after every step, with
+bulk operations interleaved (rehash, compare, exchange_get, snapshot, big
+insert batches), corruption (synctree.erl:189-227, 302-320) and the fallback
+to the bulk path (segments larger than the kernel rewrites)."""
+import numpy as np
+import pytest
+
+from riak_ensemble_amd import workload
+
+
+def _val(seq, epoch=1):
+    return bytes([0]) + epoch.to_bytes(8, 'big') + seq.to_bytes(8, 'big')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('geom', [(16, 1 << 20), (4, 4096), (16, 16)])
+def test_small_inserts_and_gets_interleaved(geom):
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip
+    W, S = geom
+    n = 20000 if S >= 4096 else 3000
+    keys = workload.keys_int63(n, workload.SEED ^ 0x51)
+    vals = workload.obj_hash_values(n)
+    dev = synctree_hip.DeviceTree(W, S)
+    ora = C.OTree(W, S)
+    assert dev.insert_int64(keys, vals) == 0
+    ora.bulk_load_int64(keys, vals)
+    assert dev.top_hash() == ora.top_hash()
+    rng = np.random.default_rng(7)
+    extra = workload.keys_int63(4000, workload.SEED ^ 0x52)
+    seq = n
+    for step in range(120):
+        m = int(rng.integers(1, 17))
+        ks, vs = [], []
+        for _ in range(m):
+            if rng.random() < 0.5:
+                k = int(keys[rng.integers(0, n)])
+            else:
+                k = int(extra[rng.integers(0, len(extra))])
+            seq += 1
+            ks.append(k)
+            vs.append(_val(seq))
+        if rng.random() < 0.2:          # a duplicate key inside the batch: last writer wins
+            ks.append(ks[0])
+            seq += 1
+            vs.append(_val(seq))
+            ks, vs = ks[-16:], vs[-16:]
+        st = dev.insert_batch(ks, vs)
+        assert all(x is None for x in st), st
+        for k, v in zip(ks, vs):
+            ora.insert(k, v)
+        assert dev.top_hash() == ora.top_hash(), 'step %d' % step
+        probe = [ks[0], int(keys[rng.integers(0, n)]), int(extra[rng.integers(0, len(extra))])]
+        assert dev.get_batch(probe) == [ora.get(k) for k in probe]
+        if step % 30 == 29:             # a bulk operation merges the overlay
+            if step % 60 == 29:
+                dev.rehash()
+            else:
+                assert dev.verify()
+            assert dev.top_hash() == ora.top_hash()
+            assert dev.num_entries() == ora.num_entries()
+    # exchange_get of a few segments and a compare against a bulk-built copy
+    segs = sorted({ora.segment_of(int(k)) for k in extra[:20]})
+    assert dev.exchange_get_batch(ora.height + 1, segs) == [ora.node(ora.height + 1, s) for s in segs]
+    for lvl in range(1, ora.height + 2):
+        pa, ha = dev.level_entries(lvl)
+        pb, hb = ora.level_entries(lvl)
+        assert (pa == pb).all() and (ha == hb).all()
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_small_path_corruption_and_notfound():
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip
+    n = 5000
+    keys = workload.keys_int63(n, workload.SEED ^ 0x53)
+    vals = workload.obj_hash_values(n)
+    dev = synctree_hip.DeviceTree()
+    ora = C.OTree()
+    dev.insert_int64(keys, vals)
+    ora.bulk_load_int64(keys, vals)
+    # get on an empty tree: undefined top => notfound
+    empty = synctree_hip.DeviceTree()
+    assert empty.get_batch([1, 2, 3]) == ['notfound'] * 3
+    assert empty.insert_batch([5], [b'x']) == [None]
+    assert empty.get_batch([5, 6]) == [b'x', 'notfound']
+    empty.close()
+    # raw corruption of one segment (a bumped value, no rehash)
+    k0 = int(keys[10])
+    s0 = ora.segment_of(k0)
+    node = ora.node(ora.height + 1, s0)
+    bad = [(node[0][0], bytes([node[0][1][0] ^ 1]) + node[0][1][1:])] + node[1:]
+    dev.store_node(ora.height + 1, s0, bad)
+    ora.store_segment(s0, bad)
+    k1 = int(keys[11])
+    got = dev.insert_batch([k0, k1], [_val(1, 9), _val(2, 9)])
+    exp = [ora.insert(k0, _val(1, 9)), ora.insert(k1, _val(2, 9))]
+    assert got[0] == exp[0] and got[0][0] == 'corrupted'
+    assert got[1] is None and not isinstance(exp[1], tuple)
+    assert dev.get_batch([k0, k1, 12345]) == [ora.get(k0), ora.get(k1), ora.get(12345)]
+    assert dev.top_hash() == ora.top_hash()
+    # a bulk rehash repairs the inner levels; then the segment verifies again
+    dev.rehash()
+    ora.rehash()
+    assert dev.get_batch([k0]) == [ora.get(k0)]
+    assert dev.top_hash() == ora.top_hash()
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_small_path_falls_back_for_big_segments():
+    """A segment larger than the kernel rewrites (1024 entries) takes the bulk
+    path: same results."""
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip
+    n = 40000          # 16 segments of ~2500 entries
+    keys = workload.keys_int63(n, workload.SEED ^ 0x54)
+    vals = workload.obj_hash_values(n)
+    dev = synctree_hip.DeviceTree(16, 16)
+    ora = C.OTree(16, 16)
+    dev.insert_int64(keys, vals)
+    ora.bulk_load_int64(keys, vals)
+    for i in range(20):
+        k = int(keys[i * 7])
+        assert dev.insert_batch([k], [_val(i, 3)]) == [None]
+        ora.insert(k, _val(i, 3))
+        assert dev.top_hash() == ora.top_hash()
+    assert dev.get_batch([int(keys[0]), int(keys[7])]) == [ora.get(int(keys[0])), ora.get(int(keys[7]))]
+    dev.close()

@@ -9,4 +9,4 @@ from riak_ensemble_amd import synctree_hip
 
 a = argparse.Namespace(part_keys=int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000, part_batches=5,
                        part_batch_keys=1_000_000)
-print(bench._bench_partition(synctree_hip, None, a, 0, torch))
+print(bench._bench_partition(synctree_hip, None, torch.device('cuda', 0), a, 0, torch))
