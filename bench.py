@@ -393,7 +393,7 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
         tree_a.compare_device(tb)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    kern = {k: round(tree_a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_frontier', 'cmp_visit', 'cmp_scan', 'cmp_reorder')}
+    kern = {k: round(tree_a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_walk', 'cmp_gather')}
     tree_a.set_timing(False)
     vis, algo = _compare_roofline(tree_a, dt * 1e3)
     t0 = time.perf_counter()

@@ -71,7 +71,7 @@ __device__ __forceinline__ uint64_t record_segment(const uint8_t *p, uint64_t le
         stmd5::init(d);
         stmd5::compress(d, m);
     } else {
-        stmd5::md5_global(p + 1, len - 1, d);
+        stmd5::md5_global_pf(p + 1, len - 1, d);
     }
     const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
     return lo & segmask;
@@ -131,7 +131,7 @@ __device__ __forceinline__ bool verify_segment_ov(const DevTree &t, const Overla
     if (!(et & TAG_PRESENT)) return v.n == 0;
     uint32_t d[4];
     const uint64_t a = v.voff(0);
-    stmd5::md5_global(v.vh + a, v.voff(v.n) - a, d);
+    stmd5::md5_global_pf(v.vh + a, v.voff(v.n) - a, d);
     const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
 }
@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         const SegView v = seg_view(t, ov, s);
         uint32_t d[4];
         const uint64_t a = v.voff(0);
-        stmd5::md5_global(v.vh + a, v.voff(v.n) - a, d);
+        stmd5::md5_global_pf(v.vh + a, v.voff(v.n) - a, d);
         const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;

@@ -143,7 +143,7 @@ __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64
             stmd5::init(d);
             stmd5::compress(d, m);
         } else {
-            stmd5::md5_global(p + 1, len - 1, d);
+            stmd5::md5_global_pf(p + 1, len - 1, d);
         }
         const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
         seg_out[i] = (uint32_t)(lo & segmask);
@@ -325,7 +325,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
                 const uint4 e = t.md5[eslot];
                 good = (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
             }
@@ -338,7 +338,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
                 const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
                 t.md5[slot] = e;
                 t.tag[slot] = TAG_PRESENT;
@@ -640,25 +640,21 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 // ---------------------------------------------------------------------------
 // K3 tree_compare: the level-synchronous diff of compare/3 (exchange,
 // exchange_level, exchange_final: synctree.erl:372-417) of two trees of the
-// same geometry, in three device passes with no host round trip in between:
+// same geometry, in passes with no host round trip in between.
 //
-//  1. k_cmp_frontier (one workgroup): the frontier of every level.  Level 0
-//     compares the two top hashes (exchange_get(0,0) is not verified); at
-//     level L the children of the frontier nodes whose entries differ under
-//     the filter (orddict_delta, riak_ensemble_util.erl:115-141, plus
-//     filter/2, synctree.erl:434-449) form the next frontier, in ascending
-//     bucket order.  Only stored child entries are compared: no hashing.
-//  2. k_cmp_visit (whole grid): every visited node is verified on both sides
-//     against its parent's entry (exchange_get's verified_hashes,
-//     synctree.erl:288-298: the ancestors are visited nodes too), and every
-//     final-level segment pair is merge-joined (exchange_final) by one wave,
-//     which writes its records, ascending by key, to a scratch area it
-//     reserves with one atomic.
-//  3. k_dscan1 scans the per-segment counts on the device; k_cmp_reorder
-//     copies each segment's records to its reference position: AccFun =
-//     Keys ++ Acc over ascending segments (synctree.erl:373-375) => the LAST
-//     frontier segment first, ascending keys within a segment.
-// err: min over (level, bucket, side) of a failed verification — the
+// The frontier is evaluated without a level-by-level loop.  Node (L, b) is
+// visited at level L iff the two top hashes differ (level 0,
+// exchange_get(0,0) is not verified) and, for every level 2 <= k <= L, the
+// two trees' entries of its level-k ancestor differ under the filter
+// (orddict_delta, riak_ensemble_util.erl:115-141, plus filter/2,
+// synctree.erl:434-449) -- exactly the set the reference's level loop reaches,
+// since a child is added to the next frontier iff its parent was visited and
+// its entries differ.  k_cmp_walk evaluates it per node, verifies every
+// visited node on both sides against its parent's entry (exchange_get's
+// verified_hashes, synctree.erl:288-298) and merge-joins every visited
+// segment pair (exchange_final); k_cmp_gather concatenates the per-wave
+// record regions.  Only the entries under visited nodes beyond level H are
+// read.  err: min over (level, bucket, side) of a failed verification -- the
 // reference's first crash in visiting order (local before remote).
 
 __device__ __forceinline__ bool verify_inner_node(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
@@ -681,7 +677,7 @@ __device__ __forceinline__ bool verify_segment(const DevTree &t, uint64_t s) {
     if (!(et & TAG_PRESENT)) return t.seg_off[s] == t.seg_off[s + 1];
     uint32_t d[4];
     const uint64_t v0 = t.seg_voff[s];
-    stmd5::md5_global(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+    stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
     const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
 }
@@ -706,133 +702,14 @@ __device__ __forceinline__ bool entry_differs(uint16_t ta, uint16_t tb, const ui
     return false;
 }
 
-// Exclusive scan of one u32 per thread over a workgroup of up to 1024
-// threads; returns the prefix, sets *total.  wsum: 17 words of LDS.
-__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t *wsum, uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t w = 0; w < nw; w++) { const uint32_t c = wsum[w]; wsum[w] = acc; acc += c; }
-        wsum[16] = acc;
-    }
-    __syncthreads();
-    const uint32_t r = wsum[wave] + x - v;
-    *total = wsum[16];
-    __syncthreads();
-    return r;
-}
-
-// Pass 1.  flist: level L's frontier at flist[base[L] - 1 ..], fcnt[L] its
-// length (levels 1..H+1).  [lo2, hi2): level-2 buckets a segment-range
-// partition owns (its level-1 frontier is cut to them); err is reset here.
-// W == 16: two threads per frontier node, 8 children each, every child entry
-// of both trees loaded before any is compared (one memory round trip per
-// level chunk); other widths loop over the children.
-__device__ __forceinline__ uint64_t child_mask8(const DevTree &A, const DevTree &B, uint64_t s0, uint64_t c0, int filter,
-                                                bool cut, uint64_t lo2, uint64_t hi2) {
-    uint16_t ta[8], tb[8];
-    uint4 x[8], y[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        ta[j] = A.tag[s0 + j];
-        tb[j] = B.tag[s0 + j];
-        x[j] = A.md5[s0 + j];
-        y[j] = B.md5[s0 + j];
-    }
-    uint64_t m = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint64_t c = c0 + j;
-        const bool keep = !cut || (c >= lo2 && c < hi2);
-        if (keep && entry_differs(ta[j], tb[j], x[j], y[j], filter)) m |= 1ull << j;
-    }
-    return m;
-}
-
-__global__ void __launch_bounds__(1024) k_cmp_frontier(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2,
-                                                       uint32_t *flist, uint32_t *fcnt, unsigned long long *err,
-                                                       uint64_t *nfinal, unsigned long long *seg_bytes) {
-    __shared__ uint32_t wsum[17];
-    __shared__ uint32_t n0;
-    const uint32_t tid = threadIdx.x;
-    if (tid < ST_MAXLEV + 2) fcnt[tid] = 0;
-    if (tid == 0) {
-        *err = ~0ull;
-        *seg_bytes = 0;
-        const uint16_t ta = A.tag[0], tb = B.tag[0];
-        bool same = (ta == tb);
-        if (same && (ta & TAG_PRESENT)) {
-            const uint4 x = A.md5[0], y = B.md5[0];
-            same = x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
-        }
-        n0 = same ? 0u : 1u;
-        flist[0] = 0;
-    }
-    __syncthreads();
-    if (tid == 0) fcnt[1] = n0;
-    uint32_t n = n0;
-    const uint32_t W = A.W;
-    const bool w16 = W == 16;
-    const uint32_t per_chunk = w16 ? blockDim.x / 2 : blockDim.x;   // frontier nodes per chunk
-    for (uint32_t L = 1; L <= A.H && n; L++) {
-        const uint32_t *cur = flist + (A.base[L] - 1);
-        uint32_t *nxt = flist + (A.base[L + 1] - 1);
-        const uint64_t cb = A.base[L + 1];
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < n; c0 += per_chunk) {
-            uint64_t mask = 0, cbase = 0;
-            if (w16) {
-                const uint32_t f = c0 + (tid >> 1), h = tid & 1;
-                if (f < n) {
-                    const uint64_t b = cur[f];
-                    cbase = b * 16 + 8 * h;
-                    mask = child_mask8(A, B, cb + cbase, cbase, filter, L == 1, lo2, hi2);
-                }
-            } else {
-                const uint32_t f = c0 + tid;
-                if (f < n) {
-                    const uint64_t b = cur[f];
-                    cbase = b * W;
-                    for (uint32_t j = 0; j < W; j++) {
-                        const uint64_t sl = cb + cbase + j;
-                        const uint16_t ta = A.tag[sl], tb = B.tag[sl];
-                        const uint4 x = A.md5[sl], y = B.md5[sl];
-                        const uint64_t c = cbase + j;
-                        const bool keep = L != 1 || (c >= lo2 && c < hi2);
-                        if (keep && entry_differs(ta, tb, x, y, filter)) mask |= 1ull << j;
-                    }
-                }
-            }
-            uint32_t tot;
-            const uint32_t pos = carry + block_scan_u32((uint32_t)__popcll(mask), wsum, &tot);
-            uint32_t q = 0;
-            while (mask) {
-                const uint32_t j = (uint32_t)(__ffsll((long long)mask) - 1);
-                nxt[pos + q++] = (uint32_t)(cbase + j);
-                mask &= mask - 1;
-            }
-            carry += tot;
-        }
-        n = carry;
-        if (tid == 0) fcnt[L + 1] = n;
-        __syncthreads();   // this level's list is the next level's input
-    }
-    if (tid == 0) *nfinal = fcnt[A.H + 1];
-}
-
 // Per-wave LDS of the segment merge-join: key offsets and key bytes of both
 // segments, and one packed record per slot of the merged key sequence.
 #define CMP_CAP 256     // entries per side handled from LDS (larger: lane 0 walks them)
 #define CMP_KB 4096     // key bytes per side
-__host__ __device__ __forceinline__ uint32_t cmp_merge_lds_bytes() { return (CMP_CAP + 1) * 4 * 2 + CMP_KB * 2 + 2 * CMP_CAP * 4; }
+#define CMP_VB 6144     // value bytes per side (larger: values compared in global memory)
+__host__ __device__ __forceinline__ uint32_t cmp_merge_lds_bytes() {
+    return (CMP_CAP + 1) * 4 * 4 + 2 * CMP_CAP * 4 + CMP_KB * 2 + CMP_VB * 2;
+}
 
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -868,237 +745,522 @@ __device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
     return (uint32_t)__popcll(bal & ((1ull << lane) - 1));
 }
 
+// Wave-cooperative copy of up to 4 byte runs from global memory into LDS:
+// dword loads (the run's first word aligned down; heaps keep >= 64 bytes of
+// slack past their end), every load of an iteration in flight together, so
+// runs up to 1 KB cost one memory round trip.
+__device__ __forceinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t *d0, const uint8_t *s1, uint32_t n1,
+                                           uint8_t *d1, const uint8_t *s2, uint32_t n2, uint8_t *d2, const uint8_t *s3,
+                                           uint32_t n3, uint8_t *d3) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint8_t *src[4] = {s0, s1, s2, s3};
+    uint8_t *dst[4] = {d0, d1, d2, d3};
+    const uint32_t len[4] = {n0, n1, n2, n3};
+    uint32_t mx = n0 > n1 ? n0 : n1;
+    mx = mx > n2 ? mx : n2;
+    mx = mx > n3 ? mx : n3;
+    for (uint32_t q0 = 0; q0 < mx + 3; q0 += 1024) {
+        uint32_t x[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(src[r]);
+            const uint32_t mis = (uint32_t)(a & 3);
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(a - mis);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t idx = q0 / 4 + u * 64 + lane;
+                x[r][u] = (4 * idx < len[r] + mis) ? w[idx] : 0u;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(src[r]) & 3);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t idx = q0 / 4 + u * 64 + lane;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int p = (int)(4 * idx + k) - (int)mis;
+                    if (p >= 0 && (uint32_t)p < len[r]) dst[r][p] = (uint8_t)(x[r][u] >> (8 * k));
+                }
+            }
+        }
+    }
+}
+
 // exchange_final for one segment pair (orddict_delta + filter), one wave:
-// writes the pair's records in ascending key order to scratch space it
-// reserves with one atomicAdd on *ctr (records past cap are counted, not
-// written: the host grows the buffer and runs the compare again) and returns
-// (count, scratch offset).  Record kinds: 0 = {K,{A,B}}, 1 = {K,{A,'$none'}},
+// writes the pair's records in ascending key order to out[base..] (records
+// at or past lim are counted, not written: the host grows the buffer and
+// runs the compare again) and returns their count.  Record kinds: 0 = {K,{A,B}}, 1 = {K,{A,'$none'}},
 // 2 = {K,{'$none',B}}.
 __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint8_t *lds,
-                                   DiffRec *out, uint64_t cap, unsigned long long *ctr, uint64_t *base_out) {
+                                   DiffRec *out, uint64_t base, uint64_t lim, uint64_t *algo_bytes) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t a0 = A.seg_off[s], a1 = A.seg_off[s + 1], b0 = B.seg_off[s], b1 = B.seg_off[s + 1];
+    const uint64_t va0 = A.seg_voff[s], va1 = A.seg_voff[s + 1], vb0 = B.seg_voff[s], vb1 = B.seg_voff[s + 1];
     const uint64_t nA = a1 - a0, nB = b1 - b0;
-    const uint64_t ka0 = A.koff[a0], kb0 = B.koff[b0];
-    const uint64_t bytesA = A.koff[a1] - ka0, bytesB = B.koff[b1] - kb0;
-    if (nA <= CMP_CAP && nB <= CMP_CAP && bytesA <= CMP_KB && bytesB <= CMP_KB) {
-        uint32_t *ao = reinterpret_cast<uint32_t *>(lds);
+    // algorithmic bytes of this segment pair (bench roofline): per side the
+    // offsets, key records, values and the parent's entry (key bytes added below)
+    *algo_bytes = 2 * (16 + 16 + 18) + 16 * (nA + nB + 2) + (va1 - va0) + (vb1 - vb0);
+    if (nA <= CMP_CAP && nB <= CMP_CAP) {
+        uint32_t *ao = reinterpret_cast<uint32_t *>(lds);    // key offsets (low 32 bits, relative after the copy)
         uint32_t *bo = ao + CMP_CAP + 1;
-        uint8_t *ak = reinterpret_cast<uint8_t *>(bo + CMP_CAP + 1);
+        uint32_t *avo = bo + CMP_CAP + 1;                     // value offsets
+        uint32_t *bvo = avo + CMP_CAP + 1;
+        uint32_t *ur = bvo + CMP_CAP + 1;
+        uint8_t *ak = reinterpret_cast<uint8_t *>(ur + 2 * CMP_CAP);
         uint8_t *bk = ak + CMP_KB;
-        uint32_t *ur = reinterpret_cast<uint32_t *>(bk + CMP_KB);
-        for (uint64_t i = lane; i <= nA; i += 64) ao[i] = (uint32_t)(A.koff[a0 + i] - ka0);
-        for (uint64_t i = lane; i <= nB; i += 64) bo[i] = (uint32_t)(B.koff[b0 + i] - kb0);
-        for (uint64_t q = lane; q < bytesA; q += 64) ak[q] = A.kheap[ka0 + q];
-        for (uint64_t q = lane; q < bytesB; q += 64) bk[q] = B.kheap[kb0 + q];
-        const uint32_t nu_max = (uint32_t)(nA + nB);
-        for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+        uint8_t *av = bk + CMP_KB;
+        uint8_t *bv = av + CMP_VB;
+        // one round trip: the four offset runs (+ both key bases, broadcast)
+        const uint64_t ka0 = A.koff[a0], kb0 = B.koff[b0];
+        for (uint64_t i = lane; i <= nA; i += 64) { ao[i] = (uint32_t)A.koff[a0 + i]; avo[i] = (uint32_t)(A.voff[a0 + i] - va0); }
+        for (uint64_t i = lane; i <= nB; i += 64) { bo[i] = (uint32_t)B.koff[b0 + i]; bvo[i] = (uint32_t)(B.voff[b0 + i] - vb0); }
         wave_sync_lds();
-        uint64_t cnt = 0;
-        uint32_t mcarry = 0;
-        for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
-            const uint32_t i = c + lane;
-            bool eq = false, emit = false;
-            uint32_t rb = 0;
-            if (i < nA) {
-                rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
-                if (eq) {
-                    const uint64_t x = a0 + i, y = b0 + rb;
-                    emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
-                                     B.voff[y + 1] - B.voff[y]);
-                } else {
-                    emit = filter != 1;
+        const uint32_t bytesA = ao[nA] - (uint32_t)ka0, bytesB = bo[nB] - (uint32_t)kb0;
+        *algo_bytes += (uint64_t)bytesA + bytesB;
+        const uint64_t vA = va1 - va0, vB = vb1 - vb0;
+        const bool vl = vA <= CMP_VB && vB <= CMP_VB;   // values staged too
+        if (bytesA <= CMP_KB && bytesB <= CMP_KB) {
+            for (uint64_t i = lane; i <= nA; i += 64) ao[i] -= (uint32_t)ka0;
+            for (uint64_t i = lane; i <= nB; i += 64) bo[i] -= (uint32_t)kb0;
+            // one round trip: key bytes and value bytes of both sides
+            wave_copy4(A.kheap + ka0, bytesA, ak, B.kheap + kb0, bytesB, bk, A.vheap + va0, vl ? (uint32_t)vA : 0u, av,
+                       B.vheap + vb0, vl ? (uint32_t)vB : 0u, bv);
+            const uint32_t nu_max = (uint32_t)(nA + nB);
+            for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+            wave_sync_lds();
+            uint64_t cnt = 0;
+            uint32_t mcarry = 0;
+            for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
+                const uint32_t i = c + lane;
+                bool eq = false, emit = false;
+                uint32_t rb = 0;
+                if (i < nA) {
+                    rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
+                    if (eq) {
+                        if (vl) {
+                            emit = lds_rec_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
+                        } else {
+                            const uint64_t x = a0 + i, y = b0 + rb;
+                            emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
+                                             B.voff[y + 1] - B.voff[y]);
+                        }
+                    } else {
+                        emit = filter != 1;
+                    }
                 }
+                const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+                mcarry += (uint32_t)__popcll(__ballot(eq));
+                cnt += (uint32_t)__popcll(__ballot(emit));
+                if (emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
             }
-            const uint32_t m = mcarry + wave_prefix_count(eq, lane);
-            mcarry += (uint32_t)__popcll(__ballot(eq));
-            cnt += (uint32_t)__popcll(__ballot(emit));
-            if (emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
-        }
-        mcarry = 0;
-        for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
-            const uint32_t j = c + lane;
-            bool eq = false, emit = false;
-            uint32_t ra = 0;
-            if (j < nB) {
-                ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
-                emit = !eq && filter != 2;
+            mcarry = 0;
+            for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
+                const uint32_t j = c + lane;
+                bool eq = false, emit = false;
+                uint32_t ra = 0;
+                if (j < nB) {
+                    ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
+                    emit = !eq && filter != 2;
+                }
+                const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+                mcarry += (uint32_t)__popcll(__ballot(eq));
+                cnt += (uint32_t)__popcll(__ballot(emit));
+                if (emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
             }
-            const uint32_t m = mcarry + wave_prefix_count(eq, lane);
-            mcarry += (uint32_t)__popcll(__ballot(eq));
-            cnt += (uint32_t)__popcll(__ballot(emit));
-            if (emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
+            wave_sync_lds();
+            uint64_t pos = base;
+            for (uint32_t c = 0; c < nu_max && cnt; c += 64) {   // union slots in key order -> records
+                const uint32_t u = c + lane;
+                const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
+                const bool e = r != 0xffffffffu;
+                const uint64_t p = pos + wave_prefix_count(e, lane);
+                if (e && p < lim) {
+                    DiffRec d;
+                    const uint32_t kind = r >> 30, x = (r >> 15) & 0x7fffu, y = r & 0x7fffu;
+                    d.kind = kind;
+                    d.pad = 0;
+                    d.seg = s;
+                    d.a = kind == 2 ? ~0ull : a0 + x;
+                    d.b = kind == 1 ? ~0ull : b0 + y;
+                    out[p] = d;
+                }
+                pos += (uint32_t)__popcll(__ballot(e));
+            }
+            wave_sync_lds();
+            return cnt;
         }
-        uint64_t base = 0;
-        if (lane == 0 && cnt) base = atomicAdd(ctr, (unsigned long long)cnt);
-        base = __shfl(base, 0, 64);
-        *base_out = base;
+        *algo_bytes -= (uint64_t)bytesA + bytesB;   // counted again below
         wave_sync_lds();
-        uint64_t pos = base;
-        for (uint32_t c = 0; c < nu_max && cnt; c += 64) {   // union slots in key order -> records
-            const uint32_t u = c + lane;
-            const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
-            const bool e = r != 0xffffffffu;
-            const uint64_t p = pos + wave_prefix_count(e, lane);
-            if (e && p < cap) {
-                DiffRec d;
-                const uint32_t kind = r >> 30, x = (r >> 15) & 0x7fffu, y = r & 0x7fffu;
-                d.kind = kind;
-                d.pad = 0;
-                d.seg = s;
-                d.a = kind == 2 ? ~0ull : a0 + x;
-                d.b = kind == 1 ? ~0ull : b0 + y;
-                out[p] = d;
-            }
-            pos += (uint32_t)__popcll(__ballot(e));
-        }
-        return cnt;
     }
-    // oversized segments: lane 0 walks the two key lists (count, reserve, write)
-    uint64_t c = 0, base = 0;
+    *algo_bytes += (A.koff[a1] - A.koff[a0]) + (B.koff[b1] - B.koff[b0]);
+    // oversized segments: lane 0 walks the two key lists
+    uint64_t c = 0;
     if (lane == 0) {
-        for (int pass = 0; pass < 2; pass++) {
-            uint64_t x = a0, y = b0, pos = base;
-            while (x < a1 || y < b1) {
-                int cmp;
-                if (x < a1 && y < b1)
-                    cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y],
-                                  B.koff[y + 1] - B.koff[y]);
-                else
-                    cmp = x < a1 ? -1 : 1;
-                DiffRec r;
-                r.seg = s;
-                r.pad = 0;
-                bool emit;
-                if (cmp < 0) {
-                    r.a = x; r.b = ~0ull; r.kind = 1;
-                    emit = filter != 1;
-                    x++;
-                } else if (cmp > 0) {
-                    r.a = ~0ull; r.b = y; r.kind = 2;
-                    emit = filter != 2;
-                    y++;
-                } else {
-                    emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
-                                     B.voff[y + 1] - B.voff[y]);
-                    r.a = x; r.b = y; r.kind = 0;
-                    x++; y++;
-                }
-                if (emit) {
-                    if (pass == 1 && pos < cap) out[pos] = r;
-                    pos++;
-                    if (pass == 0) c++;
-                }
+        uint64_t x = a0, y = b0;
+        while (x < a1 || y < b1) {
+            int cmp;
+            if (x < a1 && y < b1)
+                cmp = rec_cmp(A.kheap + A.koff[x], A.koff[x + 1] - A.koff[x], B.kheap + B.koff[y], B.koff[y + 1] - B.koff[y]);
+            else
+                cmp = x < a1 ? -1 : 1;
+            DiffRec r;
+            r.seg = s;
+            r.pad = 0;
+            bool emit;
+            if (cmp < 0) {
+                r.a = x; r.b = ~0ull; r.kind = 1;
+                emit = filter != 1;
+                x++;
+            } else if (cmp > 0) {
+                r.a = ~0ull; r.b = y; r.kind = 2;
+                emit = filter != 2;
+                y++;
+            } else {
+                emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
+                                 B.voff[y + 1] - B.voff[y]);
+                r.a = x; r.b = y; r.kind = 0;
+                x++; y++;
             }
-            if (pass == 0 && c) base = atomicAdd(ctr, (unsigned long long)c);
-            if (!c) break;
+            if (emit) {
+                if (base + c < lim) out[base + c] = r;
+                c++;
+            }
         }
     }
-    *base_out = __shfl(base, 0, 64);
     return __shfl(c, 0, 64);
 }
 
-// Pass 2: verify every visited node (lane per node and side, all levels; the
-// first waves), then merge-join each final segment pair (wave per segment,
-// assigned from the last wave down so the verifying waves get none when
-// there are fewer segments than waves) into scratch + dcnt/soff.
-__global__ void __launch_bounds__(256) k_cmp_visit(DevTree A, DevTree B, int filter, const uint32_t *flist,
-                                                  const uint32_t *fcnt, uint64_t *dcnt, uint64_t *soff, DiffRec *scratch,
-                                                  uint64_t cap, unsigned long long *ctr, unsigned long long *err,
-                                                  uint32_t slice, unsigned long long *seg_bytes) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint8_t *wl = lds + (uint64_t)wave * slice;
-    const uint32_t L1 = A.H + 1;
-    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave, nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint64_t nv = 0;
-    for (uint32_t L = 1; L <= L1; L++) nv += fcnt[L];
-    uint8_t *reg = wl + lane * lane_region_bytes(A.W);
-    for (uint64_t g = gwave * 64 + lane; g < 2 * nv; g += nwaves * 64) {
-        uint64_t k = g >> 1;
-        const uint32_t side = (uint32_t)(g & 1);
-        uint32_t L = 1;
-        while (k >= fcnt[L]) { k -= fcnt[L]; L++; }
-        const uint64_t b = flist[A.base[L] - 1 + k];
-        bool good;
-        if (side) good = L == L1 ? verify_segment(B, b) : verify_inner_node(B, L, b, reg);
-        else good = L == L1 ? verify_segment(A, b) : verify_inner_node(A, L, b, reg);
-        if (!good) atomicMin(err, err_code(L, b, side));
+// LDS of a compare-walk wave: the shared area (lane regions for inner-node
+// staging / the merge-join), then the work list, then per-level counters
+#define CMP_LIST 256
+__host__ __device__ __forceinline__ uint32_t cmp_shared_bytes(uint32_t W) {
+    const uint32_t a = 64 * lane_region_bytes(W), m = cmp_merge_lds_bytes();
+    return ((a > m ? a : m) + 15) & ~15u;
+}
+__host__ __device__ __forceinline__ uint32_t cmp_slice_bytes(uint32_t W) {
+    return cmp_shared_bytes(W) + CMP_LIST * 8 + ST_MAXLEV * 8;
+}
+
+// Does the level-k entry `anc` differ between the trees under the filter (and,
+// at level 2, lie in the partition's bucket range [lo2, hi2))?
+__device__ __forceinline__ bool cmp_entry_in(const DevTree &A, const DevTree &B, int filter, uint32_t k, uint64_t anc,
+                                             uint64_t lo2, uint64_t hi2) {
+    const uint64_t slot = A.base[k] + anc;
+    if (k == 2 && (anc < lo2 || anc >= hi2)) return false;
+    return entry_differs(A.tag[slot], B.tag[slot], A.md5[slot], B.md5[slot], filter);
+}
+
+// Is inner node (L, b) visited, given that the top hashes differ?  Every
+// ancestor entry at levels L..2 differs (deepest first: the most selective).
+__device__ __forceinline__ bool cmp_visited(const DevTree &A, const DevTree &B, int filter, uint32_t L, uint64_t b,
+                                            uint64_t lo2, uint64_t hi2) {
+    for (uint32_t k = L; k >= 2; k--)
+        if (!cmp_entry_in(A, B, filter, k, b >> (A.shift * (L - k)), lo2, hi2)) return false;
+    return true;
+}
+
+// The whole compare walk in one launch, a fixed grid of nw waves.  Wave w
+// owns the level-H nodes [w*P, (w+1)*P) (P = ceil(nodes(H) / nw)), the
+// segments under them and every inner node whose first level-H descendant
+// it owns.  Per 64 of its level-H nodes (highest first) it
+//  * evaluates the frontier top-down over the levels 2..H covering them (a
+//    lane per node, the parent's flag by a shuffle: one memory round trip per
+//    level) and lists its visited inner nodes;
+//  * checks the children of the visited level-H nodes (a lane per child,
+//    64 / W nodes per round trip) and lists the visited segments, highest
+//    first;
+//  * flushes the list: every listed node / segment is verified on both sides
+//    at once (a lane per item and side: the MD5 chains run side by side), then
+//    the segment pairs are merge-joined in list order into the wave's own
+//    scratch region [w*R, (w+1)*R).  AccFun = Keys ++ Acc over ascending
+//    segments (synctree.erl:373-375) => the wave's records are already in
+//    reference order, and the regions concatenate from the highest wave down.
+// Per-wave outputs: wcnt[w] records, wst[w*ST_STATW + l] visited nodes per
+// level, wbytes[w] algorithmic bytes of its segment pairs; *need = max
+// records of a wave that overflowed R.  No same-address atomics on the
+// success path.
+#define ST_STATW (ST_MAXLEV + 2)
+
+struct CmpWalk {
+    uint8_t *shared;       // lane regions / merge area
+    uint64_t *list;        // (level << 56) | index
+    uint32_t *cnt;         // visited per level
+    DiffRec *scratch;
+    uint64_t rb, lim, pos, bytes;
+    int filter;
+    uint64_t errmin;       // this lane's first failed verification (err_code), ~0 if none
+    uint64_t *stamp;       // diagnostic: this wave's 8 phase stamps, or null
+};
+#define CW_STAMP(c, k) do { if ((c).stamp && (threadIdx.x & 63) == 0) (c).stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    wave_sync_lds();
-    const uint64_t nf = fcnt[L1];
-    const uint32_t *seg = flist + (A.base[L1] - 1);
-    for (uint64_t i = nwaves - 1 - gwave; i < nf; i += nwaves) {
-        const uint64_t s = seg[i];
-        uint64_t base;
-        const uint64_t c = seg_merge_wave(A, B, s, filter, wl, scratch, cap, ctr, &base);
-        if (lane == 0) {
-            dcnt[i] = c;
-            soff[i] = base;
-            // algorithmic bytes of this segment pair (bench roofline): per side the
-            // offsets, key records, values and the parent's entry
-            const uint64_t na = A.seg_off[s + 1] - A.seg_off[s], nb = B.seg_off[s + 1] - B.seg_off[s];
-            const uint64_t by = 2 * (16 + 16 + 18) + 16 * (na + nb + 2) +
-                                (A.koff[A.seg_off[s + 1]] - A.koff[A.seg_off[s]]) +
-                                (B.koff[B.seg_off[s + 1]] - B.koff[B.seg_off[s]]) + (A.seg_voff[s + 1] - A.seg_voff[s]) +
-                                (B.seg_voff[s + 1] - B.seg_voff[s]);
-            atomicAdd(seg_bytes, (unsigned long long)by);
+    return x - v;
+}
+
+// Verify the listed items on both sides, then merge-join the listed segments.
+// Verification: a lane per (item, side); each message -- an inner node's
+// child entries (stage_inner) or a segment's value run (copied by the whole
+// wave, coalesced) -- is staged in the shared LDS area first, so every lane
+// runs the same md5_lds chain; runs that do not fit are hashed from global
+// memory.
+__device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, CmpWalk &c, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t L1 = A.H + 1;
+    const uint32_t SH = cmp_shared_bytes(A.W);
+    for (uint32_t k0 = 0; k0 < 2 * n; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool act = k < 2 * n;
+        const uint64_t it = act ? c.list[k >> 1] : 0;
+        const uint32_t l = (uint32_t)(it >> 56), side = k & 1;
+        const uint64_t b = it & ((1ull << 56) - 1);
+        const bool inner = act && l < L1, seg = act && l == L1;
+        const uint32_t isz = inner ? lane_region_bytes(A.W) : 0;
+        const uint32_t ioff = wave_excl_scan(isz);
+        const uint32_t itot = __shfl(ioff + isz, 63, 64);
+        uint16_t et = 0;
+        uint4 e = make_uint4(0, 0, 0, 0);
+        uint64_t v0 = 0, len = 0;
+        bool empty = false;
+        if (act) {
+            const uint64_t eslot = (l == 1) ? 0 : A.base[l] + b;
+            if (side) { et = B.tag[eslot]; e = B.md5[eslot]; } else { et = A.tag[eslot]; e = A.md5[eslot]; }
+        }
+        if (seg) {
+            if (side) { v0 = B.seg_voff[b]; len = B.seg_voff[b + 1] - v0; empty = B.seg_off[b] == B.seg_off[b + 1]; }
+            else      { v0 = A.seg_voff[b]; len = A.seg_voff[b + 1] - v0; empty = A.seg_off[b] == A.seg_off[b + 1]; }
+        }
+        // inner nodes: the child entries, loaded while the loads above are in flight
+        uint32_t mlen = 0;
+        if (inner) mlen = side ? stage_inner(B, l, b, c.shared + ioff) : stage_inner(A, l, b, c.shared + ioff);
+        const uint32_t ssz = seg ? (uint32_t)(len + 64 + 15 < SH ? ((len + 64 + 15) & ~15ull) : SH + 16) : 0;
+        const uint32_t soff = itot + wave_excl_scan(ssz);
+        const bool sfit = seg && (et & TAG_PRESENT) && soff + ssz <= SH;
+        // the fitting value runs, four per round trip
+        for (uint64_t m = __ballot(sfit); m;) {
+            const uint8_t *sp[4] = {nullptr, nullptr, nullptr, nullptr};
+            uint8_t *dp[4] = {c.shared, c.shared, c.shared, c.shared};
+            uint32_t ln[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                if (!m) break;
+                const int j = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                sp[r] = (__shfl((int)side, j, 64) ? B.vheap : A.vheap) + __shfl(v0, j, 64);
+                ln[r] = (uint32_t)__shfl(len, j, 64);
+                dp[r] = c.shared + __shfl(soff, j, 64);
+            }
+            wave_copy4(sp[0], ln[0], dp[0], sp[1], ln[1], dp[1], sp[2], ln[2], dp[2], sp[3], ln[3], dp[3]);
+        }
+        wave_sync_lds();
+        CW_STAMP(c, 7);
+        if (act) {
+            bool ok;
+            if (!(et & TAG_PRESENT)) {
+                ok = inner ? (mlen == 0) : empty;
+            } else {
+                uint32_t d[4];
+                if (inner) stmd5::md5_lds(c.shared + ioff, mlen, d);
+                else if (sfit) stmd5::md5_lds(c.shared + soff, (uint32_t)len, d);
+                else stmd5::md5_global_pf((side ? B.vheap : A.vheap) + v0, len, d);
+                ok = et == TAG_PRESENT && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+            }
+            if (!ok) {
+                const uint64_t ec = err_code(l, b, side);
+                if (ec < c.errmin) c.errmin = ec;
+            }
         }
         wave_sync_lds();
     }
-}
-
-// Exclusive scan of n = *n_ptr (read on the device) uint64 values in ONE
-// workgroup: thread t scans its contiguous range; *total receives the sum.
-__device__ __forceinline__ uint64_t block_scan_u64(uint64_t v, uint64_t *wsum, uint64_t *total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    uint64_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
+    CW_STAMP(c, 3);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t it = c.list[i];
+        if ((uint32_t)(it >> 56) != L1) continue;
+        const uint64_t sj = it & ((1ull << 56) - 1);
+        uint64_t by;
+        c.pos += seg_merge_wave(A, B, sj, c.filter, c.shared, c.scratch, c.rb + c.pos, c.lim, &by);
+        c.bytes += by;
+        wave_sync_lds();
     }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t acc = 0;
-        for (uint32_t w = 0; w < nw; w++) { const uint64_t c = wsum[w]; wsum[w] = acc; acc += c; }
-        wsum[16] = acc;
-    }
-    __syncthreads();
-    const uint64_t r = wsum[wave] + x - v;
-    *total = wsum[16];
-    __syncthreads();
-    return r;
+    CW_STAMP(c, 4);
 }
 
-__global__ void __launch_bounds__(1024) k_dscan1(const uint64_t *in, uint64_t *out, const uint64_t *n_ptr, uint64_t *total) {
-    __shared__ uint64_t wsum[17];
-    const uint64_t n = *n_ptr;
-    const uint64_t per = (n + blockDim.x - 1) / blockDim.x;
-    const uint64_t lo = (uint64_t)threadIdx.x * per, hi = lo + per < n ? lo + per : n;
-    uint64_t s = 0;
-    for (uint64_t i = lo; i < hi; i++) s += in[i];
-    uint64_t tot;
-    uint64_t acc = block_scan_u64(s, wsum, &tot);
-    for (uint64_t i = lo; i < hi; i++) { const uint64_t v = in[i]; out[i] = acc; acc += v; }
-    if (threadIdx.x == 0) *total = tot;
-}
-
-// Pass 3b: each final segment's records from scratch to their reference
-// position total - doff[i] - dcnt[i] (wave per segment, lane per record).
-__global__ void __launch_bounds__(256) k_cmp_reorder(const uint32_t *fcnt, uint32_t L1, const uint64_t *dcnt,
-                                                    const uint64_t *doff, const uint64_t *soff, const uint64_t *total,
-                                                    const DiffRec *scratch, DiffRec *out, uint64_t cap) {
+// append the ballot's lanes (item value per lane) to the list
+__device__ __forceinline__ void cmp_append(uint64_t *list, uint32_t &n, bool f, uint64_t item) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t nf = fcnt[L1], tot = *total;
-    if (tot > cap) return;
-    for (uint64_t i = gwave; i < nf; i += nwaves) {
-        const uint64_t c = dcnt[i], src = soff[i], dst = tot - doff[i] - c;
-        for (uint64_t k = lane; k < c; k += 64) out[dst + k] = scratch[src + k];
+    const uint64_t m = __ballot(f);
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (f) list[n + __popcll(m & below)] = item;
+    n += (uint32_t)__popcll(m);
+}
+
+__global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2, uint32_t nw,
+                                                 uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *wcnt,
+                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (w >= nw) return;
+    uint8_t *wl = lds + (uint64_t)wave * slice;
+    const uint32_t H = A.H, L1 = H + 1, sh = A.shift, W = A.W;
+    CmpWalk c;
+    c.stamp = stamps ? stamps + (uint64_t)w * 8 : nullptr;
+    CW_STAMP(c, 0);
+    c.shared = wl;
+    c.list = reinterpret_cast<uint64_t *>(wl + cmp_shared_bytes(W));
+    c.cnt = reinterpret_cast<uint32_t *>(c.list + CMP_LIST);
+    c.scratch = scratch;
+    c.rb = (uint64_t)w * R;
+    c.lim = c.rb + R;
+    c.pos = 0;
+    c.bytes = 0;
+    c.filter = filter;
+    c.errmin = ~0ull;
+    for (uint32_t l = lane; l < ST_STATW; l += 64) c.cnt[l] = 0;
+    bool topdiff;
+    {
+        const uint16_t ta = A.tag[0], tb = B.tag[0];
+        topdiff = ta != tb;
+        if (!topdiff && (ta & TAG_PRESENT)) {
+            const uint4 x = A.md5[0], y = B.md5[0];
+            topdiff = x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+        }
     }
+    const uint64_t nH = A.base[L1] - A.base[H];   // level-H nodes
+    const uint64_t P = (nH + nw - 1) / nw;
+    const uint64_t h0 = (uint64_t)w * P < nH ? (uint64_t)w * P : nH;
+    const uint64_t h1 = h0 + P < nH ? h0 + P : nH;
+    uint32_t n = 0;
+    wave_sync_lds();
+    if (topdiff && h1 > h0) {
+        if (h0 == 0 && H >= 1) {   // the root (level 1) belongs to wave 0
+            cmp_append(c.list, n, lane == 0, (1ull << 56));
+            if (lane == 0) c.cnt[1] += 1;
+        }
+        for (uint64_t c0 = h0 + ((h1 - h0 - 1) & ~63ull);; c0 -= 64) {
+            const uint64_t c1 = c0 + 64 < h1 ? c0 + 64 : h1;   // level-H nodes [c0, c1)
+            bool f = true;       // this lane's node flag at the previous level (level 1: the root)
+            for (uint32_t l = 2; l <= H; l++) {
+                const uint32_t up = sh * (H - l);
+                const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
+                const uint64_t b = lo + lane;
+                const uint64_t plo = lo >> sh;
+                const uint32_t plane = (uint32_t)((b >> sh) - plo);
+                const bool fp = __shfl((int)f, (int)(plane < 64 ? plane : 0), 64) != 0;
+                f = b <= hi && fp && cmp_entry_in(A, B, filter, l, b, lo2, hi2);
+                const bool owned = f && (b << up) >= c0 && (b << up) < c1;
+                if (n + 64 > CMP_LIST) { cmp_flush(A, B, c, n); n = 0; }
+                const uint32_t n0 = n;
+                cmp_append(c.list, n, owned, ((uint64_t)l << 56) | b);
+                if (lane == 0) c.cnt[l] += n - n0;
+            }
+            CW_STAMP(c, 1);
+            // f: flags of the level-H nodes c0 + lane
+            uint64_t vm = __ballot(f && c0 + lane < c1);
+            const uint32_t G = 64 / W;   // level-H nodes per children round trip
+            while (vm) {
+                // the next G visited nodes, highest first: lane -> (node, child)
+                const uint32_t g = lane / W, ch = lane % W;
+                uint64_t x = vm;
+                uint32_t j = 64;
+                for (uint32_t q = 0; q <= g && x; q++) {
+                    j = 63 - __clzll(x);
+                    x &= ~(1ull << j);
+                    if (q != g) j = 64;
+                }
+                uint32_t taken = 0;
+                for (uint32_t q = 0; q < G && vm; q++) { vm &= ~(1ull << (63 - __clzll(vm))); taken++; }
+                const bool have = g < taken && j < 64;
+                const uint64_t s = ((c0 + j) << sh) + (W - 1 - ch);   // children highest first
+                const bool in = have && cmp_entry_in(A, B, filter, L1, s, lo2, hi2);
+                if (n + 64 > CMP_LIST) { cmp_flush(A, B, c, n); n = 0; }
+                const uint32_t n0 = n;
+                cmp_append(c.list, n, in, ((uint64_t)L1 << 56) | s);
+                if (lane == 0) c.cnt[L1] += n - n0;
+            }
+            if (c0 == h0) break;
+        }
+        CW_STAMP(c, 2);
+        if (n) cmp_flush(A, B, c, n);
+    }
+    wave_sync_lds();
+    CW_STAMP(c, 5);
+    if (c.stamp && lane == 0) c.stamp[6] = c.cnt[L1];
+    uint64_t em = c.errmin;
+    for (int o = 32; o; o >>= 1) {
+        const uint64_t y = __shfl_xor(em, o, 64);
+        em = y < em ? y : em;
+    }
+    if (lane == 0) {
+        wcnt[w] = c.pos;
+        wbytes[w] = c.bytes;
+        werr[w] = em;
+    }
+    for (uint32_t l = lane; l < ST_STATW; l += 64) wst[(uint64_t)w * ST_STATW + l] = (l >= 1 && l <= L1) ? c.cnt[l] : 0;
+}
+
+// The waves' regions -> the record buffer (wave w after every higher wave).
+// Wave 0 also reduces the per-wave results into res (host-mapped): the
+// total, the largest per-wave count (the scratch a rerun needs when it
+// exceeds R) and the first failed verification.  A wave per region.
+__global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
+                                                   const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
+                                                   uint64_t *res) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nw) return;
+    uint64_t above = 0;
+    for (uint32_t v0 = w + 1; v0 < nw; v0 += 1024) {   // 16 loads per lane in flight
+        uint64_t x[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const uint32_t v = v0 + u * 64 + lane;
+            x[u] = v < nw ? wcnt[v] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) above += x[u];
+    }
+    for (int o = 32; o; o >>= 1) above += __shfl_xor(above, o, 64);
+    const uint64_t n = wcnt[w];
+    if (w == 0) {
+        uint64_t mx = 0, em = ~0ull;
+        for (uint32_t v0 = 0; v0 < nw; v0 += 512) {
+            uint64_t x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t v = v0 + u * 64 + lane;
+                x[u] = v < nw ? wcnt[v] : 0;
+                y[u] = v < nw ? werr[v] : ~0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                mx = x[u] > mx ? x[u] : mx;
+                em = y[u] < em ? y[u] : em;
+            }
+        }
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t x = __shfl_xor(mx, o, 64), y = __shfl_xor(em, o, 64);
+            mx = x > mx ? x : mx;
+            em = y < em ? y : em;
+        }
+        if (lane == 0) {
+            res[0] = above + n;
+            res[1] = mx;
+            res[2] = em;
+            __threadfence_system();
+        }
+    }
+    if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
+    const DiffRec *src = scratch + (uint64_t)w * R;
+    for (uint64_t k = lane; k < n; k += 64) out[above + k] = src[k];
 }
 
 // Diff records -> byte lengths of key / local value / remote value

@@ -40,9 +40,11 @@ static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past 
     } while (0)
 
 struct CmpWork {
-    uint32_t *flist = nullptr, *fcnt = nullptr;
-    unsigned long long *err = nullptr, *seg_bytes = nullptr, *ctr = nullptr;
-    uint64_t *dcnt = nullptr, *doff = nullptr, *soff = nullptr, *tot = nullptr;
+    uint32_t nw = 0;                 // waves of the compare walk (fixed grid)
+    uint64_t R = 0;                  // scratch records per wave
+    uint64_t *wcnt = nullptr, *wbytes = nullptr, *werr = nullptr;
+    uint32_t *wst = nullptr;         // [nw][ST_STATW] visited nodes per level
+    uint64_t *res = nullptr, *res_dev = nullptr;   // host-mapped: total, max per-wave count, first error
     DiffRec *rec = nullptr, *scratch = nullptr;
     uint64_t cap = 0;
 };
@@ -54,6 +56,7 @@ struct Pending {
 
 struct st_tree {
     int device = 0;
+    int ncu = 256;   // compute units of the device (fixed-grid kernels)
     hipStream_t own_stream = nullptr, stream = nullptr;
     uint64_t W = 16, S = 1 << 20;
     uint32_t shift = 4, H = 5;
@@ -274,6 +277,8 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
         return ST_EDEVICE;
     }
     t->stream = t->own_stream;
+    if (hipDeviceGetAttribute(&t->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || t->ncu <= 0)
+        t->ncu = 256;
     if (hipHostMalloc((void **)&t->pin, 64 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
         g_err = "hipHostMalloc failed";
         t->pin = nullptr;
@@ -318,15 +323,15 @@ extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.flist, t->cw.fcnt, t->cw.err,
-                  t->cw.dcnt, t->cw.doff, t->cw.soff, t->cw.tot, t->cw.rec, t->cw.scratch, t->cw.seg_bytes,
-                  t->cw.ctr, t->mail};
+                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     dfree(t, t->ov.idx);
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
     if (t->pin) (void)hipHostFree(t->pin);
     if (t->sout) (void)hipHostFree(t->sout);
+    if (t->cw.res) (void)hipHostFree(t->cw.res);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -1688,32 +1693,46 @@ extern "C" int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype,
 }
 
 // ------------------------------------------------------------------ compare (K3)
+static uint32_t cmp_slice(const st_tree *t) { return cmp_slice_bytes((uint32_t)t->W); }
+static const uint32_t CMP_WPG = 4;   // waves per compare-walk workgroup
+
 static int ensure_cmp_work(st_tree *t) {
     CmpWork &w = t->cw;
-    if (w.flist) return ST_OK;
-    CHK(dalloc_t(t, &w.flist, t->nslots));
-    CHK(dalloc_t(t, &w.fcnt, ST_MAXLEV + 2));
-    CHK(dalloc_t(t, &w.err, 1));
-    CHK(dalloc_t(t, &w.seg_bytes, 1));
-    CHK(dalloc_t(t, &w.ctr, 1));
-    CHK(dalloc_t(t, &w.dcnt, t->S + 1));
-    CHK(dalloc_t(t, &w.doff, t->S + 1));
-    CHK(dalloc_t(t, &w.soff, t->S + 1));
-    CHK(dalloc_t(t, &w.tot, 8));
+    if (w.wcnt) return ST_OK;
+    const uint32_t per_cu = std::max<uint32_t>(1, (160 * 1024) / (CMP_WPG * cmp_slice(t)));
+    w.nw = (uint32_t)std::max(1, t->ncu) * per_cu * CMP_WPG;
+    CHK(dalloc_t(t, &w.wcnt, w.nw));
+    CHK(dalloc_t(t, &w.wbytes, w.nw));
+    CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
+    CHK(dalloc_t(t, &w.werr, w.nw));
+    if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped) != hipSuccess) {
+        w.res = nullptr;
+        g_err = "hipHostMalloc failed";
+        return ST_EDEVICE;
+    }
+    HIPCHK(hipHostGetDevicePointer((void **)&w.res_dev, w.res, 0));
     return ST_OK;
 }
 
-static int grow_records(st_tree *t, uint64_t need) {
+// record buffer >= cap records, scratch >= nw * R records
+static int grow_records(st_tree *t, uint64_t cap, uint64_t R) {
     CmpWork &w = t->cw;
-    if (need <= w.cap) return ST_OK;
-    dfree(t, w.rec);
-    dfree(t, w.scratch);
-    w.rec = w.scratch = nullptr;
-    w.cap = 0;
-    const uint64_t cap = need + need / 4 + 1024;
-    CHK(dalloc_t(t, &w.rec, cap));
-    CHK(dalloc_t(t, &w.scratch, cap));
-    w.cap = cap;
+    if (cap > w.cap) {
+        dfree(t, w.rec);
+        w.rec = nullptr;
+        w.cap = 0;
+        cap += cap / 4 + 1024;
+        CHK(dalloc_t(t, &w.rec, cap));
+        w.cap = cap;
+    }
+    if (R > w.R) {
+        dfree(t, w.scratch);
+        w.scratch = nullptr;
+        w.R = 0;
+        R += R / 4 + 64;
+        CHK(dalloc_t(t, &w.scratch, (uint64_t)w.nw * R));
+        w.R = R;
+    }
     return ST_OK;
 }
 
@@ -1722,15 +1741,10 @@ struct CompareOut {
     const DiffRec *rec = nullptr;   // device, in the local tree's compare workspace
 };
 
-static uint32_t cmp_slice(const st_tree *t) {
-    uint32_t s = std::max<uint32_t>(64 * lane_region_bytes((uint32_t)t->W), cmp_merge_lds_bytes());
-    return (s + 15) & ~15u;
-}
-
-// K3: frontier, verify + merge-join into scratch, device scan, reorder; ONE
-// host round trip (a second compare when the record buffers have to grow).
-// A partitioned pair compares its own segment range only (same partition on
-// both sides).
+// K3: the compare walk (frontier, verification, merge-join: one launch) and
+// the gather of its per-wave records; ONE host round trip (a second compare
+// when the record buffers have to grow).  A partitioned pair compares its own
+// segment range only (same partition on both sides).
 static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint32_t *clevel, uint64_t *cbucket,
                         int *cside, int *status) {
     *status = ST_OK;
@@ -1745,33 +1759,50 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
     st_tree *t = A;   // work is enqueued on the local tree's stream
     if (B->stream != A->stream) HIPCHK(hipStreamSynchronize(B->stream));
     CHK(ensure_cmp_work(t));
-    CHK(grow_records(t, 4096));
     CmpWork &w = t->cw;
+    CHK(grow_records(t, 4096, 64));
     DevTree da = view(A), db = view(B);
-    const uint32_t L1 = A->H + 1;
     uint64_t lo2 = 0, hi2 = ~0ull;
     if (A->partitioned) {
         const uint64_t per2 = A->S / A->W;   // segments under one level-2 bucket
         lo2 = A->part_lo / per2;
         hi2 = A->part_hi / per2;
     }
-    uint64_t *nfinal = w.tot + 1, *total = w.tot;
     const uint32_t slice = cmp_slice(t);
-    const uint32_t wpg = std::max<uint32_t>(1, std::min<uint32_t>(4, (160 * 1024) / slice));
     for (int attempt = 0; attempt < 2; attempt++) {
-        HIPCHK(hipMemsetAsync(w.ctr, 0, 8, t->stream));
-        LAUNCH(t, "cmp_frontier", k_cmp_frontier, 1, 1024, 0, da, db, filter, lo2, hi2, w.flist, w.fcnt, w.err, nfinal,
-               w.seg_bytes);
-        LAUNCH(t, "cmp_visit", k_cmp_visit, 512, 64 * wpg, (size_t)wpg * slice, da, db, filter, (const uint32_t *)w.flist,
-               (const uint32_t *)w.fcnt, w.dcnt, w.soff, w.scratch, w.cap, w.ctr, w.err, slice, w.seg_bytes);
-        LAUNCH(t, "cmp_scan", k_dscan1, 1, 1024, 0, (const uint64_t *)w.dcnt, w.doff, (const uint64_t *)nfinal, total);
-        LAUNCH(t, "cmp_reorder", k_cmp_reorder, 256, 256, 0, (const uint32_t *)w.fcnt, L1, (const uint64_t *)w.dcnt,
-               (const uint64_t *)w.doff, (const uint64_t *)w.soff, (const uint64_t *)total, (const DiffRec *)w.scratch,
-               w.rec, w.cap);
-        HIPCHK(hipMemcpyAsync(t->pin, w.tot, 16, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipMemcpyAsync(t->pin + 2, w.err, 8, hipMemcpyDeviceToHost, t->stream));
+        static const int stamp = getenv("ST_CMP_STAMPS") ? atoi(getenv("ST_CMP_STAMPS")) : 0;
+        Scratch sc(t);
+        uint64_t *stamps = nullptr;
+        if (stamp) {   // diagnostic: per-wave phase stamps (100 MHz) to stderr
+            CHK(sc.alloc(&stamps, (uint64_t)w.nw * 8));
+            HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 64, t->stream));
+        }
+        LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
+        if (stamp) {
+            std::vector<uint64_t> h((uint64_t)w.nw * 8);
+            HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
+            HIPCHK(hipStreamSynchronize(t->stream));
+            uint64_t t0 = ~0ull;
+            for (uint32_t x = 0; x < w.nw; x++) t0 = std::min(t0, h[x * 8]);
+            static const char *nm[8] = {"start", "levels", "children", "verify", "merge", "end", "", "staged"};
+            for (int k = 0; k < 8; k++) {
+                if (k == 6) continue;
+                std::vector<double> v;
+                for (uint32_t x = 0; x < w.nw; x++)
+                    if (h[x * 8 + k]) v.push_back((h[x * 8 + k] - t0) / 100.0);
+                if (v.empty()) continue;
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, "cmp stamp %-9s n=%4zu min %7.2f med %7.2f p90 %7.2f max %7.2f us\n", nm[k], v.size(), v[0],
+                        v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+            }
+        }
+        w.res[0] = w.res[1] = 0;
+        w.res[2] = 0;
+        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4, 256, 0, w.nw, (const uint64_t *)w.wcnt,
+               (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
         HIPCHK(hipStreamSynchronize(t->stream));
-        const uint64_t ntot = t->pin[0], e = t->pin[2];
+        const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
         if (e != ~0ull) {
             *status = ST_CORRUPTED;
             *clevel = (uint32_t)(e >> 56);
@@ -1779,12 +1810,12 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             *cside = (int)(e & 1);
             return ST_OK;
         }
-        if (ntot <= w.cap) {
+        if (ntot <= w.cap && need <= w.R) {
             co.n = ntot;
             co.rec = w.rec;
             return ST_OK;
         }
-        CHK(grow_records(t, ntot));   // first compare with this many records
+        CHK(grow_records(t, ntot, need));   // first compare with this many records
     }
     g_err = "compare record buffer did not converge";
     return ST_EDEVICE;
@@ -1942,13 +1973,21 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
 extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_levels, uint64_t *seg_bytes) {
     CHK(use_device(local));
     CmpWork &w = local->cw;
-    if (!w.flist) { g_err = "no compare has run on this tree"; return ST_EINVAL; }
-    uint32_t f[ST_MAXLEV + 2];
-    unsigned long long b = 0;
-    HIPCHK(hipMemcpyAsync(f, w.fcnt, sizeof(f), hipMemcpyDeviceToHost, local->stream));
-    HIPCHK(hipMemcpyAsync(&b, w.seg_bytes, 8, hipMemcpyDeviceToHost, local->stream));
+    if (!w.wcnt) { g_err = "no compare has run on this tree"; return ST_EINVAL; }
+    std::vector<uint32_t> st((uint64_t)w.nw * ST_STATW);
+    std::vector<uint64_t> wb(w.nw);
+    HIPCHK(hipMemcpyAsync(st.data(), w.wst, st.size() * 4, hipMemcpyDeviceToHost, local->stream));
+    HIPCHK(hipMemcpyAsync(wb.data(), w.wbytes, wb.size() * 8, hipMemcpyDeviceToHost, local->stream));
     HIPCHK(hipStreamSynchronize(local->stream));
-    for (uint32_t l = 0; l < max_levels && l < ST_MAXLEV + 2; l++) visited[l] = f[l];
+    const uint32_t L1 = local->H + 1;
+    for (uint32_t l = 0; l < max_levels; l++) {
+        uint64_t v = 0;
+        if (l >= 1 && l <= L1)
+            for (uint32_t x = 0; x < w.nw; x++) v += st[(uint64_t)x * ST_STATW + l];
+        visited[l] = v;
+    }
+    uint64_t b = 0;
+    for (uint32_t x = 0; x < w.nw; x++) b += wb[x];
     *seg_bytes = b;
     return ST_OK;
 }
