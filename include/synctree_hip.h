@@ -160,6 +160,15 @@ int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hash
 int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
                       uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside);
 
+/* Dry run of st_exchange_apply: compare + valid_obj_hash selection, nothing
+ * inserted.  *n_take = remote values an apply would insert (those before the
+ * first crash), *crashed = the apply would end in the function_clause crash.
+ * Used by the partitioned exchange (parallel.py) to apply only the
+ * partitions that precede the first crash in the reference's diff order
+ * (riak_ensemble_exchange.erl:71-97).  Returns ST_CORRUPTED like st_compare. */
+int st_exchange_plan(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_take, int *crashed,
+                     uint32_t *clevel, uint64_t *cbucket, int *cside);
+
 /* ---- multi-GPU: segment-range partition of one tree ------
  * No reference counterpart: riak_ensemble keeps a tree on one node.  This is
  * the sharding of a single huge tree across the GPUs of one node.

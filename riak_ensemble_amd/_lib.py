@@ -68,6 +68,7 @@ _SIGS = {
     'st_exchange_apply': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    'st_exchange_plan': (ctypes.c_int, [ctypes.c_void_p] * 8),
     'st_rehash_group': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     'st_set_partition': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]),
     'st_combine_upper': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

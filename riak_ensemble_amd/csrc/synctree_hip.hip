@@ -1838,8 +1838,8 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
 // the local tree, with insert/3 semantics, every remote value the exchange
 // would take (k_diff_apply_*), as ONE device batch instead of one
 // peer_tree:insert gen_server call per diff.
-extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
-                                 uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
+static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *n_diffs, uint64_t *n_applied,
+                         uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
     CHK(use_device(local));
     CHK(flush_overlay(local));
     CHK(flush_overlay(remote));
@@ -1883,6 +1883,10 @@ extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_di
     HIPCHK(hipStreamSynchronize(t->stream));
     const uint64_t m = t->pin[0], kb = t->pin[1], vb = t->pin[2];
     *crashed = t->pin[3] != ~0ull ? 1 : 0;
+    if (!apply) {
+        *n_applied = m;   // what an apply would take
+        return ST_OK;
+    }
     if (m) {
         CHK(sc.bytes(&kh, kb + HEAP_SLACK));
         CHK(sc.bytes(&vh, vb + HEAP_SLACK));
@@ -1904,6 +1908,22 @@ extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_di
     }
     HIPCHK(hipStreamSynchronize(t->stream));
     return ST_OK;
+}
+
+extern "C" int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_applied,
+                                 uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
+    return exchange_core(local, remote, true, n_diffs, n_applied, n_rejected, crashed, clevel, cbucket, cside);
+}
+
+// The same compare + valid_obj_hash selection with nothing applied: the
+// number of diffs, how many remote values an apply would take (before the
+// first crash), whether it would crash, or the corruption.  A partitioned
+// exchange plans on every rank first so that only the partitions before the
+// first crash (in the reference's order: highest segments first) apply.
+extern "C" int st_exchange_plan(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_take, int *crashed,
+                                uint32_t *clevel, uint64_t *cbucket, int *cside) {
+    uint64_t rej = 0;
+    return exchange_core(local, remote, false, n_diffs, n_take, &rej, crashed, clevel, cbucket, cside);
 }
 
 extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,

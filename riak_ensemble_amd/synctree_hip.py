@@ -297,6 +297,17 @@ class DeviceTree:
         info = {'diffs': int(nd.value), 'applied': int(na.value), 'rejected': int(nr.value)}
         return ('exchange_failed' if cr.value else 'ok', info)
 
+    def exchange_plan(self, remote):
+        """Dry run of exchange_apply (st_exchange_plan): ('ok' | 'exchange_failed',
+        {'diffs', 'take'}) or ('corrupted', side, tuple); nothing applied."""
+        nd, nt, cr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        cl, cb, cs = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int()
+        rc = _lib.check(self.L.st_exchange_plan(self.h, remote.h, ctypes.byref(nd), ctypes.byref(nt), ctypes.byref(cr),
+                                                ctypes.byref(cl), ctypes.byref(cb), ctypes.byref(cs)), 'st_exchange_plan')
+        if rc == _lib.ST_CORRUPTED:
+            return ('corrupted', 'local' if cs.value == 0 else 'remote', (terms.CORRUPTED, int(cl.value), int(cb.value)))
+        return ('exchange_failed' if cr.value else 'ok', {'diffs': int(nd.value), 'take': int(nt.value)})
+
     # ------------------------------------------------------------ LevelDB format
     def snapshot_leveldb(self, tree_id=b''):
         """The synctree_leveldb records of this tree (src/synctree_leveldb.erl:
