@@ -21,9 +21,15 @@
  *                    ordered numerically)
  *      ST_KEY_ATOM   bytes = atom_to_binary(Key, utf8)
  *      ST_KEY_BINARY bytes = the binary
- *    Erlang term order on that domain: integer < atom < binary; atoms and
- *    binaries compare bytewise with a proper prefix first.  Other terms (which
- *    the reference hashes via term_to_binary) are rejected with ST_EINVAL.
+ *      ST_KEY_TERM   bytes = term_to_binary(Key) (any other key: tuples,
+ *                    lists, floats, integers outside int64; the reference
+ *                    hashes term_to_binary(Key), or <<Key:64>> for an
+ *                    integer; riak_ensemble_amd/csrc/term_key.h)
+ *    Keys are kept in Erlang term order (number < atom < tuple < nil < list <
+ *    binary; numbers by value, atoms and binaries bytewise with a proper
+ *    prefix first).  Pids, ports, refs, funs, maps and bitstrings are
+ *    rejected with ST_EINVAL; an int64 / atom / binary passed as ST_KEY_TERM
+ *    is the same key as its plain form.
  *  - Packed variable-length arrays: element i of a heap is
  *    heap[off[i] .. off[i+1]) with off[] of n+1 entries.
  *  - Hashes are 17 bytes: <<?H_MD5 = 0, md5/binary>> (src/synctree.erl:255-259).
@@ -46,6 +52,7 @@ extern "C" {
 #define ST_KEY_INT 0
 #define ST_KEY_ATOM 1
 #define ST_KEY_BINARY 2
+#define ST_KEY_TERM 3
 
 #define ST_FILTER_ALL 0
 #define ST_FILTER_LOCAL_ONLY 1   /* drops {K,{_, '$none'}}  (synctree.erl:438-442) */
@@ -168,6 +175,15 @@ int st_exchange_apply(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64
  * (riak_ensemble_exchange.erl:71-97).  Returns ST_CORRUPTED like st_compare. */
 int st_exchange_plan(st_tree *local, st_tree *remote, uint64_t *n_diffs, uint64_t *n_take, int *crashed,
                      uint32_t *clevel, uint64_t *cbucket, int *cside);
+
+/* ETF atom forms written by st_snapshot_leveldb (synctree_leveldb.erl:134-
+ * 152 term_to_binary): utf8 = 0 (default) as OTP < 26 writes them (ATOM_EXT
+ * for Latin-1 atoms, the reference's era), 1 = OTP >= 26 (UTF-8 forms). */
+int st_set_etf_atoms(st_tree *t, int utf8);
+
+/* The device key record of one key (host-only helper, no device needed):
+ * memcmp-then-length order of records is Erlang term order. */
+int st_key_record(uint8_t ktype, const uint8_t *bytes, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *out_len);
 
 /* ---- multi-GPU: segment-range partition of one tree ------
  * No reference counterpart: riak_ensemble keeps a tree on one node.  This is

@@ -15,10 +15,12 @@ Imported only by ``tests/`` (never by the product package).  Restates:
 reference, OTP version unpinned).  They are restated from
 the published external term format (version byte 131) for the node domain:
 integers (SMALL_INTEGER_EXT 97, INTEGER_EXT 98, SMALL_BIG_EXT 110), atoms
-(SMALL_ATOM_UTF8_EXT 119 / ATOM_UTF8_EXT 118, as term_to_binary writes them
-from OTP 26; the Latin-1 ATOM_EXT 100 / SMALL_ATOM_EXT 115 of older releases
-are decoded too), binaries (BINARY_EXT 109), 2-tuples (SMALL_TUPLE_EXT 104)
-and proper lists (LIST_EXT 108 ... NIL_EXT 106; [] = 106).  The byte
+(ATOM_EXT 100 for Latin-1 atoms as term_to_binary writes them before OTP 26
+-- the reference's era, the default -- or SMALL_ATOM_UTF8_EXT 119 /
+ATOM_UTF8_EXT 118 as from OTP 26: synctree_ref.ETF_ATOMS), binaries
+(BINARY_EXT 109), tuples (SMALL_TUPLE_EXT 104), floats (NEW_FLOAT_EXT 70) and
+lists (STRING_EXT 107, LIST_EXT 108 ... NIL_EXT 106; [] = 106); the encoder
+is synctree_ref's ETF restatement.  The byte
 layouts are pinned by known-answer vectors in tests/test_leveldb_format.py
 (classic published examples such as term_to_binary(256) =
 <<131,98,0,0,1,0>>); the reference's own tests hold no ETF bytes, so the
@@ -40,40 +42,7 @@ class BadTerm(Exception):
 
 # ------------------------------------------------------------------ ETF
 def _enc(t, out):
-    if isinstance(t, bool):
-        raise TypeError('booleans are atoms')
-    if isinstance(t, int):
-        if 0 <= t < 256:
-            out += bytes([97, t])
-        elif -(1 << 31) <= t < (1 << 31):
-            out += bytes([98]) + struct.pack('>i', t)
-        else:
-            m = abs(t)
-            mag = m.to_bytes((m.bit_length() + 7) // 8, 'little')
-            if len(mag) > 255:
-                raise TypeError('LARGE_BIG_EXT outside the node domain')
-            out += bytes([110, len(mag), 1 if t < 0 else 0]) + mag
-    elif isinstance(t, str):
-        b = t.encode('utf-8')
-        out += (bytes([119, len(b)]) if len(b) < 256 else bytes([118]) + struct.pack('>H', len(b))) + b
-    elif isinstance(t, (bytes, bytearray)):
-        out += bytes([109]) + struct.pack('>I', len(t)) + bytes(t)
-    elif isinstance(t, tuple):
-        if len(t) > 255:
-            raise TypeError('LARGE_TUPLE_EXT outside the node domain')
-        out += bytes([104, len(t)])
-        for x in t:
-            _enc(x, out)
-    elif isinstance(t, list):
-        if not t:
-            out += bytes([106])
-        else:
-            out += bytes([108]) + struct.pack('>I', len(t))
-            for x in t:
-                _enc(x, out)
-            out += bytes([106])
-    else:
-        raise TypeError('term outside the restated domain: %r' % (t,))
+    out += ST._ext(t)   # the ETF restatement (atoms in the era ST.ETF_ATOMS selects)
 
 
 def term_to_binary(t):
@@ -136,6 +105,14 @@ def _dec(b, i):
         return tuple(xs), i
     if tg == 106:
         return [], i
+    if tg == 107:
+        need(2)
+        n = struct.unpack('>H', b[i:i + 2])[0]
+        need(2 + n)
+        return list(b[i + 2:i + 2 + n]), i + 2 + n
+    if tg == 70:
+        need(8)
+        return struct.unpack('>d', b[i:i + 8])[0], i + 8
     if tg == 108:
         need(4)
         n = struct.unpack('>I', b[i:i + 4])[0]

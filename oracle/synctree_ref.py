@@ -24,11 +24,15 @@ Every function cites the reference line it restates
 * ETS backend ..................... src/synctree_ets.erl:32-66
 * orddict backend ................. src/synctree_orddict.erl:32-66
 
-Erlang terms are modelled as: integers -> ``int``, binaries -> ``bytes``,
-atoms -> ``str``.  Erlang term order for that domain is number < atom <
-bitstring (ERTS type order), atoms compare by their text, binaries bytewise
-with a prefix sorting first.  Other key types (tuples, lists, ...) would go
-through ``term_to_binary`` (synctree.erl:267-268) and are outside the domain.
+Erlang terms are modelled as: integers -> ``int``, floats -> ``float``,
+binaries -> ``bytes``, atoms -> ``str``, tuples -> ``tuple``, proper lists ->
+``list``.  Erlang term order (ERTS): number < atom < tuple < nil < list <
+bitstring; numbers by value (an integer and a float compare as numbers),
+atoms by their text, tuples by size then elements, lists element-wise with a
+prefix first, binaries bytewise with a prefix first.  Keys outside
+integer/atom/binary are hashed through term_to_binary (synctree.erl:267-268),
+restated below from the ERTS external term format (ETF_ATOMS selects the OTP
+era of atom encoding: 'latin1' = before OTP 26, 'utf8' = OTP 26+).
 
 Parity of the hash bytes is pinned by RFC 1321 (MD5 via ``hashlib``) and the
 reference's own tests (test/synctree_pure.erl, test/synctree_remote.erl);
@@ -46,9 +50,14 @@ UNDEFINED = 'undefined'
 NOTFOUND = 'notfound'
 CORRUPTED = 'corrupted'
 
-_TYPE_RANK_INT = 0
+_TYPE_RANK_NUMBER = 0
 _TYPE_RANK_ATOM = 1
-_TYPE_RANK_BITSTRING = 9
+_TYPE_RANK_TUPLE = 6
+_TYPE_RANK_NIL = 8
+_TYPE_RANK_LIST = 9
+_TYPE_RANK_BITSTRING = 10
+
+ETF_ATOMS = 'latin1'
 
 
 class ErlangCrash(Exception):
@@ -59,16 +68,72 @@ class ErlangCrash(Exception):
 # Term helpers
 
 def term_key(t):
-    """Sort key realising Erlang term order on the supported domain."""
+    """Sort key realising Erlang term order (ERTS) on the modelled terms."""
     if isinstance(t, bool):
         raise ErlangCrash('booleans are atoms in Erlang; pass "true"/"false"')
-    if isinstance(t, int):
-        return (_TYPE_RANK_INT, t)
+    if isinstance(t, (int, float)):
+        return (_TYPE_RANK_NUMBER, t)
     if isinstance(t, str):
         return (_TYPE_RANK_ATOM, t.encode('utf-8'))
+    if isinstance(t, tuple):
+        return (_TYPE_RANK_TUPLE, len(t), tuple(term_key(e) for e in t))
+    if isinstance(t, list):
+        if not t:
+            return (_TYPE_RANK_NIL,)
+        return (_TYPE_RANK_LIST, [term_key(e) for e in t])
     if isinstance(t, (bytes, bytearray)):
         return (_TYPE_RANK_BITSTRING, bytes(t))
     raise ErlangCrash('term outside the restated domain: %r' % (t,))
+
+
+def _atom_ext(a):
+    if ETF_ATOMS == 'latin1' and max((ord(c) for c in a), default=0) < 256:
+        raw = a.encode('latin-1')
+        return b'd' + len(raw).to_bytes(2, 'big') + raw                   # ATOM_EXT
+    raw = a.encode('utf-8')
+    if len(raw) < 256:
+        return b'w' + bytes([len(raw)]) + raw                             # SMALL_ATOM_UTF8_EXT
+    return b'v' + len(raw).to_bytes(2, 'big') + raw                       # ATOM_UTF8_EXT
+
+
+def _ext(t):
+    """One term in the external term format (erts external.c, default options)."""
+    if isinstance(t, bool):
+        raise ErlangCrash('booleans unsupported')
+    if isinstance(t, int):
+        if 0 <= t < 256:
+            return b'a' + bytes([t])                                      # SMALL_INTEGER_EXT
+        if -2 ** 31 <= t < 2 ** 31:
+            return b'b' + (t & 0xFFFFFFFF).to_bytes(4, 'big')             # INTEGER_EXT
+        mag = abs(t)
+        digits = []
+        while mag:
+            digits.append(mag & 0xFF)
+            mag >>= 8
+        if len(digits) < 256:
+            return b'n' + bytes([len(digits), 1 if t < 0 else 0] + digits)  # SMALL_BIG_EXT
+        return b'o' + len(digits).to_bytes(4, 'big') + bytes([1 if t < 0 else 0] + digits)
+    if isinstance(t, float):
+        import struct
+        return b'F' + struct.pack('>d', t)                                # NEW_FLOAT_EXT
+    if isinstance(t, str):
+        return _atom_ext(t)
+    if isinstance(t, (bytes, bytearray)):
+        return b'm' + len(t).to_bytes(4, 'big') + bytes(t)                # BINARY_EXT
+    if isinstance(t, tuple):
+        head = b'h' + bytes([len(t)]) if len(t) < 256 else b'i' + len(t).to_bytes(4, 'big')
+        return head + b''.join(_ext(e) for e in t)
+    if isinstance(t, list):
+        if not t:
+            return b'j'                                                   # NIL_EXT
+        if len(t) < 65536 and all(type(e) is int and 0 <= e < 256 for e in t):
+            return b'k' + len(t).to_bytes(2, 'big') + bytes(t)            # STRING_EXT
+        return b'l' + len(t).to_bytes(4, 'big') + b''.join(_ext(e) for e in t) + b'j'
+    raise ErlangCrash('term outside the restated domain: %r' % (t,))
+
+
+def term_to_binary(t):
+    return b'\x83' + _ext(t)
 
 
 def ensure_binary(key):
@@ -81,7 +146,7 @@ def ensure_binary(key):
         return key.encode('utf-8')                             # atom_to_binary(K, utf8)
     if isinstance(key, (bytes, bytearray)):
         return bytes(key)
-    raise ErlangCrash('term_to_binary keys are outside the restated domain')
+    return term_to_binary(key)                                 # term_to_binary(Key)
 
 
 def md5(data):

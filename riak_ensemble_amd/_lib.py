@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, 'libsynctree_hip.so')
 
 ST_OK, ST_NOTFOUND, ST_CORRUPTED = 0, 1, 2
 ST_EINVAL, ST_EDEVICE, ST_ENOMEM = -1, -2, -3
-ST_KEY_INT, ST_KEY_ATOM, ST_KEY_BINARY = 0, 1, 2
+ST_KEY_INT, ST_KEY_ATOM, ST_KEY_BINARY, ST_KEY_TERM = 0, 1, 2, 3
 ST_FILTER_ALL, ST_FILTER_LOCAL_ONLY, ST_FILTER_REMOTE_ONLY = 0, 1, 2
 ST_DIFF_BOTH, ST_DIFF_LOCAL_ONLY, ST_DIFF_REMOTE_ONLY = 0, 1, 2
 
@@ -95,6 +95,9 @@ _SIGS = {
                                           u64p]),
     'st_compare_stats': (ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32, u64p]),
     'st_tops_to_device': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    'st_set_etf_atoms': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    'st_key_record': (ctypes.c_int, [ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                     u64p]),
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
 }

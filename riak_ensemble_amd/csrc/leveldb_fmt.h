@@ -87,18 +87,62 @@ __device__ inline int64_t krec_int(const uint8_t *p) {
     return (int64_t)(u ^ 0x8000000000000000ull);
 }
 
-// ETF size of the key of record bytes p[0..len)
-__device__ inline uint32_t etf_key_size(const uint8_t *p, uint64_t len) {
-    if (p[0] == KEYTAG_INT) return etf_int_size(krec_int(p));
+// Is a UTF-8 atom text representable in Latin-1 (every code point < 256)?
+// Its Latin-1 length in *n.
+__device__ inline bool utf8_latin1(const uint8_t *u, uint64_t l, uint32_t *n) {
+    uint32_t c = 0;
+    for (uint64_t i = 0; i < l; i++) {
+        const uint8_t b = u[i];
+        if (b < 0x80) { c++; continue; }
+        if ((b == 0xC2 || b == 0xC3) && i + 1 < l) { c++; i++; continue; }
+        return false;
+    }
+    *n = c;
+    return true;
+}
+
+// ETF size of the key of record bytes p[0..len).  Atoms: ATOM_EXT (Latin-1)
+// as term_to_binary writes them before OTP 26 (the reference's era, R16 -
+// OTP 19: SURVEY §8c), the UTF-8 forms otherwise or with ST_FLAG_ATOM_UTF8.
+// Term records carry their term_to_binary bytes (term_key.h).
+__device__ inline uint32_t etf_key_size(const uint8_t *p, uint64_t len, uint32_t flags) {
+    if (p[0] == KEYTAG_INT && len == 9) return etf_int_size(krec_int(p));
+    if (krec_is_term(p, len)) {
+        uint64_t ea, sa;
+        uint32_t el, sl;
+        krec_term_parts(p, len, &ea, &el, &sa, &sl);
+        return el - 1;   // without the version byte
+    }
     const uint64_t l = len - 1;
-    if (p[0] == KEYTAG_ATOM) return (uint32_t)(l < 256 ? 2 + l : 3 + l);
+    if (p[0] == KEYTAG_ATOM) {
+        uint32_t n;
+        if (!(flags & ST_FLAG_ATOM_UTF8) && utf8_latin1(p + 1, l, &n)) return 3 + n;
+        return (uint32_t)(l < 256 ? 2 + l : 3 + l);
+    }
     return (uint32_t)(5 + l);
 }
 
-__device__ inline uint8_t *etf_key_write(uint8_t *o, const uint8_t *p, uint64_t len) {
-    if (p[0] == KEYTAG_INT) return etf_int_write(o, krec_int(p));
+__device__ inline uint8_t *etf_key_write(uint8_t *o, const uint8_t *p, uint64_t len, uint32_t flags) {
+    if (p[0] == KEYTAG_INT && len == 9) return etf_int_write(o, krec_int(p));
+    if (krec_is_term(p, len)) {
+        uint64_t ea, sa;
+        uint32_t el, sl;
+        krec_term_parts(p, len, &ea, &el, &sa, &sl);
+        for (uint32_t i = 1; i < el; i++) o[i - 1] = p[ea + i];
+        return o + el - 1;
+    }
     const uint32_t l = (uint32_t)(len - 1);
     if (p[0] == KEYTAG_ATOM) {
+        uint32_t n;
+        if (!(flags & ST_FLAG_ATOM_UTF8) && utf8_latin1(p + 1, l, &n)) {
+            o[0] = 100; o[1] = (uint8_t)(n >> 8); o[2] = (uint8_t)n; o += 3;
+            for (uint32_t i = 0; i < l; i++) {
+                const uint8_t b = p[1 + i];
+                if (b < 0x80) *o++ = b;
+                else { *o++ = (uint8_t)(((b & 0x1F) << 6) | (p[2 + i] & 0x3F)); i++; }
+            }
+            return o;
+        }
         if (l < 256) { o[0] = 119; o[1] = (uint8_t)l; o += 2; }
         else { o[0] = 118; o[1] = (uint8_t)(l >> 8); o[2] = (uint8_t)l; o += 3; }
     } else {
@@ -120,7 +164,7 @@ __global__ void k_snap_entry_sizes(DevTree t, uint64_t n, uint64_t *es) {
     for (uint64_t e = gtid(); e <= n; e += gstride()) {
         if (e == n) { es[e] = 0; break; }
         const uint64_t k0 = t.koff[e];
-        es[e] = 2 + etf_key_size(t.kheap + k0, t.koff[e + 1] - k0) + 5 + (t.voff[e + 1] - t.voff[e]);
+        es[e] = 2 + etf_key_size(t.kheap + k0, t.koff[e + 1] - k0, t.flags) + 5 + (t.voff[e + 1] - t.voff[e]);
     }
 }
 
@@ -226,7 +270,7 @@ __global__ void k_snap_entries(DevTree t, uint64_t n, uint64_t sb, const uint64_
         uint8_t *v = vout + vo[sb + lo] + 6 + (eo[e] - eo[t.seg_off[lo]]);
         v[0] = 104; v[1] = 2;
         const uint64_t k0 = t.koff[e];
-        v = etf_key_write(v + 2, t.kheap + k0, t.koff[e + 1] - k0);
+        v = etf_key_write(v + 2, t.kheap + k0, t.koff[e + 1] - k0, t.flags);
         const uint64_t v0 = t.voff[e], vl = t.voff[e + 1] - v0;
         v[0] = 109; v = etf_u32be(v + 1, (uint32_t)vl);
         for (uint64_t i = 0; i < vl; i++) v[i] = t.vheap[v0 + i];

@@ -71,7 +71,10 @@ __device__ __forceinline__ uint64_t record_segment(const uint8_t *p, uint64_t le
         stmd5::init(d);
         stmd5::compress(d, m);
     } else {
-        stmd5::md5_global_pf(p + 1, len - 1, d);
+        const uint8_t *sp;
+        uint64_t sl;
+        krec_seg_bytes(p, len, &sp, &sl);
+        stmd5::md5_global_pf(sp, sl, d);
     }
     const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
     return lo & segmask;

@@ -20,18 +20,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "md5_dev.h"
+#include "term_key.h"
 
 #define ST_MAXLEV 33
 #define TAG_PRESENT 0x100u
-#define KEYTAG_INT 0
-#define KEYTAG_ATOM 1
-#define KEYTAG_BINARY 2
 
 #define MODE_STORE 0
 #define MODE_VERIFY 1
 
+#define ST_FLAG_ATOM_UTF8 1u   // DevTree.flags: ETF atoms as OTP >= 26 writes them (utf8 forms only)
+
 struct DevTree {
-    uint32_t W, shift, H, pad0;
+    uint32_t W, shift, H, flags;
     uint64_t S;
     uint64_t base[ST_MAXLEV + 2];
     uint4 *md5;
@@ -43,6 +43,37 @@ struct DevTree {
     const uint64_t *voff;
     const uint8_t *vheap;
 };
+
+// Key records (term_key.h): the plain int64 / atom / binary form, or a term
+// record [SK][ETF][Seg][etf_len u16][seg_len u16].
+__host__ __device__ __forceinline__ bool krec_is_term(const uint8_t *p, uint64_t len) {
+    const uint8_t t = p[0];
+    return !(t == KEYTAG_ATOM || t == KEYTAG_BINARY || (t == KEYTAG_INT && len == 9));
+}
+// term record -> offsets of its ETF and Seg bytes
+__host__ __device__ __forceinline__ void krec_term_parts(const uint8_t *p, uint64_t len, uint64_t *etf_at, uint32_t *etf_len,
+                                                         uint64_t *seg_at, uint32_t *seg_len) {
+    const uint32_t el = (uint32_t)p[len - 4] | ((uint32_t)p[len - 3] << 8);
+    const uint32_t sl = (uint32_t)p[len - 2] | ((uint32_t)p[len - 1] << 8);
+    const uint64_t tail = len - 4 - (sl == 0xFFFF ? 0 : sl);
+    *etf_at = tail - el;
+    *etf_len = el;
+    *seg_at = sl == 0xFFFF ? tail - el : tail;
+    *seg_len = sl == 0xFFFF ? el : sl;
+}
+// ensure_binary(Key) bytes of a non-int64 record (synctree.erl:261-268)
+__host__ __device__ __forceinline__ void krec_seg_bytes(const uint8_t *p, uint64_t len, const uint8_t **sp, uint64_t *sl) {
+    if (krec_is_term(p, len)) {
+        uint64_t ea, sa;
+        uint32_t el, sln;
+        krec_term_parts(p, len, &ea, &el, &sa, &sln);
+        *sp = p + sa;
+        *sl = sln;
+    } else {
+        *sp = p + 1;
+        *sl = len - 1;
+    }
+}
 
 __device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
@@ -143,7 +174,10 @@ __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64
             stmd5::init(d);
             stmd5::compress(d, m);
         } else {
-            stmd5::md5_global_pf(p + 1, len - 1, d);
+            const uint8_t *sp;
+            uint64_t sl;
+            krec_seg_bytes(p, len, &sp, &sl);
+            stmd5::md5_global_pf(sp, sl, d);
         }
         const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
         seg_out[i] = (uint32_t)(lo & segmask);
@@ -1140,8 +1174,15 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
     const uint64_t h1 = h0 + P < nH ? h0 + P : nH;
     uint32_t n = 0;
     wave_sync_lds();
-    if (topdiff && h1 > h0) {
-        if (h0 == 0 && H >= 1) {   // the root (level 1) belongs to wave 0
+    if (topdiff && H == 0) {   // one segment under the top hash (segments = 1): wave 0
+        if (w == 0) {
+            cmp_append(c.list, n, lane == 0, (1ull << 56));
+            if (lane == 0) c.cnt[1] += 1;
+            cmp_flush(A, B, c, n);
+            n = 0;
+        }
+    } else if (topdiff && h1 > h0) {
+        if (h0 == 0) {   // the root (level 1) belongs to wave 0
             cmp_append(c.list, n, lane == 0, (1ull << 56));
             if (lane == 0) c.cnt[1] += 1;
         }

@@ -57,6 +57,7 @@ struct Pending {
 struct st_tree {
     int device = 0;
     int ncu = 256;   // compute units of the device (fixed-grid kernels)
+    uint32_t flags = 0;   // DevTree.flags (ST_FLAG_ATOM_UTF8)
     hipStream_t own_stream = nullptr, stream = nullptr;
     uint64_t W = 16, S = 1 << 20;
     uint32_t shift = 4, H = 5;
@@ -149,6 +150,7 @@ static DevTree view(const st_tree *t) {
     d.W = (uint32_t)t->W;
     d.shift = t->shift;
     d.H = t->H;
+    d.flags = t->flags;
     d.S = t->S;
     for (int i = 0; i < ST_MAXLEV + 2; i++) d.base[i] = t->base[i];
     d.md5 = t->md5;
@@ -404,10 +406,13 @@ static int pack_records(uint64_t n, const uint8_t *ktype, const uint8_t *kheap, 
             r.heap.push_back(p[0] ^ 0x80);
             r.heap.insert(r.heap.end(), p + 1, p + 8);
         } else if (ty == ST_KEY_ATOM || ty == ST_KEY_BINARY) {
-            r.heap.push_back(ty);
+            r.heap.push_back(ty == ST_KEY_ATOM ? KEYTAG_ATOM : KEYTAG_BINARY);
             r.heap.insert(r.heap.end(), p, p + len);
+        } else if (ty == ST_KEY_TERM) {
+            const std::string e = termkey::record_from_etf(p, len, r.heap);
+            if (!e.empty()) { g_err = "key " + std::to_string(i) + ": " + e; return ST_EINVAL; }
         } else {
-            g_err = "key type outside the device domain (term_to_binary keys)";
+            g_err = "unknown key type";
             return ST_EINVAL;
         }
     }
@@ -1413,7 +1418,16 @@ static void records_to_keys(st_result *res, uint64_t n) {
         const uint64_t len = res->koff[i + 1] - res->koff[i];
         nk[i] = o;
         if (len == 0) continue;
-        res->ktype[i] = p[0];
+        if (krec_is_term(p, len)) {   // the caller's term_to_binary bytes
+            uint64_t ea, sa;
+            uint32_t el, sl;
+            krec_term_parts(p, len, &ea, &el, &sa, &sl);
+            res->ktype[i] = ST_KEY_TERM;
+            memcpy(nh + o, p + ea, el);
+            o += el;
+            continue;
+        }
+        res->ktype[i] = p[0] == KEYTAG_INT ? ST_KEY_INT : (p[0] == KEYTAG_ATOM ? ST_KEY_ATOM : ST_KEY_BINARY);
         memcpy(nh + o, p + 1, len - 1);
         if (p[0] == KEYTAG_INT) nh[o] ^= 0x80;
         o += len - 1;
@@ -2009,6 +2023,29 @@ extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_
     uint64_t b = 0;
     for (uint32_t x = 0; x < w.nw; x++) b += wb[x];
     *seg_bytes = b;
+    return ST_OK;
+}
+
+// ETF atom forms of snapshots: 0 = as term_to_binary writes them before OTP
+// 26 (ATOM_EXT for Latin-1 atoms: the reference's era), 1 = OTP >= 26
+// (SMALL_ATOM_UTF8_EXT / ATOM_UTF8_EXT only).
+extern "C" int st_set_etf_atoms(st_tree *t, int utf8) {
+    if (!t) { g_err = "NULL tree"; return ST_EINVAL; }
+    t->flags = utf8 ? (t->flags | ST_FLAG_ATOM_UTF8) : (t->flags & ~ST_FLAG_ATOM_UTF8);
+    return ST_OK;
+}
+
+// The device key record of one key (host only, no device): memcmp order of
+// records = Erlang term order (term_key.h).  *out_len = record length (the
+// record is written when it fits in cap).
+extern "C" int st_key_record(uint8_t ktype, const uint8_t *bytes, uint64_t len, uint8_t *out, uint64_t cap,
+                             uint64_t *out_len) {
+    const uint64_t off[2] = {0, len};
+    HostRecords r;
+    CHK(pack_records(1, &ktype, bytes, off, r));
+    const uint64_t n = r.off[1];
+    *out_len = n;
+    if (out && n <= cap) memcpy(out, r.heap.data(), n);
     return ST_OK;
 }
 

@@ -216,3 +216,18 @@ class PartitionedTree:
             tot = g.copy().view(np.uint64).reshape(self.world, 3).sum(axis=0)
         summary = {'diffs': int(tot[0]), 'applied': int(tot[1]), 'rejected': int(tot[2])}
         return ('exchange_failed' if crashing else 'ok', summary)
+
+
+def gather_tops(dist, tops, group=None, device='cpu'):
+    """Ensemble sharding: all-gather per-ensemble top hashes.
+
+    `tops` is this rank's list of 17-byte hashes (or ``'undefined'``), one per
+    local ensemble, the same count on every rank.  Returns the list of all
+    ensembles' tops in (rank, local index) order."""
+    rows = np.zeros((len(tops), 18), np.uint8)
+    for i, h in enumerate(tops):
+        if isinstance(h, (bytes, bytearray)):
+            rows[i, 0] = 1
+            rows[i, 1:] = np.frombuffer(bytes(h), np.uint8)
+    allr = _allgather_bytes(dist, group, rows.reshape(-1), device).reshape(-1, 18)
+    return [bytes(r[1:]) if r[0] else 'undefined' for r in allr]

@@ -156,6 +156,11 @@ class DeviceTree:
         return present, hashes
 
     # ------------------------------------------------------------ partition
+    def set_etf_atoms(self, utf8):
+        """ETF atom forms of leveldb snapshots: False = before OTP 26 (ATOM_EXT
+        for Latin-1 atoms, the default), True = OTP 26+ (st_set_etf_atoms)."""
+        _lib.check(self.L.st_set_etf_atoms(self.h, 1 if utf8 else 0), 'st_set_etf_atoms')
+
     def set_partition(self, seg_lo, seg_hi):
         """Own segments [seg_lo, seg_hi) only (st_set_partition)."""
         _lib.check(self.L.st_set_partition(self.h, int(seg_lo), int(seg_hi)), 'st_set_partition')

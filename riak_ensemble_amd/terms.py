@@ -1,16 +1,25 @@
 """Erlang-term view of synctree keys and values for the host mirror.
 
-Keys on the device path are (type, ensure_binary bytes)
-(src/synctree.erl:261-268): integers -> <<K:64/big>>, atoms ->
-atom_to_binary(K, utf8), binaries -> themselves.  In Python: ``int`` is an
-Erlang integer (int64 range), ``str`` an atom, ``bytes`` a binary.  Keys the
-reference would pass through term_to_binary (tuples, lists, ...) are outside
-the device domain and raise ``TypeError``.
+Keys on the device path are (type, bytes) (src/synctree.erl:261-268):
+integers in int64 -> <<K:64/big>>, atoms -> atom_to_binary(K, utf8),
+binaries -> themselves, and every other key (tuples, lists, floats, integers
+outside int64) -> term_to_binary(K) (ST_KEY_TERM; the device derives the
+order-preserving record, riak_ensemble_amd/csrc/term_key.h).  In Python:
+``int`` is an Erlang integer, ``float`` a float, ``str`` an atom, ``bytes`` a
+binary, ``tuple`` a tuple and ``list`` a proper list.
+
+term_to_binary here writes what ERTS writes with default options: atoms in
+the form of the configured OTP era (:data:`ETF_ATOMS`: ``'latin1'`` = before
+OTP 26, ATOM_EXT for Latin-1 atoms -- the reference's era; ``'utf8'`` = OTP
+26+), floats as NEW_FLOAT_EXT (OTP 17+), lists of bytes as STRING_EXT.
 
 Atoms returned by the API are plain strings: ``'notfound'``,
 ``'undefined'``, ``'$none'``; corruption is the tuple
 ``('corrupted', Level, Bucket)``.
 """
+import ctypes
+import struct
+
 import numpy as np
 
 from . import _lib
@@ -22,20 +31,144 @@ CORRUPTED = 'corrupted'
 
 _I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
 
+ETF_ATOMS = 'latin1'
+
+
+def _etf(t, out, atoms):
+    if isinstance(t, bool):
+        raise TypeError('Python bools are not Erlang terms (use the atoms "true"/"false")')
+    if isinstance(t, int):
+        if 0 <= t <= 255:
+            out += bytes([97, t])
+        elif -(1 << 31) <= t < (1 << 31):
+            out += b'b' + struct.pack('>i', t)
+        else:
+            m = abs(t)
+            mag = m.to_bytes((m.bit_length() + 7) // 8, 'little')
+            sign = 1 if t < 0 else 0
+            if len(mag) <= 255:
+                out += bytes([110, len(mag), sign]) + mag
+            else:
+                out += bytes([111]) + struct.pack('>I', len(mag)) + bytes([sign]) + mag
+    elif isinstance(t, float):
+        out += b'F' + struct.pack('>d', t)
+    elif isinstance(t, str):
+        if len(t) > 255:
+            raise TypeError('atom longer than 255 characters (system_limit)')
+        if atoms == 'latin1' and all(ord(c) < 256 for c in t):
+            b = t.encode('latin-1')
+            out += bytes([100]) + struct.pack('>H', len(b)) + b
+        else:
+            b = t.encode('utf-8')
+            out += (bytes([119, len(b)]) if len(b) < 256 else bytes([118]) + struct.pack('>H', len(b))) + b
+    elif isinstance(t, (bytes, bytearray, memoryview)):
+        b = bytes(t)
+        out += bytes([109]) + struct.pack('>I', len(b)) + b
+    elif isinstance(t, tuple):
+        out += bytes([104, len(t)]) if len(t) <= 255 else bytes([105]) + struct.pack('>I', len(t))
+        for e in t:
+            _etf(e, out, atoms)
+    elif isinstance(t, list):
+        if not t:
+            out += bytes([106])
+        elif len(t) <= 65535 and all(isinstance(e, int) and not isinstance(e, bool) and 0 <= e <= 255 for e in t):
+            out += bytes([107]) + struct.pack('>H', len(t)) + bytes(t)
+        else:
+            out += bytes([108]) + struct.pack('>I', len(t))
+            for e in t:
+                _etf(e, out, atoms)
+            out += bytes([106])
+    else:
+        raise TypeError('%r is not a term of the key domain (pids, ports, refs, funs, maps are not)' % (t,))
+
+
+def term_to_binary(t, atoms=None):
+    """ERTS term_to_binary/1 on the key domain (see the module doc)."""
+    out = bytearray([131])
+    _etf(t, out, atoms or ETF_ATOMS)
+    return bytes(out)
+
+
+def _dec(b, i):
+    tag = b[i]
+    i += 1
+    if tag == 97:
+        return b[i], i + 1
+    if tag == 98:
+        return struct.unpack_from('>i', b, i)[0], i + 4
+    if tag in (110, 111):
+        if tag == 110:
+            n, i = b[i], i + 1
+        else:
+            n, i = struct.unpack_from('>I', b, i)[0], i + 4
+        sign, i = b[i], i + 1
+        v = int.from_bytes(b[i:i + n], 'little')
+        return (-v if sign else v), i + n
+    if tag == 70:
+        return struct.unpack_from('>d', b, i)[0], i + 8
+    if tag == 99:
+        return float(b[i:i + 31].split(b'\0')[0].decode('ascii')), i + 31
+    if tag in (100, 115, 118, 119):
+        if tag in (100, 118):
+            n, i = struct.unpack_from('>H', b, i)[0], i + 2
+        else:
+            n, i = b[i], i + 1
+        raw = b[i:i + n]
+        return (raw.decode('latin-1') if tag in (100, 115) else raw.decode('utf-8')), i + n
+    if tag in (104, 105):
+        if tag == 104:
+            n, i = b[i], i + 1
+        else:
+            n, i = struct.unpack_from('>I', b, i)[0], i + 4
+        el = []
+        for _ in range(n):
+            e, i = _dec(b, i)
+            el.append(e)
+        return tuple(el), i
+    if tag == 106:
+        return [], i
+    if tag == 107:
+        n = struct.unpack_from('>H', b, i)[0]
+        return list(b[i + 2:i + 2 + n]), i + 2 + n
+    if tag == 108:
+        n, i = struct.unpack_from('>I', b, i)[0], i + 4
+        el = []
+        for _ in range(n):
+            e, i = _dec(b, i)
+            el.append(e)
+        tail, i = _dec(b, i)
+        if tail != []:
+            if isinstance(tail, list):
+                return el + tail, i
+            raise ValueError('improper lists have no Python form')
+        return el, i
+    if tag == 109:
+        n = struct.unpack_from('>I', b, i)[0]
+        return bytes(b[i + 4:i + 4 + n]), i + 4 + n
+    raise ValueError('ETF tag %d outside the key domain' % tag)
+
+
+def binary_to_term(b):
+    b = bytes(b)
+    if not b or b[0] != 131:
+        raise ValueError('not a term_to_binary encoding')
+    t, i = _dec(b, 1)
+    if i != len(b):
+        raise ValueError('trailing bytes')
+    return t
+
 
 def key_parts(key):
-    """(ST_KEY_*, ensure_binary bytes)."""
+    """(ST_KEY_*, bytes): ensure_binary bytes, or term_to_binary for ST_KEY_TERM."""
     if isinstance(key, bool):
         raise TypeError('Python bools are not Erlang keys (use the atoms "true"/"false")')
-    if isinstance(key, int):
-        if not _I64_MIN <= key <= _I64_MAX:
-            raise TypeError('integer key outside int64: the device path covers int64 keys')
+    if isinstance(key, int) and _I64_MIN <= key <= _I64_MAX:
         return _lib.ST_KEY_INT, (key & 0xFFFFFFFFFFFFFFFF).to_bytes(8, 'big')
     if isinstance(key, str):
         return _lib.ST_KEY_ATOM, key.encode('utf-8')
     if isinstance(key, (bytes, bytearray, memoryview)):
         return _lib.ST_KEY_BINARY, bytes(key)
-    raise TypeError('key %r needs term_to_binary (outside the device key domain)' % (key,))
+    return _lib.ST_KEY_TERM, term_to_binary(key)
 
 
 def key_from_parts(kt, kb):
@@ -43,16 +176,27 @@ def key_from_parts(kt, kb):
         return int.from_bytes(kb, 'big', signed=True)
     if kt == _lib.ST_KEY_ATOM:
         return kb.decode('utf-8')
+    if kt == _lib.ST_KEY_TERM:
+        return binary_to_term(kb)
     return bytes(kb)
 
 
 def order_key(key):
-    """A bytes key whose lexicographic order is Erlang term order on the domain
-    (the same record encoding the device sorts by)."""
+    """The device key record of `key` (bytes): their lexicographic order is
+    Erlang term order (riak_ensemble_amd/csrc/term_key.h)."""
     kt, kb = key_parts(key)
     if kt == _lib.ST_KEY_INT:
-        return bytes([kt, kb[0] ^ 0x80]) + kb[1:]
-    return bytes([kt]) + kb
+        return bytes([0x10, kb[0] ^ 0x80]) + kb[1:]
+    if kt == _lib.ST_KEY_ATOM:
+        return b'\x20' + kb
+    if kt == _lib.ST_KEY_BINARY:
+        return b'\x50' + kb
+    L = _lib.load()
+    n = ctypes.c_uint64()
+    _lib.check(L.st_key_record(kt, kb, len(kb), None, 0, ctypes.byref(n)), 'st_key_record')
+    buf = ctypes.create_string_buffer(int(n.value))
+    _lib.check(L.st_key_record(kt, kb, len(kb), buf, n.value, ctypes.byref(n)), 'st_key_record')
+    return buf.raw
 
 
 def pack_keys(keys):

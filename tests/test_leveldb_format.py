@@ -35,11 +35,35 @@ import synctree_ref as R
     (b'', [131, 109, 0, 0, 0, 0]),
     ([], [131, 106]),
     ([(1, b'\x00')], [131, 108, 0, 0, 0, 1, 104, 2, 97, 1, 109, 0, 0, 0, 1, 0, 106]),
-    ('foo', [131, 119, 3, 102, 111, 111]),
+    ('foo', [131, 100, 0, 3, 102, 111, 111]),          # ATOM_EXT: before OTP 26 (the reference's era)
+    ('é', [131, 100, 0, 1, 0xE9]),
+    ((1, 'a'), [131, 104, 2, 97, 1, 100, 0, 1, 97]),
+    ([1, 2, 3], [131, 107, 0, 3, 1, 2, 3]),            # STRING_EXT
+    ([1, -1], [131, 108, 0, 0, 0, 2, 97, 1, 98, 255, 255, 255, 255, 106]),
+    (1.5, [131, 70, 0x3F, 0xF8, 0, 0, 0, 0, 0, 0]),     # NEW_FLOAT_EXT
+    ((), [131, 104, 0]),
 ])
 def test_term_to_binary_known_answers(term, expected):
     assert LR.term_to_binary(term) == bytes(expected)
     assert LR.binary_to_term(bytes(expected)) == term
+    # the product's host encoder (riak_ensemble_amd.terms, an independent
+    # restatement) writes the same bytes
+    from riak_ensemble_amd import terms
+    assert terms.term_to_binary(term) == bytes(expected)
+    assert terms.binary_to_term(bytes(expected)) == term
+
+
+@pytest.mark.parametrize('term,expected', [
+    ('foo', [131, 119, 3, 102, 111, 111]),              # SMALL_ATOM_UTF8_EXT: OTP 26+
+    ('é', [131, 119, 2, 0xC3, 0xA9]),
+    ((1, 'a'), [131, 104, 2, 97, 1, 119, 1, 97]),
+])
+def test_term_to_binary_otp26_atoms(term, expected, monkeypatch):
+    from riak_ensemble_amd import terms
+    monkeypatch.setattr(R, 'ETF_ATOMS', 'utf8')
+    monkeypatch.setattr(terms, 'ETF_ATOMS', 'utf8')
+    assert LR.term_to_binary(term) == bytes(expected)
+    assert terms.term_to_binary(term) == bytes(expected)
 
 
 def test_binary_to_term_old_atoms_and_errors():

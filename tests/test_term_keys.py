@@ -1,0 +1,162 @@
+"""term_to_binary keys (synctree.erl:261-268): tuples,
+lists, floats and integers outside int64.  The host passes
+term_to_binary(Key) (ST_KEY_TERM); the library derives an order-preserving
+record (riak_ensemble_amd/csrc/term_key.h) whose memcmp order is Erlang term
+order, and hashes term_to_binary(Key) -- or <<Key:64>> for an integer -- for
+the segment.
+
+CPU: the record order against the Python restatement's term order
+(oracle/synctree_ref.py term_key, the checker) over random nested terms;
+ETF round trips.  GPU: trees of mixed keys built through the device path
+against synctree_ref (top hash, every level's entries, get, exchange_get,
+ordered compare), through both the small-batch and the bulk path."""
+import random
+
+import numpy as np
+import pytest
+
+import synctree_ref as R
+from riak_ensemble_amd import terms
+
+
+def rand_atom(rng):
+    pool = ['a', 'b', 'ab', 'abc', 'z', 'é', 'ñandú', 'xÿ', '中', 'true', '', 'a\u0000b']
+    return rng.choice(pool) if rng.random() < 0.7 else ''.join(rng.choice('abcxyz') for _ in range(rng.randint(1, 6)))
+
+
+def rand_term(rng, depth=0):
+    r = rng.random()
+    leaf = depth >= 3 or r < 0.55
+    if leaf:
+        k = rng.randrange(9)
+        if k == 0:
+            return rng.randint(-300, 300)
+        if k == 1:
+            return rng.choice([(1 << 63) - 1, -(1 << 63), (1 << 31), -(1 << 31) - 1, 0])
+        if k == 2:   # bignums, both signs
+            return rng.choice([1, -1]) * rng.randint(1 << 63, 1 << rng.choice([64, 70, 100, 200]))
+        if k == 3:   # non-integral floats
+            return rng.choice([-1, 1]) * (rng.randint(0, 1 << 20) + rng.choice([0.5, 0.25, 0.1, 1e-9]))
+        if k == 4:   # floats beyond int64 (integral)
+            return rng.choice([-1.0, 1.0]) * 2.0 ** rng.randint(64, 300) * (1 + rng.random())
+        if k == 5:
+            return rand_atom(rng)
+        if k == 6:
+            return bytes(rng.choice([0, 1, 97, 255]) for _ in range(rng.randint(0, 5)))
+        if k == 7:
+            return []
+        return rng.randint(0, 255)
+    if r < 0.8:
+        return tuple(rand_term(rng, depth + 1) for _ in range(rng.randint(0, 4)))
+    if rng.random() < 0.3:   # a "string"
+        return [rng.randint(0, 255) for _ in range(rng.randint(1, 5))]
+    return [rand_term(rng, depth + 1) for _ in range(rng.randint(1, 4))]
+
+
+def distinct_terms(n, seed):
+    rng = random.Random(seed)
+    out, seen = [], set()
+    while len(out) < n:
+        t = rand_term(rng)
+        k = repr(R.term_key(t))
+        if k in seen:
+            continue
+        seen.add(k)
+        out.append(t)
+    return out
+
+
+def test_etf_round_trip_and_parts():
+    for t in distinct_terms(500, 1):
+        b = terms.term_to_binary(t)
+        assert b == R.term_to_binary(t), t        # two independent restatements agree
+        assert terms.binary_to_term(b) == t
+        kt, kb = terms.key_parts(t)
+        assert terms.key_from_parts(kt, kb) == t
+
+
+def test_key_record_order_is_erlang_term_order():
+    """memcmp order of the library's key records (st_key_record: host code,
+    no device) == Erlang term order of the restatement, for nested terms of
+    every supported type, plain keys included."""
+    ts = distinct_terms(3000, 2) + [0, -1, 1, 255, 256, 'a', b'a', (), [], [[]], {0: 1}.get(0), 1.5, -1.5]
+    # no two keys equal as Erlang numbers (1 vs 1.0 are distinct records here: DESIGN.md)
+    uniq = {}
+    for t in ts:
+        uniq.setdefault(repr(R.term_key(t)), t)
+    ts = list(uniq.values())
+    by_erlang = sorted(ts, key=R.term_key)
+    by_record = sorted(ts, key=terms.order_key)
+    bad = [(a, b) for a, b in zip(by_erlang, by_record) if a != b or type(a) != type(b)]
+    assert not bad, bad[:5]
+    # plain-domain keys keep their short records
+    assert terms.order_key(5) == bytes([0x10, 0x80, 0, 0, 0, 0, 0, 0, 5])
+    assert terms.order_key('ab') == b'\x20ab'
+    assert terms.order_key(b'ab') == b'\x50ab'
+
+
+def test_term_key_rejects_outside_domain():
+    with pytest.raises(TypeError):
+        terms.key_parts(True)
+    with pytest.raises(TypeError):
+        terms.key_parts({1: 2})
+    from riak_ensemble_amd import _lib
+    # a malformed ETF is refused by the library (ST_EINVAL)
+    with pytest.raises(ValueError):
+        import ctypes
+        n = ctypes.c_uint64()
+        _lib.check(_lib.load().st_key_record(3, b'\x83\x68\x02\x61', 4, None, 0, ctypes.byref(n)), 'st_key_record')
+
+
+def test_bignum_segment_is_low_64_bits():
+    """ensure_binary(Integer) = <<Key:64>> even for bignums: the segment of
+    2^64 + 5 is the segment of 5 (synctree.erl:261-262)."""
+    assert R.get_segment((1 << 64) + 5, 1 << 20) == R.get_segment(5, 1 << 20)
+    assert R.get_segment(-(1 << 64) - 1, 1 << 20) == R.get_segment(-1, 1 << 20)
+
+
+# ------------------------------------------------------------------ GPU
+def _ref_tree(keys, vals, width, segments):
+    t = R.new(b'ref', width, segments)
+    for k, v in zip(keys, vals):
+        t = R.insert(k, v, t)
+    return t
+
+
+def _val(i):
+    return bytes([0]) + (1).to_bytes(8, 'big') + i.to_bytes(8, 'big')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('geom,n,batch', [((16, 256), 3000, 4096), ((16, 256), 600, 16), ((16, 1 << 20), 2000, 4096),
+                                          ((4, 64), 800, 7)])
+def test_term_keys_device_parity(geom, n, batch):
+    from riak_ensemble_amd import synctree_hip
+    W, S = geom
+    keys = distinct_terms(n, 10 + n) + [5, -7, 'atom', b'bin', (1 << 64) + 5, 5.5]
+    vals = [_val(i) for i in range(len(keys))]
+    ref = _ref_tree(keys, vals, W, S)
+    dev = synctree_hip.DeviceTree(W, S)
+    for i in range(0, len(keys), batch):
+        st = dev.insert_batch(keys[i:i + batch], vals[i:i + batch])
+        assert all(x is None for x in st)
+    assert dev.top_hash() == R.top_hash(ref)
+    H = R.height(ref)
+    for lvl in range(1, H + 2):
+        buckets = list(range(min(W ** (lvl - 1), 4096)))
+        got = dev.exchange_get_batch(lvl, buckets)
+        exp = [R.exchange_get(lvl, b, ref) for b in buckets]
+        assert got == exp, 'level %d' % lvl
+    probe = keys[::7] + [(9, 9, 9), [1, 2, 3, 4, 5, 6], -(1 << 99)]
+    assert dev.get_batch(probe) == [R.get(k, ref) for k in probe]
+    # compare against a modified copy: diff order = descending segment, ascending Erlang term order
+    keys2 = keys[: n // 2] + distinct_terms(200, 99)
+    vals2 = [_val(i + 7) for i in range(len(keys2))]
+    ref2 = _ref_tree(keys2, vals2, W, S)
+    dev2 = synctree_hip.DeviceTree(W, S)
+    dev2.insert_batch(keys2, vals2)
+    res = dev.compare(dev2)
+    assert res[0] == 'ok'
+    assert [(k, v) for _, k, v in res[1]] == R.local_compare(ref, ref2)
+    dev.close()
+    dev2.close()
