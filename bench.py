@@ -743,6 +743,25 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
     return out
 
 
+def _host_cores():
+    """Host cores this process may use: the CPU quota of its cgroup (cpu.max),
+    else OMP_NUM_THREADS, else the affinity mask.  (On the GPU box the
+    affinity mask shows the whole machine while the job's share is 16.)"""
+    cands = []
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()[:2]
+        if q != 'max':
+            cands.append(max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get('OMP_NUM_THREADS', '').isdigit():
+        cands.append(int(os.environ['OMP_NUM_THREADS']))
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    cands.append(aff)
+    return max(1, min(cands))
+
+
 def _cpu_baseline(keys_h, vals_h, top0, reps=3):
     """The C port (oracle/synctree_oracle.c) rehashing the same 10M-key tree:
     (a) the reference-faithful DFS rehash (synctree.erl:497-543) on one host
@@ -751,7 +770,7 @@ def _cpu_baseline(keys_h, vals_h, top0, reps=3):
     About 10-20 s of CPU work in total."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import oracle_c
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else os.cpu_count()
+    ncpu = _host_cores()
     t0 = time.perf_counter()
     ot = oracle_c.OTree().bulk_load_int64(keys_h, vals_h)
     load_s = time.perf_counter() - t0
@@ -778,8 +797,8 @@ def _cpu_baseline(keys_h, vals_h, top0, reps=3):
             'all_cores': {'value': round(n / bestp, 1), 'unit': 'keys/s', 'cores': ncpu, 'kind': 'port',
                           'seconds_per_rehash': round(bestp, 3),
                           'sample': 'ot_rehash_par: the same rehash level by level over flat entry arrays, every '
-                                    'level\'s nodes spread over %d OpenMP threads (host cores available to this '
-                                    'process), best of %d' % (ncpu, reps)}}
+                                    'level\'s nodes spread over %d OpenMP threads (the host cores this job may use: '
+                                    'cgroup quota / OMP_NUM_THREADS / affinity, the smallest), best of %d' % (ncpu, reps)}}
 
 
 if __name__ == '__main__':

@@ -282,10 +282,15 @@ int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_levels, uin
  * node {Level, Bucket}, key <<0, TreeId/binary, Level:8,
  * (binary:encode_unsigned(Bucket))/binary>> (synctree_leveldb.erl:104-109),
  * value term_to_binary(Node) (:134-152): the 17-byte top hash at {0,0},
- * [{ChildId, Hash17}] for inner nodes, [{Key, Value}] for segments.  Nodes
- * the device holds as empty are not written (rehash/1 deletes them,
- * synctree.erl:529-531).  Records are in (Level, Bucket) order.  Atoms are
- * written in the UTF-8 forms (SMALL_)ATOM_UTF8_EXT of term_to_binary. */
+ * [{ChildId, Hash17}] for inner nodes, [{Key, Value}] for segments.  Empty
+ * nodes are not written (rehash/1 deletes them, synctree.erl:529-531) unless
+ * their own entry is still present -- the [] record a raw store or corrupt/2
+ * leaves (synctree.erl:246-247) until the next rehash.  Records are in
+ * (Level, Bucket) order.  Atom keys: ATOM_EXT for Latin-1 atoms as
+ * term_to_binary writes them before OTP 26 (default), or the UTF-8 forms
+ * (st_set_etf_atoms); term keys: the caller's term_to_binary bytes.  A
+ * checkpoint into an existing DB must also delete the tree's records that
+ * the new snapshot no longer holds. */
 typedef struct st_kv {
     uint64_t n;          /* records */
     uint64_t *koff;      /* n+1 */
@@ -310,8 +315,9 @@ int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, uint32_t id_l
  * leaves that node absent, as fetch/3 answers Default for it
  * (synctree_leveldb.erl:111-123), and counts in *n_skipped.  A decodable node
  * the device cannot hold (non-17-byte hashes, child ids outside the node,
- * keys outside the int64/atom/binary domain, non-binary values, unsorted
- * orddicts, compressed terms) returns ST_EINVAL and changes nothing. */
+ * keys outside the int64/atom/binary domain -- term keys are restored with
+ * st_store_segment --, non-binary values, unsorted orddicts, compressed
+ * terms) returns ST_EINVAL and changes nothing. */
 int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t n, const uint8_t *kheap,
                        const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff, uint64_t *n_loaded,
                        uint64_t *n_skipped);

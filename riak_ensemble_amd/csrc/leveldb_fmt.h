@@ -192,6 +192,10 @@ __global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64
                 const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
                 if (e1 > e0) { p = 1; vl = 7 + eo[e1] - eo[e0]; }
             }
+            // an empty node whose own entry is still present: the [] record a
+            // raw store / corrupt/2 leaves until the next rehash deletes it
+            // (synctree.erl:246-247 vs :529-531)
+            if (!p && (t.tag[r] & TAG_PRESENT)) { p = 1; vl = 2; }
             if (p) kl = 2 + idlen + enc_unsigned_len(b);
         }
         pres[r] = p; klen[r] = kl; vlen[r] = vl;
@@ -232,6 +236,7 @@ __global__ void k_snap_write(DevTree t, const uint8_t *id, uint32_t idlen, uint6
             const uint64_t c0 = t.base[L + 1] + b * t.W;
             uint32_t cnt = 0;
             for (uint32_t j = 0; j < t.W; j++) cnt += (t.tag[c0 + j] & TAG_PRESENT) ? 1 : 0;
+            if (!cnt) { v[1] = 106; continue; }   // []
             v[1] = 108; v = etf_u32be(v + 2, cnt);
             for (uint32_t j = 0; j < t.W; j++) {
                 const uint16_t tg = t.tag[c0 + j];
@@ -249,6 +254,7 @@ __global__ void k_snap_write(DevTree t, const uint8_t *id, uint32_t idlen, uint6
             continue;
         }
         const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
+        if (e1 == e0) { v[1] = 106; continue; }   // []
         v[1] = 108; v = etf_u32be(v + 2, (uint32_t)(e1 - e0));
         v[eo[e1] - eo[e0]] = 106;
     }

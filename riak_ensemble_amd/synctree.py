@@ -89,6 +89,30 @@ def checkpoint(t, tree_id=b''):
     return _device_state(t).snapshot_leveldb(tree_id)
 
 
+def checkpoint_into(t, db, tree_id=b''):
+    """Checkpoint tree t into an existing DB (a dict standing in for the peer's
+    LevelDB): one write batch that deletes this tree's records the new
+    snapshot no longer holds -- nodes emptied and deleted by rehash since the
+    last checkpoint (synctree.erl:529-531) -- and puts every record of the
+    snapshot.  Returns the number of deletes."""
+    recs = checkpoint(t, tree_id)
+    new_keys = {k for k, _ in recs}
+    prefix = bytes([0]) + bytes(tree_id)
+    height = _device_state(t).height
+    stale = [k for k in db if k.startswith(prefix) and k not in new_keys and _is_tree_key(k, prefix, height)]
+    for k in stale:
+        del db[k]
+    db.update(recs)
+    return len(stale)
+
+
+def _is_tree_key(k, prefix, height):
+    """Could db_key(Id, Level, Bucket) of this tree have produced k?
+    (<<0, Id, Level:8, encode_unsigned(Bucket)>>, synctree_leveldb.erl:104-109)"""
+    rest = k[len(prefix):]
+    return len(rest) >= 2 and rest[0] <= height + 1 and (len(rest) == 2 or rest[1] != 0)
+
+
 def new(id_=None, width='default', segments='default', mod=synctree_hip, opts=()):
     """synctree.erl:135-170 (+ reload_top_hash, 172-175)."""
     if width == 'default':

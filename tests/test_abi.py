@@ -49,3 +49,14 @@ def test_error_codes_map_to_exceptions():
     with pytest.raises(_lib.DeviceError):
         _lib.check(_lib.ST_EDEVICE, 'x')
     assert _lib.check(_lib.ST_CORRUPTED) == _lib.ST_CORRUPTED
+
+
+def test_library_is_built_from_current_sources():
+    """The in-tree .so is newer than every source it is built from (a stale
+    build would test old kernels)."""
+    import glob
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, 'riak_ensemble_amd', 'libsynctree_hip.so')
+    srcs = glob.glob(os.path.join(root, 'riak_ensemble_amd', 'csrc', '*'))
+    stale = [s for s in srcs if os.path.getmtime(s) > os.path.getmtime(lib) + 1]
+    assert not stale, 'rebuild (make): %s' % stale

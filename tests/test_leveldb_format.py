@@ -275,3 +275,43 @@ def test_newdb_reopens_checkpoint_like_synctree_leveldb():
     t = S.insert(7, b'new', t)
     o2 = R.insert(7, b'new', o2)
     assert dict(S.checkpoint(t, b'p')) == LR.tree_records(o2.modstate.db, b'p')
+
+
+@pytest.mark.gpu
+def test_checkpoint_into_tracks_corrupt_and_rehash():
+    """a checkpoint into the same DB after corrupt/2 empties a
+    segment holds its [] record (synctree.erl:246-247); after rehash/1 the
+    record is gone (deleted, :529-531) -- in both cases the DB equals the
+    oracle's synctree_leveldb DB, and reopening it answers like the oracle."""
+    from riak_ensemble_amd import synctree as S
+    LR.reset_dbs()
+    keys = list(range(1, 3001))
+    vals = [(k * 10).to_bytes(8, 'big') for k in keys]
+    o, d = _pair(keys, vals, width=16, segments=4096, tid=b'c')
+    segs = {}
+    for k in keys:
+        segs.setdefault(R.get_segment(k, 4096), []).append(k)
+    lone = next(ks[0] for ks in segs.values() if len(ks) == 1)      # a segment with one key
+    pair = next(ks for ks in segs.values() if len(ks) >= 2)         # and one that keeps keys
+    db = {}
+    assert S.checkpoint_into(d, db, b'c') == 0
+    assert db == LR.tree_records(o.modstate.db, b'c')
+    for k in (lone, pair[0]):
+        o = R.corrupt(k, o)
+        d = S.corrupt(k, d)
+    assert S.checkpoint_into(d, db, b'c') == 0
+    assert db == LR.tree_records(o.modstate.db, b'c')
+    empty = LR.db_key(b'c', o.height + 1, R.get_segment(lone, 4096))
+    assert db[empty] == b'\x83j'                                     # the [] record
+    # reopen the corrupted checkpoint: same answers as the oracle on its DB
+    t2 = S.new(None, 16, 4096)
+    t2.modstate.restore_leveldb(list(db.items()), b'c')
+    o2 = R.new(None, 16, 4096, 'synctree_leveldb', {'path': 'gpu', 'tree_id': b'c'})
+    probe = [lone, pair[0], pair[1], 5, 77]
+    assert t2.modstate.get_batch(probe) == [R.get(k, o2) for k in probe]
+    assert t2.modstate.verify() == R.verify(o2) is False
+    o = R.rehash(o)
+    d = S.rehash(d)
+    n_del = S.checkpoint_into(d, db, b'c')
+    assert n_del >= 1 and empty not in db
+    assert db == LR.tree_records(o.modstate.db, b'c')
