@@ -1731,10 +1731,21 @@ struct TileInfo {
 
 // Per-tree pointers of a batched (multi-tree) rehash: trees of one geometry,
 // e.g. the ensembles one GPU hosts.
+// Mailbox of one inner-node entry that a climbing lane of another workgroup
+// (possibly on another XCD, behind another L2) reads: written and read with
+// agent-scope atomics, which are coherent across XCDs without a write-back of
+// the writer's L2 or an invalidate of the reader's.
+struct MailEntry {
+    unsigned long long lo, hi;
+    uint32_t tag, pad0;
+    uint64_t pad1;
+};
+
 struct TreeTiles {
     uint4 *md5;
     uint16_t *tag;
     uint32_t *cnt;
+    MailEntry *mail;
     const TileInfo *tinfo;
     const uint32_t *tseg, *tnb;
     const uint4 *tiles;
@@ -1886,16 +1897,6 @@ __host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return levels3_
 
 // STAMP (diagnostic, ST_LEVEL_STAMPS=1): wall-clock stamps (100 MHz) per
 // workgroup at phase boundaries into stamps[blockIdx.x * 8 + k].
-// Mailbox of one inner-node entry that a climbing lane of another workgroup
-// (possibly on another XCD, behind another L2) reads: written and read with
-// agent-scope atomics, which are coherent across XCDs without a write-back of
-// the writer's L2 or an invalidate of the reader's.
-struct MailEntry {
-    unsigned long long lo, hi;
-    uint32_t tag, pad0;
-    uint64_t pad1;
-};
-
 __device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg) {
     __hip_atomic_store(&m->lo, ((unsigned long long)e.y << 32) | e.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&m->hi, ((unsigned long long)e.w << 32) | e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1909,11 +1910,20 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
     e = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-template <bool STAMP>
-__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, uint32_t *cnt, MailEntry *mail,
-                                                       uint64_t root0, uint32_t lmin, uint64_t *stamps) {
+// GROUP: the windows of many trees of one geometry in one launch (the
+// ensembles one GPU hosts, riak_ensemble_peer.erl:1845-1846): workgroup g
+// takes window g % nwin of tree group[g / nwin], each tree with its own slot
+// arrays, tiles, counters and mailboxes.
+template <bool STAMP, bool GROUP>
+__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
+                                                       uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
 #define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     RF_STAMP(0);
+    const uint32_t gi = GROUP ? blockIdx.x / nwin : 0;
+    const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
+    // the tree's arrays, read where used (kernel arguments, or the group
+    // entry through the scalar cache): no long-lived pointer registers
+#define RFT(f) (GROUP ? group[gi].f : tt0.f)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *A = lds;
     uint8_t *At = A + 256 * NB16;
@@ -1926,7 +1936,6 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
     // block stream below then runs on the scalar unit with scalar branches
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t H = t.H;
-    const uint64_t root = root0 + blockIdx.x;
     const uint64_t seg0 = root * 4096;
 
     // ---- phase 1: K1 over this wave's tiles, one flat block stream
@@ -1937,13 +1946,13 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
 #pragma unroll
     for (int q = 0; q < RF_TILES; q++) {
         const uint64_t tl = root * 64 + wave + 16 * q;
-        const TileInfo ti = tt.tinfo[tl];
+        const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
         const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ti.base),
                        bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ti.base >> 32));
         bq[q] = ((uint64_t)bhi << 32) | blo;
-        liq[q] = (uint32_t)(tt.tseg[tl * 64 + lane] - seg0);
-        nbq[q] = tt.tnb[tl * 64 + lane];
+        liq[q] = (uint32_t)(RFT(tseg)[tl * 64 + lane] - seg0);
+        nbq[q] = RFT(tnb)[tl * 64 + lane];
         P[q + 1] = P[q] + Bq[q];
     }
     const uint32_t T = P[RF_TILES];
@@ -1963,8 +1972,8 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
     {
         uint4 r0a, r0b, r0c, r0d, r1a, r1b, r1c, r1d;
         uint32_t q, k;
-        if (T > 0) { locate(0, q, k); tile_block_load(tt.tiles, pick64(bq, q), lane, k, r0a, r0b, r0c, r0d); }
-        if (T > 1) { locate(1, q, k); tile_block_load(tt.tiles, pick64(bq, q), lane, k, r1a, r1b, r1c, r1d); }
+        if (T > 0) { locate(0, q, k); tile_block_load(RFT(tiles), pick64(bq, q), lane, k, r0a, r0b, r0c, r0d); }
+        if (T > 1) { locate(1, q, k); tile_block_load(RFT(tiles), pick64(bq, q), lane, k, r1a, r1b, r1c, r1d); }
         uint32_t st[4];
         stmd5::init(st);
         for (uint32_t f = 0; f < T; f++) {
@@ -1974,7 +1983,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
             if (f + 2 < T) {
                 uint32_t q2, k2;
                 locate(f + 2, q2, k2);
-                tile_block_load(tt.tiles, pick64(bq, q2), lane, k2, r1a, r1b, r1c, r1d);
+                tile_block_load(RFT(tiles), pick64(bq, q2), lane, k2, r1a, r1b, r1c, r1d);
             }
             locate(f, q, k);
             const uint32_t nb = pick(nbq, q);
@@ -1997,8 +2006,8 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
 #pragma unroll
         for (int it = 0; it < 4; it++) {
             const uint32_t i = it * 1024 + tid;
-            t.md5[c0 + i] = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
-            t.tag[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
+            (GROUP ? group[gi].md5 : t.md5)[c0 + i] = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
+            (GROUP ? group[gi].tag : t.tag)[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
         }
     }
     __syncthreads();
@@ -2020,14 +2029,14 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
             uint32_t tg;
             node16_any(ent, tgs, reg, e, tg);
             const uint64_t slot = t.base[l] + b;
-            if (tg) t.md5[slot] = e;
-            t.tag[slot] = (uint16_t)tg;
-            if (l == 1) { t.md5[0] = e; t.tag[0] = (uint16_t)tg; }
+            if (tg) (GROUP ? group[gi].md5 : t.md5)[slot] = e;
+            (GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
+            if (l == 1) { (GROUP ? group[gi].md5 : t.md5)[0] = e; (GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
             if (phase < 2) {
                 *reinterpret_cast<uint4 *>(nxE) = e;
                 *reinterpret_cast<uint16_t *>(nxT) = (uint16_t)tg;
             } else if (l > lmin) {
-                mail_put(mail + slot, e, tg);   // read by the climbing lane of another workgroup
+                mail_put(RFT(mail) + slot, e, tg);   // read by the climbing lane of another workgroup
             }
         }
         if (phase < 2) {
@@ -2052,7 +2061,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
         if (phase == 2) RF_STAMP(5);
         if (tid != 0 || l <= lmin) break;
         const uint64_t p = b >> 4;
-        uint32_t *c = cnt + t.base[l - 1] + p;
+        uint32_t *c = RFT(cnt) + t.base[l - 1] + p;
         // the mailbox stores above have completed (agent-coherent) before the
         // counter moves; no L2 write-back / invalidate is needed
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2066,7 +2075,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
         uint4 h[16];
         uint16_t g[16];
 #pragma unroll
-        for (int j = 0; j < 16; j++) mail_get(mail + cc + j, h[j], g[j]);
+        for (int j = 0; j < 16; j++) mail_get(RFT(mail) + cc + j, h[j], g[j]);
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             *reinterpret_cast<uint4 *>(Cb + j * 16) = h[j];
@@ -2076,6 +2085,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt, 
         tgs = reinterpret_cast<const uint16_t *>(Ct);
         RF_STAMP(6 + (l == 1));
     }
+#undef RFT
 #undef RF_STAMP
 }
 
@@ -2144,18 +2154,15 @@ __device__ __forceinline__ void tile_store(const DevTree &t, uint4 *md5, uint16_
     if (L1 == 1) { md5[0] = e; tag[0] = TAG_PRESENT; }
 }
 
-// Persistent K1: wave w hashes global tiles w, w + nw, ...; GROUP: global
-// tile g is tile g % ntpt of tree g / ntpt (trees[]), else all tiles belong
-// to `one`.
-template <bool GROUP>
-__global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTiles one, const TreeTiles *__restrict__ trees,
-                                                              uint64_t ntpt, uint64_t ntiles) {
+// Persistent K1 (geometries the fused kernel does not cover): wave w hashes
+// tiles w, w + nw, ... of `one`.
+__global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTiles one, uint64_t ntiles) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * 4;
     uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= ntiles) return;
-    TreeTiles cur = GROUP ? trees[g / ntpt] : one;
-    uint64_t tl = GROUP ? g % ntpt : g;
+    TreeTiles cur = one;
+    uint64_t tl = g;
     TileInfo ti = cur.tinfo[tl];
     uint32_t seg = cur.tseg[tl * 64 + lane], nb = cur.tnb[tl * 64 + lane];
     uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
@@ -2171,8 +2178,7 @@ __global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTil
         tn.base = 0; tn.B = 0; tn.pad = 0;
         uint32_t segn = 0xffffffffu, nbn = 0;
         if (gx < ntiles) {
-            if (GROUP) nxt = trees[gx / ntpt];
-            tn_l = GROUP ? gx % ntpt : gx;
+            tn_l = gx;
             tn = nxt.tinfo[tn_l];
             segn = nxt.tseg[tn_l * 64 + lane];
             nbn = nxt.tnb[tn_l * 64 + lane];
@@ -2205,21 +2211,6 @@ __global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTil
     }
 }
 
-// One inner level of a batch of trees (W == 16): node i is node i % per of
-// tree i / per.  Throughput form for many trees: every lane hashes one node
-// from global memory at full occupancy (st_rehash_group).
-__global__ void __launch_bounds__(64) k_level16_group(DevTree g, const TreeTiles *__restrict__ trees, uint32_t l,
-                                                      uint64_t per, uint64_t total) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
-    for (uint64_t i = gtid(); i < total; i += gstride()) {
-        DevTree t = g;
-        const TreeTiles &tt = trees[i / per];
-        t.md5 = tt.md5;
-        t.tag = tt.tag;
-        hash_node16(t, l, i % per, reg);
-    }
-}
 
 // Top-hash records of many trees into one device array, 18 bytes per tree
 // (present byte + the 17-byte hash): the payload of the cross-GPU all-gather

@@ -508,6 +508,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.md5 = t->md5;
     x.tag = t->tag;
     x.cnt = t->lvl_cnt;
+    x.mail = t->mail;
     x.tinfo = t->tinfo;
     x.tseg = t->tseg;
     x.tnb = t->tnb;
@@ -556,8 +557,8 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", k_rehash_fused<false>, nwg, 1024, fused_lds_bytes(), d, tree_tiles(t), t->lvl_cnt,
-                   t->mail, root0, lmin, (uint64_t *)nullptr);
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
@@ -565,8 +566,8 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 8));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 8 * 8, t->stream));
-        LAUNCH(t, "rehash_fused", k_rehash_fused<true>, nwg, 1024, fused_lds_bytes(), d, tree_tiles(t), t->lvl_cnt, t->mail,
-               root0, lmin, st);
+        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+               (const TreeTiles *)nullptr, 0u, root0, lmin, st);
         std::vector<uint64_t> h((uint64_t)nwg * 8);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipStreamSynchronize(t->stream));
@@ -585,8 +586,8 @@ static int rehash_tiled(st_tree *t) {
         return ST_OK;
     }
     const uint64_t ntl = num_tiles(t);
-    LAUNCH(t, "segment_hash", k_segment_hash_tiled_p<false>, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, 1024u), 256, 0, d,
-           tree_tiles(t), (const TreeTiles *)nullptr, ntl, ntl);
+    LAUNCH(t, "segment_hash", k_segment_hash_tiled_p, (uint32_t)std::min<uint64_t>((ntl + 3) / 4, 1024u), 256, 0, d,
+           tree_tiles(t), ntl);
     if (t->H == 0) return ST_OK;
     if (t->W == 16) return levels16(t, t->H, nullptr);
     return rehash_levels(t, t->H, nullptr);
@@ -1207,12 +1208,11 @@ extern "C" int st_rehash(st_tree *t, int upper) {
     return ST_OK;
 }
 
-// rehash/1 of n trees of one geometry (W == 16, H >= 3) as one batch: K1
-// over every tree's tiles (persistent waves, global tile index = tree x
-// tiles-per-tree + tile), then one k_level16_group launch per level over
-// every tree's nodes at full occupancy.  The latency-bound level chain is
-// paid once per batch instead of once per tree, and the level work runs as
-// throughput (many ensembles per GPU).
+// rehash/1 of n trees of one geometry (W == 16, H >= 3) as one batch: one
+// launch of the fused rehash over the windows of every tree (workgroup =
+// (tree, window)), each tree climbing to its own top hash.  The
+// latency-bound level chains of the trees overlap one another's K1 (SURVEY
+// §8d config 4: many ensembles per GPU).
 extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     if (n == 0) return ST_OK;
     st_tree *t = trees[0];
@@ -1229,35 +1229,25 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {
         CHK(flush_overlay(trees[i]));
         CHK(ensure_tiles(trees[i]));
+        CHK(ensure_lvl_cnt(trees[i]));
         HIPCHK(hipStreamSynchronize(trees[i]->stream));
     }
+    // every window of every tree in ONE launch of the fused kernel (K1 +
+    // levels + top per tree): the trees' tails overlap each other's K1
     std::vector<TreeTiles> h(n);
     for (uint32_t i = 0; i < n; i++) h[i] = tree_tiles(trees[i]);
+    Scratch sc(t);
     TreeTiles *dtt = nullptr;
-    CHK(dalloc_t(t, &dtt, n));
+    CHK(sc.alloc(&dtt, n));
     HIPCHK(hipMemcpyAsync(dtt, h.data(), n * sizeof(TreeTiles), hipMemcpyHostToDevice, t->stream));
-    DevTree d = view(t);
-    const uint64_t ntpt = num_tiles(t);
-    int r = ST_OK;
-    do {
-        // 7 waves per SIMD (1792 x 4 waves): small trees have mostly 1-block
-        // tiles, so the per-tile load chain, not MD5, bounds the batch
-        hipLaunchKernelGGL((k_segment_hash_tiled_p<true>), dim3((uint32_t)std::min<uint64_t>((ntpt * n + 3) / 4, 1792)),
-                           dim3(256), 0, t->stream, d, h[0], (const TreeTiles *)dtt, ntpt, ntpt * n);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) { g_err = std::string("launch segment_hash group: ") + hipGetErrorString(e); r = ST_EDEVICE; break; }
-        for (uint32_t l = t->H; l >= 1 && r == ST_OK; l--) {
-            const uint64_t per = t->base[l + 1] - t->base[l];
-            hipLaunchKernelGGL(k_level16_group, dim3(grid_for(per * n, 64, 65536)), dim3(64),
-                               (size_t)64 * lane_region_bytes(16), t->stream, d, (const TreeTiles *)dtt, l, per, per * n);
-            e = hipGetLastError();
-            if (e != hipSuccess) { g_err = std::string("launch level_rehash group: ") + hipGetErrorString(e); r = ST_EDEVICE; }
-        }
-    } while (0);
-    dfree(t, dtt);
+    const uint32_t nwin = (uint32_t)(t->S / 4096);
+    const uint64_t nwg = (uint64_t)nwin * n;
+    if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
+    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
+           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
     HIPCHK(hipStreamSynchronize(t->stream));
     for (uint32_t i = 0; i < n; i++) trees[i]->fresh = false;
-    return r;
+    return ST_OK;
 }
 
 extern "C" int st_verify(st_tree *t, int upper, int *ok) {
