@@ -710,13 +710,24 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
     st = [t.insert_batch([k], [newv])[0] for k in kl]
     gpu_ins_us = (time.perf_counter() - t0) / len(kl) * 1e6
     assert all(s is None for s in st), 'per-key insert rejected'
+    # the device part of those calls: the k_small kernel alone (HIP events)
+    kern_us = {}
+    for name, fn in (('get', lambda k: t.get_batch([k])), ('insert', lambda k: t.insert_batch([k], [newv]))):
+        t.set_timing(True)
+        t.kernel_stats('*reset*')
+        for k in kl[:50]:
+            fn(k)
+        launches, ms = t.kernel_stats('small')
+        t.set_timing(False)
+        kern_us[name] = round(ms / max(launches, 1) * 1e3, 1)
     t.close()
     out = {'gpu_keys_per_s': round(n / best, 1), 'gpu_ms': round(best * 1e3, 3),
            'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)',
            'per_key_latency_us': {'gpu_get': round(gpu_get_us, 1), 'gpu_insert': round(gpu_ins_us, 1),
+                                  'kernel_us': kern_us,
                                   'what': 'one get/2 or insert/3 per C-ABI call (verified path + dirty-path '
                                           'rehash on the device), 200 calls after a warm-up, ctypes overhead '
-                                          'included; results checked'}}
+                                          'included; results checked; kernel_us: the k_small kernel alone'}}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle_c

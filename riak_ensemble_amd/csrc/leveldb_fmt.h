@@ -170,8 +170,8 @@ __global__ void k_snap_entry_sizes(DevTree t, uint64_t n, uint64_t *es) {
 
 // Per record: present flag, key length, value length.  eo: exclusive scan of
 // k_snap_entry_sizes (n + 1 entries).
-__global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64_t *eo, uint64_t *pres, uint64_t *klen,
-                             uint64_t *vlen) {
+__global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64_t *eo, const uint8_t *erec,
+                             uint64_t *pres, uint64_t *klen, uint64_t *vlen) {
     for (uint64_t r = gtid(); r <= R; r += gstride()) {
         uint64_t p = 0, kl = 0, vl = 0;
         if (r == 0) {
@@ -192,10 +192,9 @@ __global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64
                 const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
                 if (e1 > e0) { p = 1; vl = 7 + eo[e1] - eo[e0]; }
             }
-            // an empty node whose own entry is still present: the [] record a
-            // raw store / corrupt/2 leaves until the next rehash deletes it
-            // (synctree.erl:246-247 vs :529-531)
-            if (!p && (t.tag[r] & TAG_PRESENT)) { p = 1; vl = 2; }
+            // an empty node the backend holds as [] (a raw store of [], or the
+            // segment a corrupt/2 emptied, synctree.erl:246-247)
+            if (!p && erec && erec[r]) { p = 1; vl = 2; }
             if (p) kl = 2 + idlen + enc_unsigned_len(b);
         }
         pres[r] = p; klen[r] = kl; vlen[r] = vl;
@@ -477,7 +476,7 @@ __global__ void k_rest_keys(DevTree t, const uint8_t *id, uint32_t idlen, uint64
 // segment is validated and sized (entries, key-record bytes, value bytes).
 __global__ void k_rest_nodes(DevTree t, uint64_t R, const unsigned long long *recof, const uint8_t *vh,
                              const uint64_t *vo, uint16_t *stag, uint4 *smd, uint64_t *ecnt, uint64_t *kcnt,
-                             uint64_t *vcnt, uint8_t *segok, unsigned long long *ctr) {
+                             uint64_t *vcnt, uint8_t *segok, uint8_t *serec, unsigned long long *ctr) {
     const uint64_t sb = t.base[t.H + 1];
     for (uint64_t r = gtid(); r < R; r += gstride()) {
         const bool seg = r >= sb;
@@ -519,6 +518,7 @@ __global__ void k_rest_nodes(DevTree t, uint64_t R, const unsigned long long *re
             good = good && !in.dom && in.end();
             if (in.dom) { rst_dom(ctr, r); continue; }
             if (!good) { atomicAdd(&ctr[RST_SKIPPED], 1ull); continue; }
+            if (cnt == 0) serec[r] = 1;      // a [] record
             DEtf w(first, vh + vo[i + 1]);   // second pass: store the validated children
             for (uint32_t j = 0; j < cnt; j++) {
                 int64_t c = 0;
@@ -548,6 +548,7 @@ __global__ void k_rest_nodes(DevTree t, uint64_t R, const unsigned long long *re
         if (!good) { atomicAdd(&ctr[RST_SKIPPED], 1ull); continue; }   // fetch/3 answers []
         ecnt[r - sb] = cnt; kcnt[r - sb] = kb; vcnt[r - sb] = vb;
         segok[r - sb] = 1;
+        if (cnt == 0) serec[r] = 1;
         atomicAdd(&ctr[RST_LOADED], 1ull);
     }
 }

@@ -473,3 +473,11 @@ __global__ void k_ov_gather(Overlay ov, uint64_t S, const uint64_t *eoff, const 
 __global__ void k_ov_terminate(uint64_t n, const uint64_t *ktot, const uint64_t *vtot, uint64_t *koff, uint64_t *voff) {
     if (gtid() == 0) { koff[n] = *ktot; voff[n] = *vtot; }
 }
+
+// After corrupt/2 (synctree.erl:241-247): if the key's segment is now empty
+// the backend holds [] for it (erec).  One thread.
+__global__ void k_erec_emptied(DevTree t, const uint8_t *krec, const uint64_t *koff, uint8_t *erec) {
+    if (threadIdx.x != 0) return;
+    const uint64_t s = record_segment(krec + koff[0], koff[1] - koff[0], t.S - 1);
+    if (t.seg_off[s] == t.seg_off[s + 1]) erec[t.base[t.H + 1] + s] = 1;
+}

@@ -1297,6 +1297,8 @@ __global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t 
             res[1] = mx;
             res[2] = em;
             __threadfence_system();
+            res[3] = 1;   // the host spins on this word
+            __threadfence_system();
         }
     }
     if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
@@ -1889,6 +1891,13 @@ __device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t bas
     a = q[0]; b = q[64]; c = q[128]; d = q[192];
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its global stores (those are read by later kernels or,
+// for the climb, published by an explicit vmcnt wait before the counter).
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // LDS of k_rehash_fused: the k_levels3_16 node blocks, then one 272-byte
 // message region per level-H node (a node's message may not be packed over its
 // own entries: they are read from LDS while the message is written).
@@ -1997,20 +2006,18 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         for (int q0 = 0; q0 < RF_TILES; q0++)
             if (Bq[q0] == 0) put_entry(liq[q0], 0, st);   // a tile of empty segments
     }
-    __syncthreads();
+    lds_barrier();
 
     RF_STAMP(1);
-    // ---- phase 2: the window's segment entries to the slot arrays, coalesced
-    {
+    // ---- phase 2: the window's segment entries to the slot arrays, coalesced,
+    // by waves 4..15 while waves 0..3 hash level H (phase 3) from the same LDS
+    if (tid >= 256) {
         const uint64_t c0 = t.base[H + 1] + seg0;
-#pragma unroll
-        for (int it = 0; it < 4; it++) {
-            const uint32_t i = it * 1024 + tid;
+        for (uint32_t i = tid - 256; i < 4096; i += 768) {
             (GROUP ? group[gi].md5 : t.md5)[c0 + i] = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
             (GROUP ? group[gi].tag : t.tag)[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
         }
     }
-    __syncthreads();
 
     RF_STAMP(2);
     // ---- phase 3: levels H, H-1, H-2 from LDS, then the climb
@@ -2040,7 +2047,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             }
         }
         if (phase < 2) {
-            __syncthreads();
+            lds_barrier();   // the next level reads this one's LDS entries only
             RF_STAMP(3 + phase);
             l--;
             if (phase == 0) {

@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
+#include <chrono>
 #include <map>
 #include <string>
 #include <vector>
@@ -66,6 +67,11 @@ struct st_tree {
     uint4 *md5 = nullptr;
     uint16_t *tag = nullptr;
     uint8_t *mark = nullptr, *ok = nullptr;
+    // erec[slot] = 1: the backend holds the [] record for this node (a raw
+    // store of [] or a corrupt/2 that emptied the segment, synctree.erl:
+    // 246-247); snapshots write it while the node is empty.  Allocated on
+    // first use.
+    uint8_t *erec = nullptr;
     uint32_t *flag = nullptr;
     unsigned long long *cnt64 = nullptr;
     // segment CSR
@@ -201,6 +207,21 @@ struct TimedLaunch {
         }                                                                         \
     } while (0)
 
+// Wait for a device-written flag in host-mapped memory (the kernel writes it
+// after a system-scope fence, last): a spin of a few microseconds instead of
+// a stream synchronisation call; after 5 ms fall back to the blocking sync
+// (which also reports a faulted kernel).
+static int wait_mapped(st_tree *t, volatile uint32_t *flag) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        if (*flag) return ST_OK;
+        if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+        __builtin_ia32_pause();
+    }
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
+}
+
 static int use_device(st_tree *t) {
     HIPCHK(hipSetDevice(t->device));
     return ST_OK;
@@ -324,7 +345,7 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
 extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
-    void *ps[] = {t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
+    void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
                   t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
@@ -521,6 +542,28 @@ static int ensure_lvl_cnt(st_tree *t) {
     CHK(dalloc_t(t, &t->mail, t->base[t->H - 1]));
     CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
     HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
+    return ST_OK;
+}
+
+static int ensure_erec(st_tree *t) {
+    if (t->erec) return ST_OK;
+    CHK(dalloc_t(t, &t->erec, t->nslots));
+    HIPCHK(hipMemsetAsync(t->erec, 0, t->nslots, t->stream));
+    return ST_OK;
+}
+
+static int set_erec(st_tree *t, uint64_t slot, uint8_t v) {
+    if (!t->erec && !v) return ST_OK;
+    CHK(ensure_erec(t));
+    HIPCHK(hipMemsetAsync(t->erec + slot, v, 1, t->stream));
+    return ST_OK;
+}
+
+// rehash/1 deletes every empty inner node (delete_existing_batch,
+// synctree.erl:529-531) but keeps a stored [] segment (its final level only
+// fetches, :510-513)
+static int erec_after_rehash(st_tree *t) {
+    if (t->erec && t->H >= 1) HIPCHK(hipMemsetAsync(t->erec + 1, 0, t->base[t->H + 1] - 1, t->stream));
     return ST_OK;
 }
 
@@ -897,7 +940,7 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     }
     t->sout->done = 0;
     LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev);
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(wait_mapped(t, &t->sout->done));
     if (!t->sout->done) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
     if (t->sout->retry) return ST_OK;
     *served = 1;
@@ -1057,6 +1100,12 @@ extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
         in.verify_rehash = false;
         r = ingest(t, in);
     }
+    if (!r) r = ensure_erec(t);
+    if (!r) {   // the segment it emptied now holds the [] record
+        hipLaunchKernelGGL(k_erec_emptied, dim3(1), dim3(64), 0, t->stream, view(t), (const uint8_t *)krec,
+                           (const uint64_t *)dko, t->erec);
+        if (hipGetLastError() != hipSuccess) { g_err = "launch erec_emptied"; r = ST_EDEVICE; }
+    }
     dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, bop);
     if (!r) HIPCHK(hipStreamSynchronize(t->stream));
     return r;
@@ -1123,6 +1172,7 @@ extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const 
         }
     }
     dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, dseg); dfree(t, rep); dfree(t, bop);
+    if (!r) r = set_erec(t, t->base[t->H + 1] + segment, n == 0 ? 1 : 0);
     if (!r) HIPCHK(hipStreamSynchronize(t->stream));
     return r;
 }
@@ -1154,6 +1204,7 @@ extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint3
     const uint64_t c0 = t->base[level + 1] + bucket * t->W;
     CHK(h2d(t, t->tag + c0, tags.data(), t->W * 2));
     CHK(h2d(t, t->md5 + c0, md.data(), t->W * 16));
+    CHK(set_erec(t, t->base[level] + bucket, n == 0 ? 1 : 0));
     HIPCHK(hipStreamSynchronize(t->stream));
     t->fresh = false;
     return ST_OK;
@@ -1161,8 +1212,11 @@ extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint3
 
 extern "C" int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket) {
     if (level == 0) return st_store_top(t, nullptr, 0);
-    if (level == t->H + 1) return st_store_segment(t, bucket, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
-    return st_store_inner(t, level, bucket, 0, nullptr, nullptr);
+    if (level == t->H + 1) CHK(st_store_segment(t, bucket, 0, nullptr, nullptr, nullptr, nullptr, nullptr));
+    else CHK(st_store_inner(t, level, bucket, 0, nullptr, nullptr));
+    CHK(set_erec(t, t->base[level] + bucket, 0));   // no record at all
+    HIPCHK(hipStreamSynchronize(t->stream));
+    return ST_OK;
 }
 
 extern "C" int st_store_top(st_tree *t, const uint8_t *hash17, int also_record) {
@@ -1204,6 +1258,7 @@ extern "C" int st_rehash(st_tree *t, int upper) {
     }
     if (upper) CHK(rehash_levels(t, t->H, nullptr));
     else CHK(rehash_all(t, nullptr));
+    CHK(erec_after_rehash(t));
     t->fresh = false;
     return ST_OK;
 }
@@ -1246,7 +1301,11 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
            (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
     HIPCHK(hipStreamSynchronize(t->stream));
-    for (uint32_t i = 0; i < n; i++) trees[i]->fresh = false;
+    for (uint32_t i = 0; i < n; i++) {
+        CHK(erec_after_rehash(trees[i]));
+        HIPCHK(hipStreamSynchronize(trees[i]->stream));
+        trees[i]->fresh = false;
+    }
     return ST_OK;
 }
 
@@ -1801,11 +1860,10 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
                         v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
         }
-        w.res[0] = w.res[1] = 0;
-        w.res[2] = 0;
+        w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
         LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4, 256, 0, w.nw, (const uint64_t *)w.wcnt,
                (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
-        HIPCHK(hipStreamSynchronize(t->stream));
+        CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
         const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
         if (e != ~0ull) {
             *status = ST_CORRUPTED;
@@ -2091,7 +2149,8 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
         (r = dalloc(t, (void **)&did, id_len + 1)) || (r = h2d(t, did, tree_id, id_len))) { done(); return r; }
     LAUNCH(t, "snap_entry_sizes", k_snap_entry_sizes, grid_for(ne + 1), 256, 0, d, ne, es);
     if ((r = exclusive_scan<uint64_t>(t, es, eo, ne + 1))) { done(); return r; }
-    LAUNCH(t, "snap_sizes", k_snap_sizes, grid_for(R + 1), 256, 0, d, id_len, R, (const uint64_t *)eo, pres, kl, vl);
+    LAUNCH(t, "snap_sizes", k_snap_sizes, grid_for(R + 1), 256, 0, d, id_len, R, (const uint64_t *)eo,
+           (const uint8_t *)t->erec, pres, kl, vl);
     if ((r = exclusive_scan<uint64_t>(t, pres, rank, R + 1)) || (r = exclusive_scan<uint64_t>(t, kl, ko, R + 1)) ||
         (r = exclusive_scan<uint64_t>(t, vl, vo, R + 1))) { done(); return r; }
     HIPCHK(hipMemcpyAsync(&tot[0], rank + R, 8, hipMemcpyDeviceToHost, t->stream));
@@ -2170,7 +2229,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     const uint64_t kin = n ? koff[n] - koff[0] : 0, vin = n ? voff[n] - voff[0] : 0;
     DevTree d = view(t);
     // staging: nothing of the tree changes until every record has decoded
-    uint8_t *dkh = nullptr, *dvh = nullptr, *did = nullptr, *segok = nullptr;
+    uint8_t *dkh = nullptr, *dvh = nullptr, *did = nullptr, *segok = nullptr, *serec = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr, *ec = nullptr, *kc = nullptr, *vc = nullptr;
     uint64_t *nso = nullptr, *kbase = nullptr, *vbase = nullptr, *nsvo = nullptr, *nko = nullptr, *nvo = nullptr;
     uint8_t *nkh = nullptr, *nvh = nullptr;
@@ -2178,7 +2237,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     uint16_t *stag = nullptr;
     uint4 *smd = nullptr;
     auto done = [&](bool keep_new) {
-        void *ps[] = {dkh, dvh, did, segok, dko, dvo, ec, kc, vc, kbase, vbase, recof, ctr, stag, smd};
+        void *ps[] = {dkh, dvh, did, segok, serec, dko, dvo, ec, kc, vc, kbase, vbase, recof, ctr, stag, smd};
         for (void *p : ps) dfree(t, p);
         if (!keep_new) { dfree(t, nso); dfree(t, nsvo); dfree(t, nko); dfree(t, nvo); dfree(t, nkh); dfree(t, nvh); }
     };
@@ -2197,6 +2256,8 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     RCHK(h2d(t, did, tree_id, id_len));
     RCHK(dalloc_t(t, &recof, R)); RCHK(dalloc_t(t, &ctr, 4)); RCHK(dalloc_t(t, &stag, R)); RCHK(dalloc_t(t, &smd, R));
     RCHK(dalloc_t(t, &ec, S + 1)); RCHK(dalloc_t(t, &kc, S + 1)); RCHK(dalloc_t(t, &vc, S + 1)); RCHK(dalloc_t(t, &segok, S));
+    RCHK(dalloc_t(t, &serec, R));
+    HIPCHK(hipMemsetAsync(serec, 0, R, t->stream));
     HIPCHK(hipMemsetAsync(recof, 0, R * 8, t->stream));
     HIPCHK(hipMemsetAsync(ctr, 0, 3 * 8, t->stream));
     HIPCHK(hipMemsetAsync(ctr + RST_DOMSLOT, 0xFF, 8, t->stream));
@@ -2208,7 +2269,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     if (n) LAUNCH(t, "rest_keys", k_rest_keys, grid_for(n), 256, 0, d, (const uint8_t *)did, id_len, n,
                   (const uint8_t *)dkh, (const uint64_t *)dko, recof);
     LAUNCH(t, "rest_nodes", k_rest_nodes, grid_for(R), 256, 0, d, R, (const unsigned long long *)recof,
-           (const uint8_t *)dvh, (const uint64_t *)dvo, stag, smd, ec, kc, vc, segok, ctr);
+           (const uint8_t *)dvh, (const uint64_t *)dvo, stag, smd, ec, kc, vc, segok, serec, ctr);
     unsigned long long hc[4] = {0, 0, 0, 0};
     auto domain_error = [&]() {
         const uint64_t r = hc[RST_DOMSLOT];
@@ -2247,6 +2308,8 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     // commit: node arrays and the new CSR
     HIPCHK(hipMemcpyAsync(t->tag, stag, R * 2, hipMemcpyDeviceToDevice, t->stream));
     HIPCHK(hipMemcpyAsync(t->md5, smd, R * 16, hipMemcpyDeviceToDevice, t->stream));
+    RCHK(ensure_erec(t));   // the [] records among them
+    HIPCHK(hipMemcpyAsync(t->erec, serec, R, hipMemcpyDeviceToDevice, t->stream));
     dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
     t->seg_off = nso; t->seg_voff = nsvo; t->koff = nko; t->voff = nvo; t->kheap = nkh; t->vheap = nvh;
     t->n = ne; t->kbytes = kb; t->vbytes = vb;

@@ -310,8 +310,21 @@ def test_checkpoint_into_tracks_corrupt_and_rehash():
     probe = [lone, pair[0], pair[1], 5, 77]
     assert t2.modstate.get_batch(probe) == [R.get(k, o2) for k in probe]
     assert t2.modstate.verify() == R.verify(o2) is False
+    # rehash/1 keeps a stored [] segment (its final level only fetches,
+    # synctree.erl:510-513) and deletes empty inner nodes (:529-531)
     o = R.rehash(o)
     d = S.rehash(d)
-    n_del = S.checkpoint_into(d, db, b'c')
-    assert n_del >= 1 and empty not in db
+    S.checkpoint_into(d, db, b'c')
+    assert db[empty] == b'\x83j'
+    assert db == LR.tree_records(o.modstate.db, b'c')
+    # a raw store of [] into an inner node, then a rehash deletes it; a delete
+    # of the segment record removes the [] record
+    o = R.m_store((2, 3), [], o)
+    d.modstate.store_node(2, 3, [])
+    S.checkpoint_into(d, db, b'c')
+    assert db[LR.db_key(b'c', 2, 3)] == b'\x83j'
+    assert db == LR.tree_records(o.modstate.db, b'c')
+    o = R.rehash(o)
+    d = S.rehash(d)
+    S.checkpoint_into(d, db, b'c')
     assert db == LR.tree_records(o.modstate.db, b'c')
