@@ -213,6 +213,37 @@ __device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
 
+// The state after the first nfull (complete) blocks of an LDS message: the
+// prefix a later md5_lds_resume continues from.
+__device__ __forceinline__ void md5_lds_prefix(const uint8_t *p, uint32_t nfull, uint32_t st[4]) {
+    init(st);
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(p);
+    for (uint32_t k = 0; k < nfull; k++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) m[w] = pw[16 * k + w];
+        compress(st, m);
+    }
+}
+
+// md5_lds of the whole `len`-byte message, given the state after its first
+// k0 blocks (md5_lds_prefix): only blocks k0.. are compressed.
+__device__ __forceinline__ void md5_lds_resume(const uint8_t *p, uint32_t len, uint32_t k0, const uint32_t st0[4],
+                                               uint32_t out[4]) {
+    uint32_t st[4] = {st0[0], st0[1], st0[2], st0[3]};
+    const uint32_t nblk = (len + 8) / 64 + 1;
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(p);
+    for (uint32_t k = k0; k < nblk; k++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) m[w] = pw[16 * k + w];
+        const int32_t rem = (int32_t)len - (int32_t)(64 * k);
+        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
+        compress(st, m);
+    }
+    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+}
+
 // MD5 of a FULL W=16 inner node: 16 present children, message = 16 x
 // (prefix byte ‖ 16 md5 bytes) = 272 bytes = 5 blocks, assembled in
 // registers.  Chunk j starts at byte 17j, so the byte alignment cycles every

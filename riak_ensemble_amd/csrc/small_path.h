@@ -29,6 +29,7 @@
 
 struct SmallIn {
     uint32_t n, op;       // op: 0 = get/2, 1 = insert/3
+    uint32_t dbg, pad;    // dbg: phase stamps into SmallOut.stamp (ST_SMALL_STAMPS)
     uint32_t koff[SB_MAX + 1];
     uint32_t voff[SB_MAX + 1];
     uint8_t kb[SB_KB];
@@ -44,6 +45,7 @@ struct SmallOut {
     uint32_t new_entries;      // insert: keys that were not in their segment before
     uint32_t done;             // set last (host sanity check)
     uint32_t pad;
+    uint64_t stamp[8];         // diagnostic phase stamps (100 MHz), in.dbg only
     uint8_t vbytes[SB_OUT_VB];
 };
 
@@ -157,6 +159,201 @@ __host__ __device__ __forceinline__ uint32_t small_lds_bytes(uint32_t W) {
     return SB_VERIFY * lane_region_bytes(W) + 4 * (SB_SEG_CAP + SB_MAX) * 12;
 }
 
+// insert/3 of ONE key (the per-key latency case, peer_tree do_insert,
+// riak_ensemble_peer_tree.erl:224-234), speculatively: wave 0 verifies the
+// root->segment path (get_path, synctree.erl:302-320) while wave 2 prefetches
+// the path nodes' child entries, writes the segment's new overlay record
+// (orddict:store, :206), hashes it from an LDS copy of its values and hashes
+// the new path bottom-up from LDS (update_path, :201-209) -- all without
+// touching the tree.  Only if the path verified are the overlay index and
+// the path's slot entries committed; a corrupted path commits nothing
+// ({corrupted, L, B}, :193-194); the overlay space of the discarded record is
+// reclaimed at the next flush.
+#define SB_STAMP(k) do { if (in.dbg && threadIdx.x == 0) out->stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SB_STAMPW(k) do { if (in.dbg && (threadIdx.x & 63) == 0) out->stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define S1_VBUF 4096   // value bytes of a segment hashed from LDS (larger: bulk path)
+#define S1_PATH 192    // path child entries (H x W <= 192 for W <= 32, S <= 2^31)
+__device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay &ov, const SmallIn &in, SmallOut *out, uint8_t *dyn,
+                                 const uint8_t *kb, const uint8_t *vb, uint64_t s, uint32_t *bad) {
+    __shared__ uint64_t s1_off;
+    __shared__ uint32_t s1_news, s1_retry, s1_n, s1_kb, s1_vb;
+    __shared__ uint4 s1_new[ST_MAXLEV + 2];    // new entry per level (H+1 = the segment)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t H = t.H, L1 = H + 1, W = t.W;
+    // wave 3's plan area of the dynamic LDS: path entries, the value copy, a message region
+    uint8_t *area = dyn + SB_VERIFY * lane_region_bytes(W) + 3 * (SB_SEG_CAP + SB_MAX) * 12;
+    uint4 *pe = reinterpret_cast<uint4 *>(area);                       // [H][W]
+    uint16_t *pt = reinterpret_cast<uint16_t *>(pe + S1_PATH);         // [H][W]
+    uint8_t *vbuf = reinterpret_cast<uint8_t *>(pt + S1_PATH);         // S1_VBUF + 64
+    uint8_t *regs = vbuf + S1_VBUF + 64;                               // H x lane_region_bytes(W)
+    __shared__ uint32_t s1_pre[ST_MAXLEV + 2][4];                      // per level: prefix state
+    __shared__ uint32_t s1_p[ST_MAXLEV + 2], s1_len[ST_MAXLEV + 2];     // changed entry's offset, length
+    uint32_t *plan = reinterpret_cast<uint32_t *>(dyn + SB_VERIFY * lane_region_bytes(W)) + 2 * 3 * (SB_SEG_CAP + SB_MAX);
+    uint32_t *pk = plan + (SB_SEG_CAP + SB_MAX), *pv = pk + (SB_SEG_CAP + SB_MAX);
+    if (tid == 0) { s1_retry = 0; s1_news = 0; }
+    __syncthreads();
+    SB_STAMP(1);
+    if (wave == 0) {
+        if (lane < L1) {   // path verification, level lane + 1
+            const uint32_t l = lane + 1;
+            bool good;
+            if (l == L1) good = verify_segment_ov(t, ov, s);
+            else good = verify_inner_node(t, l, s >> (t.shift * (L1 - l)), dyn + lane * lane_region_bytes(W));
+            if (!good) atomicMin(&bad[0], l);
+        }
+        if (lane == 0 && in.dbg) out->stamp[2] = __builtin_amdgcn_s_memrealtime();
+    } else if (wave == 2) {
+        // path nodes' child entries: level l node b_l, children base[l+1] + b_l*W + j
+        for (uint32_t x = lane; x < H * W; x += 64) {
+            const uint32_t l = x / W + 1, j = x % W;
+            const uint64_t bl = s >> (t.shift * (L1 - l));
+            const uint64_t c = t.base[l + 1] + bl * W + j;
+            pe[x] = t.md5[c];
+            pt[x] = t.tag[c];
+        }
+        const SegView v = seg_view(t, ov, s);
+        const uint8_t *k = kb + in.koff[0];
+        const uint64_t kl = in.koff[1] - in.koff[0];
+        const uint32_t vl = in.voff[1] - in.voff[0];
+        if (lane == 0) {   // the merged entry list: old entries, the key replaced or inserted
+            bool eq;
+            const uint64_t pos = seg_lower_bound(v, k, kl, &eq);
+            uint64_t out_n = 0, kbytes = 0, vbytes = 0;
+            bool fits = v.n + 1 <= SB_SEG_CAP;
+            for (uint64_t x = 0; x < v.n + 1 && fits; x++) {
+                uint32_t src, a, b;
+                if (x < pos) { src = (uint32_t)x; a = (uint32_t)v.klen(x); b = (uint32_t)v.vlen(x); }
+                else if (x == pos) { src = 0x80000000u; a = (uint32_t)kl; b = vl; }
+                else {
+                    const uint64_t y = eq ? x : x - 1;
+                    if (y >= v.n) break;
+                    src = (uint32_t)y; a = (uint32_t)v.klen(y); b = (uint32_t)v.vlen(y);
+                }
+                plan[out_n] = src; pk[out_n] = a; pv[out_n] = b;
+                kbytes += a; vbytes += b; out_n++;
+            }
+            if (!fits || vbytes > S1_VBUF) {
+                s1_retry = 1;
+            } else {
+                const uint64_t bytes = ov_record_bytes(out_n, kbytes, vbytes);
+                const uint64_t off = atomicAdd(ov.used, (unsigned long long)bytes);
+                if (off + bytes > ov.cap) s1_retry = 1;
+                s1_off = off;
+                s1_n = (uint32_t)out_n; s1_kb = (uint32_t)kbytes; s1_vb = (uint32_t)vbytes;
+                s1_news = eq ? 0 : 1;
+                if (!s1_retry) {   // header and offset tables
+                    uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + off);
+                    uint32_t *ko = h + 4, *vo = h + 4 + (out_n + 1);
+                    h[0] = (uint32_t)out_n; h[1] = (uint32_t)kbytes; h[2] = (uint32_t)vbytes; h[3] = 0;
+                    uint32_t a = 0, c = 0;
+                    for (uint32_t q = 0; q < out_n; q++) {   // lengths -> offsets (LDS and the record)
+                        const uint32_t kq = pk[q], vq = pv[q];
+                        ko[q] = a; vo[q] = c; pk[q] = a; pv[q] = c;
+                        a += kq; c += vq;
+                    }
+                    ko[out_n] = a; vo[out_n] = c; pk[out_n] = a; pv[out_n] = c;
+                }
+            }
+        }
+        wave_sync_lds();
+        if (!s1_retry) {   // entry bytes, lane per entry; values also into the LDS copy
+            uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + s1_off);
+            const uint32_t m = s1_n;
+            uint8_t *kd = reinterpret_cast<uint8_t *>(h + 4 + 2 * (m + 1));
+            uint8_t *vd = kd + s1_kb;
+            for (uint32_t q = lane; q < m; q += 64) {
+                const uint32_t src = plan[q];
+                const uint8_t *ks, *vs;
+                if (src & 0x80000000u) { ks = k; vs = vb + in.voff[0]; }
+                else { ks = v.key(src); vs = v.val(src); }
+                const uint32_t kq = pk[q + 1] - pk[q], vq = pv[q + 1] - pv[q];
+                for (uint32_t b = 0; b < kq; b++) kd[pk[q] + b] = ks[b];
+                for (uint32_t b = 0; b < vq; b++) { const uint8_t c = vs[b]; vd[pv[q] + b] = c; vbuf[pv[q] + b] = c; }
+            }
+                wave_sync_lds();
+            if (lane == 0 && in.dbg) out->stamp[3] = __builtin_amdgcn_s_memrealtime();
+            // lanes 1..H: level `lane`'s node message with the path child's
+            // entry as a placeholder, and the MD5 state over the blocks before
+            // that entry (they do not depend on the new hashes below it)
+            if (lane >= 1 && lane <= H) {
+                const uint32_t l = lane;
+                const uint32_t j = (uint32_t)((s >> (t.shift * (L1 - (l + 1)))) % W);
+                uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
+                MsgWriter mw;
+                mw.init(reg);
+                uint32_t before = 0;
+                for (uint32_t q = 0; q < W; q++) {
+                    const bool pres = q == j || (pt[(l - 1) * W + q] & TAG_PRESENT);
+                    if (!pres) continue;
+                    if (q < j) before++;
+                    mw.entry(q == j ? (uint32_t)TAG_PRESENT : pt[(l - 1) * W + q], pe[(l - 1) * W + q]);
+                }
+                const uint32_t len = mw.finish();
+                s1_p[l] = 17 * before;
+                s1_len[l] = len;
+                uint32_t st[4];
+                stmd5::md5_lds_prefix(reg, (17 * before) / 64, st);
+                s1_pre[l][0] = st[0]; s1_pre[l][1] = st[1]; s1_pre[l][2] = st[2]; s1_pre[l][3] = st[3];
+            }
+            if (lane == 0) {   // the new segment hash (in parallel with the prefixes)
+                uint32_t d[4];
+                stmd5::md5_lds(vbuf, s1_vb, d);
+                s1_new[L1] = make_uint4(d[0], d[1], d[2], d[3]);
+            }
+            wave_sync_lds();
+            if (lane == 0) {   // the path bottom-up: patch the child's entry, resume each node's MD5
+                uint4 e = s1_new[L1];
+                for (uint32_t l = H; l >= 1; l--) {
+                    uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
+                    uint8_t *q = reg + s1_p[l];
+                    q[0] = 0;   // ?H_MD5
+                    const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+                    for (int b = 0; b < 16; b++) q[1 + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
+                    uint32_t d[4];
+                    stmd5::md5_lds_resume(reg, s1_len[l], s1_p[l] / 64, s1_pre[l], d);
+                    e = make_uint4(d[0], d[1], d[2], d[3]);
+                    s1_new[l] = e;
+                }
+                if (in.dbg) out->stamp[4] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
+    }
+    __syncthreads();
+    SB_STAMP(5);
+    const bool ok = bad[0] == ~0u;
+    if (s1_retry) {   // nothing was committed: the host takes the bulk path
+        if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = 1; }
+        return;
+    }
+    if (ok) {   // commit: the overlay record and the path's entries
+        if (tid == 0) ov.idx[s] = s1_off;
+        if (tid < L1) {
+            const uint32_t l = tid + 1;
+            const uint64_t slot = t.base[l] + (s >> (t.shift * (L1 - l)));
+            t.md5[slot] = s1_new[l];
+            t.tag[slot] = TAG_PRESENT;
+            if (l == 1) { t.md5[0] = s1_new[l]; t.tag[0] = TAG_PRESENT; }
+        }
+    }
+    if (tid == 0) {
+        if (ok) {
+            out->status[0] = ST_OK; out->clevel[0] = 0; out->cbucket[0] = 0;
+        } else {
+            out->status[0] = ST_CORRUPTED;
+            out->clevel[0] = bad[0];
+            out->cbucket[0] = s >> (t.shift * (L1 - bad[0]));
+        }
+        out->new_entries = ok ? s1_news : 0;
+        out->retry = 0;
+    }
+    SB_STAMP(6);
+    __threadfence_system();
+    __syncthreads();
+    SB_STAMP(7);
+    if (tid == 0) out->done = 1;
+}
+
 // The small-batch kernel (one workgroup of 256 threads, 4 waves).
 //  1. key -> segment (lane per key; key records copied from the kernel
 //     arguments into LDS first)
@@ -188,6 +385,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     __shared__ uint32_t vlen_out[SB_MAX + 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = in.n, L1 = t.H + 1;
+    SB_STAMP(0);
     for (uint32_t i = tid; i < in.koff[n]; i += blockDim.x) kb[i] = in.kb[i];
     for (uint32_t i = tid; in.op == 1 && i < in.voff[n]; i += blockDim.x) vb[i] = in.vb[i];
     if (tid < SB_MAX) { bad[tid] = ~0u; keep[tid] = 0; }
@@ -204,7 +402,15 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         if (tid == 0) { out->retry = 0; out->new_entries = 0; __threadfence_system(); out->done = 1; }
         return;
     }
-    // ---- 2. path verification: thread x = key * L1 + (level - 1)
+    if (in.op == 1 && n == 1) {   // insert/3 of one key: the speculative path below
+        small_insert_one(t, ov, in, out, dyn, kb, vb, seg[0], bad);
+        return;
+    }
+    // ---- 2. path verification: thread x = key * L1 + (level - 1); for a
+    // get, wave 2 looks the keys up at the same time (the answer is used only
+    // if the key's path verified)
+    __shared__ const uint8_t *gsrc[SB_MAX];
+    __shared__ uint32_t glen[SB_MAX], gfound[SB_MAX];
     for (uint32_t x = tid; x < n * L1; x += SB_VERIFY) {
         if (tid >= SB_VERIFY) break;
         const uint32_t i = x / L1, l = x % L1 + 1;
@@ -214,11 +420,20 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         else good = verify_inner_node(t, l, s >> (t.shift * (L1 - l)), dyn + tid * lane_region_bytes(t.W));
         if (!good) atomicMin(&bad[i], l);
     }
+    if (in.op == 0 && tid >= 128 && tid < 128 + n) {   // orddict_find (synctree.erl:342-348)
+        const uint32_t i = tid - 128;
+        const SegView v = seg_view(t, ov, seg[i]);
+        bool eq;
+        const uint64_t at = seg_lower_bound(v, kb + in.koff[i], in.koff[i + 1] - in.koff[i], &eq);
+        gfound[i] = eq ? 1 : 0;
+        glen[i] = eq ? (uint32_t)v.vlen(at) : 0;
+        gsrc[i] = eq ? v.val(at) : nullptr;
+    }
     __syncthreads();
+    SB_STAMP(2);
     if (in.op == 0) {
-        // ---- 3 (get): orddict_find (synctree.erl:342-348)
+        // ---- 3 (get): the verified answers
         uint32_t len = 0;
-        uint64_t at = 0;
         const uint8_t *src = nullptr;
         if (tid < n) {
             if (bad[tid] != ~0u) {
@@ -226,13 +441,11 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
                 out->clevel[tid] = bad[tid];
                 out->cbucket[tid] = seg[tid] >> (t.shift * (L1 - bad[tid]));
             } else {
-                const SegView v = seg_view(t, ov, seg[tid]);
-                bool eq;
-                at = seg_lower_bound(v, kb + in.koff[tid], in.koff[tid + 1] - in.koff[tid], &eq);
-                out->status[tid] = eq ? ST_OK : ST_NOTFOUND;
+                out->status[tid] = gfound[tid] ? ST_OK : ST_NOTFOUND;
                 out->clevel[tid] = 0;
                 out->cbucket[tid] = 0;
-                if (eq) { len = (uint32_t)v.vlen(at); src = v.val(at); }
+                len = glen[tid];
+                src = gsrc[tid];
             }
             vlen_out[tid + 1] = len;
         }
@@ -246,8 +459,10 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         if (tid <= n) out->voff[tid] = vlen_out[tid];
         if (tid < n && !retry && src)
             for (uint32_t b = 0; b < len; b++) out->vbytes[vlen_out[tid] + b] = src[b];
+        SB_STAMP(6);
         __threadfence_system();
         __syncthreads();
+        SB_STAMP(7);
         if (tid == 0) { out->retry = retry; out->new_entries = 0; __threadfence_system(); out->done = 1; }
         return;
     }

@@ -214,7 +214,10 @@ struct TimedLaunch {
 static int wait_mapped(st_tree *t, volatile uint32_t *flag) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
-        if (*flag) return ST_OK;
+        // acquire: the reads of the results the kernel wrote before the flag
+        // may not move above this load (a volatile read alone does not order
+        // the plain reads that follow it)
+        if (__atomic_load_n(const_cast<uint32_t *>(flag), __ATOMIC_ACQUIRE)) return ST_OK;
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
         __builtin_ia32_pause();
     }
@@ -932,6 +935,8 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     memset(&in, 0, sizeof(in));
     in.n = (uint32_t)n;
     in.op = (uint32_t)op;
+    static const int sdbg = getenv("ST_SMALL_STAMPS") ? atoi(getenv("ST_SMALL_STAMPS")) : 0;
+    in.dbg = sdbg ? 1u : 0u;
     for (uint64_t i = 0; i <= n; i++) in.koff[i] = (uint32_t)hr.off[i];
     memcpy(in.kb, hr.heap.data(), kbytes);
     if (op == 1) {
@@ -942,6 +947,14 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev);
     CHK(wait_mapped(t, &t->sout->done));
     if (!t->sout->done) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
+    if (sdbg) {   // diagnostic: phase times (µs from kernel start) to stderr
+        const uint64_t *st = t->sout->stamp;
+        fprintf(stderr, "small op=%d n=%llu:", op, (unsigned long long)n);
+        for (int k = 1; k < 8; k++)
+            if (st[k]) fprintf(stderr, " %d:%.2f", k, (st[k] - st[0]) / 100.0);
+        fprintf(stderr, "\n");
+        memset((void *)t->sout->stamp, 0, sizeof(t->sout->stamp));
+    }
     if (t->sout->retry) return ST_OK;
     *served = 1;
     if (op == 1) {
