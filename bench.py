@@ -699,20 +699,21 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
     # per-key verified-path calls (get/2, insert/3, synctree.erl:189-227) one at
     # a time through the C-ABI (ctypes), i.e. the low-batch latency path
     kl = [int(k) for k in keys[:200]]
-    t.get_batch([kl[0]])                                # untimed warm-up
-    t.insert_batch([kl[0]], [bytes(vals[0])])
+    t.get1(kl[0])                                       # untimed warm-up
+    t.insert1(kl[0], bytes(vals[0]))
     t0 = time.perf_counter()
-    got = [t.get_batch([k])[0] for k in kl]
+    got = [t.get1(k) for k in kl]
     gpu_get_us = (time.perf_counter() - t0) / len(kl) * 1e6
     assert got == [bytes(vals[i]) for i in range(len(kl))], 'per-key get returned wrong values'
     newv = bytes(17)
     t0 = time.perf_counter()
-    st = [t.insert_batch([k], [newv])[0] for k in kl]
+    st = [t.insert1(k, newv) for k in kl]
     gpu_ins_us = (time.perf_counter() - t0) / len(kl) * 1e6
     assert all(s is None for s in st), 'per-key insert rejected'
+    assert [t.get1(k) for k in kl[:20]] == [newv] * 20, 'per-key insert did not store'
     # the device part of those calls: the k_small kernel alone (HIP events)
     kern_us = {}
-    for name, fn in (('get', lambda k: t.get_batch([k])), ('insert', lambda k: t.insert_batch([k], [newv]))):
+    for name, fn in (('get', lambda k: t.get1(k)), ('insert', lambda k: t.insert1(k, newv))):
         t.set_timing(True)
         t.kernel_stats('*reset*')
         for k in kl[:50]:
@@ -725,9 +726,10 @@ def _bench_config1(synctree_hip, workload, local, torch, n=100_000, cpu=True):
            'what': 'config1: 100k keys, build + rehash + top_hash (GPU: host arrays in, one insert batch)',
            'per_key_latency_us': {'gpu_get': round(gpu_get_us, 1), 'gpu_insert': round(gpu_ins_us, 1),
                                   'kernel_us': kern_us,
-                                  'what': 'one get/2 or insert/3 per C-ABI call (verified path + dirty-path '
-                                          'rehash on the device), 200 calls after a warm-up, ctypes overhead '
-                                          'included; results checked; kernel_us: the k_small kernel alone'}}
+                                  'what': 'one get/2 or insert/3 per C-ABI call (st_get1 / st_insert1: verified '
+                                          'path + dirty-path rehash on the device), 200 calls after a warm-up, '
+                                          'ctypes overhead included; results checked; kernel_us: the k_small '
+                                          'kernel alone'}}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import oracle_c

@@ -232,12 +232,10 @@ static ERL_NIF_TERM nif_insert(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv
     (void)argc;
     if (!get_tree(env, argv[0], &t) || !get_key(env, argv[1], &ty, &kb) || !enif_inspect_binary(env, argv[2], &vb))
         return enif_make_badarg(env);   /* a non-binary value: function_clause (synctree.erl:190) */
-    const uint8_t k8 = (uint8_t)ty;
-    const uint64_t ko[2] = {0, kb.size}, vo[2] = {0, vb.size};
-    int32_t st;
     uint32_t cl;
     uint64_t cb;
-    if (st_insert_batch(t, 1, &k8, kb.data, ko, vb.data, vo, &st, &cl, &cb) < 0) return err(env);
+    const int st = st_insert1(t, (uint8_t)ty, kb.data, (uint32_t)kb.size, vb.data, (uint32_t)vb.size, &cl, &cb);
+    if (st < 0) return err(env);
     return st == ST_CORRUPTED ? corrupted(env, cl, cb) : A_OK;
 }
 

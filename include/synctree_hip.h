@@ -238,6 +238,17 @@ void st_free_result(st_result *r);
 int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                  st_result **out);
 
+/* get/2 and insert/3 of ONE key (synctree.erl:189-227) with caller buffers
+ * (no result block): the per-key path of the NIF and of
+ * riak_ensemble_peer_tree (peer_tree.erl:224-246).  st_get1 returns ST_OK
+ * (value in vout[0..*vlen)), ST_NOTFOUND or ST_CORRUPTED (clevel, cbucket);
+ * a value longer than vcap sets *vlen and returns ST_EINVAL.  st_insert1
+ * returns ST_OK or ST_CORRUPTED. */
+int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, uint8_t *vout, uint32_t vcap,
+            uint32_t *vlen, uint32_t *clevel, uint64_t *cbucket);
+int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, const uint8_t *value, uint32_t vlen,
+               uint32_t *clevel, uint64_t *cbucket);
+
 /* exchange_get/3 (synctree.erl:231-237) at one level for n buckets, each
  * verified root->node (verified_hashes, synctree.erl:288-298).  Level 0
  * (bucket 0) is answered as [{0, TopHash}] by the caller from st_top_hash.

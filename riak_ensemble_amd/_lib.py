@@ -96,6 +96,10 @@ _SIGS = {
     'st_compare_stats': (ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32, u64p]),
     'st_tops_to_device': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     'st_set_etf_atoms': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    'st_get1': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    'st_insert1': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     'st_key_record': (ctypes.c_int, [ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                      u64p]),
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

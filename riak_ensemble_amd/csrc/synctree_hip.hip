@@ -1517,6 +1517,58 @@ __global__ void k_u32_to_u64(const uint32_t *a, uint64_t n, uint64_t *b) {
     for (uint64_t i = gtid(); i < n; i += gstride()) b[i] = a[i];
 }
 
+// get/2 of ONE key (synctree.erl:213-227) into caller buffers: ST_OK (value
+// bytes in vout, *vlen; a value longer than vcap sets *vlen and returns
+// ST_EINVAL), ST_NOTFOUND, or ST_CORRUPTED with (clevel, cbucket).  The NIF's
+// get/2 path: no result block.
+extern "C" int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, uint8_t *vout, uint32_t vcap,
+                       uint32_t *vlen, uint32_t *clevel, uint64_t *cbucket) {
+    CHK(use_device(t));
+    const uint64_t koff[2] = {0, klen};
+    HostRecords hr;
+    CHK(pack_records(1, &ktype, kbytes, koff, hr));
+    int served = 0;
+    CHK(small_call(t, 0, 1, hr, nullptr, nullptr, &served));
+    int32_t st;
+    if (served) {
+        const SmallOut *so = t->sout;
+        st = so->status[0];
+        *clevel = so->clevel[0];
+        *cbucket = so->cbucket[0];
+        *vlen = so->voff[1];
+        if (st == ST_OK) {
+            if (*vlen > vcap) { g_err = "value longer than the buffer"; return ST_EINVAL; }
+            memcpy(vout, so->vbytes, *vlen);
+        }
+        return st;
+    }
+    st_result *res = nullptr;
+    CHK(st_get_batch(t, 1, &ktype, kbytes, koff, &res));
+    st = res->status[0];
+    *clevel = res->clevel ? res->clevel[0] : 0;
+    *cbucket = res->cbucket ? res->cbucket[0] : 0;
+    *vlen = 0;
+    if (st == ST_OK) {
+        const uint64_t e = res->eoff[0];
+        *vlen = (uint32_t)(res->aoff[e + 1] - res->aoff[e]);
+        if (*vlen > vcap) { st_free_result(res); g_err = "value longer than the buffer"; return ST_EINVAL; }
+        memcpy(vout, res->aheap + res->aoff[e], *vlen);
+    }
+    st_free_result(res);
+    return st;
+}
+
+// insert/3 of ONE key (synctree.erl:189-209): ST_OK or ST_CORRUPTED with
+// (clevel, cbucket).  The NIF's insert/3 and riak_ensemble_peer_tree's
+// do_insert (peer_tree.erl:224-234).
+extern "C" int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, const uint8_t *value,
+                          uint32_t vlen, uint32_t *clevel, uint64_t *cbucket) {
+    const uint64_t koff[2] = {0, klen}, voff[2] = {0, vlen};
+    int32_t st = ST_OK;
+    CHK(st_insert_batch(t, 1, &ktype, kbytes, koff, value, voff, &st, clevel, cbucket));
+    return st;
+}
+
 extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                             st_result **out) {
     CHK(use_device(t));

@@ -54,6 +54,7 @@ class DeviceTree:
         self.segments = int(L.st_segments(h))
         self.height = int(L.st_height(h))
         self.shift = self.width.bit_length() - 1
+        self._g1 = self._i1 = None   # cached ctypes buffers of get1 / insert1
 
     def close(self):
         """Free the device tree; any later call raises (the handle is gone)."""
@@ -183,6 +184,39 @@ class DeviceTree:
             return rp.contents
         except ValueError:
             raise _lib.DeviceError('null result')
+
+    def get1(self, key):
+        """get/2 of one key through st_get1 (no result block): the value,
+        'notfound' or ('corrupted', L, B)."""
+        kt, kb = terms.key_parts(key)
+        if self._g1 is None:
+            self._g1 = (ctypes.create_string_buffer(4096), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint64())
+        buf, vl, cl, cb = self._g1
+        rc = self.L.st_get1(self.h, kt, kb, len(kb), buf, 4096, ctypes.byref(vl), ctypes.byref(cl), ctypes.byref(cb))
+        if rc == _lib.ST_OK:
+            return buf.raw[:vl.value]
+        if rc == _lib.ST_NOTFOUND:
+            return terms.NOTFOUND
+        if rc == _lib.ST_CORRUPTED:
+            return (terms.CORRUPTED, int(cl.value), int(cb.value))
+        if rc == _lib.ST_EINVAL and vl.value > 4096:   # a long value: the batch call
+            return self.get_batch([key])[0]
+        _lib.check(rc, 'st_get1')
+
+    def insert1(self, key, value):
+        """insert/3 of one key through st_insert1: None or ('corrupted', L, B)."""
+        if not isinstance(value, (bytes, bytearray)):
+            raise TypeError('function_clause: synctree values are binaries (synctree.erl:190)')
+        kt, kb = terms.key_parts(key)
+        if self._i1 is None:
+            self._i1 = (ctypes.c_uint32(), ctypes.c_uint64())
+        cl, cb = self._i1
+        rc = self.L.st_insert1(self.h, kt, kb, len(kb), bytes(value), len(value), ctypes.byref(cl), ctypes.byref(cb))
+        if rc == _lib.ST_OK:
+            return None
+        if rc == _lib.ST_CORRUPTED:
+            return (terms.CORRUPTED, int(cl.value), int(cb.value))
+        _lib.check(rc, 'st_insert1')
 
     def get_batch(self, keys):
         n = len(keys)

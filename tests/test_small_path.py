@@ -131,3 +131,39 @@ def test_small_path_falls_back_for_big_segments():
         assert dev.top_hash() == ora.top_hash()
     assert dev.get_batch([int(keys[0]), int(keys[7])]) == [ora.get(int(keys[0])), ora.get(int(keys[7]))]
     dev.close()
+
+
+@pytest.mark.gpu
+def test_single_key_entry_points():
+    """st_get1 / st_insert1 (the NIF's per-key calls) agree with the batch
+    calls and with the C restatement, corruption included."""
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip
+    n = 5000
+    keys = workload.keys_int63(n, workload.SEED ^ 0x57)
+    vals = workload.obj_hash_values(n)
+    dev = synctree_hip.DeviceTree()
+    ora = C.OTree()
+    assert dev.get1(5) == 'notfound'   # empty tree
+    dev.insert_int64(keys, vals)
+    ora.bulk_load_int64(keys, vals)
+    for i in range(0, 200, 7):
+        k = int(keys[i])
+        assert dev.get1(k) == ora.get(k) == dev.get_batch([k])[0]
+        assert dev.insert1(k, _val(i, 4)) is None
+        ora.insert(k, _val(i, 4))
+        assert dev.top_hash() == ora.top_hash()
+    assert dev.insert1(('t', 1), b'\x00x') is None            # a term key
+    assert dev.get1(('t', 1)) == b'\x00x'
+    assert dev.get1(123456789) == ora.get(123456789) == 'notfound'
+    k0 = int(keys[3])
+    s0 = ora.segment_of(k0)
+    node = ora.node(ora.height + 1, s0)
+    bad = [(node[0][0], bytes([node[0][1][0] ^ 1]) + node[0][1][1:])] + node[1:]
+    dev.store_node(ora.height + 1, s0, bad)
+    ora.store_segment(s0, bad)
+    assert dev.insert1(k0, _val(9, 9)) == ora.insert(k0, _val(9, 9))
+    assert dev.get1(k0) == ora.get(k0)
+    with pytest.raises(TypeError):
+        dev.insert1(k0, 'not a binary')
+    dev.close()
