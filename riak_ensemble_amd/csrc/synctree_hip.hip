@@ -1439,32 +1439,30 @@ extern "C" void st_free_result(st_result *r) {
 // Device entries (by index, ~0 = none) -> host key/value heaps of a result.
 static int fetch_entries(st_tree *t, const uint64_t *d_idx, uint64_t n, st_result *res, bool keys) {
     DevTree d = view(t);
+    Scratch sc(t);   // every device temporary is freed on every return path
     uint64_t *kl = nullptr, *vl = nullptr, *ko = nullptr, *vo = nullptr;
     uint8_t *kh = nullptr, *vh = nullptr;
-    int r = ST_OK;
-    auto done = [&]() { dfree(t, kl); dfree(t, vl); dfree(t, ko); dfree(t, vo); dfree(t, kh); dfree(t, vh); };
-    if ((r = dalloc_t(t, &kl, n + 1)) || (r = dalloc_t(t, &vl, n + 1)) || (r = dalloc_t(t, &ko, n + 1)) ||
-        (r = dalloc_t(t, &vo, n + 1))) { done(); return r; }
+    CHK(sc.alloc(&kl, n + 1));
+    CHK(sc.alloc(&vl, n + 1));
+    CHK(sc.alloc(&ko, n + 1));
+    CHK(sc.alloc(&vo, n + 1));
     LAUNCH(t, "entry_lengths", k_entry_lengths, grid_for(n + 1), 256, 0, d, d_idx, n, kl, vl);
-    if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, vl, vo, n + 1))) { done(); return r; }
+    CHK(exclusive_scan<uint64_t>(t, kl, ko, n + 1));
+    CHK(exclusive_scan<uint64_t>(t, vl, vo, n + 1));
     res->koff = (uint64_t *)calloc(n + 1, 8);
     res->aoff = (uint64_t *)calloc(n + 1, 8);
-    if (hipMemcpyAsync(res->koff, ko, (n + 1) * 8, hipMemcpyDeviceToHost, t->stream) != hipSuccess) {
-        done(); g_err = "hipMemcpyAsync"; return ST_EDEVICE;
-    }
-    if ((r = d2h(t, res->aoff, vo, (n + 1) * 8))) { done(); return r; }
+    HIPCHK(hipMemcpyAsync(res->koff, ko, (n + 1) * 8, hipMemcpyDeviceToHost, t->stream));
+    CHK(d2h(t, res->aoff, vo, (n + 1) * 8));
     const uint64_t kb = res->koff[n], vb = res->aoff[n];
-    if ((r = dalloc(t, (void **)&kh, kb + 16)) || (r = dalloc(t, (void **)&vh, vb + 16))) { done(); return r; }
+    CHK(sc.bytes(&kh, kb + 16));
+    CHK(sc.bytes(&vh, vb + 16));
     LAUNCH(t, "entry_gather", k_entry_gather, grid_for(n), 256, 0, d, d_idx, n, (const uint64_t *)ko, kh,
            (const uint64_t *)vo, vh);
     res->kheap = (uint8_t *)malloc(kb + 1);
     res->aheap = (uint8_t *)malloc(vb + 1);
-    if (kb && hipMemcpyAsync(res->kheap, kh, kb, hipMemcpyDeviceToHost, t->stream) != hipSuccess) {
-        done(); g_err = "hipMemcpyAsync"; return ST_EDEVICE;
-    }
-    if ((r = d2h(t, res->aheap, vh, vb))) { done(); return r; }
-    if (!vb) HIPCHK(hipStreamSynchronize(t->stream));
-    done();
+    if (kb) HIPCHK(hipMemcpyAsync(res->kheap, kh, kb, hipMemcpyDeviceToHost, t->stream));
+    CHK(d2h(t, res->aheap, vh, vb));
+    HIPCHK(hipStreamSynchronize(t->stream));
     (void)keys;
     return ST_OK;
 }
@@ -1623,20 +1621,36 @@ extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const 
     if (!r) r = dalloc_t(t, &pst, n);
     if (!r) r = dalloc_t(t, &found, n);
     DevTree d = view(t);
+    auto launched = [&](const char *what) {
+        const hipError_t e = hipGetLastError();
+        if (e == hipSuccess) return ST_OK;
+        g_err = std::string("launch ") + what + ": " + hipGetErrorString(e);
+        return ST_EDEVICE;
+    };
     if (!r) {
         hipLaunchKernelGGL(k_key_segment, dim3(grid_for(n)), dim3(256), 0, t->stream, krec, dko, n, t->S - 1, seg);
-        hipLaunchKernelGGL(k_u32_to_u64, dim3(grid_for(n)), dim3(256), 0, t->stream, seg, n, tg64);
-        r = verify_paths(t, t->H + 1, tg64, n, pst);
+        r = launched("key_segment");
     }
+    if (!r) {
+        hipLaunchKernelGGL(k_u32_to_u64, dim3(grid_for(n)), dim3(256), 0, t->stream, seg, n, tg64);
+        r = launched("u32_to_u64");
+    }
+    if (!r) r = verify_paths(t, t->H + 1, tg64, n, pst);
     if (!r) {
         BatchView bv{krec, dko};
         hipLaunchKernelGGL(k_lookup, dim3(grid_for(n)), dim3(256), 0, t->stream, d, bv, seg, n, found);
+        r = launched("lookup");
+    }
+    if (!r) {
         std::vector<uint32_t> ps(n), sg(n);
         std::vector<uint64_t> fd(n);
         // one sync for the three per-key outputs
-        if (hipMemcpyAsync(ps.data(), pst, n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess ||
-            hipMemcpyAsync(sg.data(), seg, n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess)
+        hipError_t e = hipMemcpyAsync(ps.data(), pst, n * 4, hipMemcpyDeviceToHost, t->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(sg.data(), seg, n * 4, hipMemcpyDeviceToHost, t->stream);
+        if (e != hipSuccess) {
+            g_err = std::string("hipMemcpyAsync: ") + hipGetErrorString(e);
             r = ST_EDEVICE;
+        }
         if (!r) r = d2h(t, fd.data(), found, n * 8);
         if (!r) {
             for (uint64_t i = 0; i < n; i++) {
