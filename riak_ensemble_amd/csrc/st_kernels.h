@@ -496,6 +496,8 @@ struct MergeArgs {
     const uint64_t *seg_off;
     const uint64_t *koff;
     const uint8_t *kheap;
+    const uint64_t *voff;
+    const uint8_t *vheap;
     // batch (sorted order = perm, runs = bseg_off, keep = last writer)
     const uint32_t *perm;
     const uint64_t *bseg_off;
@@ -504,34 +506,67 @@ struct MergeArgs {
     const uint8_t *seg_reject;  // NULL or per segment: nonzero => batch run ignored
     const uint8_t *seg_replace; // NULL or per segment: nonzero => old run dropped
     BatchView bv;
+    const uint64_t *bvoff;
+    const uint8_t *bvheap;
     uint64_t S;
 };
 
+// Running sums of the merge: per sorted batch record (BatchSums: eq = kept and
+// overwrites/erases an old entry, ne = kept and not an ERASE, i.e. produces an
+// entry; ke/ve = key/value bytes of the old entry it drops, kn/vn = its own
+// key/value bytes when it produces an entry) and per segment (SegSums: entry
+// count, key bytes, value bytes of the merged segment).  Exclusive scans of
+// both give every merged entry its index and heap offsets in closed form.
+template <int N>
+struct USum {
+    uint64_t v[N];
+    __host__ __device__ USum() {}
+    __host__ __device__ USum(int z) {
+        for (int i = 0; i < N; i++) v[i] = (uint64_t)z;
+    }
+    __host__ __device__ USum operator+(const USum &o) const {
+        USum r;
+        for (int i = 0; i < N; i++) r.v[i] = v[i] + o.v[i];
+        return r;
+    }
+};
+typedef USum<6> BatchSums;   // eq, ne, ke, kn, ve, vn
+typedef USum<3> SegSums;     // count, key bytes, value bytes
+enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
+
 // ---------------------------------------------------------------------------
-// Parallel merge.  k_merge walks every segment's old entries serially (one
-// thread per segment, ~100 entries per segment in a 100M-key tree) and writes
-// src[] with uncoalesced stores; for batches much smaller than the tree that
-// walk is the whole ingest.  Here only the batch runs are walked: every kept
-// batch record r of segment s gets pos_r = lower_bound(old keys of s, key_r),
-// eq_r (key present) and ne_r (not an ERASE).  With exclusive scans ceq/cne
-// of those flags over the sorted batch, the merged order is closed-form:
-//   old entry li (dropped iff some eq_r has pos_r == li):
-//     new = li - #{r: eq_r, pos_r < li} + #{r: ne_r, pos_r <= li}
+// Parallel merge.  Only the batch runs are walked: every kept batch record r
+// of segment s gets pos_r = lower_bound(old keys of s, key_r), eq_r (key
+// present) and ne_r (not an ERASE).  With exclusive scans of the BatchSums
+// over the sorted batch (E = eq count, N = ne count, KE/KN/VE/VN = bytes) and
+// of the SegSums over the segments (C, K, V), the merged layout is closed-form:
+//   old entry li of s (dropped iff some eq_r has pos_r == li), with
+//   k = #{r in run: pos_r <= li}, k2 = #{r in run: pos_r < li}:
+//     index = C[s] + li - E(k2) + N(k)
+//     key   = K[s] + (okoff[li] - okoff[0]) - KE(k2) + KN(k)   (values alike)
 //   batch record r with ne_r:
-//     new = pos_r - #{r' < r: eq_r'} + #{r' < r: ne_r'}
-// so old entries are placed by a coalesced pass (k_merge_old) and batch
-// records by one thread each (k_merge_new).  Same result as k_merge<true>.
-__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, uint64_t *feq, uint64_t *fne, uint64_t *cnt, uint8_t *dirty) {
+//     index = C[s] + pos_r - E(r) + N(r)
+//     key   = K[s] + (okoff[pos_r] - okoff[0]) - KE(r) + KN(r)
+// (run-relative sums), so k_merge_old moves every old entry -- offsets and
+// bytes -- in one coalesced pass and k_merge_new places the batch records:
+// the whole CSR is rewritten once, with no per-entry source list, length
+// arrays or entry-sized scans.
+__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty) {
     for (uint64_t s = gtid(); s < a.S; s += gstride()) {
         const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
         uint64_t nold = a.seg_off ? a.seg_off[s + 1] - i0 : 0;
         const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
         const bool rej = a.seg_reject && a.seg_reject[s];
         if (a.seg_replace && a.seg_replace[s]) nold = 0;
-        uint64_t lo = 0, neq = 0, nne = 0;
+        SegSums tot;
+        tot.v[0] = nold;
+        tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
+        tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
+        uint64_t lo = 0;
         bool changed = false;
         for (uint64_t j = j0; j < je; j++) {
-            if (rej) { pos[j] = 0; feq[j] = fne[j] = 0; continue; }
+            BatchSums f(0);
+            if (rej) { pos[j] = 0; bs[j] = f; continue; }
             const uint32_t bi = a.perm[j];
             const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
             const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
@@ -540,23 +575,32 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, uint64_t *feq, uint64_t 
                 const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
                 if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
             }
-            const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[i0 + lo], a.koff[i0 + lo + 1] - a.koff[i0 + lo], kb, kl) == 0;
+            const uint64_t e = i0 + lo;
+            const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
             pos[j] = (uint32_t)lo;
             const bool kept = a.keep[j] != 0;
             const bool ne = kept && !(a.bop && a.bop[bi]);
-            feq[j] = kept && eq ? 1 : 0;
-            fne[j] = ne ? 1 : 0;
+            if (kept && eq) {
+                f.v[BS_EQ] = 1;
+                f.v[BS_KE] = a.koff[e + 1] - a.koff[e];
+                f.v[BS_VE] = a.voff[e + 1] - a.voff[e];
+            }
+            if (ne) {
+                f.v[BS_NE] = 1;
+                f.v[BS_KN] = kl;
+                f.v[BS_VN] = a.bvoff[bi + 1] - a.bvoff[bi];
+            }
+            bs[j] = f;
             changed |= kept;
-            neq += kept && eq;
-            nne += ne;
+            tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
+            tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
+            tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
         }
-        cnt[s] = nold - neq + nne;
+        ss[s] = tot;
         if (dirty) dirty[s] = changed ? 1 : 0;
     }
 }
 
-// Old entries: a workgroup per 256 consecutive segments walks their old
-// entries with consecutive threads on consecutive entries.
 __device__ __forceinline__ uint64_t bound_pos(const uint32_t *pos, uint64_t lo, uint64_t hi, uint64_t li, bool upper) {
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
@@ -566,12 +610,31 @@ __device__ __forceinline__ uint64_t bound_pos(const uint32_t *pos, uint64_t lo, 
     return lo;
 }
 
-__global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *pos, const uint64_t *ceq, const uint64_t *cne,
-                                                   const uint64_t *noff, uint64_t *src) {
+// Output of the merge: the new CSR.
+struct MergeOut {
+    uint64_t *seg_off, *seg_voff;   // S + 1
+    uint64_t *koff, *voff;          // n_new + 1
+    uint8_t *kheap, *vheap;
+};
+
+// Old entries: a workgroup per 256 consecutive segments walks their old
+// entries with consecutive threads on consecutive entries, writing each
+// surviving entry's new offsets and bytes; it also writes the new segment
+// offsets of its segments (and the terminal offsets, from the last segment).
+__global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *pos, const BatchSums *bx,
+                                                   const SegSums *sx, MergeOut o) {
     __shared__ uint64_t so[257];
     const uint64_t s0 = (uint64_t)blockIdx.x * 256;
     const uint64_t ns = a.S - s0 < 256 ? a.S - s0 : 256;
-    for (uint32_t i = threadIdx.x; i <= ns; i += 256) so[i] = a.seg_off[s0 + i];
+    for (uint32_t i = threadIdx.x; i <= ns; i += 256) {
+        so[i] = a.seg_off ? a.seg_off[s0 + i] : 0;
+        if (i < ns || s0 + i == a.S) {
+            const SegSums x = sx[s0 + i];
+            o.seg_off[s0 + i] = x.v[0];
+            o.seg_voff[s0 + i] = x.v[2];
+            if (s0 + i == a.S) { o.koff[x.v[0]] = x.v[1]; o.voff[x.v[0]] = x.v[2]; }
+        }
+    }
     __syncthreads();
     const uint64_t e0 = so[0], e1 = so[ns];
     for (uint64_t e = e0 + threadIdx.x; e < e1; e += 256) {
@@ -580,64 +643,52 @@ __global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *
             const uint32_t mid = (lo + hi) >> 1;
             if (so[mid] <= e) lo = mid; else hi = mid;
         }
-        const uint64_t s = s0 + lo, li = e - so[lo];
+        const uint64_t s = s0 + lo, i0 = so[lo], li = e - i0;
         if (a.seg_replace && a.seg_replace[s]) continue;
+        const SegSums base = sx[s];
+        const uint64_t okb = a.koff[e], ovb = a.voff[e];
+        const uint64_t kl = a.koff[e + 1] - okb, vl = a.voff[e + 1] - ovb;
+        uint64_t nw = base.v[0] + li, nk = base.v[1] + (okb - a.koff[i0]), nv = base.v[2] + (ovb - a.voff[i0]);
         const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-        uint64_t nw = noff[s] + li;
         if (j0 != je && !(a.seg_reject && a.seg_reject[s])) {
             const uint64_t k = bound_pos(pos, j0, je, li, true), k2 = bound_pos(pos, j0, je, li, false);
-            if (ceq[k] != ceq[k2]) continue;   // overwritten or erased by the batch
-            nw = noff[s] + li - (ceq[k2] - ceq[j0]) + (cne[k] - cne[j0]);
+            const BatchSums &B0 = bx[j0], &Bk = bx[k], &Bk2 = bx[k2];
+            if (Bk.v[BS_EQ] != Bk2.v[BS_EQ]) continue;   // overwritten or erased by the batch
+            nw += (Bk.v[BS_NE] - B0.v[BS_NE]) - (Bk2.v[BS_EQ] - B0.v[BS_EQ]);
+            nk += (Bk.v[BS_KN] - B0.v[BS_KN]) - (Bk2.v[BS_KE] - B0.v[BS_KE]);
+            nv += (Bk.v[BS_VN] - B0.v[BS_VN]) - (Bk2.v[BS_VE] - B0.v[BS_VE]);
         }
-        src[nw] = e;
+        o.koff[nw] = nk;
+        o.voff[nw] = nv;
+        copy_bytes(o.kheap + nk, a.kheap + okb, kl);
+        copy_bytes(o.vheap + nv, a.vheap + ovb, vl);
     }
 }
 
 // Batch records that produce an entry (kept, not ERASE, run not rejected).
-__global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const uint32_t *pos, const uint64_t *ceq,
-                            const uint64_t *cne, const uint64_t *noff, uint64_t *src) {
+__global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const uint32_t *pos, const BatchSums *bx,
+                            const SegSums *sx, MergeOut o) {
     for (uint64_t j = gtid(); j < n; j += gstride()) {
-        if (cne[j + 1] == cne[j]) continue;
-        const uint64_t s = sseg[j], j0 = a.bseg_off[s];
-        src[noff[s] + pos[j] - (ceq[j] - ceq[j0]) + (cne[j] - cne[j0])] = (1ull << 63) | a.perm[j];
-    }
-}
-
-// Per new entry: key/value byte lengths (for the offset scans).
-__global__ void k_src_lengths(const uint64_t *src, uint64_t n, const uint64_t *okoff, const uint64_t *ovoff,
-                              const uint64_t *bkoff, const uint64_t *bvoff, uint64_t *klen, uint64_t *vlen) {
-    for (uint64_t j = gtid(); j <= n; j += gstride()) {
-        if (j == n) { klen[j] = 0; vlen[j] = 0; break; }
-        const uint64_t s = src[j];
-        if (s >> 63) {
-            const uint64_t b = s & 0x7fffffffffffffffull;
-            klen[j] = bkoff[b + 1] - bkoff[b];
-            vlen[j] = bvoff[b + 1] - bvoff[b];
-        } else {
-            klen[j] = okoff[s + 1] - okoff[s];
-            vlen[j] = ovoff[s + 1] - ovoff[s];
+        const BatchSums &Bj = bx[j];
+        if (bx[j + 1].v[BS_NE] == Bj.v[BS_NE]) continue;
+        const uint64_t s = sseg[j], j0 = a.bseg_off[s], p = pos[j];
+        const BatchSums &B0 = bx[j0];
+        const SegSums base = sx[s];
+        uint64_t dk = 0, dv = 0;   // old bytes before pos (none when the old run is replaced)
+        if (p) {
+            const uint64_t i0 = a.seg_off[s];
+            dk = a.koff[i0 + p] - a.koff[i0];
+            dv = a.voff[i0 + p] - a.voff[i0];
         }
-    }
-}
-
-__global__ void k_gather_entries(const uint64_t *src, uint64_t n, const uint64_t *okoff, const uint8_t *okheap,
-                                 const uint64_t *ovoff, const uint8_t *ovheap, const uint64_t *bkoff,
-                                 const uint8_t *bkheap, const uint64_t *bvoff, const uint8_t *bvheap,
-                                 const uint64_t *nkoff, uint8_t *nkheap, const uint64_t *nvoff, uint8_t *nvheap) {
-    for (uint64_t j = gtid(); j < n; j += gstride()) {
-        const uint64_t s = src[j];
-        const uint8_t *kp, *vp;
-        uint64_t kl, vl;
-        if (s >> 63) {
-            const uint64_t b = s & 0x7fffffffffffffffull;
-            kp = bkheap + bkoff[b]; kl = bkoff[b + 1] - bkoff[b];
-            vp = bvheap + bvoff[b]; vl = bvoff[b + 1] - bvoff[b];
-        } else {
-            kp = okheap + okoff[s]; kl = okoff[s + 1] - okoff[s];
-            vp = ovheap + ovoff[s]; vl = ovoff[s + 1] - ovoff[s];
-        }
-        copy_bytes(nkheap + nkoff[j], kp, kl);
-        copy_bytes(nvheap + nvoff[j], vp, vl);
+        const uint64_t nw = base.v[0] + p + (Bj.v[BS_NE] - B0.v[BS_NE]) - (Bj.v[BS_EQ] - B0.v[BS_EQ]);
+        const uint64_t nk = base.v[1] + dk + (Bj.v[BS_KN] - B0.v[BS_KN]) - (Bj.v[BS_KE] - B0.v[BS_KE]);
+        const uint64_t nv = base.v[2] + dv + (Bj.v[BS_VN] - B0.v[BS_VN]) - (Bj.v[BS_VE] - B0.v[BS_VE]);
+        const uint32_t bi = a.perm[j];
+        const uint64_t bk = a.bv.koff[bi], bv = a.bvoff[bi];
+        o.koff[nw] = nk;
+        o.voff[nw] = nv;
+        copy_bytes(o.kheap + nk, a.bv.kheap + bk, a.bv.koff[bi + 1] - bk);
+        copy_bytes(o.vheap + nv, a.bvheap + bv, a.bvoff[bi + 1] - bv);
     }
 }
 
@@ -648,6 +699,15 @@ __global__ void k_seg_voff(const uint64_t *seg_off, const uint64_t *voff, uint64
 // Per batch key: insert status from its segment's path status.
 __global__ void k_key_status(const uint32_t *seg, uint64_t n, const uint8_t *seg_reject, uint32_t *clevel) {
     for (uint64_t i = gtid(); i < n; i += gstride()) clevel[i] = seg_reject[seg[i]];
+}
+
+// Number of nonzero statuses (rejected keys of an insert batch): a wave
+// reduction per wave, one global add per wave into *out (zeroed by the host).
+__global__ void k_count_nonzero(const uint32_t *v, uint64_t n, unsigned long long *out) {
+    unsigned long long c = 0;
+    for (uint64_t i = gtid(); i < n; i += gstride()) c += v[i] != 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
 
 // ---------------------------------------------------------------------------

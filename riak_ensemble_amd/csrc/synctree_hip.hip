@@ -55,6 +55,13 @@ struct Pending {
     hipEvent_t a, b;
 };
 
+// One segment CSR's buffers (st_tree's current arrays or its spare set).
+struct CsrSet {
+    uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
+    uint8_t *kheap = nullptr, *vheap = nullptr;
+    uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
+};
+
 struct st_tree {
     int device = 0;
     int ncu = 256;   // compute units of the device (fixed-grid kernels)
@@ -78,6 +85,10 @@ struct st_tree {
     uint64_t n = 0, kbytes = 0, vbytes = 0;
     uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
     uint8_t *kheap = nullptr, *vheap = nullptr;
+    // capacities of the current koff/voff (entries) and heaps (bytes), and the
+    // retired previous CSR kept as the next merge's output buffers (csr_take)
+    uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
+    CsrSet spare;
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -148,6 +159,83 @@ struct Scratch {
         for (auto &q : ps)
             if (q == p) q = nullptr;
     }
+};
+
+// ------------------------------------------------------------------ CSR buffers
+// A merge writes a whole new CSR.  Allocating (and first touching) GBs of
+// fresh pool memory per batch costs milliseconds at 100M keys, so the CSR a
+// merge retires is kept as the spare set and becomes the next merge's output
+// (grown with 1/4 headroom when too small).  Small trees (< 16 MB of CSR)
+// keep no spare.
+static const uint64_t CSR_KEEP_SPARE = 16ull << 20;
+
+static void csr_free(st_tree *t, CsrSet &c) {
+    for (void *p : {(void *)c.seg_off, (void *)c.seg_voff, (void *)c.koff, (void *)c.voff, (void *)c.kheap, (void *)c.vheap})
+        dfree(t, p);
+    c = CsrSet();
+}
+
+// Output buffers for a CSR of n1 offsets (n entries + 1) and kb / vb heap
+// bytes: the spare set, grown where too small.  On failure the spare keeps
+// what it has.
+static int csr_take(st_tree *t, uint64_t n1, uint64_t kb, uint64_t vb, CsrSet &o) {
+    CsrSet &sp = t->spare;
+    if (!sp.seg_off) CHK(dalloc_t(t, &sp.seg_off, t->S + 1));
+    if (!sp.seg_voff) CHK(dalloc_t(t, &sp.seg_voff, t->S + 1));
+    if (sp.cap_n < n1 || !sp.koff || !sp.voff) {
+        dfree(t, sp.koff); dfree(t, sp.voff);
+        sp.koff = sp.voff = nullptr;
+        sp.cap_n = 0;
+        const uint64_t want = n1 + n1 / 4;
+        CHK(dalloc_t(t, &sp.koff, want));
+        CHK(dalloc_t(t, &sp.voff, want));
+        sp.cap_n = want;
+    }
+    if (sp.cap_k < kb || !sp.kheap) {
+        dfree(t, sp.kheap);
+        sp.kheap = nullptr;
+        sp.cap_k = 0;
+        CHK(dalloc(t, (void **)&sp.kheap, kb + kb / 4));
+        sp.cap_k = kb + kb / 4;
+    }
+    if (sp.cap_v < vb || !sp.vheap) {
+        dfree(t, sp.vheap);
+        sp.vheap = nullptr;
+        sp.cap_v = 0;
+        CHK(dalloc(t, (void **)&sp.vheap, vb + vb / 4));
+        sp.cap_v = vb + vb / 4;
+    }
+    o = sp;
+    sp = CsrSet();
+    return ST_OK;
+}
+
+// Make o the tree's CSR; the retired one becomes the spare set.
+static void csr_install(st_tree *t, const CsrSet &o) {
+    CsrSet old;
+    old.seg_off = t->seg_off; old.seg_voff = t->seg_voff; old.koff = t->koff; old.voff = t->voff;
+    old.kheap = t->kheap; old.vheap = t->vheap;
+    old.cap_n = t->cap_n; old.cap_k = t->cap_k; old.cap_v = t->cap_v;
+    csr_free(t, t->spare);
+    if (old.cap_n * 16 + old.cap_k + old.cap_v >= CSR_KEEP_SPARE) t->spare = old; else csr_free(t, old);
+    t->seg_off = o.seg_off; t->seg_voff = o.seg_voff; t->koff = o.koff; t->voff = o.voff;
+    t->kheap = o.kheap; t->vheap = o.vheap;
+    t->cap_n = o.cap_n; t->cap_k = o.cap_k; t->cap_v = o.cap_v;
+}
+
+// A taken set goes back to the spare slot unless installed.
+struct CsrTaken {
+    st_tree *t;
+    CsrSet o;
+    bool installed = false;
+    explicit CsrTaken(st_tree *t_) : t(t_) {}
+    CsrTaken(const CsrTaken &) = delete;
+    ~CsrTaken() {
+        if (installed) return;
+        csr_free(t, t->spare);
+        t->spare = o;
+    }
+    void install() { csr_install(t, o); installed = true; }
 };
 
 static DevTree view(const st_tree *t) {
@@ -352,6 +440,9 @@ extern "C" void st_destroy(st_tree *t) {
                   t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
+    for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
+                    (void *)t->spare.kheap, (void *)t->spare.vheap})
+        dfree(t, p);
     dfree(t, t->ov.idx);
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
@@ -706,9 +797,7 @@ static int ingest(st_tree *t, IngestIn &in) {
     DevTree d = view(t);
     Scratch sc(t);
     uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr, *mpos = nullptr;
-    uint64_t *bseg_off = nullptr, *cnt = nullptr, *nseg_off = nullptr, *src = nullptr, *klen = nullptr, *vlen = nullptr;
-    uint64_t *nkoff = nullptr, *nvoff = nullptr, *nseg_voff = nullptr, *feq = nullptr, *fne = nullptr, *ceq = nullptr,
-             *cne = nullptr;
+    uint64_t *bseg_off = nullptr;
     uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr, *nkheap = nullptr, *nvheap = nullptr;
     CHK(sc.alloc(&seg, n));
     CHK(sc.alloc(&sseg, n));
@@ -766,6 +855,8 @@ static int ingest(st_tree *t, IngestIn &in) {
     ma.seg_off = t->seg_off;
     ma.koff = t->koff;
     ma.kheap = t->kheap;
+    ma.voff = t->voff;
+    ma.vheap = t->vheap;
     ma.perm = perm;
     ma.bseg_off = bseg_off;
     ma.keep = keep;
@@ -773,58 +864,41 @@ static int ingest(st_tree *t, IngestIn &in) {
     ma.seg_reject = reject;
     ma.seg_replace = in.seg_replace;
     ma.bv = bv;
+    ma.bvoff = in.voff;
+    ma.bvheap = in.vheap;
     ma.S = S;
-    CHK(sc.alloc(&cnt, S + 1));
+    BatchSums *bs = nullptr, *bx = nullptr;
+    SegSums *ss = nullptr, *sx = nullptr;
+    CHK(sc.alloc(&ss, S + 1));
+    CHK(sc.alloc(&sx, S + 1));
     CHK(sc.alloc(&dirty, S));
     CHK(sc.alloc(&mpos, n));
-    CHK(sc.alloc(&feq, n + 1));
-    CHK(sc.alloc(&fne, n + 1));
-    CHK(sc.alloc(&ceq, n + 1));
-    CHK(sc.alloc(&cne, n + 1));
-    HIPCHK(hipMemsetAsync(cnt + S, 0, 8, t->stream));
-    // records outside every run (a partition's clamped runs) keep flags 0
-    HIPCHK(hipMemsetAsync(feq, 0, (n + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(fne, 0, (n + 1) * 8, t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, feq, fne, cnt, dirty);
-    CHK(exclusive_scan<uint64_t>(t, feq, ceq, n + 1));
-    CHK(exclusive_scan<uint64_t>(t, fne, cne, n + 1));
-    CHK(sc.alloc(&nseg_off, S + 1));
-    CHK(exclusive_scan<uint64_t>(t, cnt, nseg_off, S + 1));
-    uint64_t n_new = 0;
-    CHK(d2h(t, &n_new, nseg_off + S, 8));
-    CHK(sc.alloc(&src, n_new + 1));
+    CHK(sc.alloc(&bs, n + 1));
+    CHK(sc.alloc(&bx, n + 1));
+    HIPCHK(hipMemsetAsync(ss + S, 0, sizeof(SegSums), t->stream));
+    // records outside every run (a partition's clamped runs) keep sums 0
+    HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
+    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty);
+    CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
+    CHK(exclusive_scan<SegSums>(t, ss, sx, S + 1));
+    SegSums tot(0);
+    CHK(d2h(t, &tot, sx + S, sizeof(SegSums)));
+    const uint64_t n_new = tot.v[0];
+    CsrTaken out(t);
+    CHK(csr_take(t, n_new + 1, tot.v[1] + HEAP_SLACK, tot.v[2] + HEAP_SLACK, out.o));
+    HIPCHK(hipMemsetAsync(out.o.kheap + tot.v[1], 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(out.o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
+    MergeOut mo;
+    mo.seg_off = out.o.seg_off; mo.seg_voff = out.o.seg_voff; mo.koff = out.o.koff; mo.voff = out.o.voff;
+    mo.kheap = out.o.kheap; mo.vheap = out.o.vheap;
     LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
-           (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
+           (const BatchSums *)bx, (const SegSums *)sx, mo);
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
-           (const uint64_t *)ceq, (const uint64_t *)cne, (const uint64_t *)nseg_off, src);
-    CHK(sc.alloc(&klen, n_new + 1));
-    CHK(sc.alloc(&vlen, n_new + 1));
-    LAUNCH(t, "src_lengths", k_src_lengths, grid_for(n_new + 1), 256, 0, (const uint64_t *)src, n_new,
-           (const uint64_t *)t->koff, (const uint64_t *)t->voff, in.koff, in.voff, klen, vlen);
-    CHK(sc.alloc(&nkoff, n_new + 1));
-    CHK(sc.alloc(&nvoff, n_new + 1));
-    CHK(exclusive_scan<uint64_t>(t, klen, nkoff, n_new + 1));
-    CHK(exclusive_scan<uint64_t>(t, vlen, nvoff, n_new + 1));
-    uint64_t tot[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&tot[0], nkoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipMemcpyAsync(&tot[1], nvoff + n_new, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
-    CHK(sc.bytes(&nkheap, tot[0] + HEAP_SLACK));
-    CHK(sc.bytes(&nvheap, tot[1] + HEAP_SLACK));
-    HIPCHK(hipMemsetAsync(nkheap + tot[0], 0, HEAP_SLACK, t->stream));
-    HIPCHK(hipMemsetAsync(nvheap + tot[1], 0, HEAP_SLACK, t->stream));
-    LAUNCH(t, "gather_entries", k_gather_entries, grid_for(n_new), 256, 0, (const uint64_t *)src, n_new,
-           (const uint64_t *)t->koff, (const uint8_t *)t->kheap, (const uint64_t *)t->voff, (const uint8_t *)t->vheap,
-           in.koff, in.krec, in.voff, in.vheap, (const uint64_t *)nkoff, nkheap, (const uint64_t *)nvoff, nvheap);
-    CHK(sc.alloc(&nseg_voff, S + 1));
-    LAUNCH(t, "seg_voff", k_seg_voff, grid_for(S + 1), 256, 0, (const uint64_t *)nseg_off, (const uint64_t *)nvoff, S,
-           nseg_voff);
-    // swap in the new CSR (the old one is freed in stream order)
-    dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
-    t->seg_off = nseg_off; t->seg_voff = nseg_voff; t->koff = nkoff; t->voff = nvoff; t->kheap = nkheap; t->vheap = nvheap;
-    for (void *p : {(void *)nseg_off, (void *)nseg_voff, (void *)nkoff, (void *)nvoff, (void *)nkheap, (void *)nvheap})
-        sc.release(p);
-    t->n = n_new; t->kbytes = tot[0]; t->vbytes = tot[1];
+           (const BatchSums *)bx, (const SegSums *)sx, mo);
+    const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
+    // swap in the new CSR (the old one becomes the spare set, in stream order)
+    out.install();
+    t->n = n_new; t->kbytes = tot_k; t->vbytes = tot_v;
     t->perm_valid = false;
     // the hash-ready tiles are stale now; the next full rehash rebuilds them
     // (streaming batches never pay for a tile rebuild they do not use)
@@ -1083,12 +1157,14 @@ extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, cons
         r = ingest(t, in);
     }
     if (!r && n_corrupted && dcl) {
-        // count per-key rejections
-        std::vector<uint32_t> cl(n);
-        r = d2h(t, cl.data(), dcl, n * 4);
-        uint64_t c = 0;
-        for (uint64_t i = 0; i < n && !r; i++) c += cl[i] != 0;
-        *n_corrupted = c;
+        // count per-key rejections on the device (8 bytes back, not n statuses)
+        if (hipMemsetAsync(t->cnt64, 0, 8, t->stream) != hipSuccess) { r = ST_EDEVICE; g_err = "memset"; }
+        if (!r) {
+            hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(n)), dim3(256), 0, t->stream, (const uint32_t *)dcl, n, t->cnt64);
+            if (hipGetLastError() != hipSuccess) { r = ST_EDEVICE; g_err = "count_nonzero launch"; }
+        }
+        if (!r) r = d2h(t, t->pin, t->cnt64, 8);
+        if (!r) *n_corrupted = t->pin[0];
     }
     dfree(t, tk); dfree(t, tv); dfree(t, krec); dfree(t, dko); dfree(t, dvo); dfree(t, dcl);
     if (!r) HIPCHK(hipStreamSynchronize(t->stream));
@@ -2389,8 +2465,12 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     HIPCHK(hipMemcpyAsync(t->md5, smd, R * 16, hipMemcpyDeviceToDevice, t->stream));
     RCHK(ensure_erec(t));   // the [] records among them
     HIPCHK(hipMemcpyAsync(t->erec, serec, R, hipMemcpyDeviceToDevice, t->stream));
-    dfree(t, t->seg_off); dfree(t, t->seg_voff); dfree(t, t->koff); dfree(t, t->voff); dfree(t, t->kheap); dfree(t, t->vheap);
-    t->seg_off = nso; t->seg_voff = nsvo; t->koff = nko; t->voff = nvo; t->kheap = nkh; t->vheap = nvh;
+    {
+        CsrSet o;
+        o.seg_off = nso; o.seg_voff = nsvo; o.koff = nko; o.voff = nvo; o.kheap = nkh; o.vheap = nvh;
+        o.cap_n = ne + 1; o.cap_k = kb + HEAP_SLACK; o.cap_v = vb + HEAP_SLACK;
+        csr_install(t, o);
+    }
     t->n = ne; t->kbytes = kb; t->vbytes = vb;
     t->perm_valid = false;
     t->tiles_valid = false;
