@@ -31,12 +31,38 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_a
 #define STMD5_G(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xE4)   // (b & d) | (c & ~d)
 #define STMD5_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)   // b ^ c ^ d
 #define STMD5_I(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x39)   // c ^ (b | ~d)
-#define STMD5_STEP(f, a, b, c, d, m, k, s) a = (b) + rotl(((a) + (m) + (k)) + f((b), (c), (d)), (s))
+#define STMD5_STEP_L(f, a, b, c, d, m, k, s) a = (b) + rotl(((a) + (m) + (k)) + f((b), (c), (d)), (s))
+
+// Throughput form of a step: ((a + K) + M) + F as three v_add_u32 (K as the
+// 32-bit literal of a VOP2 add) instead of v_add_u32 + v_add3_u32 (the
+// compiler fuses a three-term sum into add3).  On gfx950 a SIMD running >= 2
+// waves of MD5 issues this mix ~40 % faster (tools/microbench/md5_variants.cpp
+// V9: 149 vs 106 G lane-blocks/s at 16 waves/CU), while a lone wave's
+// dependent chain is ~35 % slower (0.77 vs 0.58 us per block).  Hence two forms:
+// compress<true> for the bulk segment hashing (K1, 16 waves per CU), the
+// default for the latency-bound inner-node chains.
+__device__ __forceinline__ uint32_t vadd(uint32_t x, uint32_t y) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ uint32_t vaddk(uint32_t x, uint32_t k) {
+    uint32_t r;
+    asm("v_add_u32 %0, %2, %1" : "=v"(r) : "v"(x), "i"(k));
+    return r;
+}
+#define STMD5_STEP_T(f, a, b, c, d, m, k, s) a = (b) + rotl(vadd(vadd(vaddk((a), (k)), (m)), f((b), (c), (d))), (s))
+#define STMD5_STEP(f, a, b, c, d, m, k, s)                     \
+    do {                                                       \
+        if (TPUT) STMD5_STEP_T(f, a, b, c, d, m, k, s);        \
+        else STMD5_STEP_L(f, a, b, c, d, m, k, s);             \
+    } while (0)
 
 __device__ __forceinline__ void init(uint32_t s[4]) {
     s[0] = 0x67452301u; s[1] = 0xefcdab89u; s[2] = 0x98badcfeu; s[3] = 0x10325476u;
 }
 
+template <bool TPUT = false>
 __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
     STMD5_STEP(STMD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
@@ -166,6 +192,7 @@ __device__ __forceinline__ void md5_global(const uint8_t *p, uint64_t len, uint3
 // Same, with the next block's loads issued before the current block is
 // compressed (software pipelining: the loads' latency hides under ~330 VALU
 // ops of the compression).
+template <bool TPUT = false>
 __device__ __forceinline__ void md5_global_pf(const uint8_t *p, uint64_t len, uint32_t out[4]) {
     uint32_t st[4];
     init(st);
@@ -181,7 +208,7 @@ __device__ __forceinline__ void md5_global_pf(const uint8_t *p, uint64_t len, ui
         const int64_t rem = (int64_t)len - (int64_t)(64 * k);
         if (rem - 64 > 0) load_block_global(p + 64 * (k + 1), nx);
         if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        compress(st, m);
+        compress<TPUT>(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
@@ -271,8 +298,13 @@ __device__ __forceinline__ void pack4(const uint32_t *pf, const uint4 *h, uint32
     w[16] = h[3].w;
 }
 
-// Message words 16k..16k+15 of the 80-word padded message of a full node.
-__device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const uint4 h[16], uint32_t m[16]) {
+// Message words 16k..16k+15 of the 80-word padded message of a node with n
+// (15 or 16) present children compacted into h[0..n-1], pf[0..n-1].  For n ==
+// 15 the caller sets pf[15] = 0x80 (the terminator lands on byte 255, where
+// the 16th tag byte would be) and h[15] = 0; the last block then differs only
+// in word 68 (0x80 for n == 16, zero for n == 15) and the bit length.
+__device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const uint4 h[16], uint32_t m[16],
+                                             uint32_t n = 16) {
     uint32_t a[17], b[17];
     switch (k) {
     case 0:
@@ -310,10 +342,10 @@ __device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const
         m[1] = a[14];
         m[2] = a[15];
         m[3] = a[16];
-        m[4] = 0x80u;
+        m[4] = n == 16 ? 0x80u : 0u;
 #pragma unroll
         for (int w = 5; w < 16; w++) m[w] = 0u;
-        m[14] = 272u * 8u;
+        m[14] = 17u * 8u * n;
         break;
     }
 }
@@ -321,13 +353,13 @@ __device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const
 // One compress in a rolled loop: these kernels run a few waves per CU once
 // through the code, so straight-line unrolled MD5 (~14 KB) would be bound by
 // instruction-cache misses.
-__device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[16], uint32_t out[4]) {
+__device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[16], uint32_t out[4], uint32_t n = 16) {
     uint32_t st[4];
     init(st);
 #pragma unroll 1
     for (int k = 0; k < 5; k++) {
         uint32_t m[16];
-        node16_block(k, pf, h, m);
+        node16_block(k, pf, h, m, n);
         compress(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];

@@ -29,7 +29,8 @@
 
 struct SmallIn {
     uint32_t n, op;       // op: 0 = get/2, 1 = insert/3
-    uint32_t dbg, pad;    // dbg: phase stamps into SmallOut.stamp (ST_SMALL_STAMPS)
+    uint32_t dbg, seq;    // dbg: phase stamps into SmallOut.stamp (ST_SMALL_STAMPS); seq: the call's
+                          // sequence number (never 0), echoed in SmallOut.sseq / done
     uint32_t koff[SB_MAX + 1];
     uint32_t voff[SB_MAX + 1];
     uint8_t kb[SB_KB];
@@ -41,13 +42,26 @@ struct SmallOut {
     uint32_t clevel[SB_MAX];
     uint64_t cbucket[SB_MAX];
     uint32_t voff[SB_MAX + 1]; // get: value i = vbytes[voff[i] .. voff[i+1])
+    uint32_t sseq[SB_MAX];     // key i's results are complete once sseq[i] == the call's seq
     uint32_t retry;            // 1: not served (overlay full, segment too large): use the bulk path
     uint32_t new_entries;      // insert: keys that were not in their segment before
-    uint32_t done;             // set last (host sanity check)
+    uint32_t done;             // the call's seq, written last
     uint32_t pad;
     uint64_t stamp[8];         // diagnostic phase stamps (100 MHz), in.dbg only
     uint8_t vbytes[SB_OUT_VB];
 };
+
+// Completion protocol of the result block (mapped host memory).  Each key's
+// results (status, level, bucket, value offset and bytes) are written by one
+// thread, which then fences at system scope and writes the key's sequence
+// word; thread 0 writes `done` = seq after a barrier and its own fence.  The
+// host waits for done == seq AND every sseq[i] == seq, so it never acts on a
+// result word of an earlier call: a call's words are tagged, not just
+// ordered (an earlier build read an earlier call's statuses, intermittently).
+__device__ __forceinline__ void key_done(SmallOut *out, uint32_t i, uint32_t seq) {
+    __threadfence_system();
+    out->sseq[i] = seq;
+}
 
 struct Overlay {
     uint64_t *idx;              // [S], ~0 = segment not in the overlay
@@ -323,7 +337,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
     SB_STAMP(5);
     const bool ok = bad[0] == ~0u;
     if (s1_retry) {   // nothing was committed: the host takes the bulk path
-        if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = 1; }
+        if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = in.seq; }
         return;
     }
     if (ok) {   // commit: the overlay record and the path's entries
@@ -346,12 +360,13 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
         }
         out->new_entries = ok ? s1_news : 0;
         out->retry = 0;
+        key_done(out, 0, in.seq);
     }
     SB_STAMP(6);
     __threadfence_system();
     __syncthreads();
     SB_STAMP(7);
-    if (tid == 0) out->done = 1;
+    if (tid == 0) { __threadfence_system(); out->done = in.seq; }
 }
 
 // The small-batch kernel (one workgroup of 256 threads, 4 waves).
@@ -395,11 +410,14 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     __syncthreads();
     const bool undefined_top = (t.tag[0] & TAG_PRESENT) == 0;
     if (in.op == 0 && undefined_top) {   // get/2: undefined top => notfound (synctree.erl:216-218)
-        if (tid < n) { out->status[tid] = ST_NOTFOUND; out->clevel[tid] = 0; out->cbucket[tid] = 0; }
-        if (tid <= n) out->voff[tid] = 0;
-        __threadfence_system();
+        if (tid < n) {
+            out->status[tid] = ST_NOTFOUND; out->clevel[tid] = 0; out->cbucket[tid] = 0;
+            out->voff[tid + 1] = 0;
+            if (tid == 0) out->voff[0] = 0;
+            key_done(out, tid, in.seq);
+        }
         __syncthreads();
-        if (tid == 0) { out->retry = 0; out->new_entries = 0; __threadfence_system(); out->done = 1; }
+        if (tid == 0) { out->retry = 0; out->new_entries = 0; __threadfence_system(); out->done = in.seq; }
         return;
     }
     if (in.op == 1 && n == 1) {   // insert/3 of one key: the speculative path below
@@ -436,14 +454,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         uint32_t len = 0;
         const uint8_t *src = nullptr;
         if (tid < n) {
-            if (bad[tid] != ~0u) {
-                out->status[tid] = ST_CORRUPTED;
-                out->clevel[tid] = bad[tid];
-                out->cbucket[tid] = seg[tid] >> (t.shift * (L1 - bad[tid]));
-            } else {
-                out->status[tid] = gfound[tid] ? ST_OK : ST_NOTFOUND;
-                out->clevel[tid] = 0;
-                out->cbucket[tid] = 0;
+            if (bad[tid] == ~0u) {
                 len = glen[tid];
                 src = gsrc[tid];
             }
@@ -456,14 +467,26 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
             retry = vlen_out[n] > SB_OUT_VB;
         }
         __syncthreads();
-        if (tid <= n) out->voff[tid] = vlen_out[tid];
-        if (tid < n && !retry && src)
-            for (uint32_t b = 0; b < len; b++) out->vbytes[vlen_out[tid] + b] = src[b];
+        if (tid < n) {   // this key's value bytes and result words, then its sequence word
+            if (!retry && src)
+                for (uint32_t b = 0; b < len; b++) out->vbytes[vlen_out[tid] + b] = src[b];
+            if (tid == 0) out->voff[0] = 0;
+            out->voff[tid + 1] = vlen_out[tid + 1];
+            if (bad[tid] != ~0u) {
+                out->status[tid] = ST_CORRUPTED;
+                out->clevel[tid] = bad[tid];
+                out->cbucket[tid] = seg[tid] >> (t.shift * (L1 - bad[tid]));
+            } else {
+                out->status[tid] = gfound[tid] ? ST_OK : ST_NOTFOUND;
+                out->clevel[tid] = 0;
+                out->cbucket[tid] = 0;
+            }
+            key_done(out, tid, in.seq);
+        }
         SB_STAMP(6);
-        __threadfence_system();
         __syncthreads();
         SB_STAMP(7);
-        if (tid == 0) { out->retry = retry; out->new_entries = 0; __threadfence_system(); out->done = 1; }
+        if (tid == 0) { out->retry = retry; out->new_entries = 0; __threadfence_system(); out->done = in.seq; }
         return;
     }
     // ---- 3 (insert): groups = distinct verified segments, last writer per key
@@ -578,7 +601,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         }
         __syncthreads();
         if (pass == 0 && retry) {   // nothing was written: the host takes the bulk path
-            if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = 1; }
+            if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = in.seq; }
             return;
         }
     }
@@ -636,6 +659,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
             out->clevel[tid] = 0;
             out->cbucket[tid] = 0;
         }
+        key_done(out, tid, in.seq);
     }
     if (tid == 0) {
         uint32_t c = 0;
@@ -643,9 +667,8 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         out->new_entries = c;
         out->retry = 0;
     }
-    __threadfence_system();
     __syncthreads();
-    if (tid == 0) out->done = 1;
+    if (tid == 0) { __threadfence_system(); out->done = in.seq; }
 }
 
 // Overlay flush, step 1: per segment, the number of overlay entries and

@@ -172,12 +172,12 @@ __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64
             for (int w = 3; w < 16; w++) m[w] = 0u;
             m[14] = 64u;
             stmd5::init(d);
-            stmd5::compress(d, m);
+            stmd5::compress<true>(d, m);
         } else {
             const uint8_t *sp;
             uint64_t sl;
             krec_seg_bytes(p, len, &sp, &sl);
-            stmd5::md5_global_pf(sp, sl, d);
+            stmd5::md5_global_pf<true>(sp, sl, d);
         }
         const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
         seg_out[i] = (uint32_t)(lo & segmask);
@@ -1572,7 +1572,7 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
         }
         uint32_t dg[4];
         const uint64_t v0 = t.seg_voff[s];
-        stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, dg);
+        stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, dg);
         const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;
@@ -1911,21 +1911,32 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
     uint32_t t16[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) t16[j] = tags[j];
-    uint32_t full = 1;
+    uint32_t pm = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j++) full &= (t16[j] >> 8) & 1u;
+    for (int j = 0; j < 16; j++) pm |= ((t16[j] >> 8) & 1u) << j;
+    const uint32_t np = __builtin_popcount(pm);
     uint32_t dg[4];
     // The path is chosen per WAVE, not per lane: a wave whose active lanes
-    // all hold full nodes hashes from registers (md5_node16, the common case
-    // in big trees); otherwise every lane packs its present entries into its
-    // LDS region and hashes from there.  Lanes of one wave never split
-    // between the two paths (that would run both, one after the other).
-    if (__ballot(!full) == 0) {
+    // all hold nodes with 15 or 16 present children hashes from registers
+    // (md5_node16, the common case in big trees: an empty segment leaves its
+    // level-H parent with 15); otherwise every lane packs its present entries
+    // into its LDS region and hashes from there.  Lanes of one wave never
+    // split between the two paths (that would run both, one after the other).
+    if (__ballot(np < 15) == 0) {
         uint32_t pf[16];
         uint4 hr[16];   // one LDS round trip for the whole node
 #pragma unroll
         for (int j = 0; j < 16; j++) { pf[j] = t16[j] & 0xffu; hr[j] = h[j]; }
-        stmd5::md5_node16(pf, hr, dg);
+        if (__ballot(np == 15)) {
+            // one absent child ja: the entries after it move down one place
+            // (selects with compile-time indices, no register indexing)
+            const uint32_t ja = np == 15 ? (uint32_t)__builtin_ctz(~pm & 0xffffu) : 16u;
+#pragma unroll
+            for (int r = 0; r < 15; r++)
+                if ((uint32_t)r >= ja) { hr[r] = hr[r + 1]; pf[r] = pf[r + 1]; }
+            if (np == 15) { hr[15] = make_uint4(0, 0, 0, 0); pf[15] = 0x80u; }
+        }
+        stmd5::md5_node16(pf, hr, dg, np);
         tg = TAG_PRESENT;
         e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         return;
@@ -1965,7 +1976,10 @@ __device__ __forceinline__ void lds_barrier() {
 __host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return levels3_16_lds_bytes() + 256 * MSG16 + 64; }
 
 // STAMP (diagnostic, ST_LEVEL_STAMPS=1): wall-clock stamps (100 MHz) per
-// workgroup at phase boundaries into stamps[blockIdx.x * 8 + k].
+// workgroup at phase boundaries into stamps[blockIdx.x * 16 + k] (thread 0's
+// view: 0 start, 1 K1 done, 2/4/6 level H/H-1/H-2 hashed, 3/5 level H/H-1
+// barrier passed, 7 mailbox stored, 8/12 climb counter won, 9/13 mailboxes
+// read, 10/14 level 2/1 hashed, 11 level-2 mailbox stored, 15 exit).
 __device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg) {
     __hip_atomic_store(&m->lo, ((unsigned long long)e.y << 32) | e.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&m->hi, ((unsigned long long)e.w << 32) | e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1986,7 +2000,7 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
 template <bool STAMP, bool GROUP>
 __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
                                                        uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
-#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     RF_STAMP(0);
     const uint32_t gi = GROUP ? blockIdx.x / nwin : 0;
     const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
@@ -2056,7 +2070,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             }
             locate(f, q, k);
             const uint32_t nb = pick(nbq, q);
-            if (k < nb) stmd5::compress(st, m);
+            if (k < nb) stmd5::compress<true>(st, m);
             if (k + 1 == pick(Bq, q)) {
                 put_entry(pick(liq, q), nb, st);
                 stmd5::init(st);
@@ -2079,7 +2093,6 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         }
     }
 
-    RF_STAMP(2);
     // ---- phase 3: levels H, H-1, H-2 from LDS, then the climb
     uint32_t l = H;
     uint64_t b = root * 256 + tid;
@@ -2095,6 +2108,8 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             uint4 e;
             uint32_t tg;
             node16_any(ent, tgs, reg, e, tg);
+            if (phase <= 2) RF_STAMP(2 + 2 * phase);
+            else RF_STAMP(l == 2 ? 10 : 14);
             const uint64_t slot = t.base[l] + b;
             if (tg) (GROUP ? group[gi].md5 : t.md5)[slot] = e;
             (GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
@@ -2108,7 +2123,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         }
         if (phase < 2) {
             lds_barrier();   // the next level reads this one's LDS entries only
-            RF_STAMP(3 + phase);
+            RF_STAMP(3 + 2 * phase);
             l--;
             if (phase == 0) {
                 act = tid < 16;
@@ -2125,15 +2140,16 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             }
             continue;
         }
-        if (phase == 2) RF_STAMP(5);
         if (tid != 0 || l <= lmin) break;
         const uint64_t p = b >> 4;
         uint32_t *c = RFT(cnt) + t.base[l - 1] + p;
         // the mailbox stores above have completed (agent-coherent) before the
         // counter moves; no L2 write-back / invalidate is needed
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RF_STAMP(l == H - 2 ? 7 : 11);
         const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old != 15u) break;
+        RF_STAMP(l == H - 2 ? 8 : 12);
         __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         l--;
         b = p;
@@ -2150,7 +2166,11 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         }
         ent = reinterpret_cast<const uint4 *>(Cb);
         tgs = reinterpret_cast<const uint16_t *>(Ct);
-        RF_STAMP(6 + (l == 1));
+        RF_STAMP(l == 1 ? 13 : 9);
+    }
+    if (STAMP && tid == 0) {
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        RF_STAMP(15);
     }
 #undef RFT
 #undef RF_STAMP
@@ -2262,7 +2282,7 @@ __global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTil
                 const uint4 *q = nxt.tiles + tn.base + lane;
                 n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
             }
-            if (k < nb) stmd5::compress(st, m);
+            if (k < nb) stmd5::compress<true>(st, m);
         }
         tile_store(t, cur.md5, cur.tag, seg, nb, st);
         if (gx >= ntiles) break;

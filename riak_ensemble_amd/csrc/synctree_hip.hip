@@ -112,6 +112,7 @@ struct st_tree {
     Overlay ov{nullptr, nullptr, nullptr, 0};
     bool ov_pending = false;
     SmallOut *sout = nullptr, *sout_dev = nullptr;
+    uint32_t small_seq = 0;   // sequence number of the last k_small call
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -299,13 +300,15 @@ struct TimedLaunch {
 // after a system-scope fence, last): a spin of a few microseconds instead of
 // a stream synchronisation call; after 5 ms fall back to the blocking sync
 // (which also reports a faulted kernel).
-static int wait_mapped(st_tree *t, volatile uint32_t *flag) {
+static int wait_mapped(st_tree *t, volatile uint32_t *flag, uint32_t want = 0) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
         // acquire: the reads of the results the kernel wrote before the flag
         // may not move above this load (a volatile read alone does not order
-        // the plain reads that follow it)
-        if (__atomic_load_n(const_cast<uint32_t *>(flag), __ATOMIC_ACQUIRE)) return ST_OK;
+        // the plain reads that follow it).  want != 0: wait for that value
+        // (a call's sequence number), else for any non-zero value.
+        const uint32_t v = __atomic_load_n(const_cast<uint32_t *>(flag), __ATOMIC_ACQUIRE);
+        if (want ? v == want : v != 0) return ST_OK;
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
         __builtin_ia32_pause();
     }
@@ -701,20 +704,30 @@ static int rehash_tiled(st_tree *t) {
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
         Scratch sc(t);
         uint64_t *st = nullptr;
-        CHK(sc.alloc(&st, (uint64_t)nwg * 8));
-        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 8 * 8, t->stream));
+        CHK(sc.alloc(&st, (uint64_t)nwg * 16));
+        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
         LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
                (const TreeTiles *)nullptr, 0u, root0, lmin, st);
-        std::vector<uint64_t> h((uint64_t)nwg * 8);
+        std::vector<uint64_t> h((uint64_t)nwg * 16);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipStreamSynchronize(t->stream));
         uint64_t t0 = ~0ull;
-        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 8]);
-        static const char *names[8] = {"start", "K1 done", "entries stored", "level H", "level H-1", "level H-2",
-                                       "climb level", "level 1 + top"};
-        for (int k = 0; k < 8; k++) {
+        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
+        if (const char *dump = getenv("ST_STAMP_DUMP")) {   // raw per-window stamps (ticks from t0)
+            if (FILE *f = fopen(dump, "a")) {
+                for (uint32_t w = 0; w < nwg; w++) {
+                    for (int k = 0; k < 16; k++) fprintf(f, "%lld ", h[w * 16 + k] ? (long long)(h[w * 16 + k] - t0) : -1ll);
+                    fprintf(f, "\n");
+                }
+                fclose(f);
+            }
+        }
+        static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
+                                        "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
+                                        "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
+        for (int k = 0; k < 16; k++) {
             std::vector<double> v;
-            for (uint32_t w = 0; w < nwg; w++) if (h[w * 8 + k]) v.push_back((h[w * 8 + k] - t0) / 100.0);
+            for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
             if (v.empty()) continue;
             std::sort(v.begin(), v.end());
             fprintf(stderr, "fused stamp %d %-15s n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, names[k], v.size(), v[0],
@@ -983,11 +996,16 @@ static int ensure_small(st_tree *t) {
         t->ov.cap = cap;
     }
     if (!t->sout) {
-        if (hipHostMalloc((void **)&t->sout, sizeof(SmallOut), hipHostMallocMapped) != hipSuccess) {
+        // fine-grained (coherent) host memory: the GPU's writes bypass its
+        // L2, so no stale cached copy of an earlier call's line (with its
+        // done flag) can be written back over the host's reset, and the host
+        // sees the results in the order the kernel fences them
+        if (hipHostMalloc((void **)&t->sout, sizeof(SmallOut), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
             t->sout = nullptr;
             g_err = "hipHostMalloc (mapped) failed";
             return ST_EDEVICE;
         }
+        memset(t->sout, 0, sizeof(SmallOut));   // no stale sequence words
         HIPCHK(hipHostGetDevicePointer((void **)&t->sout_dev, t->sout, 0));
     }
     return ST_OK;
@@ -1017,10 +1035,18 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
         for (uint64_t i = 0; i <= n; i++) in.voff[i] = (uint32_t)(voff[i] - voff[0]);
         memcpy(in.vb, vheap + voff[0], vbytes);
     }
-    t->sout->done = 0;
+    if (++t->small_seq == 0) t->small_seq = 1;
+    in.seq = t->small_seq;
     LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev);
-    CHK(wait_mapped(t, &t->sout->done));
-    if (!t->sout->done) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
+    CHK(wait_mapped(t, &t->sout->done, in.seq));
+    if (t->sout->done != in.seq) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
+    if (!t->sout->retry)
+        for (uint64_t i = 0; i < n; i++) {
+            if (sdbg && __atomic_load_n(&t->sout->sseq[i], __ATOMIC_ACQUIRE) != in.seq)
+                fprintf(stderr, "small: key %llu result word behind done (seq %u)\n", (unsigned long long)i, in.seq);
+            CHK(wait_mapped(t, &t->sout->sseq[i], in.seq));
+            if (t->sout->sseq[i] != in.seq) { g_err = "small-batch results incomplete"; return ST_EDEVICE; }
+        }
     if (sdbg) {   // diagnostic: phase times (µs from kernel start) to stderr
         const uint64_t *st = t->sout->stamp;
         fprintf(stderr, "small op=%d n=%llu:", op, (unsigned long long)n);
@@ -1923,7 +1949,7 @@ static int ensure_cmp_work(st_tree *t) {
     CHK(dalloc_t(t, &w.wbytes, w.nw));
     CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
     CHK(dalloc_t(t, &w.werr, w.nw));
-    if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         w.res = nullptr;
         g_err = "hipHostMalloc failed";
         return ST_EDEVICE;
