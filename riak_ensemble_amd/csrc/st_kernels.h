@@ -1788,8 +1788,37 @@ __host__ __device__ __forceinline__ uint32_t levels3_16_lds_bytes() {
 struct TileInfo {
     uint64_t base;   // in uint4 units
     uint32_t B;      // blocks of the longest message in the tile
-    uint32_t pad;
+    uint32_t R;      // 16-byte rows stored per lane: the longest message's data rows
 };
+
+// Per-lane message descriptor of a tile (tln): 0 = no message (an empty
+// segment or a padding lane), else the message length + 1.  A tile stores
+// only the rows that hold message bytes of some lane (R); the rows past them
+// (padding zeros, the 0x80 terminator, the bit length) are synthesized in
+// registers by the hashing wave, so they cost no HBM traffic.
+__host__ __device__ __forceinline__ uint32_t ln_blocks(uint32_t ln) {
+    return ln ? (uint32_t)(((uint64_t)ln - 1 + 8) / 64 + 1) : 0u;
+}
+__host__ __device__ __forceinline__ uint32_t ln_rows(uint32_t ln) { return ln ? (uint32_t)(((uint64_t)ln - 1 + 15) / 16) : 0u; }
+
+// Row `row` (bytes 16 row .. 16 row + 15) of a lane's padded message: loaded
+// when the tile stores it, else zeros plus the terminator / bit length where
+// they fall (RFC 1321 §3.1-3.2).  R is wave-uniform: the branch is scalar.
+__device__ __forceinline__ uint4 tile_synth(uint32_t row, uint32_t ln) {
+    const uint32_t len = ln - 1;   // ln == 0: the lane hashes nothing
+    uint4 c = make_uint4(0, 0, 0, 0);
+    if ((len >> 4) == row) {       // only when len == 16 R: the terminator opens this row
+        const uint32_t v = 0x80u << (8 * (len & 3)), w = (len >> 2) & 3;
+        c.x = w == 0 ? v : 0u; c.y = w == 1 ? v : 0u; c.z = w == 2 ? v : 0u; c.w = w == 3 ? v : 0u;
+    }
+    if (row == 4 * ln_blocks(ln) - 1) { c.z |= len << 3; c.w |= len >> 29; }
+    return c;
+}
+__device__ __forceinline__ uint4 tile_row(const uint4 *tiles, uint64_t base, uint32_t lane, uint32_t row, uint32_t R,
+                                          uint32_t ln) {
+    if (row < R) return tiles[base + (uint64_t)row * 64 + lane];
+    return tile_synth(row, ln);
+}
 
 // Per-tree pointers of a batched (multi-tree) rehash: trees of one geometry,
 // e.g. the ensembles one GPU hosts.
@@ -1809,48 +1838,59 @@ struct TreeTiles {
     uint32_t *cnt;
     MailEntry *mail;
     const TileInfo *tinfo;
-    const uint32_t *tseg, *tnb;
+    const uint32_t *tseg, *tln;
     const uint4 *tiles;
 };
 
 
-// One workgroup per tile: write the padded messages in tiled order.
+// One workgroup per tile: write the tile's stored rows (row r of lane j at
+// tiles[base + r * 64 + j]) of the padded messages.
 __global__ void __launch_bounds__(256) k_tile_fill(const uint64_t *__restrict__ seg_voff, const uint8_t *__restrict__ vheap,
-                                                   const uint32_t *__restrict__ tseg, const uint64_t *__restrict__ tbase,
-                                                   const uint64_t *__restrict__ tsize, uint4 *__restrict__ tiles) {
+                                                   const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ tln,
+                                                   const TileInfo *__restrict__ tinfo, uint4 *__restrict__ tiles) {
     const uint32_t tid = threadIdx.x, q = tid >> 6, j = tid & 63;
     const uint64_t tl = blockIdx.x;
-    const uint32_t B = (uint32_t)(tsize[tl] / 256);
-    if (B == 0) return;
-    const uint32_t s = tseg[tl * 64 + j];
-    const bool pad = s == 0xffffffffu;
-    const uint64_t v0 = pad ? 0 : seg_voff[s];
-    const uint64_t len = pad ? 0 : seg_voff[s + 1] - v0;
-    const uint32_t nb = len ? (uint32_t)((len + 8) / 64 + 1) : 0u;
-    uint4 *dst = tiles + tbase[tl] + q * 64 + j;
-    for (uint32_t k = 0; k < B; k++) {
+    const TileInfo ti = tinfo[tl];
+    if (ti.R == 0) return;
+    const uint32_t ln = tln[tl * 64 + j];
+    const uint64_t v0 = ln ? seg_voff[tseg[tl * 64 + j]] : 0;
+    const uint64_t len = ln ? ln - 1 : 0;
+    const uint32_t nb = ln_blocks(ln);
+    for (uint32_t row = q; row < ti.R; row += 4) {
         uint4 c = make_uint4(0, 0, 0, 0);
-        if (k < nb) {
-            const uint64_t off = 64ull * k + 16ull * q;
+        if ((row >> 2) < nb) {
+            const uint64_t off = 16ull * row;
             if (off < len) __builtin_memcpy(&c, vheap + v0 + off, 16);
             const int64_t rem = (int64_t)len - (int64_t)off;
             c.x = stmd5::tail_word(c.x, rem >= 4 ? 4 : (int)rem);
             c.y = stmd5::tail_word(c.y, rem - 4 >= 4 ? 4 : (int)(rem - 4));
             c.z = stmd5::tail_word(c.z, rem - 8 >= 4 ? 4 : (int)(rem - 8));
             c.w = stmd5::tail_word(c.w, rem - 12 >= 4 ? 4 : (int)(rem - 12));
-            if (k + 1 == nb && q == 3) { c.z = (uint32_t)(len << 3); c.w = (uint32_t)(len >> 29); }
+            if (row == 4 * nb - 1) { c.z = (uint32_t)(len << 3); c.w = (uint32_t)(len >> 29); }
         }
-        dst[(uint64_t)k * 256] = c;
+        tiles[ti.base + (uint64_t)row * 64 + j] = c;
     }
 }
 
-__global__ void k_tile_info(const uint64_t *tbase, const uint64_t *tsize, uint64_t ntiles, TileInfo *info) {
-    for (uint64_t i = gtid(); i < ntiles; i += gstride()) {
-        TileInfo x;
-        x.base = tbase[i];
-        x.B = (uint32_t)(tsize[i] / 256);
-        x.pad = 0;
-        info[i] = x;
+__global__ void k_tile_info(const uint64_t *tbase, uint64_t ntiles, TileInfo *info) {
+    for (uint64_t i = gtid(); i < ntiles; i += gstride()) info[i].base = tbase[i];
+}
+
+// Tile shape from its 64 lanes' descriptors (one wave per tile): B = the
+// most blocks, R = the most data rows; tsize = the stored uint4s (scanned
+// into the tile bases).
+__device__ __forceinline__ void tile_shape(uint32_t ln, uint64_t tl, bool lead, TileInfo *tinfo, uint64_t *tsize) {
+    uint32_t b = ln_blocks(ln), r = ln_rows(ln);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t yb = __shfl_xor(b, o, 64), yr = __shfl_xor(r, o, 64);
+        b = yb > b ? yb : b;
+        r = yr > r ? yr : r;
+    }
+    if (lead) {
+        tinfo[tl].B = b;
+        tinfo[tl].R = r;
+        tsize[tl] = (uint64_t)r * 64;
     }
 }
 
@@ -1861,26 +1901,21 @@ __global__ void k_tile_info(const uint64_t *tbase, const uint64_t *tsize, uint64
 // instruction reads 1 KiB contiguous.  Positions past S are padding
 // (tseg = 0xffffffff, nb = 0).
 __global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint32_t *__restrict__ perm,
-                                                           uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
-                                                           uint64_t *__restrict__ tsize, uint64_t ntiles) {
+                                                           uint32_t *__restrict__ tseg, uint32_t *__restrict__ tln,
+                                                           TileInfo *__restrict__ tinfo, uint64_t *__restrict__ tsize,
+                                                           uint64_t ntiles) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t tl = i >> 6;
-    uint32_t s = 0xffffffffu, nb = 0;
+    uint32_t s = 0xffffffffu, ln = 0;
     if (i < t.S) {
         s = perm[i];
-        if (t.seg_off[s] != t.seg_off[s + 1]) nb = (uint32_t)((t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1);
+        if (t.seg_off[s] != t.seg_off[s + 1]) ln = (uint32_t)(t.seg_voff[s + 1] - t.seg_voff[s] + 1);
     }
     if (tl < ntiles) {
         tseg[i] = s;
-        tnb[i] = nb;
+        tln[i] = ln;
     }
-    uint32_t m = nb;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t y = __shfl_xor(m, o, 64);
-        m = y > m ? y : m;
-    }
-    if ((threadIdx.x & 63) == 0 && tl < ntiles) tsize[tl] = (uint64_t)m * 256;
+    tile_shape(ln, tl, (threadIdx.x & 63) == 0 && tl < ntiles, tinfo, tsize);
 }
 
 // ---------------------------------------------------------------------------
@@ -1956,10 +1991,12 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
 
 #define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
 
-__device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t lane, uint32_t k, uint4 &a,
-                                                uint4 &b, uint4 &c, uint4 &d) {
-    const uint4 *q = tiles + base + lane + 256ull * k;
-    a = q[0]; b = q[64]; c = q[128]; d = q[192];
+__device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t R, uint32_t ln, uint32_t lane,
+                                                uint32_t k, uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
+    a = tile_row(tiles, base, lane, 4 * k, R, ln);
+    b = tile_row(tiles, base, lane, 4 * k + 1, R, ln);
+    c = tile_row(tiles, base, lane, 4 * k + 2, R, ln);
+    d = tile_row(tiles, base, lane, 4 * k + 3, R, ln);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
@@ -1976,7 +2013,8 @@ __device__ __forceinline__ void lds_barrier() {
 __host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return levels3_16_lds_bytes() + 256 * MSG16 + 64; }
 
 // STAMP (diagnostic, ST_LEVEL_STAMPS=1): wall-clock stamps (100 MHz) per
-// workgroup at phase boundaries into stamps[blockIdx.x * 16 + k] (thread 0's
+// workgroup at phase boundaries into stamps[blockIdx.x * 32 + k], the shader
+// clock (s_memtime) at the same points into [.. + 16 + k] (thread 0's
 // view: 0 start, 1 K1 done, 2/4/6 level H/H-1/H-2 hashed, 3/5 level H/H-1
 // barrier passed, 7 mailbox stored, 8/12 climb counter won, 9/13 mailboxes
 // read, 10/14 level 2/1 hashed, 11 level-2 mailbox stored, 15 exit).
@@ -2000,7 +2038,8 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
 template <bool STAMP, bool GROUP>
 __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
                                                        uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
-#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+                                                          stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
     RF_STAMP(0);
     const uint32_t gi = GROUP ? blockIdx.x / nwin : 0;
     const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
@@ -2022,27 +2061,22 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
     const uint64_t seg0 = root * 4096;
 
     // ---- phase 1: K1 over this wave's tiles, one flat block stream
-    uint32_t Bq[RF_TILES], nbq[RF_TILES], liq[RF_TILES];
+    uint32_t Bq[RF_TILES], Rq[RF_TILES], lnq[RF_TILES], liq[RF_TILES];
     uint64_t bq[RF_TILES];
-    uint32_t P[RF_TILES + 1];
-    P[0] = 0;
+    uint32_t T = 0;   // blocks in the wave's stream
 #pragma unroll
     for (int q = 0; q < RF_TILES; q++) {
         const uint64_t tl = root * 64 + wave + 16 * q;
         const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
+        Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
         const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ti.base),
                        bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ti.base >> 32));
         bq[q] = ((uint64_t)bhi << 32) | blo;
         liq[q] = (uint32_t)(RFT(tseg)[tl * 64 + lane] - seg0);
-        nbq[q] = RFT(tnb)[tl * 64 + lane];
-        P[q + 1] = P[q] + Bq[q];
+        lnq[q] = RFT(tln)[tl * 64 + lane];
+        T += Bq[q];
     }
-    const uint32_t T = P[RF_TILES];
-    auto locate = [&](uint32_t f, uint32_t &q, uint32_t &k) {
-        q = (f >= P[1]) + (f >= P[2]) + (f >= P[3]);
-        k = f - (q == 0 ? P[0] : q == 1 ? P[1] : q == 2 ? P[2] : P[3]);
-    };
     auto pick = [&](const uint32_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
     auto pick64 = [&](const uint64_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
     auto put_entry = [&](uint32_t li, uint32_t nb, const uint32_t st[4]) {
@@ -2053,28 +2087,72 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         *reinterpret_cast<uint16_t *>(At + (li >> 4) * TB16 + (li & 15) * 2) = tg;
     };
     {
-        uint4 r0a, r0b, r0c, r0d, r1a, r1b, r1c, r1d;
-        uint32_t q, k;
-        if (T > 0) { locate(0, q, k); tile_block_load(RFT(tiles), pick64(bq, q), lane, k, r0a, r0b, r0c, r0d); }
-        if (T > 1) { locate(1, q, k); tile_block_load(RFT(tiles), pick64(bq, q), lane, k, r1a, r1b, r1c, r1d); }
+        // Two cursors walk the wave's tiles: the fetch cursor (lq, lk) two
+        // blocks ahead of the hash cursor (cq, ck).  Per-tile values are
+        // picked only when a cursor crosses into the next tile (wave-uniform:
+        // scalar registers and branches); per block the hash cursor costs one
+        // compare.
+        auto next_tile = [&](uint32_t q) {
+            while (q < RF_TILES && pick(Bq, q) == 0) q++;
+            return q;
+        };
+        uint32_t lq = next_tile(0), lk = 0, lR = 0, lB = 0;
+        uint64_t lbase = 0;
+        if (lq < RF_TILES) { lbase = pick64(bq, lq); lR = pick(Rq, lq); lB = pick(Bq, lq); }
+        // Always four loads per block (rows past the stored ones re-read the
+        // last stored row; hash_block replaces them), so the wait before a
+        // buffer is hashed leaves the other buffer's four loads in flight.
+        auto fetch = [&](uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
+            const uint32_t r = 4 * lk, last = lR ? lR - 1 : 0;
+            const uint4 *p = RFT(tiles) + lbase + lane;
+            a = p[(uint64_t)(r < last ? r : last) * 64];
+            b = p[(uint64_t)(r + 1 < last ? r + 1 : last) * 64];
+            c = p[(uint64_t)(r + 2 < last ? r + 2 : last) * 64];
+            d = p[(uint64_t)(r + 3 < last ? r + 3 : last) * 64];
+            if (lq >= RF_TILES) return;   // past the stream: a dummy fetch (the loop's fixed load pattern)
+            if (++lk == lB) {
+                lk = 0;
+                lq = next_tile(lq + 1);
+                if (lq < RF_TILES) { lbase = pick64(bq, lq); lR = pick(Rq, lq); lB = pick(Bq, lq); }
+            }
+        };
+        // Ping-pong buffers, no register rotation: hashing buffer A waits only
+        // for A's loads (vmcnt leaves B's four in flight), then A is refilled
+        // with the block after B, and so on.
+        uint4 a0, a1, a2, a3, b0, b1, b2, b3;
+        fetch(a0, a1, a2, a3);
+        fetch(b0, b1, b2, b3);
+        uint32_t cq = next_tile(0), ck = 0, cB = 0, cR = 0, cnb = 0, cln = 0;
+        if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
         uint32_t st[4];
         stmd5::init(st);
-        for (uint32_t f = 0; f < T; f++) {
-            uint32_t m[16] = {r0a.x, r0a.y, r0a.z, r0a.w, r0b.x, r0b.y, r0b.z, r0b.w,
-                              r0c.x, r0c.y, r0c.z, r0c.w, r0d.x, r0d.y, r0d.z, r0d.w};
-            r0a = r1a; r0b = r1b; r0c = r1c; r0d = r1d;
-            if (f + 2 < T) {
-                uint32_t q2, k2;
-                locate(f + 2, q2, k2);
-                tile_block_load(RFT(tiles), pick64(bq, q2), lane, k2, r1a, r1b, r1c, r1d);
+        auto hash_block = [&](uint4 x0, uint4 x1, uint4 x2, uint4 x3) {
+            const uint32_t r = 4 * ck;
+            if (r + 3 >= cR) {   // rows past the stored ones (a tile's last block or two)
+                if (r >= cR) x0 = tile_synth(r, cln);
+                if (r + 1 >= cR) x1 = tile_synth(r + 1, cln);
+                if (r + 2 >= cR) x2 = tile_synth(r + 2, cln);
+                x3 = tile_synth(r + 3, cln);
             }
-            locate(f, q, k);
-            const uint32_t nb = pick(nbq, q);
-            if (k < nb) stmd5::compress<true>(st, m);
-            if (k + 1 == pick(Bq, q)) {
-                put_entry(pick(liq, q), nb, st);
+            const uint32_t m[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                                    x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+            if (ck < cnb) stmd5::compress<true>(st, m);
+            if (++ck == cB) {
+                put_entry(pick(liq, cq), cnb, st);
                 stmd5::init(st);
+                ck = 0;
+                cq = next_tile(cq + 1);
+                if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
             }
+        };
+        // Every iteration issues both refills (dummies past the end), so the
+        // compiler's wait before each hash counts the other buffer's four
+        // loads as still in flight on every path.
+        for (uint32_t f = 0; f < T; f += 2) {
+            hash_block(a0, a1, a2, a3);
+            fetch(a0, a1, a2, a3);
+            if (f + 1 < T) hash_block(b0, b1, b2, b3);
+            fetch(b0, b1, b2, b3);
         }
 #pragma unroll
         for (int q0 = 0; q0 < RF_TILES; q0++)
@@ -2177,23 +2255,25 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
 }
 
 // Window-local tile order (fused rehash): one workgroup per window of 4096
-// segments sorts them by MD5 block count (descending; LDS counting sort) into
-// the window's 64 tiles: tseg/tnb[window*4096 + position], tsize[tile] = 256 x
-// the largest block count in the tile.
-__global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tnb,
-                                                           uint64_t *__restrict__ tsize) {
+// segments sorts them by stored rows (message length in 16-byte rows,
+// descending; LDS counting sort) into the window's 64 tiles:
+// tseg/tln[window*4096 + position]; tinfo[tile].B / .R and tsize[tile] from
+// tile_shape.
+__global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tln,
+                                                           TileInfo *__restrict__ tinfo, uint64_t *__restrict__ tsize) {
     __shared__ uint32_t hist[256];
-    __shared__ uint32_t pnb[4096];
+    __shared__ uint32_t pln[4096];
     const uint32_t tid = threadIdx.x;
     const uint64_t seg0 = (uint64_t)blockIdx.x * 4096;
     hist[tid] = 0;
     __syncthreads();
-    uint32_t nb[16], bin[16];
+    uint32_t ln[16], bin[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const uint64_t s = seg0 + k * 256 + tid;
-        nb[k] = t.seg_off[s] != t.seg_off[s + 1] ? (uint32_t)((t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1) : 0u;
-        bin[k] = 255u - (nb[k] > 255u ? 255u : nb[k]);
+        ln[k] = t.seg_off[s] != t.seg_off[s + 1] ? (uint32_t)(t.seg_voff[s + 1] - t.seg_voff[s] + 1) : 0u;
+        const uint32_t r = ln_rows(ln[k]) + (ln[k] != 0);   // present-but-empty values sort above absent
+        bin[k] = 255u - (r > 255u ? 255u : r);
         atomicAdd(&hist[bin[k]], 1u);
     }
     __syncthreads();
@@ -2206,20 +2286,12 @@ __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *
     for (int k = 0; k < 16; k++) {
         const uint32_t pos = atomicAdd(&hist[bin[k]], 1u);
         tseg[seg0 + pos] = (uint32_t)(seg0 + k * 256 + tid);
-        tnb[seg0 + pos] = nb[k];
-        pnb[pos] = nb[k];
+        tln[seg0 + pos] = ln[k];
+        pln[pos] = ln[k];
     }
     __syncthreads();
     const uint32_t lane = tid & 63, wave = tid >> 6;
-    for (uint32_t j = wave; j < 64; j += 4) {
-        uint32_t m = pnb[j * 64 + lane];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const uint32_t y = __shfl_xor(m, o, 64);
-            m = y > m ? y : m;
-        }
-        if (lane == 0) tsize[blockIdx.x * 64 + j] = (uint64_t)m * 256;
-    }
+    for (uint32_t j = wave; j < 64; j += 4) tile_shape(pln[j * 64 + lane], blockIdx.x * 64 + j, lane == 0, tinfo, tsize);
 }
 
 // K1 over the tiles: persistent waves, grid-stride over tiles; the next
@@ -2251,50 +2323,51 @@ __global__ void __launch_bounds__(256) k_segment_hash_tiled_p(DevTree t, TreeTil
     TreeTiles cur = one;
     uint64_t tl = g;
     TileInfo ti = cur.tinfo[tl];
-    uint32_t seg = cur.tseg[tl * 64 + lane], nb = cur.tnb[tl * 64 + lane];
+    uint32_t seg = cur.tseg[tl * 64 + lane], ln = cur.tln[tl * 64 + lane];
     uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
     if (ti.B) {
-        const uint4 *b = cur.tiles + ti.base + lane;
-        n0 = b[0]; n1 = b[64]; n2 = b[128]; n3 = b[192];
+        n0 = tile_row(cur.tiles, ti.base, lane, 0, ti.R, ln); n1 = tile_row(cur.tiles, ti.base, lane, 1, ti.R, ln);
+        n2 = tile_row(cur.tiles, ti.base, lane, 2, ti.R, ln); n3 = tile_row(cur.tiles, ti.base, lane, 3, ti.R, ln);
     }
     for (;;) {
         const uint64_t gx = g + nw;
         TreeTiles nxt = cur;
         uint64_t tn_l = 0;
         TileInfo tn;
-        tn.base = 0; tn.B = 0; tn.pad = 0;
-        uint32_t segn = 0xffffffffu, nbn = 0;
+        tn.base = 0; tn.B = 0; tn.R = 0;
+        uint32_t segn = 0xffffffffu, lnn = 0;
         if (gx < ntiles) {
             tn_l = gx;
             tn = nxt.tinfo[tn_l];
             segn = nxt.tseg[tn_l * 64 + lane];
-            nbn = nxt.tnb[tn_l * 64 + lane];
+            lnn = nxt.tln[tn_l * 64 + lane];
         }
         uint32_t st[4];
         stmd5::init(st);
-        const uint4 *b = cur.tiles + ti.base + lane;
+        const uint32_t nb = ln_blocks(ln);
         for (uint32_t k = 0; k < ti.B; k++) {
             uint32_t m[16] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, n3.x, n3.y, n3.z, n3.w};
             if (k + 1 < ti.B) {
-                const uint4 *q = b + 256 * (k + 1);
-                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+                const uint32_t r = 4 * (k + 1);
+                n0 = tile_row(cur.tiles, ti.base, lane, r, ti.R, ln); n1 = tile_row(cur.tiles, ti.base, lane, r + 1, ti.R, ln);
+                n2 = tile_row(cur.tiles, ti.base, lane, r + 2, ti.R, ln); n3 = tile_row(cur.tiles, ti.base, lane, r + 3, ti.R, ln);
             } else if (tn.B) {
-                const uint4 *q = nxt.tiles + tn.base + lane;
-                n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+                n0 = tile_row(nxt.tiles, tn.base, lane, 0, tn.R, lnn); n1 = tile_row(nxt.tiles, tn.base, lane, 1, tn.R, lnn);
+                n2 = tile_row(nxt.tiles, tn.base, lane, 2, tn.R, lnn); n3 = tile_row(nxt.tiles, tn.base, lane, 3, tn.R, lnn);
             }
             if (k < nb) stmd5::compress<true>(st, m);
         }
         tile_store(t, cur.md5, cur.tag, seg, nb, st);
         if (gx >= ntiles) break;
         if (ti.B == 0 && tn.B) {
-            const uint4 *q = nxt.tiles + tn.base + lane;
-            n0 = q[0]; n1 = q[64]; n2 = q[128]; n3 = q[192];
+            n0 = tile_row(nxt.tiles, tn.base, lane, 0, tn.R, lnn); n1 = tile_row(nxt.tiles, tn.base, lane, 1, tn.R, lnn);
+            n2 = tile_row(nxt.tiles, tn.base, lane, 2, tn.R, lnn); n3 = tile_row(nxt.tiles, tn.base, lane, 3, tn.R, lnn);
         }
         g = gx;
         cur = nxt;
         ti = tn;
         seg = segn;
-        nb = nbn;
+        ln = lnn;
     }
 }
 

@@ -95,7 +95,7 @@ struct st_tree {
     // hash-ready tiled messages in seg_perm order (K1; st_kernels.h)
     uint4 *tiles = nullptr;
     uint64_t tiles_cap = 0;         // uint4 units
-    uint32_t *tseg = nullptr, *tnb = nullptr;
+    uint32_t *tseg = nullptr, *tln = nullptr;
     TileInfo *tinfo = nullptr;
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
@@ -440,7 +440,7 @@ extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tnb, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
@@ -588,7 +588,7 @@ static int ensure_tiles(st_tree *t) {
     const uint64_t ntiles = num_tiles(t);
     if (!t->tseg) {
         CHK(dalloc_t(t, &t->tseg, ntiles * 64));
-        CHK(dalloc_t(t, &t->tnb, ntiles * 64));
+        CHK(dalloc_t(t, &t->tln, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
     Scratch sc(t);
@@ -597,10 +597,11 @@ static int ensure_tiles(st_tree *t) {
     CHK(sc.alloc(&tbase, ntiles + 1));
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
     if (fused_geometry(t))   // window-local order (k_rehash_fused)
-        LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tnb, tsize);
+        LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
+               tsize);
     else
         LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
-               (const uint32_t *)t->seg_perm, t->tseg, t->tnb, tsize, ntiles);
+               (const uint32_t *)t->seg_perm, t->tseg, t->tln, t->tinfo, tsize, ntiles);
     CHK(exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1));
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
@@ -609,14 +610,13 @@ static int ensure_tiles(st_tree *t) {
         dfree(t, t->tiles);
         t->tiles = nullptr;
         t->tiles_cap = 0;
-        const uint64_t cap = total + total / 8 + 1;
+        const uint64_t cap = total + total / 8 + 256;   // slack: a tile of zero stored rows still issues row-0 loads
         CHK(dalloc_t(t, &t->tiles, cap));
         t->tiles_cap = cap;
     }
+    LAUNCH(t, "tile_build", k_tile_info, grid_for(ntiles), 256, 0, (const uint64_t *)tbase, ntiles, t->tinfo);
     LAUNCH(t, "tile_build", k_tile_fill, (uint32_t)ntiles, 256, 0, (const uint64_t *)t->seg_voff, (const uint8_t *)t->vheap,
-           (const uint32_t *)t->tseg, (const uint64_t *)tbase, (const uint64_t *)tsize, t->tiles);
-    LAUNCH(t, "tile_build", k_tile_info, grid_for(ntiles), 256, 0, (const uint64_t *)tbase, (const uint64_t *)tsize, ntiles,
-           t->tinfo);
+           (const uint32_t *)t->tseg, (const uint32_t *)t->tln, (const TileInfo *)t->tinfo, t->tiles);
     t->tiles_valid = true;
     return ST_OK;
 }
@@ -629,7 +629,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.mail = t->mail;
     x.tinfo = t->tinfo;
     x.tseg = t->tseg;
-    x.tnb = t->tnb;
+    x.tln = t->tln;
     x.tiles = t->tiles;
     return x;
 }
@@ -704,19 +704,19 @@ static int rehash_tiled(st_tree *t) {
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
         Scratch sc(t);
         uint64_t *st = nullptr;
-        CHK(sc.alloc(&st, (uint64_t)nwg * 16));
-        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 16 * 8, t->stream));
+        CHK(sc.alloc(&st, (uint64_t)nwg * 32));
+        HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
         LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
                (const TreeTiles *)nullptr, 0u, root0, lmin, st);
-        std::vector<uint64_t> h((uint64_t)nwg * 16);
+        std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipStreamSynchronize(t->stream));
         uint64_t t0 = ~0ull;
-        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 16]);
+        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 32]);
         if (const char *dump = getenv("ST_STAMP_DUMP")) {   // raw per-window stamps (ticks from t0)
             if (FILE *f = fopen(dump, "a")) {
                 for (uint32_t w = 0; w < nwg; w++) {
-                    for (int k = 0; k < 16; k++) fprintf(f, "%lld ", h[w * 16 + k] ? (long long)(h[w * 16 + k] - t0) : -1ll);
+                    for (int k = 0; k < 16; k++) fprintf(f, "%lld ", h[w * 32 + k] ? (long long)(h[w * 32 + k] - t0) : -1ll);
                     fprintf(f, "\n");
                 }
                 fclose(f);
@@ -727,11 +727,26 @@ static int rehash_tiled(st_tree *t) {
                                         "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
         for (int k = 0; k < 16; k++) {
             std::vector<double> v;
-            for (uint32_t w = 0; w < nwg; w++) if (h[w * 16 + k]) v.push_back((h[w * 16 + k] - t0) / 100.0);
+            for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
             if (v.empty()) continue;
             std::sort(v.begin(), v.end());
             fprintf(stderr, "fused stamp %d %-15s n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, names[k], v.size(), v[0],
                     v[v.size() / 2], v.back());
+        }
+        // shader cycles and clock (s_memtime / s_memrealtime) over the hash intervals
+        const int iv[5][2] = {{1, 2}, {3, 4}, {5, 6}, {9, 10}, {13, 14}};
+        for (auto &q : iv) {
+            double cyc = 0, us = 0;
+            int m = 0;
+            for (uint32_t w = 0; w < nwg; w++) {
+                const uint64_t *r = &h[w * 32];
+                if (!r[q[0]] || !r[q[1]]) continue;
+                cyc += (double)(r[16 + q[1]] - r[16 + q[0]]);
+                us += (r[q[1]] - r[q[0]]) / 100.0;
+                m++;
+            }
+            if (m) fprintf(stderr, "fused cycles %s -> %s: %.0f cycles, %.2f us, %.2f GHz (n=%d)\n", names[q[0]], names[q[1]],
+                           cyc / m, us / m, cyc / us / 1e3, m);
         }
         return ST_OK;
     }
