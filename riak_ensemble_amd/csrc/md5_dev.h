@@ -353,10 +353,11 @@ __device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const
 // One compress in a rolled loop: these kernels run a few waves per CU once
 // through the code, so straight-line unrolled MD5 (~14 KB) would be bound by
 // instruction-cache misses.
+template <bool UNROLL = false>
 __device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[16], uint32_t out[4], uint32_t n = 16) {
     uint32_t st[4];
     init(st);
-#pragma unroll 1
+#pragma unroll (UNROLL ? 5 : 1)
     for (int k = 0; k < 5; k++) {
         uint32_t m[16];
         node16_block(k, pf, h, m, n);

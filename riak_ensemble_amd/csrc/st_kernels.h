@@ -1971,7 +1971,7 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
                 if ((uint32_t)r >= ja) { hr[r] = hr[r + 1]; pf[r] = pf[r + 1]; }
             if (np == 15) { hr[15] = make_uint4(0, 0, 0, 0); pf[15] = 0x80u; }
         }
-        stmd5::md5_node16(pf, hr, dg, np);
+        stmd5::md5_node16<true>(pf, hr, dg, np);
         tg = TAG_PRESENT;
         e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         return;
@@ -2103,12 +2103,14 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         // last stored row; hash_block replaces them), so the wait before a
         // buffer is hashed leaves the other buffer's four loads in flight.
         auto fetch = [&](uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
+            // row bases are wave-uniform (scalar address arithmetic); the lane
+            // offset is the only per-lane part of each load
             const uint32_t r = 4 * lk, last = lR ? lR - 1 : 0;
-            const uint4 *p = RFT(tiles) + lbase + lane;
-            a = p[(uint64_t)(r < last ? r : last) * 64];
-            b = p[(uint64_t)(r + 1 < last ? r + 1 : last) * 64];
-            c = p[(uint64_t)(r + 2 < last ? r + 2 : last) * 64];
-            d = p[(uint64_t)(r + 3 < last ? r + 3 : last) * 64];
+            const uint4 *p = RFT(tiles) + lbase;
+            a = (p + (uint64_t)(r < last ? r : last) * 64)[lane];
+            b = (p + (uint64_t)(r + 1 < last ? r + 1 : last) * 64)[lane];
+            c = (p + (uint64_t)(r + 2 < last ? r + 2 : last) * 64)[lane];
+            d = (p + (uint64_t)(r + 3 < last ? r + 3 : last) * 64)[lane];
             if (lq >= RF_TILES) return;   // past the stream: a dummy fetch (the loop's fixed load pattern)
             if (++lk == lB) {
                 lk = 0;
