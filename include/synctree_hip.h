@@ -138,7 +138,7 @@ int st_rehash(st_tree *t, int upper);
 
 /* rehash/1 of n independent trees (e.g. the ensembles one GPU hosts) as ONE
  * batch: same effect as st_rehash(trees[i], 0) for every i.  Width 16,
- * height >= 3, one geometry, one device, no partitions. */
+ * height 3..6, one geometry, one device, no partitions. */
 int st_rehash_group(st_tree **trees, uint32_t n);
 
 /* verify/1 (upper = 0) and verify_upper/1 (upper = 1), synctree.erl:549-571 */

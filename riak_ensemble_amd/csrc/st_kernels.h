@@ -2173,80 +2173,109 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         }
     }
 
-    // ---- phase 3: levels H, H-1, H-2 from LDS, then the climb
+    // ---- phase 3: the window's levels H, H-1, H-2 from LDS; then the levels
+    // above the windows (H-3 .. lmin) by the launch's LAST window of the tree:
+    // one counter per tree (cnt[0], one arrival per window), then the last
+    // arriver reads every window root's mailbox and hashes the upper levels a
+    // lane per node (16 nodes at H = 5) -- one counter and one mailbox round
+    // trip for all of them.  Every level runs the one node16_any call site
+    // below (the unrolled node hash stays hot in the instruction cache).
     uint32_t l = H;
     uint64_t b = root * 256 + tid;
-    const uint4 *ent = reinterpret_cast<const uint4 *>(A + (tid & 255) * NB16);
-    const uint16_t *tgs = reinterpret_cast<const uint16_t *>(At + (tid & 255) * TB16);
+    const uint8_t *ent = A + (tid & 255) * NB16, *tgs = At + (tid & 255) * TB16;
     uint8_t *reg = M + (tid & 255) * MSG16;
     uint8_t *nxE = Bb + ((tid & 255) >> 4) * NB16 + (tid & 15) * 16;
     uint8_t *nxT = Bt + ((tid & 255) >> 4) * TB16 + (tid & 15) * 2;
     bool act = tid < 256;
+    const uint32_t nw = GROUP ? nwin : gridDim.x;   // this launch's windows of the tree
+    uint64_t nlo = 0, nn = 0;                        // upper levels: this launch's nodes [nlo, nlo + nn)
+    __shared__ uint32_t s_last;
 #pragma unroll 1
     for (uint32_t phase = 0;; phase++) {
         if (act) {
             uint4 e;
             uint32_t tg;
-            node16_any(ent, tgs, reg, e, tg);
-            if (phase <= 2) RF_STAMP(2 + 2 * phase);
-            else RF_STAMP(l == 2 ? 10 : 14);
+            node16_any(reinterpret_cast<const uint4 *>(ent), reinterpret_cast<const uint16_t *>(tgs), reg, e, tg);
+            RF_STAMP(phase <= 2 ? 2 + 2 * phase : (l == 2 ? 10 : 14));
             const uint64_t slot = t.base[l] + b;
             if (tg) (GROUP ? group[gi].md5 : t.md5)[slot] = e;
             (GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
             if (l == 1) { (GROUP ? group[gi].md5 : t.md5)[0] = e; (GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
-            if (phase < 2) {
+            if (phase == 2) {
+                if (l > lmin) mail_put(RFT(mail) + slot, e, tg);   // read by the tree's last window
+            } else if (l > lmin) {
                 *reinterpret_cast<uint4 *>(nxE) = e;
                 *reinterpret_cast<uint16_t *>(nxT) = (uint16_t)tg;
-            } else if (l > lmin) {
-                mail_put(RFT(mail) + slot, e, tg);   // read by the climbing lane of another workgroup
             }
         }
-        if (phase < 2) {
-            lds_barrier();   // the next level reads this one's LDS entries only
-            RF_STAMP(3 + 2 * phase);
+        if (l <= lmin) break;
+        if (phase == 2) {
+            if (tid == 0) {
+                // this window's mailbox store has completed (agent-coherent)
+                // before the counter moves; no L2 write-back / invalidate
+                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                RF_STAMP(7);
+                uint32_t *c = RFT(cnt);
+                const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old + 1 == nw;
+                if (old + 1 == nw) {
+                    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    RF_STAMP(8);
+                }
+            }
+            __syncthreads();
+            if (!s_last) break;
+            // level H-3: the children are the window roots, from their mailboxes
             l--;
-            if (phase == 0) {
-                act = tid < 16;
-                b = root * 16 + tid;
-                ent = reinterpret_cast<const uint4 *>(Bb + (tid & 15) * NB16);
-                tgs = reinterpret_cast<const uint16_t *>(Bt + (tid & 15) * TB16);
-                nxE = Cb + (tid & 15) * 16;
-                nxT = Ct + (tid & 15) * 2;
-            } else {
-                act = tid == 0;
-                b = root;
-                ent = reinterpret_cast<const uint4 *>(Cb);
-                tgs = reinterpret_cast<const uint16_t *>(Ct);
+            nlo = (GROUP ? 0 : root0) >> 4;
+            nn = nw >> 4;
+            act = tid < nn;
+            b = nlo + tid;
+            ent = A + (tid & 255) * NB16;
+            tgs = At + (tid & 255) * TB16;
+            nxE = Bb + ((tid & 255) >> 4) * NB16 + (tid & 15) * 16;
+            nxT = Bt + ((tid & 255) >> 4) * TB16 + (tid & 15) * 2;
+            if (act) {
+                const uint64_t cc = t.base[l + 1] + b * 16;
+                uint4 h[16];
+                uint16_t g[16];
+#pragma unroll
+                for (int j = 0; j < 16; j++) mail_get(RFT(mail) + cc + j, h[j], g[j]);
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    *reinterpret_cast<uint4 *>(const_cast<uint8_t *>(ent) + j * 16) = h[j];
+                    *reinterpret_cast<uint16_t *>(const_cast<uint8_t *>(tgs) + j * 2) = g[j];
+                }
+                RF_STAMP(9);
             }
             continue;
         }
-        if (tid != 0 || l <= lmin) break;
-        const uint64_t p = b >> 4;
-        uint32_t *c = RFT(cnt) + t.base[l - 1] + p;
-        // the mailbox stores above have completed (agent-coherent) before the
-        // counter moves; no L2 write-back / invalidate is needed
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        RF_STAMP(l == H - 2 ? 7 : 11);
-        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old != 15u) break;
-        RF_STAMP(l == H - 2 ? 8 : 12);
-        __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lds_barrier();   // the next level reads this one's LDS entries only
+        if (phase < 2) RF_STAMP(3 + 2 * phase);
         l--;
-        b = p;
-        // the parent's 16 child entries from their mailboxes: one round trip into LDS
-        const uint64_t cc = t.base[l + 1] + p * 16;
-        uint4 h[16];
-        uint16_t g[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) mail_get(RFT(mail) + cc + j, h[j], g[j]);
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            *reinterpret_cast<uint4 *>(Cb + j * 16) = h[j];
-            *reinterpret_cast<uint16_t *>(Ct + j * 2) = g[j];
+        if (phase == 0) {          // level H-1: 16 nodes of the window
+            act = tid < 16;
+            b = root * 16 + tid;
+            ent = Bb + (tid & 15) * NB16;
+            tgs = Bt + (tid & 15) * TB16;
+            nxE = Cb + (tid & 15) * 16;
+            nxT = Ct + (tid & 15) * 2;
+        } else if (phase == 1) {   // level H-2: the window root
+            act = tid == 0;
+            b = root;
+            ent = Cb;
+            tgs = Ct;
+        } else {                   // above level H-3 (H = 6: levels 2, 1): from the previous level's outputs
+            const bool fromB = phase == 3;
+            nlo >>= 4;
+            nn = (nn + 15) >> 4;
+            act = tid < nn;
+            b = nlo + tid;
+            ent = (fromB ? Bb : Cb) + (tid & 15) * NB16;
+            tgs = (fromB ? Bt : Ct) + (tid & 15) * TB16;
+            nxE = (fromB ? Cb : Bb) + (tid & 15) * 16;
+            nxT = (fromB ? Ct : Bt) + (tid & 15) * 2;
         }
-        ent = reinterpret_cast<const uint4 *>(Cb);
-        tgs = reinterpret_cast<const uint16_t *>(Ct);
-        RF_STAMP(l == 1 ? 13 : 9);
     }
     if (STAMP && tid == 0) {
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -580,7 +580,9 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // Build the hash-ready tiled messages from the CSR in seg_perm order
 // (k_tile_order_global, scan, k_tile_fill).  Called at the end of every bulk
 // ingest and lazily by rehash.
-static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3; }
+// the fused kernel's last window hashes the upper levels a thread per node:
+// at most 256 nodes at level H-3 (H <= 6)
+static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
 static int ensure_tiles(st_tree *t) {
     if (t->tiles_valid) return ST_OK;
@@ -1404,8 +1406,8 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     CHK(use_device(t));
     for (uint32_t i = 0; i < n; i++) {
         st_tree *u = trees[i];
-        if (u->W != 16 || u->H < 3 || u->S != t->S || u->device != t->device || u->partitioned) {
-            g_err = "group rehash needs unpartitioned width-16 trees of one geometry (height >= 3) on one device";
+        if (!fused_geometry(u) || u->S != t->S || u->device != t->device || u->partitioned) {
+            g_err = "group rehash needs unpartitioned width-16 trees of one geometry (height 3..6) on one device";
             return ST_EINVAL;
         }
         for (uint32_t j = 0; j < i; j++)
