@@ -384,7 +384,14 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
 //     one thread per distinct node, a barrier per level (update_path,
 //     synctree.erl:201-209).
 // `out` is mapped pinned host memory: the host reads it after the stream sync.
-__global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in, SmallOut *out) {
+// Position-weighted word sum of the argument block (host: small_in_sum):
+// the kernel checks the copy of `in` it received against the sum the host
+// passed as a separate scalar argument.
+__host__ __device__ __forceinline__ uint32_t small_in_word(const SmallIn &in, uint32_t i) {
+    return reinterpret_cast<const uint32_t *>(&in)[i] * (2u * i + 1u);
+}
+
+__global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in, SmallOut *out, uint32_t in_sum) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     __shared__ uint8_t kb[SB_KB + 64];
     __shared__ uint8_t vb[SB_VB + 64];
@@ -401,6 +408,20 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = in.n, L1 = t.H + 1;
     SB_STAMP(0);
+    {   // the argument block must be this call's, whole: else nothing is done and
+        // the host takes the bulk path (pad = 0xBAD reports it)
+        __shared__ uint32_t s_sum;
+        if (tid == 0) s_sum = 0;
+        __syncthreads();
+        uint32_t x = 0;
+        for (uint32_t i = tid; i < sizeof(SmallIn) / 4; i += blockDim.x) x += small_in_word(in, i);
+        atomicAdd(&s_sum, x);
+        __syncthreads();
+        if (s_sum != in_sum) {
+            if (tid == 0) { out->retry = 1; out->pad = 0xBADu; __threadfence_system(); out->done = in.seq; }
+            return;
+        }
+    }
     for (uint32_t i = tid; i < in.koff[n]; i += blockDim.x) kb[i] = in.kb[i];
     for (uint32_t i = tid; in.op == 1 && i < in.voff[n]; i += blockDim.x) vb[i] = in.vb[i];
     if (tid < SB_MAX) { bad[tid] = ~0u; keep[tid] = 0; }

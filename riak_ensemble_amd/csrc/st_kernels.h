@@ -1989,6 +1989,8 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
     e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 #define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
 
 __device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t R, uint32_t ln, uint32_t lane,
@@ -2066,7 +2068,9 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
     uint32_t T = 0;   // blocks in the wave's stream
 #pragma unroll
     for (int q = 0; q < RF_TILES; q++) {
-        const uint64_t tl = root * 64 + wave + 16 * q;
+        // snake order over the window's tiles (longest first): wave w takes
+        // w, 31 - w, 32 + w, 63 - w, which evens out the waves' block counts
+        const uint64_t tl = root * 64 + 16 * q + ((q & 1) ? 15 - wave : wave);
         const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
         Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
@@ -2165,10 +2169,19 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
     RF_STAMP(1);
     // ---- phase 2: the window's segment entries to the slot arrays, coalesced,
     // by waves 4..15 while waves 0..3 hash level H (phase 3) from the same LDS
+    // The md5 words go out WRITE-THROUGH (sc1 buffer stores): the lines leave
+    // the XCD's L2 during the launch instead of being written back, dirty, at
+    // its end (~B / 6 TB/s added to the kernel boundary for B dirty bytes:
+    // 16.8 MB here).
     if (tid >= 256) {
         const uint64_t c0 = t.base[H + 1] + seg0;
+        const uint64_t nbytes = (t.base[H + 1] + t.S) * 16;
+        const __amdgpu_buffer_rsrc_t md5r = __builtin_amdgcn_make_buffer_rsrc(
+            GROUP ? group[gi].md5 : t.md5, (short)0, (int)(nbytes < 0xffffffffull ? nbytes : 0xffffffffull), 0x00020000);
         for (uint32_t i = tid - 256; i < 4096; i += 768) {
-            (GROUP ? group[gi].md5 : t.md5)[c0 + i] = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
+            const uint4 e = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
+            const u32x4 v = {e.x, e.y, e.z, e.w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, md5r, (int)((c0 + i) * 16), 0, 16 /* sc1 */);
             (GROUP ? group[gi].tag : t.tag)[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
         }
     }
