@@ -2063,7 +2063,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
     const uint64_t seg0 = root * 4096;
 
     // ---- phase 1: K1 over this wave's tiles, one flat block stream
-    uint32_t Bq[RF_TILES], Rq[RF_TILES], lnq[RF_TILES], liq[RF_TILES];
+    uint32_t Bq[RF_TILES], Rq[RF_TILES], RLq[RF_TILES], lnq[RF_TILES], liq[RF_TILES];
     uint64_t bq[RF_TILES];
     uint32_t T = 0;   // blocks in the wave's stream
 #pragma unroll
@@ -2074,6 +2074,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
         Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
+        RLq[q] = __builtin_amdgcn_readfirstlane(ti.R ? ti.R - 1 : 0);   // the last stored row (fetch clamp)
         const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ti.base),
                        bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ti.base >> 32));
         bq[q] = ((uint64_t)bhi << 32) | blo;
@@ -2100,16 +2101,16 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             while (q < RF_TILES && pick(Bq, q) == 0) q++;
             return q;
         };
-        uint32_t lq = next_tile(0), lk = 0, lR = 0, lB = 0;
+        uint32_t lq = next_tile(0), lk = 0, lL = 0, lB = 0;
         uint64_t lbase = 0;
-        if (lq < RF_TILES) { lbase = pick64(bq, lq); lR = pick(Rq, lq); lB = pick(Bq, lq); }
+        if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
         // Always four loads per block (rows past the stored ones re-read the
         // last stored row; hash_block replaces them), so the wait before a
         // buffer is hashed leaves the other buffer's four loads in flight.
         auto fetch = [&](uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
             // row bases are wave-uniform (scalar address arithmetic); the lane
             // offset is the only per-lane part of each load
-            const uint32_t r = 4 * lk, last = lR ? lR - 1 : 0;
+            const uint32_t r = 4 * lk, last = lL;
             const uint4 *p = RFT(tiles) + lbase;
             a = (p + (uint64_t)(r < last ? r : last) * 64)[lane];
             b = (p + (uint64_t)(r + 1 < last ? r + 1 : last) * 64)[lane];
@@ -2119,7 +2120,7 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
             if (++lk == lB) {
                 lk = 0;
                 lq = next_tile(lq + 1);
-                if (lq < RF_TILES) { lbase = pick64(bq, lq); lR = pick(Rq, lq); lB = pick(Bq, lq); }
+                if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
             }
         };
         // Ping-pong buffers, no register rotation: hashing buffer A waits only

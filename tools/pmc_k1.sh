@@ -2,7 +2,7 @@
 # PMC passes (one group per run) on the rehash kernels of a short bench.
 R=$(pwd); TAG=${1:-k1}; RX=${2:-segment_hash|level16|upper16}
 export TMPDIR=/tmp
-SHORT="$R/bench.py --steps 5 --warmup 1 --no-cpu --no-extras"
+SHORT="$R/bench.py --steps 5 --warmup 1 --no-cpu --no-extras --no-pmc"
 i=0
 for G in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
          "MeanOccupancyPerCU" \
