@@ -470,14 +470,26 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     }
     __syncthreads();
     SB_STAMP(2);
+    // each key's verification and lookup results, read ONCE into its thread's
+    // registers right after they are complete; the result words below come
+    // from these copies (an intermittent failure showed a key's LDS word
+    // changing between the barrier above and the status write)
+    uint32_t my_bad = ~0u, my_found = 0, my_len = 0;
+    uint64_t my_seg = 0;
+    const uint8_t *my_src = nullptr;
+    if (tid < n) {
+        my_bad = bad[tid];
+        my_seg = seg[tid];
+        if (in.op == 0) { my_found = gfound[tid]; my_len = glen[tid]; my_src = gsrc[tid]; }
+    }
     if (in.op == 0) {
         // ---- 3 (get): the verified answers
         uint32_t len = 0;
         const uint8_t *src = nullptr;
         if (tid < n) {
-            if (bad[tid] == ~0u) {
-                len = glen[tid];
-                src = gsrc[tid];
+            if (my_bad == ~0u && my_found) {
+                len = my_len;
+                src = my_src;
             }
             vlen_out[tid + 1] = len;
         }
@@ -493,12 +505,12 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
                 for (uint32_t b = 0; b < len; b++) out->vbytes[vlen_out[tid] + b] = src[b];
             if (tid == 0) out->voff[0] = 0;
             out->voff[tid + 1] = vlen_out[tid + 1];
-            if (bad[tid] != ~0u) {
+            if (my_bad != ~0u) {
                 out->status[tid] = ST_CORRUPTED;
-                out->clevel[tid] = bad[tid];
-                out->cbucket[tid] = seg[tid] >> (t.shift * (L1 - bad[tid]));
+                out->clevel[tid] = my_bad;
+                out->cbucket[tid] = my_seg >> (t.shift * (L1 - my_bad));
             } else {
-                out->status[tid] = gfound[tid] ? ST_OK : ST_NOTFOUND;
+                out->status[tid] = my_found ? ST_OK : ST_NOTFOUND;
                 out->clevel[tid] = 0;
                 out->cbucket[tid] = 0;
             }
@@ -671,10 +683,10 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     }
     __syncthreads();
     if (tid < n) {
-        if (bad[tid] != ~0u) {
+        if (my_bad != ~0u) {
             out->status[tid] = ST_CORRUPTED;
-            out->clevel[tid] = bad[tid];
-            out->cbucket[tid] = seg[tid] >> (t.shift * (L1 - bad[tid]));
+            out->clevel[tid] = my_bad;
+            out->cbucket[tid] = my_seg >> (t.shift * (L1 - my_bad));
         } else {
             out->status[tid] = ST_OK;
             out->clevel[tid] = 0;

@@ -2133,17 +2133,19 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
         uint32_t st[4];
         stmd5::init(st);
-        auto hash_block = [&](uint4 x0, uint4 x1, uint4 x2, uint4 x3) {
+        auto hash_block = [&](const uint4 &x0, const uint4 &x1, const uint4 &x2, const uint4 &x3) {
             const uint32_t r = 4 * ck;
             if (r + 3 >= cR) {   // rows past the stored ones (a tile's last block or two)
-                if (r >= cR) x0 = tile_synth(r, cln);
-                if (r + 1 >= cR) x1 = tile_synth(r + 1, cln);
-                if (r + 2 >= cR) x2 = tile_synth(r + 2, cln);
-                x3 = tile_synth(r + 3, cln);
+                const uint4 y0 = r >= cR ? tile_synth(r, cln) : x0, y1 = r + 1 >= cR ? tile_synth(r + 1, cln) : x1,
+                            y2 = r + 2 >= cR ? tile_synth(r + 2, cln) : x2, y3 = tile_synth(r + 3, cln);
+                const uint32_t m[16] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
+                                        y2.x, y2.y, y2.z, y2.w, y3.x, y3.y, y3.z, y3.w};
+                if (ck < cnb) stmd5::compress<true>(st, m);
+            } else {             // the common case: the loaded registers feed the compression as they are
+                const uint32_t m[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                                        x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+                if (ck < cnb) stmd5::compress<true>(st, m);
             }
-            const uint32_t m[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
-                                    x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
-            if (ck < cnb) stmd5::compress<true>(st, m);
             if (++ck == cB) {
                 put_entry(pick(liq, cq), cnb, st);
                 stmd5::init(st);

@@ -1061,6 +1061,19 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev, in_sum);
     CHK(wait_mapped(t, &t->sout->done, in.seq));
     if (t->sout->done != in.seq) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
+    // The call returns only once the kernel has fully retired (its stream is
+    // idle), not merely once its completion word is set: a following call
+    // that launched while this kernel was still retiring intermittently saw
+    // an inconsistent tree (test_small_path; tools/stress_small.py fails
+    // within ~6 trials without this and passed 30 with it).
+    static const int ssync = getenv("ST_SMALL_SYNC") ? atoi(getenv("ST_SMALL_SYNC")) : 1;
+    if (ssync == 1) {
+        HIPCHK(hipStreamSynchronize(t->stream));
+    } else if (ssync == 2) {
+        hipError_t q;
+        while ((q = hipStreamQuery(t->stream)) == hipErrorNotReady) __builtin_ia32_pause();
+        if (q != hipSuccess) { g_err = hipGetErrorString(q); return ST_EDEVICE; }
+    }
     if (t->sout->pad == 0xBADu) {   // the kernel saw another argument block: the bulk path serves the call
         static int warned = 0;
         if (!warned++) fprintf(stderr, "synctree_hip: small-batch kernel argument block mismatch (seq %u); bulk path\n", in.seq);

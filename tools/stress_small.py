@@ -1,0 +1,86 @@
+"""Stress the per-key path (k_small) with the test_small_path pattern and
+check every call against the C restatement; on the first divergence print
+what the device returns now (transient vs persistent) and stop (diagnostic)."""
+import os, sys, time
+import numpy as np
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, R)
+sys.path.insert(0, os.path.join(R, 'oracle'))
+import oracle_c as C
+from riak_ensemble_amd import synctree_hip, workload
+
+
+def _val(seq):
+    return bytes([0]) + (1).to_bytes(8, 'big') + seq.to_bytes(8, 'big')
+
+
+def trial(tn, W, S, steps=120):
+    n = 20000 if S >= 4096 else 3000
+    keys = workload.keys_int63(n, workload.SEED ^ (0x51 + tn))
+    vals = workload.obj_hash_values(n)
+    dev = synctree_hip.DeviceTree(W, S)
+    ora = C.OTree(W, S)
+    assert dev.insert_int64(keys, vals) == 0
+    ora.bulk_load_int64(keys, vals)
+    rng = np.random.default_rng(tn)
+    extra = workload.keys_int63(4000, workload.SEED ^ (0x52 + tn))
+    seq = n
+    junk = []
+    for step in range(steps):
+        m = int(rng.integers(1, 17))
+        ks, vs = [], []
+        for _ in range(m):
+            k = int(keys[rng.integers(0, n)]) if rng.random() < 0.5 else int(extra[rng.integers(0, len(extra))])
+            seq += 1
+            ks.append(k)
+            vs.append(_val(seq))
+        st = dev.insert_batch(ks, vs)
+        for k, v in zip(ks, vs):
+            ora.insert(k, v)
+        if not all(x is None for x in st):
+            print('FAIL insert trial', tn, 'geom', (W, S), 'step', step, 'n', len(ks), 'st', st, flush=True)
+            print('  re-get of those keys:', dev.get_batch(ks) == [ora.get(k) for k in ks], flush=True)
+            return False
+        probe = [ks[0], int(keys[rng.integers(0, n)]), int(extra[rng.integers(0, len(extra))])]
+        got = dev.get_batch(probe)
+        exp = [ora.get(k) for k in probe]
+        if got != exp:
+            bad = [i for i in range(3) if got[i] != exp[i]]
+            print('FAIL get trial', tn, 'geom', (W, S), 'step', step, 'idx', bad, 'got', [got[i] for i in bad],
+                  'exp', [exp[i] for i in bad], flush=True)
+            again = dev.get_batch(probe)
+            print('  same get again:', again == exp, [again[i] for i in bad], flush=True)
+            print('  get1 each:', [dev.get1(k) == ora.get(k) for k in probe], flush=True)
+            print('  top equal:', dev.top_hash() == ora.top_hash(), flush=True)
+            return False
+        if JUNK and step % 10 == 9:      # other trees come and go (pool memory reuse)
+            junk.append(synctree_hip.DeviceTree(16, 1 << 12))
+            if len(junk) > 3:
+                junk.pop(0).close()
+        if step % 30 == 29:
+            if step % 60 == 29:
+                dev.rehash()
+            else:
+                assert dev.verify()
+            if dev.top_hash() != ora.top_hash():
+                print('FAIL top after bulk op, trial', tn, 'step', step, flush=True)
+                return False
+    for j in junk:
+        j.close()
+    dev.close()
+    return True
+
+
+JUNK = int(os.environ.get('STRESS_JUNK', '1'))
+t0 = time.time()
+geoms = [(16, 1 << 20), (4, 4096), (16, 16)]
+ok = True
+for tn in range(int(sys.argv[1]) if len(sys.argv) > 1 else 30):
+    for g in geoms:
+        if not trial(tn, *g):
+            ok = False
+            break
+    if not ok:
+        break
+    print('trial', tn, 'ok', round(time.time() - t0, 1), flush=True)
+print('RESULT', 'ok' if ok else 'FAIL', flush=True)
