@@ -61,7 +61,16 @@ def trial(tn, W, S, steps=120):
             if step % 60 == 29:
                 dev.rehash()
             else:
-                assert dev.verify()
+                vok = dev.verify()
+                if not vok:
+                    print('FAIL verify trial', tn, 'geom', (W, S), 'step', step, 'top equal', dev.top_hash() == ora.top_hash(),
+                          'verify again', dev.verify(), flush=True)
+                    for lvl in range(1, ora.height + 2):
+                        pa, ha = dev.level_entries(lvl)
+                        pb, hb = ora.level_entries(lvl)
+                        d = np.nonzero((pa != pb) | np.any(ha != hb, axis=1))[0]
+                        print('  level', lvl, 'differing buckets', len(d), d[:8], flush=True)
+                    return False
             if dev.top_hash() != ora.top_hash():
                 print('FAIL top after bulk op, trial', tn, 'step', step, flush=True)
                 return False
