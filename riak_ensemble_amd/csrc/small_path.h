@@ -596,23 +596,25 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
                         gvb[g] = (uint32_t)vbytes;
                         gnew[g] = (uint32_t)news;
                     }
-                } else {   // header and offset tables
+                } else {   // header and offset tables; lengths -> offsets in LDS too
                     uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + goff[g]);
                     const uint32_t mm = gn[g];
                     uint32_t *ko = h + 4, *vo = h + 4 + (mm + 1);
                     h[0] = mm; h[1] = gkb[g]; h[2] = gvb[g]; h[3] = 0;
                     uint32_t a = 0, c = 0;
-                    for (uint32_t q = 0; q < mm; q++) { ko[q] = a; vo[q] = c; a += pk[q]; c += pv[q]; }
-                    ko[mm] = a;
-                    vo[mm] = c;
+                    for (uint32_t q = 0; q < mm; q++) {
+                        const uint32_t kq = pk[q], vq = pv[q];
+                        ko[q] = a; vo[q] = c; pk[q] = a; pv[q] = c;
+                        a += kq; c += vq;
+                    }
+                    ko[mm] = a; vo[mm] = c; pk[mm] = a; pv[mm] = c;
                 }
             }
-            if (pass == 1) {   // entry bytes, lane per entry
+            if (pass == 1) {   // entry bytes, lane per entry; offsets from the LDS plan (never read
+                               // back from the record just written: no global read-after-write)
                 wave_sync_lds();
-                __threadfence_block();
                 uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + goff[g]);
                 const uint32_t mm = gn[g];
-                const uint32_t *ko = h + 4, *vo = h + 4 + (mm + 1);
                 uint8_t *kd = reinterpret_cast<uint8_t *>(h + 4 + 2 * (mm + 1));
                 uint8_t *vd = kd + gkb[g];
                 for (uint32_t q = lane; q < mm; q += 64) {
@@ -626,8 +628,9 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
                         ks = v.key(src);
                         vs = v.val(src);
                     }
-                    for (uint32_t b = 0; b < pk[q]; b++) kd[ko[q] + b] = ks[b];
-                    for (uint32_t b = 0; b < pv[q]; b++) vd[vo[q] + b] = vs[b];
+                    const uint32_t k0 = pk[q], kn = pk[q + 1] - k0, v0 = pv[q], vn = pv[q + 1] - v0;
+                    for (uint32_t b = 0; b < kn; b++) kd[k0 + b] = ks[b];
+                    for (uint32_t b = 0; b < vn; b++) vd[v0 + b] = vs[b];
                 }
                 wave_sync_lds();
             }
@@ -638,12 +641,18 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
             return;
         }
     }
-    __threadfence_block();
+    // Global data written by other threads of this workgroup is read back
+    // below (the new records, then each level's new entries): an agent-scope
+    // release/acquire around each barrier also drops this CU's L1 lines, so
+    // no read is served from a line cached before the write.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // the new records replace the segments' content; rehash the dirty paths
     if (tid < ngrp) ov.idx[gseg[tid]] = goff[tid];
-    __threadfence_block();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (tid < ngrp) {   // level H+1: the segment entries
         const uint64_t s = gseg[tid], slot = t.base[L1] + s;
         const SegView v = seg_view(t, ov, s);
@@ -656,8 +665,9 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
     }
     for (uint32_t l = L1 - 1; l >= 1; l--) {
-        __threadfence_block();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (tid == 0) {
             uint32_t c = 0;
             for (uint32_t g = 0; g < ngrp; g++) {

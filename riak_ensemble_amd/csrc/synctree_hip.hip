@@ -219,7 +219,8 @@ static void csr_install(st_tree *t, const CsrSet &o) {
     old.kheap = t->kheap; old.vheap = t->vheap;
     old.cap_n = t->cap_n; old.cap_k = t->cap_k; old.cap_v = t->cap_v;
     csr_free(t, t->spare);
-    if (old.cap_n * 16 + old.cap_k + old.cap_v >= CSR_KEEP_SPARE) t->spare = old; else csr_free(t, old);
+    static const int nospare = getenv("ST_NO_SPARE") ? atoi(getenv("ST_NO_SPARE")) : 0;   // diagnostic
+    if (!nospare && old.cap_n * 16 + old.cap_k + old.cap_v >= CSR_KEEP_SPARE) t->spare = old; else csr_free(t, old);
     t->seg_off = o.seg_off; t->seg_voff = o.seg_voff; t->koff = o.koff; t->voff = o.voff;
     t->kheap = o.kheap; t->vheap = o.vheap;
     t->cap_n = o.cap_n; t->cap_k = o.cap_k; t->cap_v = o.cap_v;
@@ -1037,7 +1038,8 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     *served = 0;
     const uint64_t kbytes = hr.off[n];
     const uint64_t vbytes = op == 1 ? voff[n] - voff[0] : 0;
-    if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
+    static const uint64_t maxn = getenv("ST_SMALL_MAXN") ? (uint64_t)atoi(getenv("ST_SMALL_MAXN")) : SB_MAX;
+    if (n == 0 || n > SB_MAX || n > maxn || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
         small_lds_bytes((uint32_t)t->W) > 160 * 1024)
         return ST_OK;
     CHK(ensure_small(t));

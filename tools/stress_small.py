@@ -26,6 +26,8 @@ def trial(tn, W, S, steps=120):
     extra = workload.keys_int63(4000, workload.SEED ^ (0x52 + tn))
     seq = n
     junk = []
+    touched = set()
+    hist = {}
     for step in range(steps):
         m = int(rng.integers(1, 17))
         ks, vs = [], []
@@ -34,6 +36,9 @@ def trial(tn, W, S, steps=120):
             seq += 1
             ks.append(k)
             vs.append(_val(seq))
+        touched.update(ora.segment_of(k) for k in ks)
+        for k in ks:
+            hist.setdefault(ora.segment_of(k), []).append((step, len(ks)))
         st = dev.insert_batch(ks, vs)
         for k, v in zip(ks, vs):
             ora.insert(k, v)
@@ -60,11 +65,26 @@ def trial(tn, W, S, steps=120):
         if step % 30 == 29:
             if step % 60 == 29:
                 dev.rehash()
+                touched = set()
+                hist = {}
             else:
                 vok = dev.verify()
                 if not vok:
                     print('FAIL verify trial', tn, 'geom', (W, S), 'step', step, 'top equal', dev.top_hash() == ora.top_hash(),
                           'verify again', dev.verify(), flush=True)
+                    segs = sorted(touched)
+                    got = dev.exchange_get_batch(ora.height + 1, segs)
+                    exp = [ora.node(ora.height + 1, x) for x in segs]
+                    badsegs = [(x, g, e) for x, g, e in zip(segs, got, exp) if g != e]
+                    print('  touched segments', len(segs), 'differing', len(badsegs), flush=True)
+                    for x, g, e in badsegs[:4]:
+                        print('   seg', x, 'touches', hist.get(x), '\n    dev', g, '\n    ora', e, flush=True)
+                        for kk, vv in e:
+                            print('     key', kk, 'dev get1 ok', dev.get1(kk) == vv, flush=True)
+                    print('  entries dev', dev.num_entries(), 'ora', ora.num_entries(), flush=True)
+                    multi = sum(1 for x in segs if len(hist.get(x, [])) > 1)
+                    print('  touched more than once:', multi, 'of', len(segs), '; bad ones:',
+                          [len(hist.get(x, [])) for x, _, _ in badsegs], flush=True)
                     for lvl in range(1, ora.height + 2):
                         pa, ha = dev.level_entries(lvl)
                         pb, hb = ora.level_entries(lvl)
