@@ -729,6 +729,23 @@ __global__ void k_ov_sizes(Overlay ov, uint64_t S, uint64_t *cnt, uint64_t *kbyt
     }
 }
 
+// Diagnostic (ST_OV_CHECK & 256): overlay index entries whose record is not
+// a plausible one (offset at or past the fill level, or an empty record):
+// a[0] count, a[1] lowest segment, a[2] highest segment, a[3] one offset.
+__global__ void k_ov_audit(Overlay ov, uint64_t S, unsigned long long *a) {
+    const unsigned long long used = *ov.used;
+    for (uint64_t s = gtid(); s < S; s += gstride()) {
+        const uint64_t o = ov.idx[s];
+        if (o == ~0ull) continue;
+        const bool bad = o >= used || reinterpret_cast<const uint32_t *>(ov.heap + o)[0] == 0;
+        if (!bad) continue;
+        atomicAdd(&a[0], 1ull);
+        atomicMin(&a[1], (unsigned long long)s);
+        atomicMax(&a[2], (unsigned long long)s);
+        a[3] = o;
+    }
+}
+
 // Overlay flush, step 2: the overlay entries as one ingest batch (segment
 // order), with their segment ids (seg_given).
 __global__ void k_ov_gather(Overlay ov, uint64_t S, const uint64_t *eoff, const uint64_t *koff0, const uint64_t *voff0,

@@ -114,6 +114,8 @@ struct st_tree {
     SmallOut *sout = nullptr, *sout_dev = nullptr;
     uint32_t small_seq = 0;   // sequence number of the last k_small call
     uint64_t small_torn = 0;  // calls whose kernel saw a mismatched argument block (diagnostic)
+    uint64_t ov_live = 0;     // live overlay index entries (ST_OV_CHECK diagnostic)
+    std::vector<uint64_t> csr_copy;   // seg_off as installed (ST_OV_CHECK & 512 diagnostic)
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -124,6 +126,8 @@ struct st_tree {
 static int dalloc(st_tree *t, void **p, uint64_t bytes) {
     *p = nullptr;
     if (bytes == 0) bytes = 16;
+    static const int sync_alloc = getenv("ST_SYNC_ALLOC") ? atoi(getenv("ST_SYNC_ALLOC")) : 0;   // diagnostic
+    if (sync_alloc) (void)hipStreamSynchronize(t->stream);
     hipError_t e = hipMallocAsync(p, bytes, t->stream);
     if (e != hipSuccess) {
         g_err = std::string("hipMallocAsync: ") + hipGetErrorString(e);
@@ -287,6 +291,11 @@ struct TimedLaunch {
     }
 };
 
+// diagnostic (ST_SYNC_LAUNCH=1): every launch waits for its kernel
+static int sync_launch() {
+    static const int v = getenv("ST_SYNC_LAUNCH") ? atoi(getenv("ST_SYNC_LAUNCH")) : 0;
+    return v;
+}
 #define LAUNCH(t, name, kern, grid, block, shmem, ...)                            \
     do {                                                                          \
         TimedLaunch tl_(t, name);                                                 \
@@ -296,6 +305,7 @@ struct TimedLaunch {
             g_err = std::string("launch ") + name + ": " + hipGetErrorString(e_); \
             return ST_EDEVICE;                                                    \
         }                                                                         \
+        if (sync_launch()) HIPCHK(hipStreamSynchronize((t)->stream));            \
     } while (0)
 
 // Wait for a device-written flag in host-mapped memory (the kernel writes it
@@ -332,6 +342,21 @@ static int exclusive_scan(st_tree *t, const T *in, T *out, uint64_t n) {
     hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), t->stream);
     dfree(t, tmp);
     HIPCHK(e);
+    static const int chk = getenv("ST_OV_CHECK") ? atoi(getenv("ST_OV_CHECK")) : 0;
+    if (chk & 64) {   // diagnostic: the device scan against a host scan
+        std::vector<T> hi(n), ho(n);
+        HIPCHK(hipStreamSynchronize(t->stream));
+        HIPCHK(hipMemcpy(hi.data(), in, n * sizeof(T), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ho.data(), out, n * sizeof(T), hipMemcpyDeviceToHost));
+        T acc(0);
+        uint64_t bad = 0, first = ~0ull;
+        for (uint64_t i = 0; i < n; i++) {
+            if (memcmp(&acc, &ho[i], sizeof(T))) { if (!bad++) first = i; }
+            acc = acc + hi[i];
+        }
+        if (bad) fprintf(stderr, "scan_check: %llu of %llu outputs differ (first %llu), element %zu bytes\n",
+                         (unsigned long long)bad, (unsigned long long)n, (unsigned long long)first, sizeof(T));
+    }
     return ST_OK;
 }
 
@@ -822,10 +847,31 @@ struct IngestIn {
     uint64_t n_rejected;
 };
 
+static int ov_check_level() {
+    static const int v = getenv("ST_OV_CHECK") ? atoi(getenv("ST_OV_CHECK")) : 0;
+    return v;
+}
+
 static int ingest(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
     in.n_rejected = 0;
     if (n == 0) return ST_OK;
+    if ((ov_check_level() & 512) && t->csr_copy.size() == S + 1) {   // diagnostic: seg_off unchanged since installed?
+        std::vector<uint64_t> now(S + 1);
+        HIPCHK(hipStreamSynchronize(t->stream));
+        HIPCHK(hipMemcpy(now.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+        uint64_t diff = 0, first = ~0ull, last = 0;
+        for (uint64_t s = 0; s <= S; s++)
+            if (now[s] != t->csr_copy[s]) { diff++; if (first == ~0ull) first = s; last = s; }
+        if (diff) {
+            fprintf(stderr, "csr_check: seg_off changed since install at %llu of %llu words, %llu..%llu (%p)\n",
+                    (unsigned long long)diff, (unsigned long long)(S + 1), (unsigned long long)first, (unsigned long long)last,
+                    (void *)t->seg_off);
+            for (uint64_t s = first; s <= last && s < first + 6; s++)
+                fprintf(stderr, "  [%llu] was %llu now %llx\n", (unsigned long long)s, (unsigned long long)t->csr_copy[s],
+                        (unsigned long long)now[s]);
+        }
+    }
     DevTree d = view(t);
     Scratch sc(t);
     uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr, *mpos = nullptr;
@@ -928,9 +974,25 @@ static int ingest(st_tree *t, IngestIn &in) {
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
+    if (ov_check_level() & 128) {
+        uint64_t so_s = 0, so_0 = 0;
+        HIPCHK(hipStreamSynchronize(t->stream));
+        HIPCHK(hipMemcpy(&so_s, out.o.seg_off + S, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&so_0, out.o.seg_off, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "ingest_check: n %llu n_new %llu tot_k %llu tot_v %llu new seg_off[0] %llu seg_off[S] %llu new %p old %p\n",
+                (unsigned long long)n, (unsigned long long)n_new, (unsigned long long)tot_k, (unsigned long long)tot_v,
+                (unsigned long long)so_0, (unsigned long long)so_s, (void *)out.o.seg_off, (void *)t->seg_off);
+    }
     // swap in the new CSR (the old one becomes the spare set, in stream order)
     out.install();
     t->n = n_new; t->kbytes = tot_k; t->vbytes = tot_v;
+    if (ov_check_level() & 512) {
+        t->csr_copy.resize(S + 1);
+        HIPCHK(hipStreamSynchronize(t->stream));
+        HIPCHK(hipMemcpy(t->csr_copy.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+        if (t->csr_copy[S] != n_new) fprintf(stderr, "csr_check: new seg_off[S] %llu != %llu\n",
+                                             (unsigned long long)t->csr_copy[S], (unsigned long long)n_new);
+    }
     t->perm_valid = false;
     // the hash-ready tiles are stale now; the next full rehash rebuilds them
     // (streaming batches never pay for a tile rebuild they do not use)
@@ -952,8 +1014,35 @@ static int ingest(st_tree *t, IngestIn &in) {
 // records become one ingest batch with replace flags (their hashes are already
 // in the slot arrays, so nothing is rehashed).  Every entry point that reads
 // segments other than the small kernels calls this first.
+// Diagnostic (ST_OV_CHECK=1): the overlay index's live entries, checked
+// against the heap fill level; returns the number of live entries.
+static uint64_t ov_check(st_tree *t, const char *where) {
+    const uint64_t S = t->S;
+    std::vector<uint64_t> idx(S);
+    uint64_t used = 0;
+    (void)hipStreamSynchronize(t->stream);
+    (void)hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost);
+    uint64_t live = 0, wild = 0, first = ~0ull, last = 0;
+    for (uint64_t s = 0; s < S; s++) {
+        if (idx[s] == ~0ull) continue;
+        live++;
+        if (idx[s] >= used) {
+            wild++;
+            if (first == ~0ull) first = s;
+            last = s;
+        }
+    }
+    if (wild) fprintf(stderr, "ov_check %s: live %llu, beyond used (%llu): %llu in segments %llu..%llu (e.g. %llx)\n", where,
+                      (unsigned long long)live, (unsigned long long)used, (unsigned long long)wild,
+                      (unsigned long long)first, (unsigned long long)last, (unsigned long long)idx[first]);
+    return live;
+}
+
 static int flush_overlay(st_tree *t) {
     if (!t->ov_pending) return ST_OK;
+    if (ov_check_level() & 8) (void)hipStreamSynchronize(t->stream);
+    if (ov_check_level() & 1) ov_check(t, "flush");
     const uint64_t S = t->S;
     Scratch sc(t);
     uint64_t *cnt = nullptr, *kbs = nullptr, *vbs = nullptr, *eoff = nullptr, *ko0 = nullptr, *vo0 = nullptr;
@@ -966,14 +1055,32 @@ static int flush_overlay(st_tree *t) {
     CHK(sc.alloc(&vo0, S + 1));
     CHK(sc.alloc(&rep, S));
     LAUNCH(t, "ov_flush", k_ov_sizes, grid_for(S + 1), 256, 0, t->ov, S, cnt, kbs, vbs, rep);
+    std::vector<uint8_t> rep_h;
+    if (ov_check_level() & 2) {
+        rep_h.resize(S);
+        HIPCHK(hipStreamSynchronize(t->stream));
+        HIPCHK(hipMemcpy(rep_h.data(), rep, S, hipMemcpyDeviceToHost));
+    }
     CHK(exclusive_scan<uint64_t>(t, cnt, eoff, S + 1));
     CHK(exclusive_scan<uint64_t>(t, kbs, ko0, S + 1));
     CHK(exclusive_scan<uint64_t>(t, vbs, vo0, S + 1));
+    uint64_t *aud = nullptr;
+    if (ov_check_level() & 256) {   // diagnostic, no extra host sync: audited with the sizes read-back
+        CHK(sc.alloc(&aud, 4));
+        HIPCHK(hipMemsetAsync(aud, 0, 32, t->stream));
+        HIPCHK(hipMemsetAsync(aud + 1, 0xff, 8, t->stream));
+        LAUNCH(t, "ov_audit", k_ov_audit, grid_for(S), 256, 0, t->ov, S, (unsigned long long *)aud);
+        HIPCHK(hipMemcpyAsync(t->pin + 3, aud, 32, hipMemcpyDeviceToHost, t->stream));
+    }
     HIPCHK(hipMemcpyAsync(t->pin, eoff + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 1, ko0 + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 2, vo0 + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipStreamSynchronize(t->stream));
     const uint64_t n = t->pin[0], kt = t->pin[1], vt = t->pin[2];
+    if (aud && t->pin[3])
+        fprintf(stderr, "ov_audit: %llu implausible overlay entries, segments %llu..%llu (e.g. offset %llx)\n",
+                (unsigned long long)t->pin[3], (unsigned long long)t->pin[4], (unsigned long long)t->pin[5],
+                (unsigned long long)t->pin[6]);
     if (n) {
         uint8_t *krec = nullptr, *vh = nullptr;
         uint64_t *ko = nullptr, *vo = nullptr;
@@ -988,16 +1095,103 @@ static int flush_overlay(st_tree *t) {
         LAUNCH(t, "ov_flush", k_ov_gather, grid_for(S), 256, 0, t->ov, S, (const uint64_t *)eoff, (const uint64_t *)ko0,
                (const uint64_t *)vo0, krec, ko, vh, vo, segs);
         LAUNCH(t, "ov_flush", k_ov_terminate, 1, 64, 0, n, (const uint64_t *)(ko0 + S), (const uint64_t *)(vo0 + S), ko, vo);
+        if (ov_check_level() & 16) {   // diagnostic: the gathered batch against the overlay records (host)
+            HIPCHK(hipStreamSynchronize(t->stream));
+            std::vector<uint64_t> idx(S), hko(n + 1), hvo(n + 1);
+            std::vector<uint32_t> hseg(n);
+            std::vector<uint8_t> hk(kt), hv(vt);
+            uint64_t used = 0;
+            HIPCHK(hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost));
+            std::vector<uint8_t> heap(used);
+            HIPCHK(hipMemcpy(heap.data(), t->ov.heap, used, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hko.data(), ko, (n + 1) * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hvo.data(), vo, (n + 1) * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hseg.data(), segs, n * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hk.data(), krec, kt, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hv.data(), vh, vt, hipMemcpyDeviceToHost));
+            uint64_t e = 0, kb = 0, vb = 0, bad = 0, recs = 0;
+            for (uint64_t s2 = 0; s2 < S; s2++) {
+                if (idx[s2] == ~0ull) continue;
+                recs++;
+                const uint32_t *h = reinterpret_cast<const uint32_t *>(heap.data() + idx[s2]);
+                const uint32_t m = h[0], kbn = h[1], vbn = h[2];
+                const uint32_t *rk = h + 4, *rv = h + 4 + (m + 1);
+                const uint8_t *kd = reinterpret_cast<const uint8_t *>(h + 4 + 2 * (m + 1)), *vd = kd + kbn;
+                for (uint32_t i = 0; i < m; i++, e++) {
+                    const bool ok = hseg[e] == s2 && hko[e] == kb + rk[i] && hvo[e] == vb + rv[i] &&
+                                    !memcmp(hk.data() + hko[e], kd + rk[i], rk[i + 1] - rk[i]) &&
+                                    !memcmp(hv.data() + hvo[e], vd + rv[i], rv[i + 1] - rv[i]);
+                    if (!ok && bad++ < 4)
+                        fprintf(stderr, "ov_check gather: entry %llu (segment %llu) differs: seg %u ko %llu/%llu vo %llu/%llu\n",
+                                (unsigned long long)e, (unsigned long long)s2, hseg[e], (unsigned long long)hko[e],
+                                (unsigned long long)(kb + rk[i]), (unsigned long long)hvo[e], (unsigned long long)(vb + rv[i]));
+                }
+                kb += kbn; vb += vbn;
+            }
+            fprintf(stderr, "ov_check gather: %llu records, %llu entries (n %llu), %llu differ\n", (unsigned long long)recs,
+                    (unsigned long long)e, (unsigned long long)n, (unsigned long long)bad);
+        }
         const uint64_t nbefore = t->n;
         IngestIn in{};
         in.n = n; in.krec = krec; in.koff = ko; in.vheap = vh; in.voff = vo;
         in.seg_given = segs; in.seg_replace = rep; in.verify_rehash = false;
         CHK(ingest(t, in));
+        if (ov_check_level() & 32) {   // diagnostic: the merged CSR's overlay segments against the records
+            HIPCHK(hipStreamSynchronize(t->stream));
+            std::vector<uint64_t> idx(S), so(S + 1), cko(t->n + 1), cvo(t->n + 1);
+            uint64_t used = 0;
+            HIPCHK(hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost));
+            std::vector<uint8_t> heap(used), ck(t->kbytes), cv(t->vbytes);
+            HIPCHK(hipMemcpy(heap.data(), t->ov.heap, used, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(so.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cko.data(), t->koff, (t->n + 1) * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cvo.data(), t->voff, (t->n + 1) * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ck.data(), t->kheap, t->kbytes, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cv.data(), t->vheap, t->vbytes, hipMemcpyDeviceToHost));
+            uint64_t bad = 0, recs = 0;
+            for (uint64_t s2 = 0; s2 < S; s2++) {
+                if (idx[s2] == ~0ull) continue;
+                recs++;
+                const uint32_t *h = reinterpret_cast<const uint32_t *>(heap.data() + idx[s2]);
+                const uint32_t m = h[0], kbn = h[1];
+                const uint32_t *rk = h + 4, *rv = h + 4 + (m + 1);
+                const uint8_t *kd = reinterpret_cast<const uint8_t *>(h + 4 + 2 * (m + 1)), *vd = kd + kbn;
+                bool ok = so[s2 + 1] - so[s2] == m;
+                for (uint32_t i = 0; ok && i < m; i++) {
+                    const uint64_t e = so[s2] + i;
+                    ok = cko[e + 1] - cko[e] == rk[i + 1] - rk[i] && cvo[e + 1] - cvo[e] == rv[i + 1] - rv[i] &&
+                         !memcmp(ck.data() + cko[e], kd + rk[i], rk[i + 1] - rk[i]) &&
+                         !memcmp(cv.data() + cvo[e], vd + rv[i], rv[i + 1] - rv[i]);
+                }
+                if (!ok && bad++ < 4)
+                    fprintf(stderr, "ov_check merge: segment %llu: csr %llu entries, record %u\n", (unsigned long long)s2,
+                            (unsigned long long)(so[s2 + 1] - so[s2]), m);
+            }
+            fprintf(stderr, "ov_check merge: %llu records, %llu segments differ; n %llu kbytes %llu vbytes %llu so[S] %llu\n",
+                    (unsigned long long)recs, (unsigned long long)bad, (unsigned long long)t->n,
+                    (unsigned long long)t->kbytes, (unsigned long long)t->vbytes, (unsigned long long)so[S]);
+        }
+        if (ov_check_level() & 2) {   // the replace flags after the ingest's kernels: unchanged?
+            std::vector<uint8_t> r2(S);
+            HIPCHK(hipStreamSynchronize(t->stream));
+            HIPCHK(hipMemcpy(r2.data(), rep, S, hipMemcpyDeviceToHost));
+            uint64_t ones = 0, diff = 0, first = ~0ull, last = 0;
+            for (uint64_t s = 0; s < S; s++) {
+                ones += rep_h[s] != 0;
+                if (r2[s] != rep_h[s]) { diff++; if (first == ~0ull) first = s; last = s; }
+            }
+            if (diff) fprintf(stderr, "ov_check flush: replace flags %llu before, %llu changed during ingest (segments %llu..%llu)\n",
+                              (unsigned long long)ones, (unsigned long long)diff, (unsigned long long)first, (unsigned long long)last);
+            if (t->n != nbefore) fprintf(stderr, "ov_check flush: entries %llu -> %llu\n", (unsigned long long)nbefore, (unsigned long long)t->n);
+        }
         (void)nbefore;
     }
     HIPCHK(hipMemsetAsync(t->ov.idx, 0xff, S * 8, t->stream));
     HIPCHK(hipMemsetAsync(t->ov.used, 0, 8, t->stream));
     t->ov_pending = false;
+    t->ov_live = 0;
     return ST_OK;
 }
 
@@ -1039,6 +1233,8 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     const uint64_t kbytes = hr.off[n];
     const uint64_t vbytes = op == 1 ? voff[n] - voff[0] : 0;
     static const uint64_t maxn = getenv("ST_SMALL_MAXN") ? (uint64_t)atoi(getenv("ST_SMALL_MAXN")) : SB_MAX;
+    static const int small_ins = getenv("ST_SMALL_INSERT") ? atoi(getenv("ST_SMALL_INSERT")) : 1;   // diagnostic
+    if (op == 1 && !small_ins) return ST_OK;
     if (n == 0 || n > SB_MAX || n > maxn || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
         small_lds_bytes((uint32_t)t->W) > 160 * 1024)
         return ST_OK;
@@ -1096,6 +1292,12 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
             if (st[k]) fprintf(stderr, " %d:%.2f", k, (st[k] - st[0]) / 100.0);
         fprintf(stderr, "\n");
         memset((void *)t->sout->stamp, 0, sizeof(t->sout->stamp));
+    }
+    if (ov_check_level() & 4) {
+        const uint64_t live = ov_check(t, "small");
+        if (live > t->ov_live + n) fprintf(stderr, "ov_check small: live entries %llu -> %llu after a call of %llu keys\n",
+                                           (unsigned long long)t->ov_live, (unsigned long long)live, (unsigned long long)n);
+        t->ov_live = live;
     }
     if (t->sout->retry) return ST_OK;
     *served = 1;

@@ -22,12 +22,20 @@ def trial(tn, W, S, steps=120):
     ora = C.OTree(W, S)
     assert dev.insert_int64(keys, vals) == 0
     ora.bulk_load_int64(keys, vals)
+    if dev.top_hash() != ora.top_hash():
+        print('FAIL initial top, trial', tn, 'geom', (W, S), 'verify', dev.verify(), 'entries', dev.num_entries(), flush=True)
+        got = dev.get_batch([int(k) for k in keys])
+        bad = [i for i, g in enumerate(got) if g != ora.get(int(keys[i]))]
+        segs = sorted(ora.segment_of(int(keys[i])) for i in bad)
+        print('  bad keys', len(bad), 'segments', segs[:3], segs[-3:] if segs else None, 'kinds', [got[i] if not isinstance(got[i], bytes) else 'val' for i in bad[:4]], flush=True)
+        return False
     rng = np.random.default_rng(tn)
     extra = workload.keys_int63(4000, workload.SEED ^ (0x52 + tn))
     seq = n
     junk = []
     touched = set()
     hist = {}
+    model = {int(k): None for k in keys}
     for step in range(steps):
         m = int(rng.integers(1, 17))
         ks, vs = [], []
@@ -42,6 +50,11 @@ def trial(tn, W, S, steps=120):
         st = dev.insert_batch(ks, vs)
         for k, v in zip(ks, vs):
             ora.insert(k, v)
+            model[k] = v
+            INS.setdefault(k, []).append((step, v[-2:]))
+        if CHECKALL and step >= CHECKALL:
+            if not lost_report(dev, ora, model, 'after insert step %d' % step):
+                return False
         if not all(x is None for x in st):
             print('FAIL insert trial', tn, 'geom', (W, S), 'step', step, 'n', len(ks), 'st', st, flush=True)
             print('  re-get of those keys:', dev.get_batch(ks) == [ora.get(k) for k in ks], flush=True)
@@ -82,6 +95,7 @@ def trial(tn, W, S, steps=120):
                         for kk, vv in e:
                             print('     key', kk, 'dev get1 ok', dev.get1(kk) == vv, flush=True)
                     print('  entries dev', dev.num_entries(), 'ora', ora.num_entries(), flush=True)
+                    lost_report(dev, ora, model, 'at verify failure')
                     multi = sum(1 for x in segs if len(hist.get(x, [])) > 1)
                     print('  touched more than once:', multi, 'of', len(segs), '; bad ones:',
                           [len(hist.get(x, [])) for x, _, _ in badsegs], flush=True)
@@ -92,7 +106,9 @@ def trial(tn, W, S, steps=120):
                         print('  level', lvl, 'differing buckets', len(d), d[:8], flush=True)
                     return False
             if dev.top_hash() != ora.top_hash():
-                print('FAIL top after bulk op, trial', tn, 'step', step, flush=True)
+                print('FAIL top after bulk op, trial', tn, 'step', step, 'verify', dev.verify(), 'entries dev',
+                      dev.num_entries(), 'ora', ora.num_entries(), flush=True)
+                lost_report(dev, ora, model, 'after bulk op')
                 return False
     for j in junk:
         j.close()
@@ -100,6 +116,30 @@ def trial(tn, W, S, steps=120):
     return True
 
 
+def lost_report(dev, ora, model, what):
+    ks = list(model)
+    got = dev.get_batch(ks)
+    bad = [k for k, g in zip(ks, got) if g != ora.get(k)]
+    if not bad:
+        return True
+    segs = sorted(ora.segment_of(k) for k in bad)
+    print('  LOST', what, len(bad), 'of', len(ks), 'keys; segments', segs[0], '..', segs[-1], flush=True)
+    h = {}
+    for x in segs:
+        h[x >> 14] = h.get(x >> 14, 0) + 1
+    print('  per 16K-segment bin:', sorted(h.items()), flush=True)
+    print('  first/last lost segs', segs[:6], segs[-6:], flush=True)
+    shown = 0
+    for k, g in zip(ks, got):
+        if g != ora.get(k) and shown < 6:
+            shown += 1
+            print('   key', k, 'dev', g, 'ora', ora.get(k), 'hist', INS.get(k), flush=True)
+    print('  sample kinds', [type(g).__name__ if not isinstance(g, tuple) else g[:2] for g in got if g is None or isinstance(g, tuple)][:6], flush=True)
+    return False
+
+
+INS = {}
+CHECKALL = int(os.environ.get('STRESS_CHECKALL', '0'))
 JUNK = int(os.environ.get('STRESS_JUNK', '1'))
 t0 = time.time()
 geoms = [(16, 1 << 20), (4, 4096), (16, 16)]
