@@ -115,6 +115,7 @@ struct st_tree {
     uint32_t small_seq = 0;   // sequence number of the last k_small call
     uint64_t small_torn = 0;  // calls whose kernel saw a mismatched argument block (diagnostic)
     uint64_t ov_live = 0;     // live overlay index entries (ST_OV_CHECK diagnostic)
+    uint64_t csr_n_dbg = 0;
     std::vector<uint64_t> csr_copy;   // seg_off as installed (ST_OV_CHECK & 512 diagnostic)
     // timing
     bool timing = false;
@@ -333,15 +334,96 @@ static int use_device(st_tree *t) {
     return ST_OK;
 }
 
+// Exclusive scan (reduce, scan the tile sums, scan the tiles): three plain
+// launches with no inter-workgroup communication inside a kernel.  It
+// replaces rocprim::exclusive_scan, whose single-pass look-back scan returned
+// wrong prefixes for 24-byte elements (SegSums) over 2^20 + 1 items in
+// roughly one call in 100 on this device (tools/stress_small.py with
+// ST_OV_CHECK=64 caught 1,048,568 of 1,048,577 outputs wrong).
+constexpr uint32_t SCAN_T = 256, SCAN_I = 16, SCAN_TILE = SCAN_T * SCAN_I;
+
+template <typename T>
+__device__ T block_exclusive(T v, T *sh, T *total) {   // sh: SCAN_T elements of LDS
+    const uint32_t x = threadIdx.x;
+    sh[x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < SCAN_T; d <<= 1) {   // inclusive (Hillis-Steele)
+        const T a = x >= d ? sh[x - d] : T(0);
+        __syncthreads();
+        if (x >= d) sh[x] = sh[x] + a;
+        __syncthreads();
+    }
+    *total = sh[SCAN_T - 1];
+    const T r = x ? sh[x - 1] : T(0);
+    __syncthreads();
+    return r;
+}
+
+#define SCAN_SHARED(T) \
+    __shared__ __attribute__((aligned(16))) uint8_t sh_raw_[SCAN_T * sizeof(T)]; \
+    T *sh = reinterpret_cast<T *>(sh_raw_)
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_T) k_scan_reduce(const T *in, uint64_t n, T *part) {
+    SCAN_SHARED(T);
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE;
+    T acc(0);
+    for (uint32_t k = 0; k < SCAN_I; k++) {
+        const uint64_t i = base + (uint64_t)k * SCAN_T + threadIdx.x;
+        if (i < n) acc = acc + in[i];
+    }
+    T tot;
+    (void)block_exclusive(acc, sh, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_T) k_scan_parts(T *part, uint64_t nb) {
+    SCAN_SHARED(T);
+    const uint64_t per = (nb + SCAN_T - 1) / SCAN_T, b0 = threadIdx.x * per;
+    T acc(0);
+    for (uint64_t b = b0; b < b0 + per && b < nb; b++) acc = acc + part[b];
+    T tot;
+    T off = block_exclusive(acc, sh, &tot);
+    for (uint64_t b = b0; b < b0 + per && b < nb; b++) {
+        const T v = part[b];
+        part[b] = off;
+        off = off + v;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_T) k_scan_tiles(const T *in, uint64_t n, const T *part, T *out) {
+    SCAN_SHARED(T);
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_I;   // thread-contiguous items
+    T acc(0);
+    for (uint32_t k = 0; k < SCAN_I; k++)
+        if (base + k < n) acc = acc + in[base + k];
+    T tot;
+    T off = block_exclusive(acc, sh, &tot);
+    off = part[blockIdx.x] + off;
+    for (uint32_t k = 0; k < SCAN_I; k++)
+        if (base + k < n) {
+            const T v = in[base + k];
+            out[base + k] = off;
+            off = off + v;
+        }
+}
+
 template <typename T>
 static int exclusive_scan(st_tree *t, const T *in, T *out, uint64_t n) {
-    size_t bytes = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), t->stream));
-    void *tmp;
-    CHK(dalloc(t, &tmp, bytes));
-    hipError_t e = rocprim::exclusive_scan(tmp, bytes, in, out, T(0), (size_t)n, rocprim::plus<T>(), t->stream);
-    dfree(t, tmp);
-    HIPCHK(e);
+    if (n == 0) return ST_OK;
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    T *part = nullptr;
+    CHK(dalloc_t(t, &part, nb));
+    int r = ST_OK;
+    hipLaunchKernelGGL(k_scan_reduce<T>, dim3((uint32_t)nb), dim3(SCAN_T), 0, t->stream, in, n, part);
+    hipLaunchKernelGGL(k_scan_parts<T>, dim3(1), dim3(SCAN_T), 0, t->stream, part, nb);
+    hipLaunchKernelGGL(k_scan_tiles<T>, dim3((uint32_t)nb), dim3(SCAN_T), 0, t->stream, in, n, (const T *)part, out);
+    hipError_t e = hipGetLastError();
+    dfree(t, part);
+    if (e != hipSuccess) { g_err = std::string("scan launch: ") + hipGetErrorString(e); r = ST_EDEVICE; }
+    if (r) return r;
     static const int chk = getenv("ST_OV_CHECK") ? atoi(getenv("ST_OV_CHECK")) : 0;
     if (chk & 64) {   // diagnostic: the device scan against a host scan
         std::vector<T> hi(n), ho(n);
@@ -974,6 +1056,56 @@ static int ingest(st_tree *t, IngestIn &in) {
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
+    if ((ov_check_level() & 1024) && !in.bop && !in.seg_replace && S <= (1u << 22)) {
+        // diagnostic: per-segment entry counts of the merge against a host replay
+        // (old keys U kept batch keys of the segment; PUT-only batches)
+        HIPCHK(hipStreamSynchronize(t->stream));
+        const uint64_t on = t->csr_n_dbg;
+        std::vector<uint64_t> oso(S + 1), nso(S + 1), oko(on + 1), bko(n + 1);
+        std::vector<uint32_t> bseg(n);
+        std::vector<uint8_t> rj(reject ? S : 0);
+        HIPCHK(hipMemcpy(oso.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(nso.data(), out.o.seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+        const uint64_t on2 = oso[S];
+        oko.resize(on2 + 1);
+        HIPCHK(hipMemcpy(oko.data(), t->koff, (on2 + 1) * 8, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> okh(oko[on2]);
+        if (oko[on2]) HIPCHK(hipMemcpy(okh.data(), t->kheap, oko[on2], hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bko.data(), in.koff, (n + 1) * 8, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> bkh(bko[n]);
+        HIPCHK(hipMemcpy(bkh.data(), in.krec, bko[n], hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bseg.data(), seg, n * 4, hipMemcpyDeviceToHost));
+        if (reject) HIPCHK(hipMemcpy(rj.data(), reject, S, hipMemcpyDeviceToHost));
+        std::map<uint64_t, std::vector<std::string>> add;
+        for (uint64_t i = 0; i < n; i++)
+            add[bseg[i]].push_back(std::string((const char *)bkh.data() + bko[i], bko[i + 1] - bko[i]));
+        uint64_t bad = 0, exp_total = 0, rejected = 0;
+        for (uint64_t s = 0; s < S; s++) {
+            uint64_t c = oso[s + 1] - oso[s];
+            auto it = add.find(s);
+            if (it != add.end()) {
+                if (reject && rj[s]) { rejected++; }
+                else {
+                    std::vector<std::string> keys;
+                    for (uint64_t e = oso[s]; e < oso[s + 1]; e++)
+                        keys.push_back(std::string((const char *)okh.data() + oko[e], oko[e + 1] - oko[e]));
+                    for (auto &k : it->second) keys.push_back(k);
+                    std::sort(keys.begin(), keys.end());
+                    c = std::unique(keys.begin(), keys.end()) - keys.begin();
+                }
+            }
+            exp_total += c;
+            const uint64_t got = nso[s + 1] - nso[s];
+            if (got != c && bad++ < 6)
+                fprintf(stderr, "merge_check: segment %llu: %llu entries, expected %llu (old %llu, batch run %d)\n",
+                        (unsigned long long)s, (unsigned long long)got, (unsigned long long)c,
+                        (unsigned long long)(oso[s + 1] - oso[s]), it != add.end() ? 1 : 0);
+        }
+        if (bad || exp_total != n_new || nso[S] != n_new)
+            fprintf(stderr, "merge_check: n %llu: %llu segments differ, expected total %llu, n_new %llu, new seg_off[S] %llu, old %llu (%llu), rejected runs %llu\n",
+                    (unsigned long long)n, (unsigned long long)bad, (unsigned long long)exp_total, (unsigned long long)n_new,
+                    (unsigned long long)nso[S], (unsigned long long)on2, (unsigned long long)on, (unsigned long long)rejected);
+    }
     if (ov_check_level() & 128) {
         uint64_t so_s = 0, so_0 = 0;
         HIPCHK(hipStreamSynchronize(t->stream));
@@ -986,6 +1118,7 @@ static int ingest(st_tree *t, IngestIn &in) {
     // swap in the new CSR (the old one becomes the spare set, in stream order)
     out.install();
     t->n = n_new; t->kbytes = tot_k; t->vbytes = tot_v;
+    t->csr_n_dbg = n_new;
     if (ov_check_level() & 512) {
         t->csr_copy.resize(S + 1);
         HIPCHK(hipStreamSynchronize(t->stream));
