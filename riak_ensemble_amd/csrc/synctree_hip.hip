@@ -124,12 +124,28 @@ struct st_tree {
 };
 
 // ------------------------------------------------------------------ helpers
+static std::map<uintptr_t, uint64_t> g_live;   // live device allocations (ST_POOL_CHECK diagnostic)
 static int dalloc(st_tree *t, void **p, uint64_t bytes) {
     *p = nullptr;
     if (bytes == 0) bytes = 16;
     static const int sync_alloc = getenv("ST_SYNC_ALLOC") ? atoi(getenv("ST_SYNC_ALLOC")) : 0;   // diagnostic
     if (sync_alloc) (void)hipStreamSynchronize(t->stream);
     hipError_t e = hipMallocAsync(p, bytes, t->stream);
+    static const int track = getenv("ST_POOL_CHECK") ? atoi(getenv("ST_POOL_CHECK")) : 0;   // diagnostic
+    if (track && e == hipSuccess) {
+        const uintptr_t a = (uintptr_t)*p, z = a + bytes;
+        auto it = g_live.upper_bound(a);
+        if (it != g_live.end() && it->first < z)
+            fprintf(stderr, "pool_check: new [%lx,+%llu) overlaps live [%lx,+%llu)\n", (unsigned long)a,
+                    (unsigned long long)bytes, (unsigned long)it->first, (unsigned long long)it->second);
+        if (it != g_live.begin()) {
+            --it;
+            if (it->first + it->second > a)
+                fprintf(stderr, "pool_check: new [%lx,+%llu) overlaps live [%lx,+%llu)\n", (unsigned long)a,
+                        (unsigned long long)bytes, (unsigned long)it->first, (unsigned long long)it->second);
+        }
+        g_live[a] = bytes;
+    }
     if (e != hipSuccess) {
         g_err = std::string("hipMallocAsync: ") + hipGetErrorString(e);
         return e == hipErrorOutOfMemory ? ST_ENOMEM : ST_EDEVICE;
@@ -141,6 +157,7 @@ static int dalloc_t(st_tree *t, T **p, uint64_t count) {
     return dalloc(t, (void **)p, count * sizeof(T));
 }
 static void dfree(st_tree *t, void *p) {
+    if (p) g_live.erase((uintptr_t)p);
     if (p) (void)hipFreeAsync(p, t->stream);
 }
 
@@ -335,11 +352,9 @@ static int use_device(st_tree *t) {
 }
 
 // Exclusive scan (reduce, scan the tile sums, scan the tiles): three plain
-// launches with no inter-workgroup communication inside a kernel.  It
-// replaces rocprim::exclusive_scan, whose single-pass look-back scan returned
-// wrong prefixes for 24-byte elements (SegSums) over 2^20 + 1 items in
-// roughly one call in 100 on this device (tools/stress_small.py with
-// ST_OV_CHECK=64 caught 1,048,568 of 1,048,577 outputs wrong).
+// launches with no inter-workgroup communication inside a kernel (it replaced
+// rocprim's look-back scan while chasing the open issue in DESIGN.md §3.4;
+// the issue is upstream of the scan: its INPUT is seen differently).
 constexpr uint32_t SCAN_T = 256, SCAN_I = 16, SCAN_TILE = SCAN_T * SCAN_I;
 
 template <typename T>
