@@ -79,6 +79,10 @@ def lib():
         L.ot_num_entries.argtypes = [vp]
         L.ot_insert_int64_seq.restype = u64
         L.ot_insert_int64_seq.argtypes = [vp, u64, vp, vp, u32]
+        L.ot_bulk_load_int64_par.restype = ctypes.c_int
+        L.ot_bulk_load_int64_par.argtypes = [vp, u64, vp, vp, u32, ctypes.c_int]
+        L.ot_apply_int64_batch.restype = ctypes.c_int
+        L.ot_apply_int64_batch.argtypes = [vp, u64, vp, vp, u32, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -258,6 +262,26 @@ class OTree:
         keys = np.ascontiguousarray(keys, np.int64)
         values = np.ascontiguousarray(values, np.uint8)
         return int(lib().ot_insert_int64_seq(self.h, len(keys), keys.ctypes.data, values.ctypes.data, values.shape[1]))
+
+    def bulk_load_int64_par(self, keys, values, threads=0):
+        """bulk_load_int64 with OpenMP threads (0 = all): same result."""
+        keys = np.ascontiguousarray(keys, np.int64)
+        values = np.ascontiguousarray(values, np.uint8)
+        r = lib().ot_bulk_load_int64_par(self.h, len(keys), keys.ctypes.data, values.ctypes.data, values.shape[1],
+                                         threads)
+        if r != 0:
+            raise ValueError('bulk_load needs a fresh tree')
+        return self
+
+    def apply_int64_batch(self, keys, values, threads=0):
+        """len(keys) sequential insert/3 calls on a CONSISTENT tree (no
+        corruption: every path verifies), computed as merged segments + the
+        full rehash (OpenMP threads, 0 = all); same result as insert_int64_seq
+        on such a tree (pinned in tests/test_oracle.py)."""
+        keys = np.ascontiguousarray(keys, np.int64)
+        values = np.ascontiguousarray(values, np.uint8)
+        lib().ot_apply_int64_batch(self.h, len(keys), keys.ctypes.data, values.ctypes.data, values.shape[1], threads)
+        return self
 
     def bulk_load_int64(self, keys, values):
         """keys: int64 ndarray [n]; values: uint8 ndarray [n, vlen]."""

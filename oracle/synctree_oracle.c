@@ -758,3 +758,148 @@ uint64_t ot_num_entries(ot_tree *t) {
 
 /* exported for the RFC 1321 known-answer tests */
 void ot_md5(const uint8_t *p, uint64_t n, uint8_t out[16]) { md5r(p, (size_t)n, out); }
+
+/* ------------------------------------------------------------------ */
+/* Parallel forms for the 100M-key parity tests (config 5) and the group of
+ * 512 x 1M trees (config 4).  Same results as the literal forms above; tests
+ * (tests/test_oracle.py) pin the equivalence at small N.
+ *
+ * ot_bulk_load_int64_par: ot_bulk_load_int64 into a FRESH tree (sequential
+ *   insert semantics: last writer wins) with the segment ids, the per-segment
+ *   sorts and the rehash spread over `threads` OpenMP threads.
+ * ot_apply_int64_batch: n sequential insert/3 calls (synctree.erl:189-209)
+ *   on a CONSISTENT tree (every stored entry equals its node's hash, e.g. a
+ *   bulk-loaded or rehashed tree, no corruption): every path verifies, so the
+ *   result is each segment's orddict:store of its keys in batch order (last
+ *   writer wins) and every path node rehashed -- computed here as the merged
+ *   segments followed by the full rehash, which reproduces every untouched
+ *   node of a consistent tree. */
+typedef struct {
+    const int64_t *keys;
+} icmp_ctx;
+
+static int cmp_i64_idx(const void *x, const void *y, void *arg) {
+    const icmp_ctx *c = (const icmp_ctx *)arg;
+    uint64_t i = *(const uint64_t *)x, j = *(const uint64_t *)y;
+    int64_t a = c->keys[i], b = c->keys[j];
+    if (a != b) return a < b ? -1 : 1;
+    return i < j ? -1 : (i > j ? 1 : 0);
+}
+
+/* segment ids of n int64 keys (parallel) and their order by segment */
+static void group_by_segment(ot_tree *t, uint64_t n, const int64_t *keys, uint64_t **cnt_out, uint64_t **order_out) {
+    uint64_t S = t->segments;
+    uint32_t *seg = (uint32_t *)malloc(n * sizeof(uint32_t) + 4);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 65536)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        uint8_t kb[8];
+        uint64_t x = (uint64_t)keys[i];
+        for (int j = 0; j < 8; j++) kb[j] = (uint8_t)(x >> (56 - 8 * j));
+        seg[i] = (uint32_t)ot_segment_of(t, kb, 8);
+    }
+    uint64_t *cnt = (uint64_t *)calloc(S + 1, sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; i++) cnt[seg[i] + 1]++;
+    for (uint64_t s = 0; s < S; s++) cnt[s + 1] += cnt[s];
+    uint64_t *fill = (uint64_t *)malloc((S + 1) * sizeof(uint64_t));
+    memcpy(fill, cnt, (S + 1) * sizeof(uint64_t));
+    uint64_t *order = (uint64_t *)malloc(n * sizeof(uint64_t) + 8);
+    for (uint64_t i = 0; i < n; i++) order[fill[seg[i]]++] = i;
+    free(fill); free(seg);
+    *cnt_out = cnt; *order_out = order;
+}
+
+/* the batch's key bytes (<<K:64>>) and values in the tree arena */
+static void arena_int64_batch(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                              uint8_t **kh, uint8_t **vh) {
+    uint8_t *kb = (uint8_t *)malloc(n * 8 + 1);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 65536)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        uint64_t x = (uint64_t)keys[i];
+        for (int j = 0; j < 8; j++) kb[8 * i + j] = (uint8_t)(x >> (56 - 8 * j));
+    }
+    *kh = arena_put(t, kb, n * 8);
+    *vh = arena_put(t, vals, (size_t)n * vlen);
+    free(kb);
+}
+
+int ot_bulk_load_int64_par(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen, int threads) {
+    uint64_t S = t->segments, H1 = t->height + 1;
+    for (uint64_t s = 0; s < S; s++)
+        if (node_stored(node_at(t, H1, s))) return OT_EINVAL;
+    if (t->rec_top_def) return OT_EINVAL;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    uint64_t *cnt, *order;
+    group_by_segment(t, n, keys, &cnt, &order);
+    uint8_t *kh, *vh;
+    arena_int64_batch(t, n, keys, vals, vlen, &kh, &vh);
+    icmp_ctx c = {keys};
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1024)
+#endif
+    for (int64_t s = 0; s < (int64_t)S; s++) {
+        uint64_t a = cnt[s], b = cnt[s + 1];
+        if (a == b) continue;
+        qsort_r(order + a, b - a, sizeof(uint64_t), cmp_i64_idx, &c);
+        onode *nd = node_at(t, H1, (uint64_t)s);
+        node_reserve_seg(nd, (uint32_t)(b - a));
+        uint32_t m = 0;
+        for (uint64_t j = a; j < b; j++) {
+            uint64_t i = order[j];
+            if (j + 1 < b && keys[order[j + 1]] == keys[i]) continue;   /* last writer wins */
+            oent e;
+            e.ktype = 0; e.k = kh + 8 * i; e.klen = 8; e.v = vh + (uint64_t)vlen * i; e.vlen = vlen;
+            nd->e[m++] = e;
+        }
+        nd->n = m;
+    }
+    free(cnt); free(order);
+    ot_rehash_par(t, threads);
+    return OT_OK;
+}
+
+int ot_apply_int64_batch(ot_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen, int threads) {
+    uint64_t S = t->segments, H1 = t->height + 1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    uint64_t *cnt, *order;
+    group_by_segment(t, n, keys, &cnt, &order);
+    uint8_t *kh, *vh;
+    arena_int64_batch(t, n, keys, vals, vlen, &kh, &vh);
+    icmp_ctx c = {keys};
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1024)
+#endif
+    for (int64_t s = 0; s < (int64_t)S; s++) {
+        uint64_t a = cnt[s], b = cnt[s + 1];
+        if (a == b) continue;
+        qsort_r(order + a, b - a, sizeof(uint64_t), cmp_i64_idx, &c);
+        onode *nd = node_at(t, H1, (uint64_t)s);
+        uint32_t old_n = nd->n;
+        oent *merged = (oent *)malloc((old_n + (b - a)) * sizeof(oent));
+        uint32_t m = 0, x = 0;
+        for (uint64_t j = a; j < b; j++) {
+            uint64_t i = order[j];
+            if (j + 1 < b && keys[order[j + 1]] == keys[i]) continue;   /* a later write of the key wins */
+            oent e;
+            e.ktype = 0; e.k = kh + 8 * i; e.klen = 8; e.v = vh + (uint64_t)vlen * i; e.vlen = vlen;
+            while (x < old_n && key_cmp(nd->e[x].ktype, nd->e[x].k, nd->e[x].klen, 0, e.k, 8) < 0) merged[m++] = nd->e[x++];
+            if (x < old_n && key_cmp(nd->e[x].ktype, nd->e[x].k, nd->e[x].klen, 0, e.k, 8) == 0) x++;   /* replaced */
+            merged[m++] = e;
+        }
+        while (x < old_n) merged[m++] = nd->e[x++];
+        free(nd->e);
+        nd->e = merged;
+        nd->n = m;
+        nd->cap = m ? m : 1;
+    }
+    free(cnt); free(order);
+    ot_rehash_par(t, threads);
+    return OT_OK;
+}

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libsynctree_hip.so')
+# ST_LIB: another build of the library (A/B runs of tools/); the default is the in-tree build
+LIB_PATH = os.environ.get('ST_LIB') or os.path.join(_HERE, 'libsynctree_hip.so')
 
 ST_OK, ST_NOTFOUND, ST_CORRUPTED = 0, 1, 2
 ST_EINVAL, ST_EDEVICE, ST_ENOMEM = -1, -2, -3

@@ -1,8 +1,10 @@
 // small_path.h — the per-key latency path of insert/3 and get/2 (SURVEY §8f
 // rank 4; src/synctree.erl:189-227): a batch of at most SB_MAX keys is served
-// by ONE workgroup in ONE launch, with the keys passed as kernel arguments and
-// the results written straight into mapped pinned host memory, so a call costs
-// one launch and one stream synchronisation.
+// by ONE workgroup in ONE launch.  The host writes the call's request (keys,
+// values, the tree view) into a slot of fine-grained host memory; the kernel
+// copies it into LDS and writes self-validating result records straight into
+// mapped host memory, which the host spins on: a call costs one launch and no
+// stream synchronisation.
 //
 // Segments changed by small inserts are not merged into the CSR at once: the
 // new content of a segment goes to an OVERLAY record (ov.idx[s] -> offset in
@@ -30,37 +32,65 @@
 struct SmallIn {
     uint32_t n, op;       // op: 0 = get/2, 1 = insert/3
     uint32_t dbg, seq;    // dbg: phase stamps into SmallOut.stamp (ST_SMALL_STAMPS); seq: the call's
-                          // sequence number (never 0), echoed in SmallOut.sseq / done
+                          // sequence number (never 0), echoed in every result record
     uint32_t koff[SB_MAX + 1];
     uint32_t voff[SB_MAX + 1];
     uint8_t kb[SB_KB];
     uint8_t vb[SB_VB];
 };
 
-struct SmallOut {
-    int32_t status[SB_MAX];    // ST_OK / ST_NOTFOUND / ST_CORRUPTED
+// Result block (fine-grained host memory).  The GPU's writes to host memory
+// are not seen by the host in program order even across a system-scope fence
+// (round 2: a call read an earlier call's status words after the later
+// sequence word had arrived), so no result depends on the order of two
+// stores: every result is ONE self-validating 16-byte record written with a
+// single store -- {seq, word, x, check(seq, word, x)} -- and the value bytes
+// a get returns are covered by an FNV-1a sum in their key's record.  The host
+// spins until the header and every key's record carry this call's seq and a
+// valid check (and the value sums match); a record of an earlier call, or a
+// torn one, never validates.
+//   hdr:    word = retry | new_entries << 1
+//   rec[i]: word = status | clevel << 8 | vlen << 16;
+//           x = cbucket (corrupted) or the FNV-1a of the value bytes (get, found)
+// Host copy of a validated result block (synctree_hip.hip small_collect).
+struct SmallRes {
+    int32_t status[SB_MAX];
     uint32_t clevel[SB_MAX];
     uint64_t cbucket[SB_MAX];
-    uint32_t voff[SB_MAX + 1]; // get: value i = vbytes[voff[i] .. voff[i+1])
-    uint32_t sseq[SB_MAX];     // key i's results are complete once sseq[i] == the call's seq
-    uint32_t retry;            // 1: not served (overlay full, segment too large): use the bulk path
-    uint32_t new_entries;      // insert: keys that were not in their segment before
-    uint32_t done;             // the call's seq, written last
-    uint32_t pad;
-    uint64_t stamp[8];         // diagnostic phase stamps (100 MHz), in.dbg only
-    uint8_t vbytes[SB_OUT_VB];
+    uint32_t voff[SB_MAX + 1];   // get: key i's value is vbytes[voff[i] .. voff[i+1])
+    uint32_t new_entries;
+    bool retry;                  // not served (overlay full, segment too large): the bulk path serves the call
+};
+#define SMALL_SLOTS 2
+
+struct SmallOut {
+    uint4 hdr;
+    uint4 rec[SB_MAX];
+    uint64_t stamp[8];         // diagnostic phase stamps (100 MHz), in.dbg only; read after a stream sync
+    uint8_t vbytes[SB_OUT_VB]; // get: key i's value at the sum of the earlier keys' vlen
 };
 
-// Completion protocol of the result block (mapped host memory).  Each key's
-// results (status, level, bucket, value offset and bytes) are written by one
-// thread, which then fences at system scope and writes the key's sequence
-// word; thread 0 writes `done` = seq after a barrier and its own fence.  The
-// host waits for done == seq AND every sseq[i] == seq, so it never acts on a
-// result word of an earlier call: a call's words are tagged, not just
-// ordered (an earlier build read an earlier call's statuses, intermittently).
-__device__ __forceinline__ void key_done(SmallOut *out, uint32_t i, uint32_t seq) {
+__host__ __device__ __forceinline__ uint32_t small_check(uint32_t seq, uint32_t w, uint32_t x) {
+    uint32_t h = seq * 0x9E3779B1u ^ 0x85EBCA77u;
+    h = (h ^ w) * 0xC2B2AE3Du;
+    h = (h ^ (h >> 15) ^ x) * 0x27D4EB2Fu;
+    return (h ^ (h >> 13)) | 1u;   // never 0: a zeroed record does not validate
+}
+__host__ __device__ __forceinline__ uint32_t fnv1a_step(uint32_t h, uint8_t b) { return (h ^ b) * 16777619u; }
+#define FNV1A_INIT 2166136261u
+
+__device__ __forceinline__ void put_rec(uint4 *dst, uint32_t seq, uint32_t w, uint32_t x) {
+    *dst = make_uint4(seq, w, x, small_check(seq, w, x));   // one 16-byte store
+}
+// the key's record after its result words are final; the header last, after
+// a barrier and a system-scope release (the host validates each anyway)
+__device__ __forceinline__ void key_rec(SmallOut *out, uint32_t i, uint32_t seq, int32_t status, uint32_t clevel,
+                                        uint32_t vlen, uint32_t x) {
+    put_rec(&out->rec[i], seq, (uint32_t)status | (clevel << 8) | (vlen << 16), x);
+}
+__device__ __forceinline__ void hdr_rec(SmallOut *out, uint32_t seq, uint32_t retry, uint32_t new_entries) {
     __threadfence_system();
-    out->sseq[i] = seq;
+    put_rec(&out->hdr, seq, retry | (new_entries << 1), 0u);
 }
 
 struct Overlay {
@@ -68,6 +98,15 @@ struct Overlay {
     uint8_t *heap;
     unsigned long long *used;   // bump pointer (device)
     uint64_t cap;
+};
+
+// One call's whole input, written by the host into a per-tree slot of
+// fine-grained host memory before the launch; the kernel's only arguments are
+// the slot and result-block pointers (no large by-value argument block).
+struct SmallReq {
+    DevTree t;
+    Overlay ov;
+    SmallIn in;
 };
 
 // get_segment/2 (synctree.erl:251-253) of one key record (tag + payload)
@@ -337,7 +376,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
     SB_STAMP(5);
     const bool ok = bad[0] == ~0u;
     if (s1_retry) {   // nothing was committed: the host takes the bulk path
-        if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = in.seq; }
+        if (tid == 0) hdr_rec(out, in.seq, 1u, 0u);
         return;
     }
     if (ok) {   // commit: the overlay record and the path's entries
@@ -351,22 +390,13 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
         }
     }
     if (tid == 0) {
-        if (ok) {
-            out->status[0] = ST_OK; out->clevel[0] = 0; out->cbucket[0] = 0;
-        } else {
-            out->status[0] = ST_CORRUPTED;
-            out->clevel[0] = bad[0];
-            out->cbucket[0] = s >> (t.shift * (L1 - bad[0]));
-        }
-        out->new_entries = ok ? s1_news : 0;
-        out->retry = 0;
-        key_done(out, 0, in.seq);
+        if (ok) key_rec(out, 0, in.seq, ST_OK, 0, 0, 0);
+        else key_rec(out, 0, in.seq, ST_CORRUPTED, bad[0], 0, (uint32_t)(s >> (t.shift * (L1 - bad[0]))));
     }
     SB_STAMP(6);
-    __threadfence_system();
     __syncthreads();
     SB_STAMP(7);
-    if (tid == 0) { __threadfence_system(); out->done = in.seq; }
+    if (tid == 0) hdr_rec(out, in.seq, 0u, ok ? s1_news : 0u);
 }
 
 // The small-batch kernel (one workgroup of 256 threads, 4 waves).
@@ -384,15 +414,17 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
 //     one thread per distinct node, a barrier per level (update_path,
 //     synctree.erl:201-209).
 // `out` is mapped pinned host memory: the host reads it after the stream sync.
-// Position-weighted word sum of the argument block (host: small_in_sum):
-// the kernel checks the copy of `in` it received against the sum the host
-// passed as a separate scalar argument.
-__host__ __device__ __forceinline__ uint32_t small_in_word(const SmallIn &in, uint32_t i) {
-    return reinterpret_cast<const uint32_t *>(&in)[i] * (2u * i + 1u);
-}
-
-__global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in, SmallOut *out, uint32_t in_sum) {
+__global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    // the request (host memory) into LDS: one round trip, dword per thread
+    __shared__ __attribute__((aligned(16))) SmallReq rq;
+    static_assert(sizeof(SmallReq) % 4 == 0, "request is copied in dwords");
+    for (uint32_t i = threadIdx.x; i < sizeof(SmallReq) / 4; i += blockDim.x)
+        reinterpret_cast<uint32_t *>(&rq)[i] = reinterpret_cast<const uint32_t *>(req)[i];
+    __syncthreads();
+    const DevTree &t = rq.t;
+    const Overlay &ov = rq.ov;
+    const SmallIn &in = rq.in;
     __shared__ uint8_t kb[SB_KB + 64];
     __shared__ uint8_t vb[SB_VB + 64];
     __shared__ uint64_t seg[SB_MAX];
@@ -408,20 +440,6 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = in.n, L1 = t.H + 1;
     SB_STAMP(0);
-    {   // the argument block must be this call's, whole: else nothing is done and
-        // the host takes the bulk path (pad = 0xBAD reports it)
-        __shared__ uint32_t s_sum;
-        if (tid == 0) s_sum = 0;
-        __syncthreads();
-        uint32_t x = 0;
-        for (uint32_t i = tid; i < sizeof(SmallIn) / 4; i += blockDim.x) x += small_in_word(in, i);
-        atomicAdd(&s_sum, x);
-        __syncthreads();
-        if (s_sum != in_sum) {
-            if (tid == 0) { out->retry = 1; out->pad = 0xBADu; __threadfence_system(); out->done = in.seq; }
-            return;
-        }
-    }
     for (uint32_t i = tid; i < in.koff[n]; i += blockDim.x) kb[i] = in.kb[i];
     for (uint32_t i = tid; in.op == 1 && i < in.voff[n]; i += blockDim.x) vb[i] = in.vb[i];
     if (tid < SB_MAX) { bad[tid] = ~0u; keep[tid] = 0; }
@@ -431,14 +449,9 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     __syncthreads();
     const bool undefined_top = (t.tag[0] & TAG_PRESENT) == 0;
     if (in.op == 0 && undefined_top) {   // get/2: undefined top => notfound (synctree.erl:216-218)
-        if (tid < n) {
-            out->status[tid] = ST_NOTFOUND; out->clevel[tid] = 0; out->cbucket[tid] = 0;
-            out->voff[tid + 1] = 0;
-            if (tid == 0) out->voff[0] = 0;
-            key_done(out, tid, in.seq);
-        }
+        if (tid < n) key_rec(out, tid, in.seq, ST_NOTFOUND, 0, 0, 0);
         __syncthreads();
-        if (tid == 0) { out->retry = 0; out->new_entries = 0; __threadfence_system(); out->done = in.seq; }
+        if (tid == 0) hdr_rec(out, in.seq, 0u, 0u);
         return;
     }
     if (in.op == 1 && n == 1) {   // insert/3 of one key: the speculative path below
@@ -500,26 +513,23 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
             retry = vlen_out[n] > SB_OUT_VB;
         }
         __syncthreads();
-        if (tid < n) {   // this key's value bytes and result words, then its sequence word
-            if (!retry && src)
-                for (uint32_t b = 0; b < len; b++) out->vbytes[vlen_out[tid] + b] = src[b];
-            if (tid == 0) out->voff[0] = 0;
-            out->voff[tid + 1] = vlen_out[tid + 1];
-            if (my_bad != ~0u) {
-                out->status[tid] = ST_CORRUPTED;
-                out->clevel[tid] = my_bad;
-                out->cbucket[tid] = my_seg >> (t.shift * (L1 - my_bad));
-            } else {
-                out->status[tid] = my_found ? ST_OK : ST_NOTFOUND;
-                out->clevel[tid] = 0;
-                out->cbucket[tid] = 0;
-            }
-            key_done(out, tid, in.seq);
+        if (tid < n && !retry) {   // this key's value bytes, then its record (with their FNV-1a)
+            uint32_t h = FNV1A_INIT;
+            if (src)
+                for (uint32_t b = 0; b < len; b++) {
+                    const uint8_t c = src[b];
+                    out->vbytes[vlen_out[tid] + b] = c;
+                    h = fnv1a_step(h, c);
+                }
+            if (my_bad != ~0u)
+                key_rec(out, tid, in.seq, ST_CORRUPTED, my_bad, 0, (uint32_t)(my_seg >> (t.shift * (L1 - my_bad))));
+            else
+                key_rec(out, tid, in.seq, my_found ? ST_OK : ST_NOTFOUND, 0, len, my_found ? h : 0u);
         }
         SB_STAMP(6);
         __syncthreads();
         SB_STAMP(7);
-        if (tid == 0) { out->retry = retry; out->new_entries = 0; __threadfence_system(); out->done = in.seq; }
+        if (tid == 0) hdr_rec(out, in.seq, retry, 0u);
         return;
     }
     // ---- 3 (insert): groups = distinct verified segments, last writer per key
@@ -637,7 +647,7 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
         }
         __syncthreads();
         if (pass == 0 && retry) {   // nothing was written: the host takes the bulk path
-            if (tid == 0) { out->retry = 1; __threadfence_system(); out->done = in.seq; }
+            if (tid == 0) hdr_rec(out, in.seq, 1u, 0u);
             return;
         }
     }
@@ -693,25 +703,17 @@ __global__ void __launch_bounds__(256) k_small(DevTree t, Overlay ov, SmallIn in
     }
     __syncthreads();
     if (tid < n) {
-        if (my_bad != ~0u) {
-            out->status[tid] = ST_CORRUPTED;
-            out->clevel[tid] = my_bad;
-            out->cbucket[tid] = my_seg >> (t.shift * (L1 - my_bad));
-        } else {
-            out->status[tid] = ST_OK;
-            out->clevel[tid] = 0;
-            out->cbucket[tid] = 0;
-        }
-        key_done(out, tid, in.seq);
+        if (my_bad != ~0u)
+            key_rec(out, tid, in.seq, ST_CORRUPTED, my_bad, 0, (uint32_t)(my_seg >> (t.shift * (L1 - my_bad))));
+        else
+            key_rec(out, tid, in.seq, ST_OK, 0, 0, 0);
     }
+    __syncthreads();
     if (tid == 0) {
         uint32_t c = 0;
         for (uint32_t g = 0; g < ngrp; g++) c += gnew[g];
-        out->new_entries = c;
-        out->retry = 0;
+        hdr_rec(out, in.seq, 0u, c);
     }
-    __syncthreads();
-    if (tid == 0) { __threadfence_system(); out->done = in.seq; }
 }
 
 // Overlay flush, step 1: per segment, the number of overlay entries and

@@ -12,7 +12,10 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
 #include <chrono>
+#include <atomic>
 #include <map>
+#include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 #include <algorithm>
@@ -112,44 +115,94 @@ struct st_tree {
     Overlay ov{nullptr, nullptr, nullptr, 0};
     bool ov_pending = false;
     SmallOut *sout = nullptr, *sout_dev = nullptr;
+    SmallReq *sreq = nullptr, *sreq_dev = nullptr;   // SMALL_SLOTS request slots (host memory)
+    SmallRes sres;                                    // the last call's validated results
     uint32_t small_seq = 0;   // sequence number of the last k_small call
-    uint64_t small_torn = 0;  // calls whose kernel saw a mismatched argument block (diagnostic)
-    uint64_t ov_live = 0;     // live overlay index entries (ST_OV_CHECK diagnostic)
-    uint64_t csr_n_dbg = 0;
-    std::vector<uint64_t> csr_copy;   // seg_off as installed (ST_OV_CHECK & 512 diagnostic)
+    std::atomic<uint64_t> sync_epoch{0};   // host synchronisations of `stream` (tsync; block reuse)
     // timing
     bool timing = false;
     std::vector<Pending> pending;
     std::map<std::string, std::pair<uint64_t, double>> stats;
 };
 
-// ------------------------------------------------------------------ helpers
-static std::map<uintptr_t, uint64_t> g_live;   // live device allocations (ST_POOL_CHECK diagnostic)
+// ------------------------------------------------------------------ device memory
+// Every device buffer of the library comes from one process-wide cache of
+// hipMalloc'd blocks, never from the stream-ordered pool (hipMallocAsync /
+// hipFreeAsync).  With the pool, the round-2 small-batch ingest lost CSR
+// entries and faulted on some MI355X boxes (deterministically on those, at
+// the same step of tools/stress_small.py) and never on others; on a failing
+// box, plain hipMalloc/hipFree and a never-unmapped block cache both ran the
+// same sequence clean (gpurun_out A/B logs in profiles/).
+//
+// A freed block becomes reusable only after the stream of the tree that freed
+// it has been synchronised by the host (tsync): every GPU use enqueued before
+// the free has then completed, on any stream.  Blocks are cached by size class
+// (1/8-power-of-two steps, <= 12.5 % slack) per device and released to the
+// driver only when an allocation runs out of memory.
+struct MemBlock {
+    void *p;
+    uint64_t cls;
+    int device;
+    const st_tree *owner;   // tree that freed it (nullptr: no pending use)
+    uint64_t epoch;         // owner's sync epoch at the free
+};
+static std::mutex g_mem_mu;
+static std::multimap<uint64_t, MemBlock> g_mem_free;          // size class -> free blocks
+static std::unordered_map<void *, std::pair<uint64_t, int>> g_mem_live;   // live block -> (class, device)
+
+static uint64_t size_class(uint64_t b) {
+    if (b <= 4096) return (b + 255) & ~255ull;
+    const int k = 63 - __builtin_clzll(b);
+    const uint64_t step = 1ull << (k - 3);
+    return (b + step - 1) & ~(step - 1);
+}
+static bool block_ready(const MemBlock &m) {
+    return !m.owner || m.owner->sync_epoch.load(std::memory_order_acquire) > m.epoch;
+}
+// Release cached blocks of `device` to the driver (all of them after a device
+// synchronisation when `all`, else the ready ones).  g_mem_mu held.
+static void mem_release_locked(int device, bool all) {
+    for (auto it = g_mem_free.begin(); it != g_mem_free.end();) {
+        if (it->second.device == device && (all || block_ready(it->second))) {
+            (void)hipFree(it->second.p);
+            it = g_mem_free.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
 static int dalloc(st_tree *t, void **p, uint64_t bytes) {
     *p = nullptr;
-    if (bytes == 0) bytes = 16;
-    static const int sync_alloc = getenv("ST_SYNC_ALLOC") ? atoi(getenv("ST_SYNC_ALLOC")) : 0;   // diagnostic
-    if (sync_alloc) (void)hipStreamSynchronize(t->stream);
-    hipError_t e = hipMallocAsync(p, bytes, t->stream);
-    static const int track = getenv("ST_POOL_CHECK") ? atoi(getenv("ST_POOL_CHECK")) : 0;   // diagnostic
-    if (track && e == hipSuccess) {
-        const uintptr_t a = (uintptr_t)*p, z = a + bytes;
-        auto it = g_live.upper_bound(a);
-        if (it != g_live.end() && it->first < z)
-            fprintf(stderr, "pool_check: new [%lx,+%llu) overlaps live [%lx,+%llu)\n", (unsigned long)a,
-                    (unsigned long long)bytes, (unsigned long)it->first, (unsigned long long)it->second);
-        if (it != g_live.begin()) {
-            --it;
-            if (it->first + it->second > a)
-                fprintf(stderr, "pool_check: new [%lx,+%llu) overlaps live [%lx,+%llu)\n", (unsigned long)a,
-                        (unsigned long long)bytes, (unsigned long)it->first, (unsigned long long)it->second);
+    const uint64_t c = size_class(bytes ? bytes : 16);
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    auto rng = g_mem_free.equal_range(c);
+    for (auto it = rng.first; it != rng.second; ++it)
+        if (it->second.device == t->device && block_ready(it->second)) {
+            *p = it->second.p;
+            g_mem_free.erase(it);
+            g_mem_live[*p] = {c, t->device};
+            return ST_OK;
         }
-        g_live[a] = bytes;
+    hipError_t e = hipMalloc(p, c);
+    if (e == hipErrorOutOfMemory) {   // give cached blocks back: the ready ones, then all after a device sync
+        (void)hipGetLastError();
+        mem_release_locked(t->device, false);
+        e = hipMalloc(p, c);
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();
+            (void)hipDeviceSynchronize();
+            mem_release_locked(t->device, true);
+            e = hipMalloc(p, c);
+        }
     }
     if (e != hipSuccess) {
-        g_err = std::string("hipMallocAsync: ") + hipGetErrorString(e);
+        *p = nullptr;
+        (void)hipGetLastError();
+        g_err = std::string("hipMalloc: ") + hipGetErrorString(e);
         return e == hipErrorOutOfMemory ? ST_ENOMEM : ST_EDEVICE;
     }
+    g_mem_live[*p] = {c, t->device};
     return ST_OK;
 }
 template <typename T>
@@ -157,8 +210,31 @@ static int dalloc_t(st_tree *t, T **p, uint64_t count) {
     return dalloc(t, (void **)p, count * sizeof(T));
 }
 static void dfree(st_tree *t, void *p) {
-    if (p) g_live.erase((uintptr_t)p);
-    if (p) (void)hipFreeAsync(p, t->stream);
+    if (!p) return;
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    auto it = g_mem_live.find(p);
+    if (it == g_mem_live.end()) return;   // not ours (never happens)
+    g_mem_free.emplace(it->second.first, MemBlock{p, it->second.first, it->second.second, t,
+                                                 t->sync_epoch.load(std::memory_order_relaxed)});
+    g_mem_live.erase(it);
+}
+// A tree's pending frees are safe once its stream is idle (st_destroy).
+static void mem_forget_owner(const st_tree *t) {
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    for (auto &kv : g_mem_free)
+        if (kv.second.owner == t) kv.second.owner = nullptr;
+}
+
+// Host synchronisation of a tree's stream; it also makes the blocks the tree
+// freed before it reusable.
+static int tsync(st_tree *t) {
+    const hipError_t e = hipStreamSynchronize(t->stream);
+    if (e != hipSuccess) {
+        g_err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
+        return ST_EDEVICE;
+    }
+    t->sync_epoch.fetch_add(1, std::memory_order_release);
+    return ST_OK;
 }
 
 // Stream-ordered scratch buffers freed when the scope ends, on every return
@@ -241,8 +317,7 @@ static void csr_install(st_tree *t, const CsrSet &o) {
     old.kheap = t->kheap; old.vheap = t->vheap;
     old.cap_n = t->cap_n; old.cap_k = t->cap_k; old.cap_v = t->cap_v;
     csr_free(t, t->spare);
-    static const int nospare = getenv("ST_NO_SPARE") ? atoi(getenv("ST_NO_SPARE")) : 0;   // diagnostic
-    if (!nospare && old.cap_n * 16 + old.cap_k + old.cap_v >= CSR_KEEP_SPARE) t->spare = old; else csr_free(t, old);
+    if (old.cap_n * 16 + old.cap_k + old.cap_v >= CSR_KEEP_SPARE) t->spare = old; else csr_free(t, old);
     t->seg_off = o.seg_off; t->seg_voff = o.seg_voff; t->koff = o.koff; t->voff = o.voff;
     t->kheap = o.kheap; t->vheap = o.vheap;
     t->cap_n = o.cap_n; t->cap_k = o.cap_k; t->cap_v = o.cap_v;
@@ -309,11 +384,6 @@ struct TimedLaunch {
     }
 };
 
-// diagnostic (ST_SYNC_LAUNCH=1): every launch waits for its kernel
-static int sync_launch() {
-    static const int v = getenv("ST_SYNC_LAUNCH") ? atoi(getenv("ST_SYNC_LAUNCH")) : 0;
-    return v;
-}
 #define LAUNCH(t, name, kern, grid, block, shmem, ...)                            \
     do {                                                                          \
         TimedLaunch tl_(t, name);                                                 \
@@ -323,7 +393,6 @@ static int sync_launch() {
             g_err = std::string("launch ") + name + ": " + hipGetErrorString(e_); \
             return ST_EDEVICE;                                                    \
         }                                                                         \
-        if (sync_launch()) HIPCHK(hipStreamSynchronize((t)->stream));            \
     } while (0)
 
 // Wait for a device-written flag in host-mapped memory (the kernel writes it
@@ -342,7 +411,7 @@ static int wait_mapped(st_tree *t, volatile uint32_t *flag, uint32_t want = 0) {
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
         __builtin_ia32_pause();
     }
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -439,28 +508,13 @@ static int exclusive_scan(st_tree *t, const T *in, T *out, uint64_t n) {
     dfree(t, part);
     if (e != hipSuccess) { g_err = std::string("scan launch: ") + hipGetErrorString(e); r = ST_EDEVICE; }
     if (r) return r;
-    static const int chk = getenv("ST_OV_CHECK") ? atoi(getenv("ST_OV_CHECK")) : 0;
-    if (chk & 64) {   // diagnostic: the device scan against a host scan
-        std::vector<T> hi(n), ho(n);
-        HIPCHK(hipStreamSynchronize(t->stream));
-        HIPCHK(hipMemcpy(hi.data(), in, n * sizeof(T), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(ho.data(), out, n * sizeof(T), hipMemcpyDeviceToHost));
-        T acc(0);
-        uint64_t bad = 0, first = ~0ull;
-        for (uint64_t i = 0; i < n; i++) {
-            if (memcmp(&acc, &ho[i], sizeof(T))) { if (!bad++) first = i; }
-            acc = acc + hi[i];
-        }
-        if (bad) fprintf(stderr, "scan_check: %llu of %llu outputs differ (first %llu), element %zu bytes\n",
-                         (unsigned long long)bad, (unsigned long long)n, (unsigned long long)first, sizeof(T));
-    }
     return ST_OK;
 }
 
 static int d2h(st_tree *t, void *dst, const void *src, uint64_t bytes) {
     if (!bytes) return ST_OK;
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 static int h2d(st_tree *t, void *dst, const void *src, uint64_t bytes) {
@@ -526,14 +580,6 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
         st_destroy(t);
         return ST_EDEVICE;
     }
-    {
-        // keep freed pool memory cached (no release to the OS at every sync)
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-            uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
-    }
     if ((r = dalloc_t(t, &t->md5, t->nslots)) || (r = dalloc_t(t, &t->tag, t->nslots)) ||
         (r = dalloc_t(t, &t->mark, t->nslots)) || (r = dalloc_t(t, &t->ok, t->nslots)) ||
         (r = dalloc_t(t, &t->flag, 4)) || (r = dalloc_t(t, &t->cnt64, 2)) ||
@@ -563,6 +609,7 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
 extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
                   t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
@@ -575,22 +622,23 @@ extern "C" void st_destroy(st_tree *t) {
     dfree(t, t->ov.used);
     if (t->pin) (void)hipHostFree(t->pin);
     if (t->sout) (void)hipHostFree(t->sout);
+    if (t->sreq) (void)hipHostFree(t->sreq);
     if (t->cw.res) (void)hipHostFree(t->cw.res);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
-    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    mem_forget_owner(t);   // the stream was idle: the blocks freed above have no pending use
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
     delete t;
 }
 
 extern "C" int st_set_stream(st_tree *t, void *s) {
     CHK(use_device(t));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     t->stream = s ? (hipStream_t)s : t->own_stream;
     return ST_OK;
 }
 
 extern "C" int st_sync(st_tree *t) {
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -605,7 +653,7 @@ extern "C" int st_set_timing(st_tree *t, int enabled) {
 }
 
 extern "C" int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *total_ms) {
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     for (auto &p : t->pending) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, p.a, p.b);
@@ -731,7 +779,7 @@ static int ensure_tiles(st_tree *t) {
     CHK(exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1));
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     if (total + 1 > t->tiles_cap) {
         dfree(t, t->tiles);
         t->tiles = nullptr;
@@ -836,7 +884,7 @@ static int rehash_tiled(st_tree *t) {
                (const TreeTiles *)nullptr, 0u, root0, lmin, st);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipStreamSynchronize(t->stream));
+        CHK(tsync(t));
         uint64_t t0 = ~0ull;
         for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 32]);
         if (const char *dump = getenv("ST_STAMP_DUMP")) {   // raw per-window stamps (ticks from t0)
@@ -944,36 +992,15 @@ struct IngestIn {
     uint64_t n_rejected;
 };
 
-static int ov_check_level() {
-    static const int v = getenv("ST_OV_CHECK") ? atoi(getenv("ST_OV_CHECK")) : 0;
-    return v;
-}
-
 static int ingest(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
     in.n_rejected = 0;
     if (n == 0) return ST_OK;
-    if ((ov_check_level() & 512) && t->csr_copy.size() == S + 1) {   // diagnostic: seg_off unchanged since installed?
-        std::vector<uint64_t> now(S + 1);
-        HIPCHK(hipStreamSynchronize(t->stream));
-        HIPCHK(hipMemcpy(now.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
-        uint64_t diff = 0, first = ~0ull, last = 0;
-        for (uint64_t s = 0; s <= S; s++)
-            if (now[s] != t->csr_copy[s]) { diff++; if (first == ~0ull) first = s; last = s; }
-        if (diff) {
-            fprintf(stderr, "csr_check: seg_off changed since install at %llu of %llu words, %llu..%llu (%p)\n",
-                    (unsigned long long)diff, (unsigned long long)(S + 1), (unsigned long long)first, (unsigned long long)last,
-                    (void *)t->seg_off);
-            for (uint64_t s = first; s <= last && s < first + 6; s++)
-                fprintf(stderr, "  [%llu] was %llu now %llx\n", (unsigned long long)s, (unsigned long long)t->csr_copy[s],
-                        (unsigned long long)now[s]);
-        }
-    }
     DevTree d = view(t);
     Scratch sc(t);
     uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr, *mpos = nullptr;
     uint64_t *bseg_off = nullptr;
-    uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr, *nkheap = nullptr, *nvheap = nullptr;
+    uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr;
     CHK(sc.alloc(&seg, n));
     CHK(sc.alloc(&sseg, n));
     CHK(sc.alloc(&idx, n));
@@ -1071,76 +1098,9 @@ static int ingest(st_tree *t, IngestIn &in) {
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
-    if ((ov_check_level() & 1024) && !in.bop && !in.seg_replace && S <= (1u << 22)) {
-        // diagnostic: per-segment entry counts of the merge against a host replay
-        // (old keys U kept batch keys of the segment; PUT-only batches)
-        HIPCHK(hipStreamSynchronize(t->stream));
-        const uint64_t on = t->csr_n_dbg;
-        std::vector<uint64_t> oso(S + 1), nso(S + 1), oko(on + 1), bko(n + 1);
-        std::vector<uint32_t> bseg(n);
-        std::vector<uint8_t> rj(reject ? S : 0);
-        HIPCHK(hipMemcpy(oso.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(nso.data(), out.o.seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
-        const uint64_t on2 = oso[S];
-        oko.resize(on2 + 1);
-        HIPCHK(hipMemcpy(oko.data(), t->koff, (on2 + 1) * 8, hipMemcpyDeviceToHost));
-        std::vector<uint8_t> okh(oko[on2]);
-        if (oko[on2]) HIPCHK(hipMemcpy(okh.data(), t->kheap, oko[on2], hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(bko.data(), in.koff, (n + 1) * 8, hipMemcpyDeviceToHost));
-        std::vector<uint8_t> bkh(bko[n]);
-        HIPCHK(hipMemcpy(bkh.data(), in.krec, bko[n], hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(bseg.data(), seg, n * 4, hipMemcpyDeviceToHost));
-        if (reject) HIPCHK(hipMemcpy(rj.data(), reject, S, hipMemcpyDeviceToHost));
-        std::map<uint64_t, std::vector<std::string>> add;
-        for (uint64_t i = 0; i < n; i++)
-            add[bseg[i]].push_back(std::string((const char *)bkh.data() + bko[i], bko[i + 1] - bko[i]));
-        uint64_t bad = 0, exp_total = 0, rejected = 0;
-        for (uint64_t s = 0; s < S; s++) {
-            uint64_t c = oso[s + 1] - oso[s];
-            auto it = add.find(s);
-            if (it != add.end()) {
-                if (reject && rj[s]) { rejected++; }
-                else {
-                    std::vector<std::string> keys;
-                    for (uint64_t e = oso[s]; e < oso[s + 1]; e++)
-                        keys.push_back(std::string((const char *)okh.data() + oko[e], oko[e + 1] - oko[e]));
-                    for (auto &k : it->second) keys.push_back(k);
-                    std::sort(keys.begin(), keys.end());
-                    c = std::unique(keys.begin(), keys.end()) - keys.begin();
-                }
-            }
-            exp_total += c;
-            const uint64_t got = nso[s + 1] - nso[s];
-            if (got != c && bad++ < 6)
-                fprintf(stderr, "merge_check: segment %llu: %llu entries, expected %llu (old %llu, batch run %d)\n",
-                        (unsigned long long)s, (unsigned long long)got, (unsigned long long)c,
-                        (unsigned long long)(oso[s + 1] - oso[s]), it != add.end() ? 1 : 0);
-        }
-        if (bad || exp_total != n_new || nso[S] != n_new)
-            fprintf(stderr, "merge_check: n %llu: %llu segments differ, expected total %llu, n_new %llu, new seg_off[S] %llu, old %llu (%llu), rejected runs %llu\n",
-                    (unsigned long long)n, (unsigned long long)bad, (unsigned long long)exp_total, (unsigned long long)n_new,
-                    (unsigned long long)nso[S], (unsigned long long)on2, (unsigned long long)on, (unsigned long long)rejected);
-    }
-    if (ov_check_level() & 128) {
-        uint64_t so_s = 0, so_0 = 0;
-        HIPCHK(hipStreamSynchronize(t->stream));
-        HIPCHK(hipMemcpy(&so_s, out.o.seg_off + S, 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&so_0, out.o.seg_off, 8, hipMemcpyDeviceToHost));
-        fprintf(stderr, "ingest_check: n %llu n_new %llu tot_k %llu tot_v %llu new seg_off[0] %llu seg_off[S] %llu new %p old %p\n",
-                (unsigned long long)n, (unsigned long long)n_new, (unsigned long long)tot_k, (unsigned long long)tot_v,
-                (unsigned long long)so_0, (unsigned long long)so_s, (void *)out.o.seg_off, (void *)t->seg_off);
-    }
     // swap in the new CSR (the old one becomes the spare set, in stream order)
     out.install();
     t->n = n_new; t->kbytes = tot_k; t->vbytes = tot_v;
-    t->csr_n_dbg = n_new;
-    if (ov_check_level() & 512) {
-        t->csr_copy.resize(S + 1);
-        HIPCHK(hipStreamSynchronize(t->stream));
-        HIPCHK(hipMemcpy(t->csr_copy.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
-        if (t->csr_copy[S] != n_new) fprintf(stderr, "csr_check: new seg_off[S] %llu != %llu\n",
-                                             (unsigned long long)t->csr_copy[S], (unsigned long long)n_new);
-    }
     t->perm_valid = false;
     // the hash-ready tiles are stale now; the next full rehash rebuilds them
     // (streaming batches never pay for a tile rebuild they do not use)
@@ -1162,35 +1122,8 @@ static int ingest(st_tree *t, IngestIn &in) {
 // records become one ingest batch with replace flags (their hashes are already
 // in the slot arrays, so nothing is rehashed).  Every entry point that reads
 // segments other than the small kernels calls this first.
-// Diagnostic (ST_OV_CHECK=1): the overlay index's live entries, checked
-// against the heap fill level; returns the number of live entries.
-static uint64_t ov_check(st_tree *t, const char *where) {
-    const uint64_t S = t->S;
-    std::vector<uint64_t> idx(S);
-    uint64_t used = 0;
-    (void)hipStreamSynchronize(t->stream);
-    (void)hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost);
-    uint64_t live = 0, wild = 0, first = ~0ull, last = 0;
-    for (uint64_t s = 0; s < S; s++) {
-        if (idx[s] == ~0ull) continue;
-        live++;
-        if (idx[s] >= used) {
-            wild++;
-            if (first == ~0ull) first = s;
-            last = s;
-        }
-    }
-    if (wild) fprintf(stderr, "ov_check %s: live %llu, beyond used (%llu): %llu in segments %llu..%llu (e.g. %llx)\n", where,
-                      (unsigned long long)live, (unsigned long long)used, (unsigned long long)wild,
-                      (unsigned long long)first, (unsigned long long)last, (unsigned long long)idx[first]);
-    return live;
-}
-
 static int flush_overlay(st_tree *t) {
     if (!t->ov_pending) return ST_OK;
-    if (ov_check_level() & 8) (void)hipStreamSynchronize(t->stream);
-    if (ov_check_level() & 1) ov_check(t, "flush");
     const uint64_t S = t->S;
     Scratch sc(t);
     uint64_t *cnt = nullptr, *kbs = nullptr, *vbs = nullptr, *eoff = nullptr, *ko0 = nullptr, *vo0 = nullptr;
@@ -1203,32 +1136,14 @@ static int flush_overlay(st_tree *t) {
     CHK(sc.alloc(&vo0, S + 1));
     CHK(sc.alloc(&rep, S));
     LAUNCH(t, "ov_flush", k_ov_sizes, grid_for(S + 1), 256, 0, t->ov, S, cnt, kbs, vbs, rep);
-    std::vector<uint8_t> rep_h;
-    if (ov_check_level() & 2) {
-        rep_h.resize(S);
-        HIPCHK(hipStreamSynchronize(t->stream));
-        HIPCHK(hipMemcpy(rep_h.data(), rep, S, hipMemcpyDeviceToHost));
-    }
     CHK(exclusive_scan<uint64_t>(t, cnt, eoff, S + 1));
     CHK(exclusive_scan<uint64_t>(t, kbs, ko0, S + 1));
     CHK(exclusive_scan<uint64_t>(t, vbs, vo0, S + 1));
-    uint64_t *aud = nullptr;
-    if (ov_check_level() & 256) {   // diagnostic, no extra host sync: audited with the sizes read-back
-        CHK(sc.alloc(&aud, 4));
-        HIPCHK(hipMemsetAsync(aud, 0, 32, t->stream));
-        HIPCHK(hipMemsetAsync(aud + 1, 0xff, 8, t->stream));
-        LAUNCH(t, "ov_audit", k_ov_audit, grid_for(S), 256, 0, t->ov, S, (unsigned long long *)aud);
-        HIPCHK(hipMemcpyAsync(t->pin + 3, aud, 32, hipMemcpyDeviceToHost, t->stream));
-    }
     HIPCHK(hipMemcpyAsync(t->pin, eoff + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 1, ko0 + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 2, vo0 + S, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     const uint64_t n = t->pin[0], kt = t->pin[1], vt = t->pin[2];
-    if (aud && t->pin[3])
-        fprintf(stderr, "ov_audit: %llu implausible overlay entries, segments %llu..%llu (e.g. offset %llx)\n",
-                (unsigned long long)t->pin[3], (unsigned long long)t->pin[4], (unsigned long long)t->pin[5],
-                (unsigned long long)t->pin[6]);
     if (n) {
         uint8_t *krec = nullptr, *vh = nullptr;
         uint64_t *ko = nullptr, *vo = nullptr;
@@ -1243,103 +1158,14 @@ static int flush_overlay(st_tree *t) {
         LAUNCH(t, "ov_flush", k_ov_gather, grid_for(S), 256, 0, t->ov, S, (const uint64_t *)eoff, (const uint64_t *)ko0,
                (const uint64_t *)vo0, krec, ko, vh, vo, segs);
         LAUNCH(t, "ov_flush", k_ov_terminate, 1, 64, 0, n, (const uint64_t *)(ko0 + S), (const uint64_t *)(vo0 + S), ko, vo);
-        if (ov_check_level() & 16) {   // diagnostic: the gathered batch against the overlay records (host)
-            HIPCHK(hipStreamSynchronize(t->stream));
-            std::vector<uint64_t> idx(S), hko(n + 1), hvo(n + 1);
-            std::vector<uint32_t> hseg(n);
-            std::vector<uint8_t> hk(kt), hv(vt);
-            uint64_t used = 0;
-            HIPCHK(hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost));
-            std::vector<uint8_t> heap(used);
-            HIPCHK(hipMemcpy(heap.data(), t->ov.heap, used, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hko.data(), ko, (n + 1) * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hvo.data(), vo, (n + 1) * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hseg.data(), segs, n * 4, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hk.data(), krec, kt, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(hv.data(), vh, vt, hipMemcpyDeviceToHost));
-            uint64_t e = 0, kb = 0, vb = 0, bad = 0, recs = 0;
-            for (uint64_t s2 = 0; s2 < S; s2++) {
-                if (idx[s2] == ~0ull) continue;
-                recs++;
-                const uint32_t *h = reinterpret_cast<const uint32_t *>(heap.data() + idx[s2]);
-                const uint32_t m = h[0], kbn = h[1], vbn = h[2];
-                const uint32_t *rk = h + 4, *rv = h + 4 + (m + 1);
-                const uint8_t *kd = reinterpret_cast<const uint8_t *>(h + 4 + 2 * (m + 1)), *vd = kd + kbn;
-                for (uint32_t i = 0; i < m; i++, e++) {
-                    const bool ok = hseg[e] == s2 && hko[e] == kb + rk[i] && hvo[e] == vb + rv[i] &&
-                                    !memcmp(hk.data() + hko[e], kd + rk[i], rk[i + 1] - rk[i]) &&
-                                    !memcmp(hv.data() + hvo[e], vd + rv[i], rv[i + 1] - rv[i]);
-                    if (!ok && bad++ < 4)
-                        fprintf(stderr, "ov_check gather: entry %llu (segment %llu) differs: seg %u ko %llu/%llu vo %llu/%llu\n",
-                                (unsigned long long)e, (unsigned long long)s2, hseg[e], (unsigned long long)hko[e],
-                                (unsigned long long)(kb + rk[i]), (unsigned long long)hvo[e], (unsigned long long)(vb + rv[i]));
-                }
-                kb += kbn; vb += vbn;
-            }
-            fprintf(stderr, "ov_check gather: %llu records, %llu entries (n %llu), %llu differ\n", (unsigned long long)recs,
-                    (unsigned long long)e, (unsigned long long)n, (unsigned long long)bad);
-        }
-        const uint64_t nbefore = t->n;
         IngestIn in{};
         in.n = n; in.krec = krec; in.koff = ko; in.vheap = vh; in.voff = vo;
         in.seg_given = segs; in.seg_replace = rep; in.verify_rehash = false;
         CHK(ingest(t, in));
-        if (ov_check_level() & 32) {   // diagnostic: the merged CSR's overlay segments against the records
-            HIPCHK(hipStreamSynchronize(t->stream));
-            std::vector<uint64_t> idx(S), so(S + 1), cko(t->n + 1), cvo(t->n + 1);
-            uint64_t used = 0;
-            HIPCHK(hipMemcpy(idx.data(), t->ov.idx, S * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(&used, t->ov.used, 8, hipMemcpyDeviceToHost));
-            std::vector<uint8_t> heap(used), ck(t->kbytes), cv(t->vbytes);
-            HIPCHK(hipMemcpy(heap.data(), t->ov.heap, used, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(so.data(), t->seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(cko.data(), t->koff, (t->n + 1) * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(cvo.data(), t->voff, (t->n + 1) * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(ck.data(), t->kheap, t->kbytes, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(cv.data(), t->vheap, t->vbytes, hipMemcpyDeviceToHost));
-            uint64_t bad = 0, recs = 0;
-            for (uint64_t s2 = 0; s2 < S; s2++) {
-                if (idx[s2] == ~0ull) continue;
-                recs++;
-                const uint32_t *h = reinterpret_cast<const uint32_t *>(heap.data() + idx[s2]);
-                const uint32_t m = h[0], kbn = h[1];
-                const uint32_t *rk = h + 4, *rv = h + 4 + (m + 1);
-                const uint8_t *kd = reinterpret_cast<const uint8_t *>(h + 4 + 2 * (m + 1)), *vd = kd + kbn;
-                bool ok = so[s2 + 1] - so[s2] == m;
-                for (uint32_t i = 0; ok && i < m; i++) {
-                    const uint64_t e = so[s2] + i;
-                    ok = cko[e + 1] - cko[e] == rk[i + 1] - rk[i] && cvo[e + 1] - cvo[e] == rv[i + 1] - rv[i] &&
-                         !memcmp(ck.data() + cko[e], kd + rk[i], rk[i + 1] - rk[i]) &&
-                         !memcmp(cv.data() + cvo[e], vd + rv[i], rv[i + 1] - rv[i]);
-                }
-                if (!ok && bad++ < 4)
-                    fprintf(stderr, "ov_check merge: segment %llu: csr %llu entries, record %u\n", (unsigned long long)s2,
-                            (unsigned long long)(so[s2 + 1] - so[s2]), m);
-            }
-            fprintf(stderr, "ov_check merge: %llu records, %llu segments differ; n %llu kbytes %llu vbytes %llu so[S] %llu\n",
-                    (unsigned long long)recs, (unsigned long long)bad, (unsigned long long)t->n,
-                    (unsigned long long)t->kbytes, (unsigned long long)t->vbytes, (unsigned long long)so[S]);
-        }
-        if (ov_check_level() & 2) {   // the replace flags after the ingest's kernels: unchanged?
-            std::vector<uint8_t> r2(S);
-            HIPCHK(hipStreamSynchronize(t->stream));
-            HIPCHK(hipMemcpy(r2.data(), rep, S, hipMemcpyDeviceToHost));
-            uint64_t ones = 0, diff = 0, first = ~0ull, last = 0;
-            for (uint64_t s = 0; s < S; s++) {
-                ones += rep_h[s] != 0;
-                if (r2[s] != rep_h[s]) { diff++; if (first == ~0ull) first = s; last = s; }
-            }
-            if (diff) fprintf(stderr, "ov_check flush: replace flags %llu before, %llu changed during ingest (segments %llu..%llu)\n",
-                              (unsigned long long)ones, (unsigned long long)diff, (unsigned long long)first, (unsigned long long)last);
-            if (t->n != nbefore) fprintf(stderr, "ov_check flush: entries %llu -> %llu\n", (unsigned long long)nbefore, (unsigned long long)t->n);
-        }
-        (void)nbefore;
     }
     HIPCHK(hipMemsetAsync(t->ov.idx, 0xff, S * 8, t->stream));
     HIPCHK(hipMemsetAsync(t->ov.used, 0, 8, t->stream));
     t->ov_pending = false;
-    t->ov_live = 0;
     return ST_OK;
 }
 
@@ -1357,83 +1183,109 @@ static int ensure_small(st_tree *t) {
         t->ov.cap = cap;
     }
     if (!t->sout) {
-        // fine-grained (coherent) host memory: the GPU's writes bypass its
-        // L2, so no stale cached copy of an earlier call's line (with its
-        // done flag) can be written back over the host's reset, and the host
-        // sees the results in the order the kernel fences them
-        if (hipHostMalloc((void **)&t->sout, sizeof(SmallOut), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            t->sout = nullptr;
+        // fine-grained (coherent) host memory for the result block and the
+        // request slots: the GPU reads the request and writes the results
+        // across PCIe, nothing of either is cached in its L2
+        if (hipHostMalloc((void **)&t->sout, sizeof(SmallOut), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostMalloc((void **)&t->sreq, SMALL_SLOTS * sizeof(SmallReq), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess) {
             g_err = "hipHostMalloc (mapped) failed";
             return ST_EDEVICE;
         }
-        memset(t->sout, 0, sizeof(SmallOut));   // no stale sequence words
+        memset(t->sout, 0, sizeof(SmallOut));   // no valid record before the first call
+        memset(t->sreq, 0, SMALL_SLOTS * sizeof(SmallReq));
         HIPCHK(hipHostGetDevicePointer((void **)&t->sout_dev, t->sout, 0));
+        HIPCHK(hipHostGetDevicePointer((void **)&t->sreq_dev, t->sreq, 0));
     }
     return ST_OK;
 }
 
+// One validated 16-byte record of the result block (small_path.h): copied
+// out with volatile reads, valid iff it carries `seq` and its check word.
+static bool small_rec(const SmallOut *o, int i, uint32_t seq, uint32_t *w, uint32_t *x) {
+    const volatile uint32_t *r = reinterpret_cast<const volatile uint32_t *>(i < 0 ? &o->hdr : &o->rec[i]);
+    const uint32_t s0 = r[0], w0 = r[1], x0 = r[2], c0 = r[3];
+    if (s0 != seq || c0 != small_check(s0, w0, x0)) return false;
+    *w = w0;
+    *x = x0;
+    return true;
+}
+
+// All of a call's results present and consistent?  Fills t->sres.
+static bool small_collect(st_tree *t, uint32_t seq, uint32_t n, int op) {
+    SmallRes &r = t->sres;
+    uint32_t w, x;
+    if (!small_rec(t->sout, -1, seq, &w, &x)) return false;
+    r.retry = (w & 1u) != 0;
+    r.new_entries = w >> 1;
+    if (r.retry) return true;
+    r.voff[0] = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!small_rec(t->sout, (int)i, seq, &w, &x)) return false;
+        r.status[i] = (int32_t)(w & 0xffu);
+        r.clevel[i] = (w >> 8) & 0xffu;
+        const uint32_t vlen = w >> 16;
+        r.cbucket[i] = r.status[i] == ST_CORRUPTED ? x : 0;
+        r.voff[i + 1] = r.voff[i] + (op == 0 && r.status[i] == ST_OK ? vlen : 0);
+        if (op == 0 && r.status[i] == ST_OK) {   // the value bytes arrived too?
+            const volatile uint8_t *v = t->sout->vbytes + r.voff[i];
+            uint32_t h = FNV1A_INIT;
+            for (uint32_t b = 0; b < vlen; b++) h = fnv1a_step(h, v[b]);
+            if (h != x) return false;
+        }
+    }
+    return true;
+}
+
 // One get/2 (op 0) or insert/3 (op 1) batch through k_small when it fits:
-// returns ST_OK with *served = 1 and t->sout filled, or *served = 0 (the
-// caller takes the bulk path).  Host pointers, records packed by the caller.
+// returns ST_OK with *served = 1 and t->sres filled (get values in
+// t->sout->vbytes), or *served = 0 (the caller takes the bulk path).  Host
+// pointers, records packed by the caller.
 static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, const uint8_t *vheap, const uint64_t *voff,
                       int *served) {
     *served = 0;
     const uint64_t kbytes = hr.off[n];
     const uint64_t vbytes = op == 1 ? voff[n] - voff[0] : 0;
-    static const uint64_t maxn = getenv("ST_SMALL_MAXN") ? (uint64_t)atoi(getenv("ST_SMALL_MAXN")) : SB_MAX;
-    static const int small_ins = getenv("ST_SMALL_INSERT") ? atoi(getenv("ST_SMALL_INSERT")) : 1;   // diagnostic
-    if (op == 1 && !small_ins) return ST_OK;
-    if (n == 0 || n > SB_MAX || n > maxn || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
+    if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
         small_lds_bytes((uint32_t)t->W) > 160 * 1024)
         return ST_OK;
     CHK(ensure_small(t));
-    SmallIn in;
-    memset(&in, 0, sizeof(in));
+    if (++t->small_seq == 0) t->small_seq = 1;
+    const uint32_t seq = t->small_seq;
+    // the request slot (alternating, so a slot is never rewritten while the
+    // previous call's kernel could still be reading it)
+    SmallReq *rq = &t->sreq[seq % SMALL_SLOTS];
+    rq->t = view(t);
+    rq->ov = t->ov;
+    SmallIn &in = rq->in;
     in.n = (uint32_t)n;
     in.op = (uint32_t)op;
     static const int sdbg = getenv("ST_SMALL_STAMPS") ? atoi(getenv("ST_SMALL_STAMPS")) : 0;
     in.dbg = sdbg ? 1u : 0u;
+    in.seq = seq;
     for (uint64_t i = 0; i <= n; i++) in.koff[i] = (uint32_t)hr.off[i];
     memcpy(in.kb, hr.heap.data(), kbytes);
     if (op == 1) {
         for (uint64_t i = 0; i <= n; i++) in.voff[i] = (uint32_t)(voff[i] - voff[0]);
         memcpy(in.vb, vheap + voff[0], vbytes);
     }
-    if (++t->small_seq == 0) t->small_seq = 1;
-    in.seq = t->small_seq;
-    uint32_t in_sum = 0;
-    for (uint32_t i = 0; i < sizeof(SmallIn) / 4; i++) in_sum += small_in_word(in, i);
-    t->sout->pad = 0;
-    LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), view(t), t->ov, in, t->sout_dev, in_sum);
-    CHK(wait_mapped(t, &t->sout->done, in.seq));
-    if (t->sout->done != in.seq) { g_err = "small-batch kernel did not complete"; return ST_EDEVICE; }
-    // The call returns only once the kernel has fully retired (its stream is
-    // idle), not merely once its completion word is set: a following call
-    // that launched while this kernel was still retiring intermittently saw
-    // an inconsistent tree (test_small_path; tools/stress_small.py fails
-    // within ~6 trials without this and passed 30 with it).
-    static const int ssync = getenv("ST_SMALL_SYNC") ? atoi(getenv("ST_SMALL_SYNC")) : 1;
-    if (ssync == 1) {
-        HIPCHK(hipStreamSynchronize(t->stream));
-    } else if (ssync == 2) {
-        hipError_t q;
-        while ((q = hipStreamQuery(t->stream)) == hipErrorNotReady) __builtin_ia32_pause();
-        if (q != hipSuccess) { g_err = hipGetErrorString(q); return ST_EDEVICE; }
+    std::atomic_thread_fence(std::memory_order_release);   // the request is in memory before the launch
+    LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), (const SmallReq *)(t->sreq_dev + seq % SMALL_SLOTS),
+           t->sout_dev);
+    // spin on the result records; after 5 ms (a faulted or very slow kernel)
+    // a stream synchronisation, after which every write of the kernel is visible
+    bool ok = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; !(ok = small_collect(t, seq, (uint32_t)n, op)); i++) {
+        if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+        __builtin_ia32_pause();
     }
-    if (t->sout->pad == 0xBADu) {   // the kernel saw another argument block: the bulk path serves the call
-        static int warned = 0;
-        if (!warned++) fprintf(stderr, "synctree_hip: small-batch kernel argument block mismatch (seq %u); bulk path\n", in.seq);
-        t->small_torn++;
-        return ST_OK;
+    if (!ok) {
+        CHK(tsync(t));
+        if (!small_collect(t, seq, (uint32_t)n, op)) { g_err = "small-batch kernel results incomplete"; return ST_EDEVICE; }
     }
-    if (!t->sout->retry)
-        for (uint64_t i = 0; i < n; i++) {
-            if (sdbg && __atomic_load_n(&t->sout->sseq[i], __ATOMIC_ACQUIRE) != in.seq)
-                fprintf(stderr, "small: key %llu result word behind done (seq %u)\n", (unsigned long long)i, in.seq);
-            CHK(wait_mapped(t, &t->sout->sseq[i], in.seq));
-            if (t->sout->sseq[i] != in.seq) { g_err = "small-batch results incomplete"; return ST_EDEVICE; }
-        }
     if (sdbg) {   // diagnostic: phase times (µs from kernel start) to stderr
+        CHK(tsync(t));
         const uint64_t *st = t->sout->stamp;
         fprintf(stderr, "small op=%d n=%llu:", op, (unsigned long long)n);
         for (int k = 1; k < 8; k++)
@@ -1441,16 +1293,10 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
         fprintf(stderr, "\n");
         memset((void *)t->sout->stamp, 0, sizeof(t->sout->stamp));
     }
-    if (ov_check_level() & 4) {
-        const uint64_t live = ov_check(t, "small");
-        if (live > t->ov_live + n) fprintf(stderr, "ov_check small: live entries %llu -> %llu after a call of %llu keys\n",
-                                           (unsigned long long)t->ov_live, (unsigned long long)live, (unsigned long long)n);
-        t->ov_live = live;
-    }
-    if (t->sout->retry) return ST_OK;
+    if (t->sres.retry) return ST_OK;
     *served = 1;
     if (op == 1) {
-        t->n += t->sout->new_entries;
+        t->n += t->sres.new_entries;
         t->ov_pending = true;
         t->fresh = false;
         t->tiles_valid = false;
@@ -1468,7 +1314,7 @@ static int upload_records(st_tree *t, uint64_t n, const uint8_t *ktype, const ui
     CHK(dalloc_t(t, d_koff, n + 1));
     CHK(h2d(t, *d_krec, hr.heap.data(), hr.heap.size()));
     CHK(h2d(t, *d_koff, hr.off.data(), (n + 1) * 8));
-    HIPCHK(hipStreamSynchronize(t->stream));   // host vectors die here
+    CHK(tsync(t));   // host vectors die here
     return ST_OK;
 }
 
@@ -1482,7 +1328,7 @@ static int upload_values(st_tree *t, uint64_t n, const uint8_t *vheap, const uin
     CHK(h2d(t, *d_vheap, vheap + voff[0], vb));
     HIPCHK(hipMemsetAsync(*d_vheap + vb, 0, HEAP_SLACK, t->stream));
     CHK(h2d(t, *d_voff, vo.data(), (n + 1) * 8));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -1498,9 +1344,9 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
         CHK(small_call(t, 1, n, hr, vheap, voff, &served));
         if (served) {
             for (uint64_t i = 0; i < n; i++) {
-                if (status) status[i] = t->sout->status[i];
-                if (clevel) clevel[i] = t->sout->clevel[i];
-                if (cbucket) cbucket[i] = t->sout->cbucket[i];
+                if (status) status[i] = t->sres.status[i];
+                if (clevel) clevel[i] = t->sres.clevel[i];
+                if (cbucket) cbucket[i] = t->sres.cbucket[i];
             }
             return ST_OK;
         }
@@ -1533,7 +1379,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
             }
     }
     dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, dcl); dfree(t, dseg);
-    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (!r) CHK(tsync(t));
     return r;
 }
 
@@ -1585,7 +1431,7 @@ extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, cons
         if (!r) *n_corrupted = t->pin[0];
     }
     dfree(t, tk); dfree(t, tv); dfree(t, krec); dfree(t, dko); dfree(t, dvo); dfree(t, dcl);
-    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (!r) CHK(tsync(t));
     return r;
 }
 
@@ -1614,7 +1460,7 @@ extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
         if (hipGetLastError() != hipSuccess) { g_err = "launch erec_emptied"; r = ST_EDEVICE; }
     }
     dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, bop);
-    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (!r) CHK(tsync(t));
     return r;
 }
 
@@ -1670,7 +1516,7 @@ extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const 
         (void)hipMemsetAsync(rep, 0, t->S, t->stream);
         (void)hipMemsetAsync(rep + segment, 1, 1, t->stream);
         if (!r) {
-            HIPCHK(hipStreamSynchronize(t->stream));
+            CHK(tsync(t));
             IngestIn in{};
             in.n = nn; in.krec = krec; in.koff = dko; in.vheap = dv; in.voff = dvo;
             in.seg_given = dseg; in.seg_replace = rep; in.bop = bop;
@@ -1680,7 +1526,7 @@ extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const 
     }
     dfree(t, krec); dfree(t, dko); dfree(t, dv); dfree(t, dvo); dfree(t, dseg); dfree(t, rep); dfree(t, bop);
     if (!r) r = set_erec(t, t->base[t->H + 1] + segment, n == 0 ? 1 : 0);
-    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (!r) CHK(tsync(t));
     return r;
 }
 
@@ -1712,7 +1558,7 @@ extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint3
     CHK(h2d(t, t->tag + c0, tags.data(), t->W * 2));
     CHK(h2d(t, t->md5 + c0, md.data(), t->W * 16));
     CHK(set_erec(t, t->base[level] + bucket, n == 0 ? 1 : 0));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     t->fresh = false;
     return ST_OK;
 }
@@ -1722,7 +1568,7 @@ extern "C" int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket) {
     if (level == t->H + 1) CHK(st_store_segment(t, bucket, 0, nullptr, nullptr, nullptr, nullptr, nullptr));
     else CHK(st_store_inner(t, level, bucket, 0, nullptr, nullptr));
     CHK(set_erec(t, t->base[level] + bucket, 0));   // no record at all
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -1737,7 +1583,7 @@ extern "C" int st_store_top(st_tree *t, const uint8_t *hash17, int also_record) 
         CHK(h2d(t, t->tag, &tg, 2));
         CHK(h2d(t, t->md5, &m, 16));
     }
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     t->fresh = false;
     return ST_OK;
 }
@@ -1749,7 +1595,7 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
     if (hash17) set_entry_host(tg, m, hash17);
     CHK(h2d(t, t->tag, &tg, 2));
     CHK(h2d(t, t->md5, &m, 16));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     if (hash17) t->fresh = false;
     return ST_OK;
 }
@@ -1792,7 +1638,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
         CHK(flush_overlay(trees[i]));
         CHK(ensure_tiles(trees[i]));
         CHK(ensure_lvl_cnt(trees[i]));
-        HIPCHK(hipStreamSynchronize(trees[i]->stream));
+        CHK(tsync(trees[i]));
     }
     // every window of every tree in ONE launch of the fused kernel (K1 +
     // levels + top per tree): the trees' tails overlap each other's K1
@@ -1807,10 +1653,10 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
     LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
            (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     for (uint32_t i = 0; i < n; i++) {
         CHK(erec_after_rehash(trees[i]));
-        HIPCHK(hipStreamSynchronize(trees[i]->stream));
+        CHK(tsync(trees[i]));
         trees[i]->fresh = false;
     }
     return ST_OK;
@@ -1853,7 +1699,7 @@ extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
     uint4 m;
     HIPCHK(hipMemcpyAsync(&tg, t->tag, 2, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&m, t->md5, 16, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     *present = (tg & TAG_PRESENT) ? 1 : 0;
     if (*present) entry_to_h17(tg, m, out17);
     return ST_OK;
@@ -1889,7 +1735,7 @@ extern "C" int st_combine_upper(st_tree *t, const uint8_t *present16, const uint
     CHK(h2d(t, t->md5 + t->base[2], m, sizeof(m)));
     DevTree d = view(t);
     LAUNCH(t, "level_rehash", k_upper16, 1, 256, (size_t)256 * lane_region_bytes(16), d, 1u, 1u, (const uint8_t *)nullptr);
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     t->fresh = false;
     return ST_OK;
 }
@@ -1902,7 +1748,7 @@ extern "C" int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, ui
     std::vector<uint4> m(n);
     HIPCHK(hipMemcpyAsync(tg.data(), t->tag + t->base[level], n * 2, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(m.data(), t->md5 + t->base[level], n * 16, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     for (uint64_t i = 0; i < n; i++) {
         present[i] = (tg[i] & TAG_PRESENT) ? 1 : 0;
         if (present[i]) entry_to_h17(tg[i], m[i], hashes17 + 17 * i);
@@ -1956,7 +1802,7 @@ static int fetch_entries(st_tree *t, const uint64_t *d_idx, uint64_t n, st_resul
     res->aheap = (uint8_t *)malloc(vb + 1);
     if (kb) HIPCHK(hipMemcpyAsync(res->kheap, kh, kb, hipMemcpyDeviceToHost, t->stream));
     CHK(d2h(t, res->aheap, vh, vb));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     (void)keys;
     return ST_OK;
 }
@@ -2023,14 +1869,14 @@ extern "C" int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_
     CHK(small_call(t, 0, 1, hr, nullptr, nullptr, &served));
     int32_t st;
     if (served) {
-        const SmallOut *so = t->sout;
-        st = so->status[0];
-        *clevel = so->clevel[0];
-        *cbucket = so->cbucket[0];
-        *vlen = so->voff[1];
+        const SmallRes &so = t->sres;
+        st = so.status[0];
+        *clevel = so.clevel[0];
+        *cbucket = so.cbucket[0];
+        *vlen = so.voff[1];
         if (st == ST_OK) {
             if (*vlen > vcap) { g_err = "value longer than the buffer"; return ST_EINVAL; }
-            memcpy(vout, so->vbytes, *vlen);
+            memcpy(vout, t->sout->vbytes, *vlen);
         }
         return st;
     }
@@ -2071,22 +1917,22 @@ extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const 
         int served = 0;
         CHK(small_call(t, 0, n, hr, nullptr, nullptr, &served));
         if (served) {
-            const SmallOut *so = t->sout;
+            const SmallRes &so = t->sres;
             st_result *res = new_result(n);
             res->n_entries = n;
             res->koff = (uint64_t *)calloc(n + 1, 8);
             res->aoff = (uint64_t *)calloc(n + 1, 8);
             res->ktype = (uint8_t *)calloc(n + 1, 1);
             res->kheap = (uint8_t *)malloc(1);
-            res->aheap = (uint8_t *)malloc(so->voff[n] + 1);
+            res->aheap = (uint8_t *)malloc(so.voff[n] + 1);
             for (uint64_t i = 0; i < n; i++) {
-                res->status[i] = so->status[i];
-                res->clevel[i] = so->clevel[i];
-                res->cbucket[i] = so->cbucket[i];
+                res->status[i] = so.status[i];
+                res->clevel[i] = so.clevel[i];
+                res->cbucket[i] = so.cbucket[i];
                 res->eoff[i + 1] = i + 1;
-                res->aoff[i + 1] = so->voff[i + 1];
+                res->aoff[i + 1] = so.voff[i + 1];
             }
-            memcpy(res->aheap, so->vbytes, so->voff[n]);
+            memcpy(res->aheap, t->sout->vbytes, so.voff[n]);
             *out = res;
             return ST_OK;
         }
@@ -2166,7 +2012,7 @@ extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const 
     }
     dfree(t, krec); dfree(t, dko); dfree(t, seg); dfree(t, tg64); dfree(t, pst); dfree(t, found);
     if (r) { st_free_result(res); return r; }
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     *out = res;
     return ST_OK;
 }
@@ -2274,7 +2120,7 @@ static int node_images(st_tree *t, uint32_t level, uint64_t n, const uint64_t *b
     }
     dfree(t, dt); dfree(t, pst); dfree(t, tg); dfree(t, md); dfree(t, cnt); dfree(t, eo); dfree(t, idx);
     if (r) { st_free_result(res); return r; }
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     *out = res;
     return ST_OK;
 }
@@ -2294,7 +2140,7 @@ extern "C" int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint
         uint4 m;
         HIPCHK(hipMemcpyAsync(&tg, t->tag + 1, 2, hipMemcpyDeviceToHost, t->stream));
         HIPCHK(hipMemcpyAsync(&m, t->md5 + 1, 16, hipMemcpyDeviceToHost, t->stream));
-        HIPCHK(hipStreamSynchronize(t->stream));
+        CHK(tsync(t));
         const uint64_t e = (tg & TAG_PRESENT) ? 1 : 0;
         res->child = (uint64_t *)calloc(n + 1, 8);
         res->hash17 = (uint8_t *)calloc(n + 1, 17);
@@ -2393,7 +2239,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         return ST_EINVAL;
     }
     st_tree *t = A;   // work is enqueued on the local tree's stream
-    if (B->stream != A->stream) HIPCHK(hipStreamSynchronize(B->stream));
+    if (B->stream != A->stream) CHK(tsync(B));
     CHK(ensure_cmp_work(t));
     CmpWork &w = t->cw;
     CHK(grow_records(t, 4096, 64));
@@ -2418,7 +2264,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 8);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
-            HIPCHK(hipStreamSynchronize(t->stream));
+            CHK(tsync(t));
             uint64_t t0 = ~0ull;
             for (uint32_t x = 0; x < w.nw; x++) t0 = std::min(t0, h[x * 8]);
             static const char *nm[8] = {"start", "levels", "children", "verify", "merge", "end", "", "staged"};
@@ -2515,7 +2361,7 @@ static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *
     HIPCHK(hipMemcpyAsync(t->pin + 1, ko + n, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 2, vo + n, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(t->pin + 3, fb, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     const uint64_t m = t->pin[0], kb = t->pin[1], vb = t->pin[2];
     *crashed = t->pin[3] != ~0ull ? 1 : 0;
     if (!apply) {
@@ -2541,7 +2387,7 @@ static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *
         *n_rejected = rej;
         *n_applied = m - rej;
     }
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -2633,7 +2479,7 @@ extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_
     std::vector<uint64_t> wb(w.nw);
     HIPCHK(hipMemcpyAsync(st.data(), w.wst, st.size() * 4, hipMemcpyDeviceToHost, local->stream));
     HIPCHK(hipMemcpyAsync(wb.data(), w.wbytes, wb.size() * 8, hipMemcpyDeviceToHost, local->stream));
-    HIPCHK(hipStreamSynchronize(local->stream));
+    CHK(tsync(local));
     const uint32_t L1 = local->H + 1;
     for (uint32_t l = 0; l < max_levels; l++) {
         uint64_t v = 0;
@@ -2679,7 +2525,7 @@ extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
     std::vector<TreeTiles> h(n);
     for (uint32_t i = 0; i < n; i++) {
         if (trees[i]->device != t->device) { g_err = "trees on different devices"; return ST_EINVAL; }
-        if (trees[i]->stream != t->stream) HIPCHK(hipStreamSynchronize(trees[i]->stream));
+        if (trees[i]->stream != t->stream) CHK(tsync(trees[i]));
         h[i] = tree_tiles(trees[i]);
     }
     Scratch sc(t);
@@ -2687,7 +2533,7 @@ extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
     CHK(sc.alloc(&dtt, n));
     HIPCHK(hipMemcpyAsync(dtt, h.data(), n * sizeof(TreeTiles), hipMemcpyHostToDevice, t->stream));
     LAUNCH(t, "tops_out", k_tops_out, grid_for((uint64_t)n * 18), 256, 0, (const TreeTiles *)dtt, n, (uint8_t *)out);
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     return ST_OK;
 }
 
@@ -2729,7 +2575,7 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
     HIPCHK(hipMemcpyAsync(&tot[0], rank + R, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&tot[1], ko + R, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&tot[2], vo + R, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     const uint64_t n = tot[0];
     if ((r = dalloc_t(t, okoff, n + 1)) || (r = dalloc_t(t, ovoff, n + 1)) || (r = dalloc(t, (void **)kout, tot[1] + 16)) ||
         (r = dalloc(t, (void **)vout, tot[2] + 16))) { done(); return r; }
@@ -2739,7 +2585,7 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
                    (const uint64_t *)eo, *vout);
     HIPCHK(hipMemcpyAsync(*okoff + n, &tot[1], 8, hipMemcpyHostToDevice, t->stream));
     HIPCHK(hipMemcpyAsync(*ovoff + n, &tot[2], 8, hipMemcpyHostToDevice, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     done();
     *n_out = n;
     return ST_OK;
@@ -2784,7 +2630,7 @@ extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, ui
     uint8_t *kout = nullptr, *vout = nullptr;
     int r = snapshot_device(t, tree_id, id_len, &n, &okoff, &kout, &ovoff, &vout, tot);
     dfree(t, okoff); dfree(t, ovoff); dfree(t, kout); dfree(t, vout);
-    if (!r) HIPCHK(hipStreamSynchronize(t->stream));
+    if (!r) CHK(tsync(t));
     if (n_records) *n_records = n;
     if (key_bytes) *key_bytes = tot[1];
     if (value_bytes) *value_bytes = tot[2];
@@ -2864,7 +2710,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     HIPCHK(hipMemcpyAsync(&tot[0], nso + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&tot[1], kbase + S, 8, hipMemcpyDeviceToHost, t->stream));
     HIPCHK(hipMemcpyAsync(&tot[2], vbase + S, 8, hipMemcpyDeviceToHost, t->stream));
-    HIPCHK(hipStreamSynchronize(t->stream));
+    CHK(tsync(t));
     const uint64_t ne = tot[0], kb = tot[1], vb = tot[2];
     RCHK(dalloc_t(t, &nko, ne + 1)); RCHK(dalloc_t(t, &nvo, ne + 1)); RCHK(dalloc_t(t, &nsvo, S + 1));
     RCHK(dalloc(t, (void **)&nkh, kb + HEAP_SLACK)); RCHK(dalloc(t, (void **)&nvh, vb + HEAP_SLACK));
@@ -2894,7 +2740,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     t->tiles_valid = false;
     t->fresh = false;
     done(true);
-    HIPCHK(hipStreamSynchronize(t->stream));   // the caller's buffers may go after return
+    CHK(tsync(t));   // the caller's buffers may go after return
 #undef RCHK
     if (n_loaded) *n_loaded = hc[RST_LOADED];
     if (n_skipped) *n_skipped = hc[RST_SKIPPED];

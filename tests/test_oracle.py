@@ -329,3 +329,32 @@ def test_rehash_par_equals_rehash():
     top = t.top_hash()
     t.rehash_par(4)
     assert t.top_hash() == top and t.verify()
+
+
+def test_parallel_oracle_forms_equal_the_literal_ones():
+    """ot_bulk_load_int64_par == ot_bulk_load_int64, and ot_apply_int64_batch
+    on a consistent tree == sequential insert/3 calls (oracle/synctree_oracle.c),
+    including duplicate keys inside a batch (last writer wins)."""
+    import oracle_c as C
+    from riak_ensemble_amd import workload
+    for W, S in ((16, 1 << 20), (4, 4096), (16, 16)):
+        n = 30000 if S > 4096 else 2000
+        k = (workload.splitmix64(11, n) & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)
+        k[5] = k[9]
+        v = workload.obj_hash_values(n)
+        a = C.OTree(W, S).bulk_load_int64(k, v)
+        b = C.OTree(W, S).bulk_load_int64_par(k, v, 4)
+        assert a.top_hash() == b.top_hash() and a.num_entries() == b.num_entries()
+        for j in range(3):
+            bk = np.concatenate([k[j::7][:n // 10],
+                                 (workload.splitmix64(20 + j, n // 10) & np.uint64(0x7FFFFFFFFFFFFFFF)).astype(np.int64)])
+            bk[3] = bk[1]
+            bv = workload.obj_hash_values(len(bk), epoch=2 + j)
+            assert a.insert_int64_seq(bk, bv) == 0
+            b.apply_int64_batch(bk, bv, 4)
+            assert a.top_hash() == b.top_hash(), (W, S, j)
+            assert a.num_entries() == b.num_entries()
+        for lvl in range(1, a.height + 2):
+            pa, ha = a.level_entries(lvl)
+            pb, hb = b.level_entries(lvl)
+            assert (pa == pb).all() and (ha == hb).all()
