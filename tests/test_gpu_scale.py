@@ -7,12 +7,13 @@ C-ABI, against the C restatement (oracle/, the checker only).
   bumped (test/synctree_intercepts.erl:96-104) plus keys only the remote tree
   holds; the full ordered diff list equals the oracle's compare/3
   (synctree.erl:372-417, Keys ++ Acc order), for every filter.
-* config 5: a 10M-key tree partitioned by segment range over G = 2, 4, 8
+* config 5: a 100M-key tree partitioned by segment range over G = 1, 2, 4, 8
   partitions taking 1M-key write batches (50 % overwrites, 50 % new keys);
   the combined top hash and the owned level entries equal sequential oracle
   inserts (synctree.erl:189-209).
-* config 4: a group of 64 ensembles x 1M keys rehashed as one device batch;
-  every tree's top hash and upper levels equal the oracle's.
+* config 4: a group of 512 ensembles x 1M keys (one GPU's share of 4096)
+  rehashed as one device batch; every tree's top hash and a sample's upper
+  levels equal the oracle's.
 
 Inputs: splitmix64 keys masked to 63 bits (riak_ensemble_amd/workload.py),
 17-byte ObjHash values <<0, Epoch:64, Seq:64>> (riak_ensemble_peer.erl:1717-1724).
@@ -128,32 +129,49 @@ def _combine(parts):
 
 
 @pytest.mark.gpu
-def test_config5_partitioned_streaming_10m():
+def test_config5_partitioned_streaming_100m():
+    """BASELINE config 5 at its size: a 100M-key tree partitioned by segment
+    range over G = 1, 2, 4, 8 partitions (one process here; the same
+    st_set_partition + level-2 all-gather + st_combine_upper path as the
+    G-rank run), two 1M-key write batches (50 % overwrites, 50 % new keys)
+    through the insert path with its dirty-path rehash; after every batch
+    the combined top hash equals the oracle's sequential inserts
+    (ot_apply_int64_batch, pinned against insert_int64_seq in test_oracle),
+    and at the end every partition's owned level-2/3/6 entries and a full
+    rehash agree."""
+    import torch
     import oracle_c as C
     from riak_ensemble_amd import synctree_hip, parallel
+    N = 100_000_000
     seed = 0x5EED0005
-    keys = _keys(seed, N10M)
-    vals = workload.obj_hash_values(N10M)
+    keys = _keys(seed, N)
+    vals = workload.obj_hash_values(N)
     rng = np.random.default_rng(5)
     batches = []
     B = 1_000_000
     for j in range(2):
-        old = rng.integers(0, N10M, B // 2)
-        k = np.concatenate([keys[old], _keys(seed, B - B // 2, N10M + j * B)])
-        seq = np.concatenate([old + 1, np.arange(N10M + j * B, N10M + j * B + (B - B // 2))]).astype(np.uint64)
+        old = rng.integers(0, N, B // 2)
+        k = np.concatenate([keys[old], _keys(seed, B - B // 2, N + j * B)])
+        seq = np.concatenate([old + 1, np.arange(N + j * B, N + j * B + (B - B // 2))]).astype(np.uint64)
         v = np.zeros((B, 17), np.uint8)
         v[:, 8] = 1
         v[:, 9:17] = seq.astype('>u8').view(np.uint8).reshape(B, 8)
         batches.append((k, v))
-    ora = C.OTree().bulk_load_int64(keys, vals)
-    tops = []
+    ora = C.OTree().bulk_load_int64_par(keys, vals)
+    tops, lv = [], {}
     for k, v in batches:
-        assert ora.insert_int64_seq(k, v) == 0
+        ora.apply_int64_batch(k, v)
         tops.append(ora.top_hash())
-    for G in (2, 4, 8):
+    for lvl in (2, 3, 6):
+        lv[lvl] = ora.level_entries(lvl)
+    del ora
+    kd = torch.from_numpy(keys).cuda()
+    vd = torch.from_numpy(vals.reshape(-1)).cuda()
+    for G in (1, 2, 4, 8):
         parts = [parallel.PartitionedTree(synctree_hip.DeviceTree(), _Local(r, G)) for r in range(G)]
         for p in parts:
-            assert p.tree.insert_int64(keys, vals) == 0
+            assert p.tree.insert_int64_device(kd.data_ptr(), vd.data_ptr(), N, 17) == 0
+        torch.cuda.synchronize()
         _combine(parts)
         for j, (k, v) in enumerate(batches):
             for p in parts:
@@ -163,12 +181,11 @@ def test_config5_partitioned_streaming_10m():
         for p in parts:
             for lvl in (2, 3, 6):
                 pa, ha = p.tree.level_entries(lvl)
-                pb, hb = ora.level_entries(lvl)
+                pb, hb = lv[lvl]
                 m = len(pa) // G
                 sl = slice(p.rank * m, (p.rank + 1) * m)
                 assert (pa[sl] == pb[sl]).all() and (ha[sl] == hb[sl]).all(), 'G=%d level %d' % (G, lvl)
-        # a full rehash of every partition reproduces the same top hash
-        for p in parts:
+        for p in parts:     # a full rehash of every partition reproduces the same top hash
             p.tree.rehash()
         _combine(parts)
         assert all(p.top_hash() == tops[-1] for p in parts)
@@ -177,17 +194,22 @@ def test_config5_partitioned_streaming_10m():
 
 
 @pytest.mark.gpu
-def test_config4_group_64_ensembles_1m():
+def test_config4_group_512_ensembles_1m():
+    """BASELINE config 4's per-GPU share at its size: 512 ensembles x 1M keys
+    (4096 over 8 GPUs) rehashed as ONE device batch (st_rehash_group); every
+    tree's top hash equals the oracle's, the upper levels of a sample too."""
     import oracle_c as C
     from riak_ensemble_amd import synctree_hip
-    E, n = 64, 1_000_000
+    E, n = 512, 1_000_000
     vals = workload.obj_hash_values(n)
 
     def oracle(e):
-        o = C.OTree().bulk_load_int64(_keys(SEED ^ (e + 1), n), vals)
-        return o.top_hash(), o.level_entries(2), o.level_entries(3)
+        o = C.OTree().bulk_load_int64_par(_keys(SEED ^ (e + 1), n), vals, 1)
+        r = (o.top_hash(), o.level_entries(2) if e % 64 == 0 else None, o.level_entries(3) if e % 64 == 0 else None)
+        del o
+        return r
 
-    with cf.ThreadPoolExecutor(8) as ex:
+    with cf.ThreadPoolExecutor(16) as ex:
         fut = [ex.submit(oracle, e) for e in range(E)]
         trees = []
         for e in range(E):
@@ -196,11 +218,12 @@ def test_config4_group_64_ensembles_1m():
             trees.append(t)
         exp = [f.result() for f in fut]
     synctree_hip.rehash_group(trees)
-    for t, (top, l2, l3) in zip(trees, exp):
-        assert t.top_hash() == top
-        for lvl, (pb, hb) in ((2, l2), (3, l3)):
-            pa, ha = t.level_entries(lvl)
-            assert (pa == pb).all() and (ha == hb).all()
+    for e, (t, (top, l2, l3)) in enumerate(zip(trees, exp)):
+        assert t.top_hash() == top, 'ensemble %d' % e
+        if l2 is not None:
+            for lvl, (pb, hb) in ((2, l2), (3, l3)):
+                pa, ha = t.level_entries(lvl)
+                assert (pa == pb).all() and (ha == hb).all()
     # per-tree rehash agrees with the batch
     for t in trees[:4]:
         t.rehash()
