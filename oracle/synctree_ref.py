@@ -185,13 +185,19 @@ def orddict_store(key, value, d):
 
 
 def orddict_erase(key, d):
-    return [(k, v) for k, v in d if k != key or type(k) is not type(key)]
+    """orddict:erase/2 (stdlib): drops the entry whose key == Key (so 1 and
+    1.0 are one key, like orddict:store above)."""
+    tk = term_key(key)
+    return [(k, v) for k, v in d if term_key(k) != tk]
 
 
 def orddict_find(key, default, d):
-    """synctree.erl:342-348 (lists:keyfind => exact match)."""
+    """synctree.erl:342-348: lists:keyfind(Key, 1, L) -- the first tuple
+    whose key compares EQUAL (==, the keyfind BIF's CMP_EQ: an integer Key
+    also finds an equal float key, and vice versa)."""
+    tk = term_key(key)
     for k, v in d:
-        if k == key and type(k) is type(key):
+        if term_key(k) == tk:
             return v
     return default
 

@@ -28,6 +28,7 @@
 #define SB_OUT_VB 4096   // value bytes a small get returns
 #define SB_SEG_CAP 1024  // entries of one segment a small insert rewrites (larger: bulk path)
 #define SB_VERIFY 96     // threads that verify path nodes (SB_MAX keys x 6 levels)
+#define SB_GVAL 128      // get: value bytes per key prefetched into LDS (longer: read at the end)
 
 struct SmallIn {
     uint32_t n, op;       // op: 0 = get/2, 1 = insert/3
@@ -185,12 +186,12 @@ __device__ __forceinline__ bool verify_segment_ov(const DevTree &t, const Overla
     const uint64_t slot = t.base[L] + s;
     const uint64_t eslot = (L == 1) ? 0 : slot;
     const uint16_t et = t.tag[eslot];
+    const uint4 e = t.md5[eslot];   // loaded up front, with the segment's offsets
     const SegView v = seg_view(t, ov, s);
     if (!(et & TAG_PRESENT)) return v.n == 0;
     uint32_t d[4];
     const uint64_t a = v.voff(0);
     stmd5::md5_global_pf(v.vh + a, v.voff(v.n) - a, d);
-    const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
 }
 
@@ -226,10 +227,30 @@ __host__ __device__ __forceinline__ uint32_t small_lds_bytes(uint32_t W) {
 #define SB_STAMPW(k) do { if (in.dbg && (threadIdx.x & 63) == 0) out->stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define S1_VBUF 4096   // value bytes of a segment hashed from LDS (larger: bulk path)
 #define S1_PATH 192    // path child entries (H x W <= 192 for W <= 32, S <= 2^31)
+// LDS flags between the waves of the one-key insert (workgroup scope)
+__device__ __forceinline__ void lds_flag_set(uint32_t *f) {
+    __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_wait(uint32_t *f) {
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+}
+// exclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t v = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += y;
+    }
+    return v - x;
+}
+
+#define S1_NEW 0x80000000u
 __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay &ov, const SmallIn &in, SmallOut *out, uint8_t *dyn,
                                  const uint8_t *kb, const uint8_t *vb, uint64_t s, uint32_t *bad) {
     __shared__ uint64_t s1_off;
-    __shared__ uint32_t s1_news, s1_retry, s1_n, s1_kb, s1_vb;
+    __shared__ uint32_t s1_news, s1_retry, s1_n, s1_kb, s1_vb, s1_plan_ready, s1_pre_ready;
     __shared__ uint4 s1_new[ST_MAXLEV + 2];    // new entry per level (H+1 = the segment)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t H = t.H, L1 = H + 1, W = t.W;
@@ -241,11 +262,15 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
     uint8_t *regs = vbuf + S1_VBUF + 64;                               // H x lane_region_bytes(W)
     __shared__ uint32_t s1_pre[ST_MAXLEV + 2][4];                      // per level: prefix state
     __shared__ uint32_t s1_p[ST_MAXLEV + 2], s1_len[ST_MAXLEV + 2];     // changed entry's offset, length
+    // the merged entry list (source entry or S1_NEW, key / value offsets in the new record)
     uint32_t *plan = reinterpret_cast<uint32_t *>(dyn + SB_VERIFY * lane_region_bytes(W)) + 2 * 3 * (SB_SEG_CAP + SB_MAX);
     uint32_t *pk = plan + (SB_SEG_CAP + SB_MAX), *pv = pk + (SB_SEG_CAP + SB_MAX);
-    if (tid == 0) { s1_retry = 0; s1_news = 0; }
+    if (tid == 0) { s1_retry = 0; s1_news = 0; s1_plan_ready = 0; s1_pre_ready = 0; }
     __syncthreads();
     SB_STAMP(1);
+    const uint8_t *k = kb + in.koff[0];
+    const uint64_t kl = in.koff[1] - in.koff[0];
+    const uint32_t vl = in.voff[1] - in.voff[0];
     if (wave == 0) {
         if (lane < L1) {   // path verification, level lane + 1
             const uint32_t l = lane + 1;
@@ -255,8 +280,11 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
             if (!good) atomicMin(&bad[0], l);
         }
         if (lane == 0 && in.dbg) out->stamp[2] = __builtin_amdgcn_s_memrealtime();
-    } else if (wave == 2) {
-        // path nodes' child entries: level l node b_l, children base[l+1] + b_l*W + j
+    } else if (wave == 1) {
+        // path nodes' child entries (level l node b_l, children base[l+1] +
+        // b_l*W + j); lanes 1..H: level `lane`'s node message with the path
+        // child's entry as a placeholder, and the MD5 state over the blocks
+        // before that entry (they do not depend on the new hashes below it)
         for (uint32_t x = lane; x < H * W; x += 64) {
             const uint32_t l = x / W + 1, j = x % W;
             const uint64_t bl = s >> (t.shift * (L1 - l));
@@ -264,111 +292,151 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
             pe[x] = t.md5[c];
             pt[x] = t.tag[c];
         }
-        const SegView v = seg_view(t, ov, s);
-        const uint8_t *k = kb + in.koff[0];
-        const uint64_t kl = in.koff[1] - in.koff[0];
-        const uint32_t vl = in.voff[1] - in.voff[0];
-        if (lane == 0) {   // the merged entry list: old entries, the key replaced or inserted
-            bool eq;
-            const uint64_t pos = seg_lower_bound(v, k, kl, &eq);
-            uint64_t out_n = 0, kbytes = 0, vbytes = 0;
-            bool fits = v.n + 1 <= SB_SEG_CAP;
-            for (uint64_t x = 0; x < v.n + 1 && fits; x++) {
-                uint32_t src, a, b;
-                if (x < pos) { src = (uint32_t)x; a = (uint32_t)v.klen(x); b = (uint32_t)v.vlen(x); }
-                else if (x == pos) { src = 0x80000000u; a = (uint32_t)kl; b = vl; }
-                else {
-                    const uint64_t y = eq ? x : x - 1;
-                    if (y >= v.n) break;
-                    src = (uint32_t)y; a = (uint32_t)v.klen(y); b = (uint32_t)v.vlen(y);
-                }
-                plan[out_n] = src; pk[out_n] = a; pv[out_n] = b;
-                kbytes += a; vbytes += b; out_n++;
+        wave_sync_lds();
+        if (lane >= 1 && lane <= H) {
+            const uint32_t l = lane;
+            const uint32_t j = (uint32_t)((s >> (t.shift * (L1 - (l + 1)))) % W);
+            uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
+            MsgWriter mw;
+            mw.init(reg);
+            uint32_t before = 0;
+            for (uint32_t q = 0; q < W; q++) {
+                const bool pres = q == j || (pt[(l - 1) * W + q] & TAG_PRESENT);
+                if (!pres) continue;
+                if (q < j) before++;
+                mw.entry(q == j ? (uint32_t)TAG_PRESENT : pt[(l - 1) * W + q], pe[(l - 1) * W + q]);
             }
-            if (!fits || vbytes > S1_VBUF) {
-                s1_retry = 1;
-            } else {
-                const uint64_t bytes = ov_record_bytes(out_n, kbytes, vbytes);
-                const uint64_t off = atomicAdd(ov.used, (unsigned long long)bytes);
-                if (off + bytes > ov.cap) s1_retry = 1;
-                s1_off = off;
-                s1_n = (uint32_t)out_n; s1_kb = (uint32_t)kbytes; s1_vb = (uint32_t)vbytes;
-                s1_news = eq ? 0 : 1;
-                if (!s1_retry) {   // header and offset tables
-                    uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + off);
-                    uint32_t *ko = h + 4, *vo = h + 4 + (out_n + 1);
-                    h[0] = (uint32_t)out_n; h[1] = (uint32_t)kbytes; h[2] = (uint32_t)vbytes; h[3] = 0;
-                    uint32_t a = 0, c = 0;
-                    for (uint32_t q = 0; q < out_n; q++) {   // lengths -> offsets (LDS and the record)
-                        const uint32_t kq = pk[q], vq = pv[q];
-                        ko[q] = a; vo[q] = c; pk[q] = a; pv[q] = c;
-                        a += kq; c += vq;
-                    }
-                    ko[out_n] = a; vo[out_n] = c; pk[out_n] = a; pv[out_n] = c;
-                }
-            }
+            const uint32_t len = mw.finish();
+            s1_p[l] = 17 * before;
+            s1_len[l] = len;
+            uint32_t st[4];
+            stmd5::md5_lds_prefix(reg, (17 * before) / 64, st);
+            s1_pre[l][0] = st[0]; s1_pre[l][1] = st[1]; s1_pre[l][2] = st[2]; s1_pre[l][3] = st[3];
         }
         wave_sync_lds();
-        if (!s1_retry) {   // entry bytes, lane per entry; values also into the LDS copy
-            uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + s1_off);
-            const uint32_t m = s1_n;
-            uint8_t *kd = reinterpret_cast<uint8_t *>(h + 4 + 2 * (m + 1));
-            uint8_t *vd = kd + s1_kb;
-            for (uint32_t q = lane; q < m; q += 64) {
-                const uint32_t src = plan[q];
-                const uint8_t *ks, *vs;
-                if (src & 0x80000000u) { ks = k; vs = vb + in.voff[0]; }
-                else { ks = v.key(src); vs = v.val(src); }
-                const uint32_t kq = pk[q + 1] - pk[q], vq = pv[q + 1] - pv[q];
-                for (uint32_t b = 0; b < kq; b++) kd[pk[q] + b] = ks[b];
-                for (uint32_t b = 0; b < vq; b++) { const uint8_t c = vs[b]; vd[pv[q] + b] = c; vbuf[pv[q] + b] = c; }
+        if (lane == 0) lds_flag_set(&s1_pre_ready);
+    } else if (wave == 2) {
+        // the merged entry list (orddict:store, synctree.erl:206) and the new
+        // segment's values in LDS; then the new segment hash and the path
+        // bottom-up (update_path, :201-209) on lane 0
+        const SegView v = seg_view(t, ov, s);
+        const uint64_t n = v.n;
+        if (n < 64) {   // a lane per old entry: lower_bound by ballot, offsets by prefix sums
+            uint32_t kli = 0, vli = 0;
+            int c = 1;
+            if (lane < n) {
+                kli = (uint32_t)v.klen(lane);
+                vli = (uint32_t)v.vlen(lane);
+                c = rec_cmp(v.key(lane), kli, k, kl);
             }
-                wave_sync_lds();
-            if (lane == 0 && in.dbg) out->stamp[3] = __builtin_amdgcn_s_memrealtime();
-            // lanes 1..H: level `lane`'s node message with the path child's
-            // entry as a placeholder, and the MD5 state over the blocks before
-            // that entry (they do not depend on the new hashes below it)
-            if (lane >= 1 && lane <= H) {
-                const uint32_t l = lane;
-                const uint32_t j = (uint32_t)((s >> (t.shift * (L1 - (l + 1)))) % W);
-                uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
-                MsgWriter mw;
-                mw.init(reg);
-                uint32_t before = 0;
-                for (uint32_t q = 0; q < W; q++) {
-                    const bool pres = q == j || (pt[(l - 1) * W + q] & TAG_PRESENT);
-                    if (!pres) continue;
-                    if (q < j) before++;
-                    mw.entry(q == j ? (uint32_t)TAG_PRESENT : pt[(l - 1) * W + q], pe[(l - 1) * W + q]);
-                }
-                const uint32_t len = mw.finish();
-                s1_p[l] = 17 * before;
-                s1_len[l] = len;
-                uint32_t st[4];
-                stmd5::md5_lds_prefix(reg, (17 * before) / 64, st);
-                s1_pre[l][0] = st[0]; s1_pre[l][1] = st[1]; s1_pre[l][2] = st[2]; s1_pre[l][3] = st[3];
+            const uint32_t pos = (uint32_t)__popcll(__ballot(lane < n && c < 0));
+            const bool eq = __ballot(lane < n && c == 0) != 0;
+            const uint32_t out_n = (uint32_t)n + (eq ? 0u : 1u);
+            const bool act = lane < out_n;
+            const uint32_t src = lane < pos ? lane : (lane == pos ? S1_NEW : (eq ? lane : lane - 1));
+            const uint32_t sk = __shfl(kli, (int)(src & 63), 64), sv = __shfl(vli, (int)(src & 63), 64);
+            const uint32_t a = !act ? 0u : (src == S1_NEW ? (uint32_t)kl : sk);
+            const uint32_t b = !act ? 0u : (src == S1_NEW ? vl : sv);
+            const uint32_t pa = wave_excl_sum(a), pb = wave_excl_sum(b);
+            const uint32_t ta = __shfl(pa + a, 63, 64), tb = __shfl(pb + b, 63, 64);
+            if (act) { plan[lane] = src; pk[lane] = pa; pv[lane] = pb; }
+            if (lane == 0) {
+                pk[out_n] = ta; pv[out_n] = tb;
+                s1_n = out_n; s1_kb = ta; s1_vb = tb;
+                s1_news = eq ? 0 : 1;
+                if (tb > S1_VBUF) s1_retry = 1;
             }
-            if (lane == 0) {   // the new segment hash (in parallel with the prefixes)
-                uint32_t d[4];
-                stmd5::md5_lds(vbuf, s1_vb, d);
-                s1_new[L1] = make_uint4(d[0], d[1], d[2], d[3]);
+            if (act && tb <= S1_VBUF) {
+                const uint8_t *vs = src == S1_NEW ? vb + in.voff[0] : v.val(src);
+                for (uint32_t q = 0; q < b; q++) vbuf[pb + q] = vs[q];
             }
             wave_sync_lds();
-            if (lane == 0) {   // the path bottom-up: patch the child's entry, resume each node's MD5
-                uint4 e = s1_new[L1];
-                for (uint32_t l = H; l >= 1; l--) {
-                    uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
-                    uint8_t *q = reg + s1_p[l];
-                    q[0] = 0;   // ?H_MD5
-                    const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
-#pragma unroll
-                    for (int b = 0; b < 16; b++) q[1 + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
-                    uint32_t d[4];
-                    stmd5::md5_lds_resume(reg, s1_len[l], s1_p[l] / 64, s1_pre[l], d);
-                    e = make_uint4(d[0], d[1], d[2], d[3]);
-                    s1_new[l] = e;
+        } else {        // larger segments: lane 0 walks the list
+            if (lane == 0) {
+                bool eq;
+                const uint64_t pos = seg_lower_bound(v, k, kl, &eq);
+                uint64_t out_n = 0, kbytes = 0, vbytes = 0;
+                bool fits = n + 1 <= SB_SEG_CAP;
+                for (uint64_t x = 0; x < n + 1 && fits; x++) {
+                    uint32_t src, a, b;
+                    if (x < pos) { src = (uint32_t)x; a = (uint32_t)v.klen(x); b = (uint32_t)v.vlen(x); }
+                    else if (x == pos) { src = S1_NEW; a = (uint32_t)kl; b = vl; }
+                    else {
+                        const uint64_t y = eq ? x : x - 1;
+                        if (y >= n) break;
+                        src = (uint32_t)y; a = (uint32_t)v.klen(y); b = (uint32_t)v.vlen(y);
+                    }
+                    plan[out_n] = src; pk[out_n] = (uint32_t)kbytes; pv[out_n] = (uint32_t)vbytes;
+                    kbytes += a; vbytes += b; out_n++;
                 }
-                if (in.dbg) out->stamp[4] = __builtin_amdgcn_s_memrealtime();
+                pk[out_n] = (uint32_t)kbytes; pv[out_n] = (uint32_t)vbytes;
+                s1_n = (uint32_t)out_n; s1_kb = (uint32_t)kbytes; s1_vb = (uint32_t)vbytes;
+                s1_news = eq ? 0 : 1;
+                if (!fits || vbytes > S1_VBUF) s1_retry = 1;
+            }
+            wave_sync_lds();
+            if (!s1_retry)
+                for (uint32_t q = lane; q < s1_n; q += 64) {
+                    const uint32_t src = plan[q];
+                    const uint8_t *vs = src == S1_NEW ? vb + in.voff[0] : v.val(src);
+                    for (uint32_t b = pv[q]; b < pv[q + 1]; b++) vbuf[b] = vs[b - pv[q]];
+                }
+            wave_sync_lds();
+        }
+        if (lane == 0) lds_flag_set(&s1_plan_ready);
+        if (lane == 0 && in.dbg) out->stamp[3] = __builtin_amdgcn_s_memrealtime();
+        if (!s1_retry && lane == 0) {
+            uint32_t d[4];
+            stmd5::md5_lds(vbuf, s1_vb, d);   // the new segment hash
+            uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
+            s1_new[L1] = e;
+            lds_flag_wait(&s1_pre_ready);
+            for (uint32_t l = H; l >= 1; l--) {   // patch the child's entry, resume each node's MD5
+                uint8_t *reg = regs + (l - 1) * lane_region_bytes(W);
+                uint8_t *q = reg + s1_p[l];
+                q[0] = 0;   // ?H_MD5
+                const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+                for (int b = 0; b < 16; b++) q[1 + b] = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
+                stmd5::md5_lds_resume(reg, s1_len[l], s1_p[l] / 64, s1_pre[l], d);
+                e = make_uint4(d[0], d[1], d[2], d[3]);
+                s1_new[l] = e;
+            }
+            if (in.dbg) out->stamp[4] = __builtin_amdgcn_s_memrealtime();
+        }
+    } else {
+        // wave 3: the segment's new overlay record (header, offset tables,
+        // key and value bytes) while wave 2 hashes; committed only if the
+        // path verified
+        if (lane == 0) lds_flag_wait(&s1_plan_ready);
+        wave_sync_lds();
+        if (!s1_retry) {
+            const uint32_t m = s1_n, kbn = s1_kb, vbn = s1_vb;
+            uint64_t off = 0;
+            if (lane == 0) {
+                const uint64_t bytes = ov_record_bytes(m, kbn, vbn);
+                off = atomicAdd(ov.used, (unsigned long long)bytes);
+                if (off + bytes > ov.cap) s1_retry = 1;
+                else s1_off = off;
+            }
+            off = __shfl(off, 0, 64);
+            wave_sync_lds();
+            if (!s1_retry) {
+                uint32_t *h = reinterpret_cast<uint32_t *>(ov.heap + off);
+                uint32_t *ko = h + 4, *vo = h + 4 + (m + 1);
+                uint8_t *kd = reinterpret_cast<uint8_t *>(h + 4 + 2 * (m + 1));
+                uint8_t *vd = kd + kbn;
+                if (lane == 0) { h[0] = m; h[1] = kbn; h[2] = vbn; h[3] = 0; }
+                const SegView v = seg_view(t, ov, s);
+                for (uint32_t q = lane; q <= m; q += 64) {
+                    ko[q] = pk[q];
+                    vo[q] = pv[q];
+                    if (q == m) continue;
+                    const uint32_t src = plan[q];
+                    const uint8_t *ks = src == S1_NEW ? k : v.key(src);
+                    for (uint32_t b = pk[q]; b < pk[q + 1]; b++) kd[b] = ks[b - pk[q]];
+                    for (uint32_t b = pv[q]; b < pv[q + 1]; b++) vd[b] = vbuf[b];
+                }
             }
         }
     }
@@ -445,9 +513,10 @@ __global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *ou
     if (tid < SB_MAX) { bad[tid] = ~0u; keep[tid] = 0; }
     if (tid == 0) { ngrp = 0; nd = 0; retry = 0; }
     __syncthreads();
+    const uint16_t top_tag = t.tag[0];   // issued before the key hash: its latency hides under it
     if (tid < n) seg[tid] = record_segment(kb + in.koff[tid], in.koff[tid + 1] - in.koff[tid], t.S - 1);
     __syncthreads();
-    const bool undefined_top = (t.tag[0] & TAG_PRESENT) == 0;
+    const bool undefined_top = (top_tag & TAG_PRESENT) == 0;
     if (in.op == 0 && undefined_top) {   // get/2: undefined top => notfound (synctree.erl:216-218)
         if (tid < n) key_rec(out, tid, in.seq, ST_NOTFOUND, 0, 0, 0);
         __syncthreads();
@@ -472,14 +541,19 @@ __global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *ou
         else good = verify_inner_node(t, l, s >> (t.shift * (L1 - l)), dyn + tid * lane_region_bytes(t.W));
         if (!good) atomicMin(&bad[i], l);
     }
+    __shared__ uint8_t gval[SB_MAX][SB_GVAL];   // values found, prefetched while the paths verify
     if (in.op == 0 && tid >= 128 && tid < 128 + n) {   // orddict_find (synctree.erl:342-348)
         const uint32_t i = tid - 128;
         const SegView v = seg_view(t, ov, seg[i]);
         bool eq;
         const uint64_t at = seg_lower_bound(v, kb + in.koff[i], in.koff[i + 1] - in.koff[i], &eq);
+        const uint32_t len = eq ? (uint32_t)v.vlen(at) : 0;
+        const uint8_t *src = eq ? v.val(at) : nullptr;
         gfound[i] = eq ? 1 : 0;
-        glen[i] = eq ? (uint32_t)v.vlen(at) : 0;
-        gsrc[i] = eq ? v.val(at) : nullptr;
+        glen[i] = len;
+        gsrc[i] = src;
+        if (len <= SB_GVAL)
+            for (uint32_t b = 0; b < len; b++) gval[i][b] = src[b];
     }
     __syncthreads();
     SB_STAMP(2);
@@ -515,6 +589,7 @@ __global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *ou
         __syncthreads();
         if (tid < n && !retry) {   // this key's value bytes, then its record (with their FNV-1a)
             uint32_t h = FNV1A_INIT;
+            if (src && len <= SB_GVAL) src = gval[tid];   // the LDS copy
             if (src)
                 for (uint32_t b = 0; b < len; b++) {
                     const uint8_t c = src[b];

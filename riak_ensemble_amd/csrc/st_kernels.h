@@ -78,8 +78,21 @@ __host__ __device__ __forceinline__ void krec_seg_bytes(const uint8_t *p, uint64
 __device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
 
-// Erlang term order on key records: memcmp over the common prefix, then length.
-__device__ __forceinline__ int rec_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+// Bytes of a key record that decide its place in Erlang term order: the
+// whole plain record, or the SK part of a term record (term_key.h).  Two keys
+// whose SKs are equal are EQUAL keys (==): 1 and 1.0, {1} and {1.0} --
+// orddict:store/erase, lists:keyfind and orddict_delta compare with ==
+// (synctree.erl:206, :342-348; riak_ensemble_util.erl:120-125), so such keys
+// share one entry; the trailing ETF/Seg bytes only say which form is stored.
+__host__ __device__ __forceinline__ uint64_t krec_order_len(const uint8_t *p, uint64_t len) {
+    if (!krec_is_term(p, len)) return len;
+    const uint32_t el = (uint32_t)p[len - 4] | ((uint32_t)p[len - 3] << 8);
+    const uint32_t sl = (uint32_t)p[len - 2] | ((uint32_t)p[len - 1] << 8);
+    return len - 4 - el - (sl == 0xFFFF ? 0 : sl);
+}
+
+// Plain byte order: memcmp over the common prefix, then length.
+__device__ __forceinline__ int bytes_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
     uint64_t m = la < lb ? la : lb;
     uint64_t i = 0;
     for (; i + 8 <= m; i += 8) {
@@ -95,6 +108,11 @@ __device__ __forceinline__ int rec_cmp(const uint8_t *a, uint64_t la, const uint
     for (; i < m; i++)
         if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
     return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// Erlang term order (== for equality) on key records.
+__device__ __forceinline__ int rec_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    return bytes_cmp(a, krec_order_len(a, la), b, krec_order_len(b, lb));
 }
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
@@ -754,12 +772,14 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 __device__ __forceinline__ bool verify_inner_node(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
     const uint64_t slot = t.base[l] + b;
     const uint64_t eslot = (l == 1) ? 0 : slot;
-    const uint32_t len = stage_inner(t, l, b, reg);
+    // the parent's entry is loaded with the children (one round trip), not
+    // after the hash: the compare at the end waits for nothing
     const uint16_t et = t.tag[eslot];
+    const uint4 e = t.md5[eslot];
+    const uint32_t len = stage_inner(t, l, b, reg);
     if (!(et & TAG_PRESENT)) return len == 0;
     uint32_t d[4];
     stmd5::md5_lds(reg, len, d);
-    const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
 }
 
@@ -811,15 +831,20 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Erlang term order of two key records staged in LDS at arbitrary byte
-// offsets (byte reads: no unaligned wide LDS access).
-__device__ __forceinline__ int lds_rec_cmp(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+// Byte order of two strings staged in LDS at arbitrary byte offsets (byte
+// reads: no unaligned wide LDS access).
+__device__ __forceinline__ int lds_bytes_cmp(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
     const uint32_t m = la < lb ? la : lb;
     for (uint32_t i = 0; i < m; i++) {
         const uint32_t x = a[i], y = b[i];
         if (x != y) return x < y ? -1 : 1;
     }
     return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// Erlang term order of two key records staged in LDS
+__device__ __forceinline__ int lds_rec_cmp(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+    return lds_bytes_cmp(a, (uint32_t)krec_order_len(a, la), b, (uint32_t)krec_order_len(b, lb));
 }
 
 // lower_bound of key k in the n staged keys (LDS); *eq: equal key found
@@ -934,7 +959,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
                     rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
                     if (eq) {
                         if (vl) {
-                            emit = lds_rec_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
+                            emit = lds_bytes_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
                         } else {
                             const uint64_t x = a0 + i, y = b0 + rb;
                             emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],

@@ -712,6 +712,8 @@ static int pack_records(uint64_t n, const uint8_t *ktype, const uint8_t *kheap, 
 }
 
 static int host_rec_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+    la = krec_order_len(a, la);
+    lb = krec_order_len(b, lb);
     uint64_t m = la < lb ? la : lb;
     int c = m ? memcmp(a, b, m) : 0;
     if (c) return c < 0 ? -1 : 1;

@@ -17,9 +17,10 @@
 //
 //   0x0F  integer < -2^63   [0x0F][255 - n][~magnitude, n bytes BE]
 //   0x10  int64             [0x10][8 bytes BE, sign bit flipped]
-//         float in [-2^63, 2^63): [0x10][floor as above][0xFE][frac, 8 bytes]
+//         float in [-2^63, 2^63): [0x10][floor as above][0xFE][frac, 8 bytes],
+//         an integral float (frac 0) without the [0xFE][frac] part
 //   0x11  integer >= 2^63   [0x11][n][magnitude, n bytes BE]
-//         (floats beyond int64 are integral: their integer SK + [0xFE][0 x 8])
+//         (floats beyond int64 are integral: the SK of the equal integer)
 //   0x20  atom              [0x20][utf8, escaped][00 01]
 //   0x30  tuple             [0x30][arity u32 BE][SK(e1)]...[SK(en)]
 //   0x38  nil               [0x38]
@@ -31,9 +32,12 @@
 // Escaping (nested atoms / binaries only): 0x00 -> 00 FF, end -> 00 01.
 // ERTS type order: number < atom < (reference < fun < port < pid) < tuple <
 // (map) < nil < list < bitstring; the bracketed types are rejected.  Numbers
-// compare by value; an integer and a float of equal value (1 and 1.0) are
-// distinct keys here, ordered integer first (the reference's orddict would
-// merge them if they shared a segment: DESIGN.md §Key domain).
+// compare by value, and an integer and a float of equal value (1 and 1.0,
+// also nested: {1} and {1.0}) have the SAME SK: they are equal keys (==), as
+// orddict:store/erase, lists:keyfind and orddict_delta treat them; the key
+// comparison (krec_order_len in st_kernels.h) looks at the SK bytes only, and
+// a store of one form replaces an entry of the other (orddict:store keeps the
+// new key).
 #pragma once
 #include <algorithm>
 #include <cmath>
@@ -122,9 +126,9 @@ inline void sk_float(std::vector<uint8_t> &o, double v) {
         const uint64_t u = (uint64_t)fi ^ 0x8000000000000000ull;
         o.push_back(KEYTAG_INT);
         for (int i = 7; i >= 0; i--) o.push_back((uint8_t)(u >> (8 * i)));
+        if (r == 0.0) return;   // integral (and -0.0): the SK of the equal integer
         uint64_t bits;
         std::memcpy(&bits, &r, 8);
-        if (r == 0.0) bits = 0;   // -0.0
         o.push_back(SK_FLOAT);
         for (int i = 7; i >= 0; i--) o.push_back((uint8_t)(bits >> (8 * i)));
         return;
@@ -142,9 +146,7 @@ inline void sk_float(std::vector<uint8_t> &o, double v) {
     unsigned __int128 x = (unsigned __int128)carry << bits;
     while (x) { le.push_back((uint8_t)x); x >>= 8; }
     std::vector<uint8_t> mag(le.rbegin(), le.rend());
-    sk_integer(o, v < 0, mag);
-    o.push_back(SK_FLOAT);
-    for (int i = 0; i < 8; i++) o.push_back(0);
+    sk_integer(o, v < 0, mag);   // integral: the SK of the equal integer
 }
 
 // term -> SK; returns the ERTS type class of the term (for list tails), or -1

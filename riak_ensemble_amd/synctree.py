@@ -389,4 +389,4 @@ def orddict_delta(d1, d2):
 
 
 def _okey(k):
-    return terms.order_key(k)
+    return terms.order_sk(k)   # Erlang-equal keys (1, 1.0) compare equal

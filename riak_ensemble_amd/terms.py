@@ -181,6 +181,18 @@ def key_from_parts(kt, kb):
     return bytes(kb)
 
 
+def order_sk(key):
+    """The part of `key`'s device record that decides its order (krec_order_len
+    in csrc/st_kernels.h): Erlang-equal keys (1 and 1.0) have equal parts."""
+    r = order_key(key)
+    kt, _ = key_parts(key)
+    if kt != _lib.ST_KEY_TERM:
+        return r
+    el = r[-4] | (r[-3] << 8)
+    sl = r[-2] | (r[-1] << 8)
+    return r[:len(r) - 4 - el - (0 if sl == 0xFFFF else sl)]
+
+
 def order_key(key):
     """The device key record of `key` (bytes): their lexicographic order is
     Erlang term order (riak_ensemble_amd/csrc/term_key.h)."""

@@ -80,7 +80,6 @@ def test_key_record_order_is_erlang_term_order():
     no device) == Erlang term order of the restatement, for nested terms of
     every supported type, plain keys included."""
     ts = distinct_terms(3000, 2) + [0, -1, 1, 255, 256, 'a', b'a', (), [], [[]], {0: 1}.get(0), 1.5, -1.5]
-    # no two keys equal as Erlang numbers (1 vs 1.0 are distinct records here: DESIGN.md)
     uniq = {}
     for t in ts:
         uniq.setdefault(repr(R.term_key(t)), t)
@@ -89,6 +88,18 @@ def test_key_record_order_is_erlang_term_order():
     by_record = sorted(ts, key=terms.order_key)
     bad = [(a, b) for a, b in zip(by_erlang, by_record) if a != b or type(a) != type(b)]
     assert not bad, bad[:5]
+    # the order part (terms.order_sk) decides too, and Erlang-equal numbers
+    # (==: 1 and 1.0, nested or not, bignums and big integral floats, 0 and
+    # -0.0) have EQUAL order parts -- one key for orddict:store/erase,
+    # lists:keyfind and orddict_delta
+    assert sorted(ts, key=terms.order_sk) == by_record
+    eq_pairs = [(1, 1.0), (0, -0.0), (-7, -7.0), ((1, 'a'), (1.0, 'a')), ([2, [3]], [2.0, [3.0]]),
+                (1 << 70, float(1 << 70)), (-(1 << 80), -float(1 << 80)), ((1 << 63) - 1024, float((1 << 63) - 1024))]
+    for a, b in eq_pairs:
+        assert R.term_key(a) == R.term_key(b)
+        assert terms.order_sk(a) == terms.order_sk(b), (a, b)
+    for a, b in [(1, 1.5), (1.5, 2), ((1, 'a'), (1.5, 'a')), (-1, -0.5)]:
+        assert (terms.order_sk(a) < terms.order_sk(b)) == (R.term_key(a) < R.term_key(b)), (a, b)
     # plain-domain keys keep their short records
     assert terms.order_key(5) == bytes([0x10, 0x80, 0, 0, 0, 0, 0, 0, 5])
     assert terms.order_key('ab') == b'\x20ab'
@@ -158,5 +169,72 @@ def test_term_keys_device_parity(geom, n, batch):
     res = dev.compare(dev2)
     assert res[0] == 'ok'
     assert [(k, v) for _, k, v in res[1]] == R.local_compare(ref, ref2)
+    dev.close()
+    dev2.close()
+
+
+def _same_segment_pairs(S, want):
+    """(integer-form, float-form) key pairs that hash to one segment of S."""
+    out = []
+    for k in range(1, 5000):
+        for a, b in ((k, float(k)), ((k, 'x'), (float(k), 'x'))):
+            if R.get_segment(a, S) == R.get_segment(b, S):
+                out.append((a, b))
+        if len(out) >= want:
+            break
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bulk', [False, True])
+def test_equal_numbers_are_one_key(bulk):
+    """1 and 1.0 (and {1,x} / {1.0,x}) in one segment are ONE key, as the
+    reference's orddict:store (synctree.erl:206: the later key form and value
+    replace the entry), lists:keyfind in get (:342-348) and orddict_delta
+    (riak_ensemble_util.erl:120-125, K1 reported) treat them; corrupt/2's
+    orddict:erase removes either form.  Device vs synctree_ref, through the
+    per-key kernel and the bulk ingest."""
+    from riak_ensemble_amd import synctree_hip
+    W, S = 4, 64
+    pairs = _same_segment_pairs(S, 6)
+    assert len(pairs) >= 4
+    ref = R.new(b'ref', W, S)
+    dev = synctree_hip.DeviceTree(W, S)
+    filler = [(i * 7919, _val(i)) for i in range(40)]
+    first = [(a, _val(100 + j)) for j, (a, _) in enumerate(pairs)]
+    second = [(b, _val(200 + j)) for j, (_, b) in enumerate(pairs)]
+    for k, v in filler + first + second:
+        ref = R.insert(k, v, ref)
+    if bulk:   # one bulk batch: last writer wins among == keys
+        kv = filler + first + second
+        assert all(x is None for x in dev.insert_batch([k for k, _ in kv], [v for _, v in kv]))
+    else:      # one key per call (the per-key kernel)
+        for k, v in filler + first + second:
+            assert dev.insert_batch([k], [v]) == [None]
+    assert dev.top_hash() == R.top_hash(ref)
+    segs = sorted({R.get_segment(a, S) for a, _ in pairs})
+    got = dev.exchange_get_batch(R.height(ref) + 1, segs)
+    exp = [R.exchange_get(R.height(ref) + 1, s, ref) for s in segs]
+    assert got == exp
+    assert all(type(k) is type(e) for g, x in zip(got, exp) for (k, _), (e, _) in zip(g, x))   # the float form is stored
+    probe = [a for a, _ in pairs] + [b for _, b in pairs]
+    assert dev.get_batch(probe) == [R.get(k, ref) for k in probe]
+    assert dev.get_batch(probe) == [v for _, v in second] * 2
+    # orddict_delta: the integer form here, the float form there, different values
+    ref2 = R.new(b'ref2', W, S)
+    dev2 = synctree_hip.DeviceTree(W, S)
+    for k, v in filler + first:
+        ref2 = R.insert(k, v, ref2)
+    dev2.insert_batch([k for k, _ in filler + first], [v for _, v in filler + first])
+    res = dev2.compare(dev)
+    assert res[0] == 'ok'
+    got, exp = [(k, v) for _, k, v in res[1]], R.local_compare(ref2, ref)
+    assert got == exp and len(exp) == len(pairs)
+    assert [repr(k) for k, _ in got] == [repr(k) for k, _ in exp]   # K1: the local (integer) form
+    # corrupt/2 with the other form erases the entry
+    a0, b0 = pairs[0]
+    dev.corrupt(a0)
+    ref = R.corrupt(a0, ref)
+    assert dev.get_batch([b0]) == [R.get(b0, ref)]
     dev.close()
     dev2.close()
