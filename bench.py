@@ -225,6 +225,7 @@ def main():
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, dev_index, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_d, vals_d, n, dev_index, torch)
             out['leveldb'] = _bench_leveldb(synctree_hip, tree, dev_index, torch)
+            out['repair'] = _bench_repair(tree, keys_h, torch)
     tree.close()
     del keys_d, vals_d
     if not args.no_extras:
@@ -331,6 +332,40 @@ def _bench_cold_l3(tree, torch, dev, k1_bytes, hot_ms, reps=5):
     return {'kernel_avg_ms': round(avg, 4), 'achieved_GBps': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 4),
             'hot_kernel_avg_ms': round(hot_ms, 4), 'launches': n,
             'what': 'rehash kernel after a 1 GiB read per launch (Infinity Cache flushed): tiles read from HBM'}
+
+
+def _bench_repair(tree, keys_h, torch, reps=10):
+    """riak_ensemble_peer_tree do_repair (peer_tree.erl:264-277) after a
+    segment-level corruption: delete the segment node, then a full rehash/1.
+    The rehash after a mutation rebuilds the hash-ready tiles first
+    (k_tile_order_window + scan + k_tile_fill), so this is the rehash a repair
+    pays, next to the headline's (tiles valid).  Reps delete different
+    non-empty segments of the 10M-key tree (last leg on it)."""
+    H1 = tree.height + 1
+    segs = tree.segments_of([int(k) for k in keys_h[:reps * 7:7]])
+    ts = []
+    for s in segs[:reps]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tree.delete_node(H1, s)
+        tree.rehash()
+        tree.sync()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    tree.set_timing(True)
+    tree.kernel_stats('*reset*')
+    tree.delete_node(H1, segs[reps] if len(segs) > reps else segs[0])
+    tree.rehash()
+    tb_n, tb_ms = tree.kernel_stats('tile_build')
+    rf_n, rf_ms = tree.kernel_stats('rehash_fused')
+    tree.set_timing(False)
+    mem = tree.mem_stats()
+    return {'ms_per_repair': round(ts[len(ts) // 2] * 1e3, 4), 'reps': reps,
+            'kernels_ms': {'tile_build': round(tb_ms, 4), 'rehash_fused': round(rf_ms, 4)},
+            'tile_bytes': mem['tiles'], 'csr_bytes': mem['csr'], 'slot_bytes': mem['slots'],
+            'what': 'repair path: delete one segment node + full rehash/1 (tile rebuild included), median of %d, '
+                    'wall incl. the C-ABI calls; tile_bytes = the device copy of every value the tiled '
+                    'layout keeps (the headline rehash reads it)' % reps}
 
 
 def _segment_histogram(tree, keys_h):

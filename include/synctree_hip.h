@@ -84,6 +84,12 @@ uint64_t st_width(const st_tree *t);
 uint64_t st_segments(const st_tree *t);
 /* number of {Key,Value} entries over all segments */
 uint64_t st_num_entries(st_tree *t);
+/* Device bytes this tree holds, by part: out[0] node slot arrays, out[1]
+ * the segment CSR, out[2] the hash-ready tiles (+ their per-segment
+ * metadata), out[3] the spare CSR kept for the next merge, out[4] the
+ * per-key overlay, out[5] bytes in the process-wide cache of freed blocks
+ * (all trees of the process).  No reference counterpart (memory report). */
+int st_mem_stats(st_tree *t, uint64_t out[6]);
 /* the last error message of this thread */
 const char *st_last_error(void);
 

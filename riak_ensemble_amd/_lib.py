@@ -48,6 +48,7 @@ _SIGS = {
     'st_width': (ctypes.c_uint64, [ctypes.c_void_p]),
     'st_segments': (ctypes.c_uint64, [ctypes.c_void_p]),
     'st_num_entries': (ctypes.c_uint64, [ctypes.c_void_p]),
+    'st_mem_stats': (ctypes.c_int, [ctypes.c_void_p, u64p]),
     'st_last_error': (ctypes.c_char_p, []),
     'st_insert_batch': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -121,6 +122,8 @@ def load():
                            'there is no CPU fallback' % LIB_PATH)
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if os.environ.get('ST_LIB') and not hasattr(L, name):
+            continue   # an older build under A/B: symbols it lacks stay unbound
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -2016,7 +2016,6 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-#define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
 
 __device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t R, uint32_t ln, uint32_t lane,
                                                 uint32_t k, uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
@@ -2062,9 +2061,12 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
 // ensembles one GPU hosts, riak_ensemble_peer.erl:1845-1846): workgroup g
 // takes window g % nwin of tree group[g / nwin], each tree with its own slot
 // arrays, tiles, counters and mailboxes.
-template <bool STAMP, bool GROUP>
-__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
-                                                       uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
+// NW waves per window workgroup (16: 4 tiles per wave, 128 VGPRs; 8: 8 tiles
+// per wave, up to 256 VGPRs) and DEPTH blocks in flight per wave in K1.
+template <bool STAMP, bool GROUP, int NW = 16, int DEPTH = 2>
+__global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
+                                                          uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
+    constexpr int RF_TILES = 64 / NW;   // tiles per wave: 64 tiles per window
 #define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
                                                           stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
     RF_STAMP(0);
@@ -2094,8 +2096,8 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
 #pragma unroll
     for (int q = 0; q < RF_TILES; q++) {
         // snake order over the window's tiles (longest first): wave w takes
-        // w, 31 - w, 32 + w, 63 - w, which evens out the waves' block counts
-        const uint64_t tl = root * 64 + 16 * q + ((q & 1) ? 15 - wave : wave);
+        // w, 2 NW - 1 - w, 2 NW + w, ..., which evens out the waves' block counts
+        const uint64_t tl = root * 64 + NW * q + ((q & 1) ? NW - 1 - wave : wave);
         const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
         Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
@@ -2107,8 +2109,19 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
         lnq[q] = RFT(tln)[tl * 64 + lane];
         T += Bq[q];
     }
-    auto pick = [&](const uint32_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
-    auto pick64 = [&](const uint64_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
+    // select by a wave-uniform index without register indexing
+    auto pick = [&](const uint32_t *v, uint32_t q) {
+        uint32_t r = v[0];
+#pragma unroll
+        for (int i = 1; i < RF_TILES; i++) r = q == (uint32_t)i ? v[i] : r;
+        return r;
+    };
+    auto pick64 = [&](const uint64_t *v, uint32_t q) {
+        uint64_t r = v[0];
+#pragma unroll
+        for (int i = 1; i < RF_TILES; i++) r = q == (uint32_t)i ? v[i] : r;
+        return r;
+    };
     auto put_entry = [&](uint32_t li, uint32_t nb, const uint32_t st[4]) {
         uint4 e = make_uint4(0, 0, 0, 0);
         uint16_t tg = 0;
@@ -2148,12 +2161,12 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
                 if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
             }
         };
-        // Ping-pong buffers, no register rotation: hashing buffer A waits only
-        // for A's loads (vmcnt leaves B's four in flight), then A is refilled
-        // with the block after B, and so on.
-        uint4 a0, a1, a2, a3, b0, b1, b2, b3;
-        fetch(a0, a1, a2, a3);
-        fetch(b0, b1, b2, b3);
+        // DEPTH buffers, no register rotation: hashing buffer d waits only for
+        // d's loads (vmcnt leaves the other buffers' loads in flight), then d
+        // is refilled with the block DEPTH ahead.
+        uint4 buf[DEPTH][4];
+#pragma unroll
+        for (int d = 0; d < DEPTH; d++) fetch(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
         uint32_t cq = next_tile(0), ck = 0, cB = 0, cR = 0, cnb = 0, cln = 0;
         if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
         uint32_t st[4];
@@ -2179,14 +2192,15 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
                 if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
             }
         };
-        // Every iteration issues both refills (dummies past the end), so the
-        // compiler's wait before each hash counts the other buffer's four
-        // loads as still in flight on every path.
-        for (uint32_t f = 0; f < T; f += 2) {
-            hash_block(a0, a1, a2, a3);
-            fetch(a0, a1, a2, a3);
-            if (f + 1 < T) hash_block(b0, b1, b2, b3);
-            fetch(b0, b1, b2, b3);
+        // Every iteration issues every refill (dummies past the end), so the
+        // compiler's wait before each hash counts the other buffers' loads as
+        // still in flight on every path.
+        for (uint32_t f = 0; f < T; f += DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; d++) {
+                if (d == 0 || f + d < T) hash_block(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
+                fetch(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
+            }
         }
 #pragma unroll
         for (int q0 = 0; q0 < RF_TILES; q0++)
@@ -2202,11 +2216,12 @@ __global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0,
     // its end (~B / 6 TB/s added to the kernel boundary for B dirty bytes:
     // 16.8 MB here).
     if (tid >= 256) {
+        constexpr uint32_t NCOPY = NW * 64 - 256;   // threads of the copying waves
         const uint64_t c0 = t.base[H + 1] + seg0;
         const uint64_t nbytes = (t.base[H + 1] + t.S) * 16;
         const __amdgpu_buffer_rsrc_t md5r = __builtin_amdgcn_make_buffer_rsrc(
             GROUP ? group[gi].md5 : t.md5, (short)0, (int)(nbytes < 0xffffffffull ? nbytes : 0xffffffffull), 0x00020000);
-        for (uint32_t i = tid - 256; i < 4096; i += 768) {
+        for (uint32_t i = tid - 256; i < 4096; i += NCOPY) {
             const uint4 e = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
             const u32x4 v = {e.x, e.y, e.z, e.w};
             __builtin_amdgcn_raw_buffer_store_b128(v, md5r, (int)((c0 + i) * 16), 0, 16 /* sc1 */);

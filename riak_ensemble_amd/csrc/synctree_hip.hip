@@ -647,6 +647,20 @@ extern "C" uint64_t st_width(const st_tree *t) { return t->W; }
 extern "C" uint64_t st_segments(const st_tree *t) { return t->S; }
 extern "C" uint64_t st_num_entries(st_tree *t) { return t->n; }
 
+static uint64_t num_tiles(const st_tree *t);
+extern "C" int st_mem_stats(st_tree *t, uint64_t out[6]) {
+    out[0] = t->nslots * (sizeof(uint4) + sizeof(uint16_t) + 2);   // md5, tag, mark, ok
+    out[1] = (t->S + 1) * 16 + t->cap_n * 16 + t->cap_k + t->cap_v;
+    out[2] = t->tiles_cap * sizeof(uint4) + (t->tseg ? num_tiles(t) * (64 * 8 + sizeof(TileInfo)) : 0);
+    out[3] = t->spare.koff ? (t->S + 1) * 16 + t->spare.cap_n * 16 + t->spare.cap_k + t->spare.cap_v : 0;
+    out[4] = t->ov.idx ? t->S * 8 + t->ov.cap : 0;
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    uint64_t c = 0;
+    for (auto &kv : g_mem_free) c += kv.first;
+    out[5] = c;
+    return ST_OK;
+}
+
 extern "C" int st_set_timing(st_tree *t, int enabled) {
     t->timing = enabled != 0;
     return ST_OK;
@@ -756,6 +770,10 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // ingest and lazily by rehash.
 // the fused kernel's last window hashes the upper levels a thread per node:
 // at most 256 nodes at level H-3 (H <= 6)
+static int rf_config() {
+    static const int v = getenv("ST_RF") ? atoi(getenv("ST_RF")) : 0;
+    return v;
+}
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
 static int ensure_tiles(st_tree *t) {
@@ -873,8 +891,23 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            switch (rf_config()) {   // waves per window x K1 blocks in flight (A/B knob ST_RF)
+            case 1:
+                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 8, 4>), nwg, 512, fused_lds_bytes(), d,
+                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+                break;
+            case 2:
+                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 8, 6>), nwg, 512, fused_lds_bytes(), d,
+                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+                break;
+            case 3:
+                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16, 3>), nwg, 1024, fused_lds_bytes(), d,
+                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+                break;
+            default:
+                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            }
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr

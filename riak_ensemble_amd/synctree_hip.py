@@ -175,6 +175,12 @@ class DeviceTree:
     def num_entries(self):
         return int(self.L.st_num_entries(self.h))
 
+    def mem_stats(self):
+        """Device bytes of this tree by part (st_mem_stats)."""
+        v = (ctypes.c_uint64 * 6)()
+        _lib.check(self.L.st_mem_stats(self.h, v), 'st_mem_stats')
+        return dict(zip(('slots', 'csr', 'tiles', 'spare_csr', 'overlay', 'freed_block_cache'), [int(x) for x in v]))
+
     def sync(self):
         _lib.check(self.L.st_sync(self.h), 'st_sync')
 
