@@ -549,7 +549,7 @@ struct USum {
     }
 };
 typedef USum<6> BatchSums;   // eq, ne, ke, kn, ve, vn
-typedef USum<3> SegSums;     // count, key bytes, value bytes
+typedef USum<4> SegSums;     // count, key bytes, value bytes, surviving old-entry spans
 enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 
 // ---------------------------------------------------------------------------
@@ -580,7 +580,7 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
         tot.v[0] = nold;
         tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
         tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
-        uint64_t lo = 0;
+        uint64_t lo = 0, nkept = 0;
         bool changed = false;
         for (uint64_t j = j0; j < je; j++) {
             BatchSums f(0);
@@ -610,10 +610,14 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
             }
             bs[j] = f;
             changed |= kept;
+            nkept += kept ? 1 : 0;
             tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
             tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
             tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
         }
+        // the surviving old entries form nkept + 1 spans (runs between the
+        // kept batch records' positions; k_merge_spans)
+        tot.v[3] = nold ? nkept + 1 : 0;
         ss[s] = tot;
         if (dirty) dirty[s] = changed ? 1 : 0;
     }
@@ -710,6 +714,100 @@ __global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const
     }
 }
 
+// ---------------------------------------------------------------------------
+// Span merge (the old entries' moves).  Between two consecutive kept batch
+// records of a segment the surviving old entries keep their order and move
+// by one constant offset in all four arrays (entry index, key bytes, value
+// bytes), so they are copied as SPANS: contiguous byte ranges, a wave per
+// span with 16-byte loads and stores, instead of an entry-by-entry walk with
+// per-entry lookups.  k_merge_spans_build: a thread per segment lists its
+// spans (at its scanned span offset) and writes the new segment offsets;
+// k_merge_spans_copy: a wave per span.  k_merge_new places the batch records.
+struct MergeSpan {
+    uint64_t se, de;   // first old entry, its new index
+    uint64_t dk, dv;   // new key / value byte offsets of the span's first entry
+    uint64_t cnt;      // entries
+};
+
+__global__ void k_merge_spans_build(MergeArgs a, const uint32_t *pos, const BatchSums *bx, const SegSums *sx, MergeOut o,
+                                    MergeSpan *spans) {
+    for (uint64_t s = gtid(); s <= a.S; s += gstride()) {
+        const SegSums base = sx[s];
+        o.seg_off[s] = base.v[0];
+        o.seg_voff[s] = base.v[2];
+        if (s == a.S) { o.koff[base.v[0]] = base.v[1]; o.voff[base.v[0]] = base.v[2]; break; }
+        const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+        uint64_t nold = a.seg_off ? a.seg_off[s + 1] - i0 : 0;
+        if (a.seg_replace && a.seg_replace[s]) nold = 0;
+        if (!nold) continue;
+        MergeSpan *sp = spans + base.v[3];
+        uint64_t li = 0, de = base.v[0], dk = base.v[1], dv = base.v[2];
+        const uint64_t k0 = a.koff[i0], v0 = a.voff[i0];
+        uint64_t kli = k0, vli = v0;   // koff / voff of old entry li
+        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
+        if (!(a.seg_reject && a.seg_reject[s])) {
+            for (uint64_t j = j0; j < je; j++) {
+                if (!a.keep[j]) continue;
+                const BatchSums &B = bx[j], &B1 = bx[j + 1];
+                const uint64_t p = pos[j];
+                const uint64_t kp = a.koff[i0 + p], vp = a.voff[i0 + p];
+                *sp++ = MergeSpan{i0 + li, de, dk, dv, p - li};
+                de += p - li; dk += kp - kli; dv += vp - vli;
+                // the record itself (k_merge_new writes it): one entry if it is not an ERASE
+                de += B1.v[BS_NE] - B.v[BS_NE];
+                dk += B1.v[BS_KN] - B.v[BS_KN];
+                dv += B1.v[BS_VN] - B.v[BS_VN];
+                if (B1.v[BS_EQ] != B.v[BS_EQ]) {   // the old entry at p is replaced or erased
+                    li = p + 1;
+                    kli = a.koff[i0 + li];
+                    vli = a.voff[i0 + li];
+                } else {
+                    li = p;
+                    kli = kp;
+                    vli = vp;
+                }
+            }
+        }
+        *sp = MergeSpan{i0 + li, de, dk, dv, nold - li};
+    }
+}
+
+__global__ void __launch_bounds__(256) k_merge_spans_copy(MergeArgs a, const MergeSpan *spans, uint64_t nspans, MergeOut o) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwv = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = w0; w < nspans; w += nwv) {
+        const MergeSpan sp = spans[w];
+        if (!sp.cnt) continue;
+        const uint64_t sk = a.koff[sp.se], ek = a.koff[sp.se + sp.cnt];
+        const uint64_t sv = a.voff[sp.se], ev = a.voff[sp.se + sp.cnt];
+        const int64_t ddk = (int64_t)sp.dk - (int64_t)sk, ddv = (int64_t)sp.dv - (int64_t)sv;
+        for (uint64_t i = lane; i < sp.cnt; i += 64) {
+            o.koff[sp.de + i] = (uint64_t)((int64_t)a.koff[sp.se + i] + ddk);
+            o.voff[sp.de + i] = (uint64_t)((int64_t)a.voff[sp.se + i] + ddv);
+        }
+        const uint64_t nk = ek - sk, nv = ev - sv;
+        for (uint64_t c = (uint64_t)lane * 16; c < nk; c += 1024) {
+            if (c + 16 <= nk) {
+                uint4 x;
+                __builtin_memcpy(&x, a.kheap + sk + c, 16);
+                __builtin_memcpy(o.kheap + sp.dk + c, &x, 16);
+            } else {
+                for (uint64_t b = c; b < nk; b++) o.kheap[sp.dk + b] = a.kheap[sk + b];
+            }
+        }
+        for (uint64_t c = (uint64_t)lane * 16; c < nv; c += 1024) {
+            if (c + 16 <= nv) {
+                uint4 x;
+                __builtin_memcpy(&x, a.vheap + sv + c, 16);
+                __builtin_memcpy(o.vheap + sp.dv + c, &x, 16);
+            } else {
+                for (uint64_t b = c; b < nv; b++) o.vheap[sp.dv + b] = a.vheap[sv + b];
+            }
+        }
+    }
+}
+
 __global__ void k_seg_voff(const uint64_t *seg_off, const uint64_t *voff, uint64_t S, uint64_t *seg_voff) {
     for (uint64_t s = gtid(); s <= S; s += gstride()) seg_voff[s] = voff[seg_off[s]];
 }
@@ -764,7 +862,7 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 // its entries differ.  k_cmp_walk evaluates it per node, verifies every
 // visited node on both sides against its parent's entry (exchange_get's
 // verified_hashes, synctree.erl:288-298) and merge-joins every visited
-// segment pair (exchange_final); k_cmp_gather concatenates the per-wave
+// segment pair (exchange_final); the last workgroup concatenates the per-wave
 // record regions.  Only the entries under visited nodes beyond level H are
 // read.  err: min over (level, bucket, side) of a failed verification -- the
 // reference's first crash in visiting order (local before remote).
@@ -1054,6 +1152,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
 // LDS of a compare-walk wave: the shared area (lane regions for inner-node
 // staging / the merge-join), then the work list, then per-level counters
 #define CMP_LIST 256
+#define CMP_PRE 7       // the walk preloads the frontier of trees up to this height
 __host__ __device__ __forceinline__ uint32_t cmp_shared_bytes(uint32_t W) {
     const uint32_t a = 64 * lane_region_bytes(W), m = cmp_merge_lds_bytes();
     return ((a > m ? a : m) + 15) & ~15u;
@@ -1221,13 +1320,77 @@ __device__ __forceinline__ void cmp_append(uint64_t *list, uint32_t &n, bool f, 
     n += (uint32_t)__popcll(m);
 }
 
+// The compare's result for the host (fine-grained host memory): ONE record
+// written last by the gathering workgroup, validated by the host (sequence
+// number + check word), so it never depends on the order in which two GPU
+// stores reach host memory (small_path.h).
+struct CmpRes {
+    uint64_t seq, total, maxw, err, check;
+};
+__host__ __device__ __forceinline__ uint64_t cmp_res_check(uint64_t seq, uint64_t a, uint64_t b, uint64_t c) {
+    uint64_t h = seq * 0x9E3779B97F4A7C15ull ^ 0xD6E8FEB86659FD93ull;
+    h = (h ^ a) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 31) ^ b) * 0x94D049BB133111EBull;
+    h = (h ^ (h >> 29) ^ c) * 0xBF58476D1CE4E5B9ull;
+    return (h ^ (h >> 32)) | 1ull;
+}
+
+// The gather (the waves' record regions -> the record buffer, wave w after
+// every higher wave, and the CmpRes) by the LAST workgroup of the walk to
+// finish: one counter, no second launch.
+__device__ __forceinline__ void cmp_gather_last(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
+                                                const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
+                                                CmpRes *res, uint64_t seq, uint64_t *above) {
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    __shared__ uint64_t s_tot, s_max, s_err;
+    if (tid == 0) { s_tot = 0; s_max = 0; s_err = ~0ull; }
+    __syncthreads();
+    // above[v] = records of the waves after v (in LDS); reduce the maximum and the first error
+    uint64_t mx = 0, em = ~0ull;
+    for (uint32_t v = tid; v < nw; v += nt) {
+        const uint64_t c = wcnt[v], e = werr[v];
+        above[v] = c;
+        mx = c > mx ? c : mx;
+        em = e < em ? e : em;
+    }
+    atomicMax(reinterpret_cast<unsigned long long *>(&s_max), (unsigned long long)mx);
+    atomicMin(reinterpret_cast<unsigned long long *>(&s_err), (unsigned long long)em);
+    __syncthreads();
+    if (tid == 0) {   // suffix sums (nw <= a few thousand)
+        uint64_t acc = 0;
+        for (uint32_t v = nw; v-- > 0;) {
+            const uint64_t c = above[v];
+            above[v] = acc;
+            acc += c;
+        }
+        s_tot = acc;
+    }
+    __syncthreads();
+    const uint64_t tot = s_tot, mxw = s_max, err = s_err;
+    if (mxw <= R && tot <= cap && err == ~0ull)   // else the host grows the buffers and runs again
+        for (uint32_t v = tid; v < nw; v += nt) {
+            const uint64_t c = wcnt[v], a = above[v];
+            const DiffRec *src = scratch + (uint64_t)v * R;
+            for (uint64_t k = 0; k < c; k++) out[a + k] = src[k];
+        }
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence_system();   // the records are in the buffer before the host reads the count
+        CmpRes r;
+        r.seq = seq; r.total = tot; r.maxw = mxw; r.err = err; r.check = cmp_res_check(seq, tot, mxw, err);
+        *res = r;
+        __threadfence_system();
+    }
+}
+
 __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2, uint32_t nw,
                                                  uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *wcnt,
-                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps) {
+                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps,
+                                                 uint32_t *done, DiffRec *out, uint64_t cap, CmpRes *res, uint64_t seq) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + wave;
-    if (w >= nw) return;
+    if (w < nw) {
     uint8_t *wl = lds + (uint64_t)wave * slice;
     const uint32_t H = A.H, L1 = H + 1, sh = A.shift, W = A.W;
     CmpWalk c;
@@ -1274,6 +1437,28 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         for (uint64_t c0 = h0 + ((h1 - h0 - 1) & ~63ull);; c0 -= 64) {
             const uint64_t c1 = c0 + 64 < h1 ? c0 + 64 : h1;   // level-H nodes [c0, c1)
             bool f = true;       // this lane's node flag at the previous level (level 1: the root)
+            // every level's entries of the chunk in ONE round trip (H <= CMP_PRE):
+            // a lane's node at level l is lo_l + lane; the flags are then
+            // evaluated top-down from registers
+            uint32_t pdiff = 0;  // bit l: this lane's level-l entry differs (and is in range)
+            if (H <= CMP_PRE) {
+                uint16_t ta[CMP_PRE + 1], tb[CMP_PRE + 1];
+                uint4 xa[CMP_PRE + 1], xb[CMP_PRE + 1];
+#pragma unroll
+                for (uint32_t l = 2; l <= CMP_PRE; l++) {
+                    ta[l] = tb[l] = 0;
+                    if (l > H) continue;
+                    const uint32_t up = sh * (H - l);
+                    const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up, b = lo + lane;
+                    if (b <= hi && !(l == 2 && (b < lo2 || b >= hi2))) {
+                        const uint64_t slot = A.base[l] + b;
+                        ta[l] = A.tag[slot]; tb[l] = B.tag[slot]; xa[l] = A.md5[slot]; xb[l] = B.md5[slot];
+                    }
+                }
+#pragma unroll
+                for (uint32_t l = 2; l <= CMP_PRE; l++)
+                    if (l <= H && entry_differs(ta[l], tb[l], xa[l], xb[l], filter)) pdiff |= 1u << l;
+            }
             for (uint32_t l = 2; l <= H; l++) {
                 const uint32_t up = sh * (H - l);
                 const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
@@ -1281,7 +1466,7 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
                 const uint64_t plo = lo >> sh;
                 const uint32_t plane = (uint32_t)((b >> sh) - plo);
                 const bool fp = __shfl((int)f, (int)(plane < 64 ? plane : 0), 64) != 0;
-                f = b <= hi && fp && cmp_entry_in(A, B, filter, l, b, lo2, hi2);
+                f = b <= hi && fp && (H <= CMP_PRE ? ((pdiff >> l) & 1u) != 0 : cmp_entry_in(A, B, filter, l, b, lo2, hi2));
                 const bool owned = f && (b << up) >= c0 && (b << up) < c1;
                 if (n + 64 > CMP_LIST) { cmp_flush(A, B, c, n); n = 0; }
                 const uint32_t n0 = n;
@@ -1331,64 +1516,23 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         werr[w] = em;
     }
     for (uint32_t l = lane; l < ST_STATW; l += 64) wst[(uint64_t)w * ST_STATW + l] = (l >= 1 && l <= L1) ? c.cnt[l] : 0;
-}
-
-// The waves' regions -> the record buffer (wave w after every higher wave).
-// Wave 0 also reduces the per-wave results into res (host-mapped): the
-// total, the largest per-wave count (the scratch a rerun needs when it
-// exceeds R) and the first failed verification.  A wave per region.
-__global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
-                                                   const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
-                                                   uint64_t *res) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nw) return;
-    uint64_t above = 0;
-    for (uint32_t v0 = w + 1; v0 < nw; v0 += 1024) {   // 16 loads per lane in flight
-        uint64_t x[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-            const uint32_t v = v0 + u * 64 + lane;
-            x[u] = v < nw ? wcnt[v] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++) above += x[u];
-    }
-    for (int o = 32; o; o >>= 1) above += __shfl_xor(above, o, 64);
-    const uint64_t n = wcnt[w];
-    if (w == 0) {
-        uint64_t mx = 0, em = ~0ull;
-        for (uint32_t v0 = 0; v0 < nw; v0 += 512) {
-            uint64_t x[8], y[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t v = v0 + u * 64 + lane;
-                x[u] = v < nw ? wcnt[v] : 0;
-                y[u] = v < nw ? werr[v] : ~0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                mx = x[u] > mx ? x[u] : mx;
-                em = y[u] < em ? y[u] : em;
-            }
-        }
-        for (int o = 32; o; o >>= 1) {
-            const uint64_t x = __shfl_xor(mx, o, 64), y = __shfl_xor(em, o, 64);
-            mx = x > mx ? x : mx;
-            em = y < em ? y : em;
-        }
-        if (lane == 0) {
-            res[0] = above + n;
-            res[1] = mx;
-            res[2] = em;
-            __threadfence_system();
-            res[3] = 1;   // the host spins on this word
-            __threadfence_system();
+    }   // w < nw
+    // the last workgroup to finish gathers (release: this workgroup's records
+    // and counts are visible to it; acquire in the last one before it reads)
+    __shared__ uint32_t s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old + 1 == gridDim.x;
+        if (s_last) {
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();
         }
     }
-    if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
-    const DiffRec *src = scratch + (uint64_t)w * R;
-    for (uint64_t k = lane; k < n; k += 64) out[above + k] = src[k];
+    __syncthreads();
+    if (!s_last) return;
+    cmp_gather_last(nw, wcnt, werr, scratch, R, out, cap, res, seq, reinterpret_cast<uint64_t *>(lds));
 }
 
 // Diff records -> byte lengths of key / local value / remote value
@@ -2016,6 +2160,7 @@ __device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tag
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+#define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
 
 __device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t R, uint32_t ln, uint32_t lane,
                                                 uint32_t k, uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
@@ -2061,12 +2206,9 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
 // ensembles one GPU hosts, riak_ensemble_peer.erl:1845-1846): workgroup g
 // takes window g % nwin of tree group[g / nwin], each tree with its own slot
 // arrays, tiles, counters and mailboxes.
-// NW waves per window workgroup (16: 4 tiles per wave, 128 VGPRs; 8: 8 tiles
-// per wave, up to 256 VGPRs) and DEPTH blocks in flight per wave in K1.
-template <bool STAMP, bool GROUP, int NW = 16, int DEPTH = 2>
-__global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
-                                                          uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
-    constexpr int RF_TILES = 64 / NW;   // tiles per wave: 64 tiles per window
+template <bool STAMP, bool GROUP>
+__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
+                                                       uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
 #define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
                                                           stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
     RF_STAMP(0);
@@ -2096,8 +2238,8 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
 #pragma unroll
     for (int q = 0; q < RF_TILES; q++) {
         // snake order over the window's tiles (longest first): wave w takes
-        // w, 2 NW - 1 - w, 2 NW + w, ..., which evens out the waves' block counts
-        const uint64_t tl = root * 64 + NW * q + ((q & 1) ? NW - 1 - wave : wave);
+        // w, 31 - w, 32 + w, 63 - w, which evens out the waves' block counts
+        const uint64_t tl = root * 64 + 16 * q + ((q & 1) ? 15 - wave : wave);
         const TileInfo ti = RFT(tinfo)[tl];
         Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
         Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
@@ -2109,19 +2251,8 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
         lnq[q] = RFT(tln)[tl * 64 + lane];
         T += Bq[q];
     }
-    // select by a wave-uniform index without register indexing
-    auto pick = [&](const uint32_t *v, uint32_t q) {
-        uint32_t r = v[0];
-#pragma unroll
-        for (int i = 1; i < RF_TILES; i++) r = q == (uint32_t)i ? v[i] : r;
-        return r;
-    };
-    auto pick64 = [&](const uint64_t *v, uint32_t q) {
-        uint64_t r = v[0];
-#pragma unroll
-        for (int i = 1; i < RF_TILES; i++) r = q == (uint32_t)i ? v[i] : r;
-        return r;
-    };
+    auto pick = [&](const uint32_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
+    auto pick64 = [&](const uint64_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
     auto put_entry = [&](uint32_t li, uint32_t nb, const uint32_t st[4]) {
         uint4 e = make_uint4(0, 0, 0, 0);
         uint16_t tg = 0;
@@ -2161,12 +2292,12 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
                 if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
             }
         };
-        // DEPTH buffers, no register rotation: hashing buffer d waits only for
-        // d's loads (vmcnt leaves the other buffers' loads in flight), then d
-        // is refilled with the block DEPTH ahead.
-        uint4 buf[DEPTH][4];
-#pragma unroll
-        for (int d = 0; d < DEPTH; d++) fetch(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
+        // Ping-pong buffers, no register rotation: hashing buffer A waits only
+        // for A's loads (vmcnt leaves B's four in flight), then A is refilled
+        // with the block after B, and so on.
+        uint4 a0, a1, a2, a3, b0, b1, b2, b3;
+        fetch(a0, a1, a2, a3);
+        fetch(b0, b1, b2, b3);
         uint32_t cq = next_tile(0), ck = 0, cB = 0, cR = 0, cnb = 0, cln = 0;
         if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
         uint32_t st[4];
@@ -2192,15 +2323,14 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
                 if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
             }
         };
-        // Every iteration issues every refill (dummies past the end), so the
-        // compiler's wait before each hash counts the other buffers' loads as
-        // still in flight on every path.
-        for (uint32_t f = 0; f < T; f += DEPTH) {
-#pragma unroll
-            for (int d = 0; d < DEPTH; d++) {
-                if (d == 0 || f + d < T) hash_block(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
-                fetch(buf[d][0], buf[d][1], buf[d][2], buf[d][3]);
-            }
+        // Every iteration issues both refills (dummies past the end), so the
+        // compiler's wait before each hash counts the other buffer's four
+        // loads as still in flight on every path.
+        for (uint32_t f = 0; f < T; f += 2) {
+            hash_block(a0, a1, a2, a3);
+            fetch(a0, a1, a2, a3);
+            if (f + 1 < T) hash_block(b0, b1, b2, b3);
+            fetch(b0, b1, b2, b3);
         }
 #pragma unroll
         for (int q0 = 0; q0 < RF_TILES; q0++)
@@ -2216,12 +2346,11 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
     // its end (~B / 6 TB/s added to the kernel boundary for B dirty bytes:
     // 16.8 MB here).
     if (tid >= 256) {
-        constexpr uint32_t NCOPY = NW * 64 - 256;   // threads of the copying waves
         const uint64_t c0 = t.base[H + 1] + seg0;
         const uint64_t nbytes = (t.base[H + 1] + t.S) * 16;
         const __amdgpu_buffer_rsrc_t md5r = __builtin_amdgcn_make_buffer_rsrc(
             GROUP ? group[gi].md5 : t.md5, (short)0, (int)(nbytes < 0xffffffffull ? nbytes : 0xffffffffull), 0x00020000);
-        for (uint32_t i = tid - 256; i < 4096; i += NCOPY) {
+        for (uint32_t i = tid - 256; i < 4096; i += 768) {
             const uint4 e = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
             const u32x4 v = {e.x, e.y, e.z, e.w};
             __builtin_amdgcn_raw_buffer_store_b128(v, md5r, (int)((c0 + i) * 16), 0, 16 /* sc1 */);

@@ -48,7 +48,9 @@ struct CmpWork {
     uint64_t R = 0;                  // scratch records per wave
     uint64_t *wcnt = nullptr, *wbytes = nullptr, *werr = nullptr;
     uint32_t *wst = nullptr;         // [nw][ST_STATW] visited nodes per level
-    uint64_t *res = nullptr, *res_dev = nullptr;   // host-mapped: total, max per-wave count, first error
+    uint32_t *done = nullptr;        // workgroups finished (the last one gathers; self-resetting)
+    CmpRes *res = nullptr, *res_dev = nullptr;   // host-mapped result record
+    uint64_t seq = 0;                // compares run (the result record's sequence number)
     DiffRec *rec = nullptr, *scratch = nullptr;
     uint64_t cap = 0;
 };
@@ -770,10 +772,6 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // ingest and lazily by rehash.
 // the fused kernel's last window hashes the upper levels a thread per node:
 // at most 256 nodes at level H-3 (H <= 6)
-static int rf_config() {
-    static const int v = getenv("ST_RF") ? atoi(getenv("ST_RF")) : 0;
-    return v;
-}
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
 static int ensure_tiles(st_tree *t) {
@@ -891,23 +889,8 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            switch (rf_config()) {   // waves per window x K1 blocks in flight (A/B knob ST_RF)
-            case 1:
-                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 8, 4>), nwg, 512, fused_lds_bytes(), d,
-                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
-                break;
-            case 2:
-                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 8, 6>), nwg, 512, fused_lds_bytes(), d,
-                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
-                break;
-            case 3:
-                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16, 3>), nwg, 1024, fused_lds_bytes(), d,
-                       tree_tiles(t), (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
-                break;
-            default:
-                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
-            }
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
@@ -1027,6 +1010,11 @@ struct IngestIn {
     uint64_t n_rejected;
 };
 
+static int merge_mode() {
+    static const int v = getenv("ST_MERGE") ? atoi(getenv("ST_MERGE")) : 0;
+    return v;
+}
+
 static int ingest(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
     in.n_rejected = 0;
@@ -1128,8 +1116,19 @@ static int ingest(st_tree *t, IngestIn &in) {
     MergeOut mo;
     mo.seg_off = out.o.seg_off; mo.seg_voff = out.o.seg_voff; mo.koff = out.o.koff; mo.voff = out.o.voff;
     mo.kheap = out.o.kheap; mo.vheap = out.o.vheap;
-    LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
-           (const BatchSums *)bx, (const SegSums *)sx, mo);
+    if (merge_mode() == 1) {   // A/B: the entry-by-entry walk
+        LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
+               (const BatchSums *)bx, (const SegSums *)sx, mo);
+    } else {
+        const uint64_t nspans = tot.v[3];
+        MergeSpan *spans = nullptr;
+        CHK(sc.alloc(&spans, nspans + 1));
+        LAUNCH(t, "merge_spans", k_merge_spans_build, grid_for(S + 1), 256, 0, ma, (const uint32_t *)mpos,
+               (const BatchSums *)bx, (const SegSums *)sx, mo, spans);
+        if (nspans)
+            LAUNCH(t, "merge_write", k_merge_spans_copy, grid_for(nspans * 64, 256, 8192), 256, 0, ma,
+                   (const MergeSpan *)spans, nspans, mo);
+    }
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
@@ -2222,13 +2221,25 @@ static int ensure_cmp_work(st_tree *t) {
     CHK(dalloc_t(t, &w.wbytes, w.nw));
     CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
     CHK(dalloc_t(t, &w.werr, w.nw));
-    if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    CHK(dalloc_t(t, &w.done, 1));
+    HIPCHK(hipMemsetAsync(w.done, 0, 4, t->stream));
+    if (hipHostMalloc((void **)&w.res, sizeof(CmpRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         w.res = nullptr;
         g_err = "hipHostMalloc failed";
         return ST_EDEVICE;
     }
+    memset(w.res, 0, sizeof(CmpRes));
     HIPCHK(hipHostGetDevicePointer((void **)&w.res_dev, w.res, 0));
     return ST_OK;
+}
+
+// The walk's result record, once it carries `seq` and a valid check.
+static bool cmp_res_ready(const CmpRes *r, uint64_t seq, uint64_t *tot, uint64_t *mx, uint64_t *err) {
+    const volatile uint64_t *v = reinterpret_cast<const volatile uint64_t *>(r);
+    const uint64_t s0 = v[0], a = v[1], b = v[2], c = v[3], k = v[4];
+    if (s0 != seq || k != cmp_res_check(s0, a, b, c)) return false;
+    *tot = a; *mx = b; *err = c;
+    return true;
 }
 
 // record buffer >= cap records, scratch >= nw * R records
@@ -2294,8 +2305,10 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             CHK(sc.alloc(&stamps, (uint64_t)w.nw * 8));
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 64, t->stream));
         }
+        const uint64_t seq = ++w.seq;
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
-               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps, w.done, w.rec, w.cap,
+               w.res_dev, seq);
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 8);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
@@ -2314,11 +2327,18 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
                         v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
         }
-        w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
-        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4, 256, 0, w.nw, (const uint64_t *)w.wcnt,
-               (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
-        CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
-        const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
+        // spin on the result record; after 5 ms a stream synchronisation
+        uint64_t ntot = 0, need = 0, e = 0;
+        bool ok = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 0; !(ok = cmp_res_ready(w.res, seq, &ntot, &need, &e)); i++) {
+            if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+            __builtin_ia32_pause();
+        }
+        if (!ok) {
+            CHK(tsync(t));
+            if (!cmp_res_ready(w.res, seq, &ntot, &need, &e)) { g_err = "compare result record incomplete"; return ST_EDEVICE; }
+        }
         if (e != ~0ull) {
             *status = ST_CORRUPTED;
             *clevel = (uint32_t)(e >> 56);
