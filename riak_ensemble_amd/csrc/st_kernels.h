@@ -2009,6 +2009,7 @@ struct TreeTiles {
     const TileInfo *tinfo;
     const uint32_t *tseg, *tln;
     const uint4 *tiles;
+    const uint64_t *pres;   // per-window segment presence bitmaps (k_rehash_prog)
 };
 
 

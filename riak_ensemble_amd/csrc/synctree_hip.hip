@@ -22,6 +22,7 @@
 
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
+#include "rehash_prog.h"
 #include "leveldb_fmt.h"
 #include "small_path.h"
 
@@ -102,6 +103,7 @@ struct st_tree {
     uint64_t tiles_cap = 0;         // uint4 units
     uint32_t *tseg = nullptr, *tln = nullptr;
     TileInfo *tinfo = nullptr;
+    uint64_t *tpres = nullptr;      // per-window segment presence (k_rehash_prog)
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
@@ -613,7 +615,7 @@ extern "C" void st_destroy(st_tree *t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->tpres, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
@@ -774,6 +776,18 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // at most 256 nodes at level H-3 (H <= 6)
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
+// Full-rehash kernel for the fused geometry: k_rehash_prog (ST_REHASH=prog:
+// window levels hashed progressively while the segments are; class-ordered
+// tiles), or k_rehash_fused (levels after K1; length-ordered tiles).  Read
+// once per process, so the tile order and the kernel always agree.
+static bool use_prog() {
+    static const bool p = [] {
+        const char *e = getenv("ST_REHASH");
+        return e && !strcmp(e, "prog");
+    }();
+    return p;
+}
+
 static int ensure_tiles(st_tree *t) {
     if (t->tiles_valid) return ST_OK;
     if (!fused_geometry(t)) CHK(ensure_perm(t));
@@ -783,12 +797,16 @@ static int ensure_tiles(st_tree *t) {
         CHK(dalloc_t(t, &t->tln, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
+    if (fused_geometry(t) && use_prog() && !t->tpres) CHK(dalloc_t(t, &t->tpres, t->S / 64));
     Scratch sc(t);
     uint64_t *tsize = nullptr, *tbase = nullptr;
     CHK(sc.alloc(&tsize, ntiles + 1));
     CHK(sc.alloc(&tbase, ntiles + 1));
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
-    if (fused_geometry(t))   // window-local order (k_rehash_fused)
+    if (fused_geometry(t) && use_prog())   // window-local class order + presence (k_rehash_prog)
+        LAUNCH(t, "tile_build", k_tile_order_cls, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
+               tsize, t->tpres);
+    else if (fused_geometry(t))   // window-local order (k_rehash_fused)
         LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
                tsize);
     else
@@ -823,6 +841,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tseg = t->tseg;
     x.tln = t->tln;
     x.tiles = t->tiles;
+    x.pres = t->tpres;
     return x;
 }
 
@@ -889,8 +908,12 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            if (use_prog())
+                LAUNCH(t, "rehash_fused", (k_rehash_prog<false, false>), nwg, 1024, prog_lds_bytes(), d, tree_tiles(t),
+                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            else
+                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
@@ -898,8 +921,12 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 32));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
-        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-               (const TreeTiles *)nullptr, 0u, root0, lmin, st);
+        if (use_prog())
+            LAUNCH(t, "rehash_fused", (k_rehash_prog<true, false>), nwg, 1024, prog_lds_bytes(), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, st);
+        else
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, st);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         CHK(tsync(t));
@@ -914,9 +941,13 @@ static int rehash_tiled(st_tree *t) {
                 fclose(f);
             }
         }
-        static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
-                                        "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
-                                        "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
+        static const char *fnames[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
+                                         "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
+                                         "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
+        static const char *pnames[16] = {"start", "staged", "w0 no tiles", "all tiles", "copy-out", "h1 waves 0-2",
+                                         "root prefix", "w15 h1 done", "root done", "cnt won", "mail read",
+                                         "climb lvl 1", "climb lvl 2", "-", "-", "exit"};
+        const char *const *names = use_prog() ? pnames : fnames;
         for (int k = 0; k < 16; k++) {
             std::vector<double> v;
             for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
@@ -1685,8 +1716,12 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const uint32_t nwin = (uint32_t)(t->S / 4096);
     const uint64_t nwg = (uint64_t)nwin * n;
     if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
-    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
-           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
+    if (use_prog())
+        LAUNCH(t, "rehash_group", (k_rehash_prog<false, true>), (uint32_t)nwg, 1024, prog_lds_bytes(), view(t), h[0],
+               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
+    else
+        LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
+               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
     CHK(tsync(t));
     for (uint32_t i = 0; i < n; i++) {
         CHK(erec_after_rehash(trees[i]));
