@@ -549,7 +549,7 @@ struct USum {
     }
 };
 typedef USum<6> BatchSums;   // eq, ne, ke, kn, ve, vn
-typedef USum<4> SegSums;     // count, key bytes, value bytes, surviving old-entry spans
+typedef USum<3> SegSums;     // count, key bytes, value bytes
 enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 
 // ---------------------------------------------------------------------------
@@ -580,7 +580,7 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
         tot.v[0] = nold;
         tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
         tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
-        uint64_t lo = 0, nkept = 0;
+        uint64_t lo = 0;
         bool changed = false;
         for (uint64_t j = j0; j < je; j++) {
             BatchSums f(0);
@@ -610,14 +610,10 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
             }
             bs[j] = f;
             changed |= kept;
-            nkept += kept ? 1 : 0;
             tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
             tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
             tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
         }
-        // the surviving old entries form nkept + 1 spans (runs between the
-        // kept batch records' positions; k_merge_spans)
-        tot.v[3] = nold ? nkept + 1 : 0;
         ss[s] = tot;
         if (dirty) dirty[s] = changed ? 1 : 0;
     }
@@ -714,100 +710,6 @@ __global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const
     }
 }
 
-// ---------------------------------------------------------------------------
-// Span merge (the old entries' moves).  Between two consecutive kept batch
-// records of a segment the surviving old entries keep their order and move
-// by one constant offset in all four arrays (entry index, key bytes, value
-// bytes), so they are copied as SPANS: contiguous byte ranges, a wave per
-// span with 16-byte loads and stores, instead of an entry-by-entry walk with
-// per-entry lookups.  k_merge_spans_build: a thread per segment lists its
-// spans (at its scanned span offset) and writes the new segment offsets;
-// k_merge_spans_copy: a wave per span.  k_merge_new places the batch records.
-struct MergeSpan {
-    uint64_t se, de;   // first old entry, its new index
-    uint64_t dk, dv;   // new key / value byte offsets of the span's first entry
-    uint64_t cnt;      // entries
-};
-
-__global__ void k_merge_spans_build(MergeArgs a, const uint32_t *pos, const BatchSums *bx, const SegSums *sx, MergeOut o,
-                                    MergeSpan *spans) {
-    for (uint64_t s = gtid(); s <= a.S; s += gstride()) {
-        const SegSums base = sx[s];
-        o.seg_off[s] = base.v[0];
-        o.seg_voff[s] = base.v[2];
-        if (s == a.S) { o.koff[base.v[0]] = base.v[1]; o.voff[base.v[0]] = base.v[2]; break; }
-        const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
-        uint64_t nold = a.seg_off ? a.seg_off[s + 1] - i0 : 0;
-        if (a.seg_replace && a.seg_replace[s]) nold = 0;
-        if (!nold) continue;
-        MergeSpan *sp = spans + base.v[3];
-        uint64_t li = 0, de = base.v[0], dk = base.v[1], dv = base.v[2];
-        const uint64_t k0 = a.koff[i0], v0 = a.voff[i0];
-        uint64_t kli = k0, vli = v0;   // koff / voff of old entry li
-        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-        if (!(a.seg_reject && a.seg_reject[s])) {
-            for (uint64_t j = j0; j < je; j++) {
-                if (!a.keep[j]) continue;
-                const BatchSums &B = bx[j], &B1 = bx[j + 1];
-                const uint64_t p = pos[j];
-                const uint64_t kp = a.koff[i0 + p], vp = a.voff[i0 + p];
-                *sp++ = MergeSpan{i0 + li, de, dk, dv, p - li};
-                de += p - li; dk += kp - kli; dv += vp - vli;
-                // the record itself (k_merge_new writes it): one entry if it is not an ERASE
-                de += B1.v[BS_NE] - B.v[BS_NE];
-                dk += B1.v[BS_KN] - B.v[BS_KN];
-                dv += B1.v[BS_VN] - B.v[BS_VN];
-                if (B1.v[BS_EQ] != B.v[BS_EQ]) {   // the old entry at p is replaced or erased
-                    li = p + 1;
-                    kli = a.koff[i0 + li];
-                    vli = a.voff[i0 + li];
-                } else {
-                    li = p;
-                    kli = kp;
-                    vli = vp;
-                }
-            }
-        }
-        *sp = MergeSpan{i0 + li, de, dk, dv, nold - li};
-    }
-}
-
-__global__ void __launch_bounds__(256) k_merge_spans_copy(MergeArgs a, const MergeSpan *spans, uint64_t nspans, MergeOut o) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwv = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t w = w0; w < nspans; w += nwv) {
-        const MergeSpan sp = spans[w];
-        if (!sp.cnt) continue;
-        const uint64_t sk = a.koff[sp.se], ek = a.koff[sp.se + sp.cnt];
-        const uint64_t sv = a.voff[sp.se], ev = a.voff[sp.se + sp.cnt];
-        const int64_t ddk = (int64_t)sp.dk - (int64_t)sk, ddv = (int64_t)sp.dv - (int64_t)sv;
-        for (uint64_t i = lane; i < sp.cnt; i += 64) {
-            o.koff[sp.de + i] = (uint64_t)((int64_t)a.koff[sp.se + i] + ddk);
-            o.voff[sp.de + i] = (uint64_t)((int64_t)a.voff[sp.se + i] + ddv);
-        }
-        const uint64_t nk = ek - sk, nv = ev - sv;
-        for (uint64_t c = (uint64_t)lane * 16; c < nk; c += 1024) {
-            if (c + 16 <= nk) {
-                uint4 x;
-                __builtin_memcpy(&x, a.kheap + sk + c, 16);
-                __builtin_memcpy(o.kheap + sp.dk + c, &x, 16);
-            } else {
-                for (uint64_t b = c; b < nk; b++) o.kheap[sp.dk + b] = a.kheap[sk + b];
-            }
-        }
-        for (uint64_t c = (uint64_t)lane * 16; c < nv; c += 1024) {
-            if (c + 16 <= nv) {
-                uint4 x;
-                __builtin_memcpy(&x, a.vheap + sv + c, 16);
-                __builtin_memcpy(o.vheap + sp.dv + c, &x, 16);
-            } else {
-                for (uint64_t b = c; b < nv; b++) o.vheap[sp.dv + b] = a.vheap[sv + b];
-            }
-        }
-    }
-}
-
 __global__ void k_seg_voff(const uint64_t *seg_off, const uint64_t *voff, uint64_t S, uint64_t *seg_voff) {
     for (uint64_t s = gtid(); s <= S; s += gstride()) seg_voff[s] = voff[seg_off[s]];
 }
@@ -862,7 +764,7 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 // its entries differ.  k_cmp_walk evaluates it per node, verifies every
 // visited node on both sides against its parent's entry (exchange_get's
 // verified_hashes, synctree.erl:288-298) and merge-joins every visited
-// segment pair (exchange_final); the last workgroup concatenates the per-wave
+// segment pair (exchange_final); k_cmp_gather concatenates the per-wave
 // record regions.  Only the entries under visited nodes beyond level H are
 // read.  err: min over (level, bucket, side) of a failed verification -- the
 // reference's first crash in visiting order (local before remote).
@@ -1152,7 +1054,6 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
 // LDS of a compare-walk wave: the shared area (lane regions for inner-node
 // staging / the merge-join), then the work list, then per-level counters
 #define CMP_LIST 256
-#define CMP_PRE 7       // the walk preloads the frontier of trees up to this height
 __host__ __device__ __forceinline__ uint32_t cmp_shared_bytes(uint32_t W) {
     const uint32_t a = 64 * lane_region_bytes(W), m = cmp_merge_lds_bytes();
     return ((a > m ? a : m) + 15) & ~15u;
@@ -1320,77 +1221,13 @@ __device__ __forceinline__ void cmp_append(uint64_t *list, uint32_t &n, bool f, 
     n += (uint32_t)__popcll(m);
 }
 
-// The compare's result for the host (fine-grained host memory): ONE record
-// written last by the gathering workgroup, validated by the host (sequence
-// number + check word), so it never depends on the order in which two GPU
-// stores reach host memory (small_path.h).
-struct CmpRes {
-    uint64_t seq, total, maxw, err, check;
-};
-__host__ __device__ __forceinline__ uint64_t cmp_res_check(uint64_t seq, uint64_t a, uint64_t b, uint64_t c) {
-    uint64_t h = seq * 0x9E3779B97F4A7C15ull ^ 0xD6E8FEB86659FD93ull;
-    h = (h ^ a) * 0xBF58476D1CE4E5B9ull;
-    h = (h ^ (h >> 31) ^ b) * 0x94D049BB133111EBull;
-    h = (h ^ (h >> 29) ^ c) * 0xBF58476D1CE4E5B9ull;
-    return (h ^ (h >> 32)) | 1ull;
-}
-
-// The gather (the waves' record regions -> the record buffer, wave w after
-// every higher wave, and the CmpRes) by the LAST workgroup of the walk to
-// finish: one counter, no second launch.
-__device__ __forceinline__ void cmp_gather_last(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
-                                                const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
-                                                CmpRes *res, uint64_t seq, uint64_t *above) {
-    const uint32_t tid = threadIdx.x, nt = blockDim.x;
-    __shared__ uint64_t s_tot, s_max, s_err;
-    if (tid == 0) { s_tot = 0; s_max = 0; s_err = ~0ull; }
-    __syncthreads();
-    // above[v] = records of the waves after v (in LDS); reduce the maximum and the first error
-    uint64_t mx = 0, em = ~0ull;
-    for (uint32_t v = tid; v < nw; v += nt) {
-        const uint64_t c = wcnt[v], e = werr[v];
-        above[v] = c;
-        mx = c > mx ? c : mx;
-        em = e < em ? e : em;
-    }
-    atomicMax(reinterpret_cast<unsigned long long *>(&s_max), (unsigned long long)mx);
-    atomicMin(reinterpret_cast<unsigned long long *>(&s_err), (unsigned long long)em);
-    __syncthreads();
-    if (tid == 0) {   // suffix sums (nw <= a few thousand)
-        uint64_t acc = 0;
-        for (uint32_t v = nw; v-- > 0;) {
-            const uint64_t c = above[v];
-            above[v] = acc;
-            acc += c;
-        }
-        s_tot = acc;
-    }
-    __syncthreads();
-    const uint64_t tot = s_tot, mxw = s_max, err = s_err;
-    if (mxw <= R && tot <= cap && err == ~0ull)   // else the host grows the buffers and runs again
-        for (uint32_t v = tid; v < nw; v += nt) {
-            const uint64_t c = wcnt[v], a = above[v];
-            const DiffRec *src = scratch + (uint64_t)v * R;
-            for (uint64_t k = 0; k < c; k++) out[a + k] = src[k];
-        }
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence_system();   // the records are in the buffer before the host reads the count
-        CmpRes r;
-        r.seq = seq; r.total = tot; r.maxw = mxw; r.err = err; r.check = cmp_res_check(seq, tot, mxw, err);
-        *res = r;
-        __threadfence_system();
-    }
-}
-
 __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2, uint32_t nw,
                                                  uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *wcnt,
-                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps,
-                                                 uint32_t *done, DiffRec *out, uint64_t cap, CmpRes *res, uint64_t seq) {
+                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + wave;
-    if (w < nw) {
+    if (w >= nw) return;
     uint8_t *wl = lds + (uint64_t)wave * slice;
     const uint32_t H = A.H, L1 = H + 1, sh = A.shift, W = A.W;
     CmpWalk c;
@@ -1437,28 +1274,6 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         for (uint64_t c0 = h0 + ((h1 - h0 - 1) & ~63ull);; c0 -= 64) {
             const uint64_t c1 = c0 + 64 < h1 ? c0 + 64 : h1;   // level-H nodes [c0, c1)
             bool f = true;       // this lane's node flag at the previous level (level 1: the root)
-            // every level's entries of the chunk in ONE round trip (H <= CMP_PRE):
-            // a lane's node at level l is lo_l + lane; the flags are then
-            // evaluated top-down from registers
-            uint32_t pdiff = 0;  // bit l: this lane's level-l entry differs (and is in range)
-            if (H <= CMP_PRE) {
-                uint16_t ta[CMP_PRE + 1], tb[CMP_PRE + 1];
-                uint4 xa[CMP_PRE + 1], xb[CMP_PRE + 1];
-#pragma unroll
-                for (uint32_t l = 2; l <= CMP_PRE; l++) {
-                    ta[l] = tb[l] = 0;
-                    if (l > H) continue;
-                    const uint32_t up = sh * (H - l);
-                    const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up, b = lo + lane;
-                    if (b <= hi && !(l == 2 && (b < lo2 || b >= hi2))) {
-                        const uint64_t slot = A.base[l] + b;
-                        ta[l] = A.tag[slot]; tb[l] = B.tag[slot]; xa[l] = A.md5[slot]; xb[l] = B.md5[slot];
-                    }
-                }
-#pragma unroll
-                for (uint32_t l = 2; l <= CMP_PRE; l++)
-                    if (l <= H && entry_differs(ta[l], tb[l], xa[l], xb[l], filter)) pdiff |= 1u << l;
-            }
             for (uint32_t l = 2; l <= H; l++) {
                 const uint32_t up = sh * (H - l);
                 const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
@@ -1466,7 +1281,7 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
                 const uint64_t plo = lo >> sh;
                 const uint32_t plane = (uint32_t)((b >> sh) - plo);
                 const bool fp = __shfl((int)f, (int)(plane < 64 ? plane : 0), 64) != 0;
-                f = b <= hi && fp && (H <= CMP_PRE ? ((pdiff >> l) & 1u) != 0 : cmp_entry_in(A, B, filter, l, b, lo2, hi2));
+                f = b <= hi && fp && cmp_entry_in(A, B, filter, l, b, lo2, hi2);
                 const bool owned = f && (b << up) >= c0 && (b << up) < c1;
                 if (n + 64 > CMP_LIST) { cmp_flush(A, B, c, n); n = 0; }
                 const uint32_t n0 = n;
@@ -1516,23 +1331,64 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         werr[w] = em;
     }
     for (uint32_t l = lane; l < ST_STATW; l += 64) wst[(uint64_t)w * ST_STATW + l] = (l >= 1 && l <= L1) ? c.cnt[l] : 0;
-    }   // w < nw
-    // the last workgroup to finish gathers (release: this workgroup's records
-    // and counts are visible to it; acquire in the last one before it reads)
-    __shared__ uint32_t s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const uint32_t old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old + 1 == gridDim.x;
-        if (s_last) {
-            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __threadfence();
+}
+
+// The waves' regions -> the record buffer (wave w after every higher wave).
+// Wave 0 also reduces the per-wave results into res (host-mapped): the
+// total, the largest per-wave count (the scratch a rerun needs when it
+// exceeds R) and the first failed verification.  A wave per region.
+__global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
+                                                   const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
+                                                   uint64_t *res) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nw) return;
+    uint64_t above = 0;
+    for (uint32_t v0 = w + 1; v0 < nw; v0 += 1024) {   // 16 loads per lane in flight
+        uint64_t x[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const uint32_t v = v0 + u * 64 + lane;
+            x[u] = v < nw ? wcnt[v] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) above += x[u];
+    }
+    for (int o = 32; o; o >>= 1) above += __shfl_xor(above, o, 64);
+    const uint64_t n = wcnt[w];
+    if (w == 0) {
+        uint64_t mx = 0, em = ~0ull;
+        for (uint32_t v0 = 0; v0 < nw; v0 += 512) {
+            uint64_t x[8], y[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t v = v0 + u * 64 + lane;
+                x[u] = v < nw ? wcnt[v] : 0;
+                y[u] = v < nw ? werr[v] : ~0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                mx = x[u] > mx ? x[u] : mx;
+                em = y[u] < em ? y[u] : em;
+            }
+        }
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t x = __shfl_xor(mx, o, 64), y = __shfl_xor(em, o, 64);
+            mx = x > mx ? x : mx;
+            em = y < em ? y : em;
+        }
+        if (lane == 0) {
+            res[0] = above + n;
+            res[1] = mx;
+            res[2] = em;
+            __threadfence_system();
+            res[3] = 1;   // the host spins on this word
+            __threadfence_system();
         }
     }
-    __syncthreads();
-    if (!s_last) return;
-    cmp_gather_last(nw, wcnt, werr, scratch, R, out, cap, res, seq, reinterpret_cast<uint64_t *>(lds));
+    if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
+    const DiffRec *src = scratch + (uint64_t)w * R;
+    for (uint64_t k = lane; k < n; k += 64) out[above + k] = src[k];
 }
 
 // Diff records -> byte lengths of key / local value / remote value
@@ -2009,7 +1865,6 @@ struct TreeTiles {
     const TileInfo *tinfo;
     const uint32_t *tseg, *tln;
     const uint4 *tiles;
-    const uint64_t *pres;   // per-window segment presence bitmaps (k_rehash_prog)
 };
 
 

@@ -22,7 +22,6 @@
 
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
-#include "rehash_prog.h"
 #include "leveldb_fmt.h"
 #include "small_path.h"
 
@@ -49,9 +48,7 @@ struct CmpWork {
     uint64_t R = 0;                  // scratch records per wave
     uint64_t *wcnt = nullptr, *wbytes = nullptr, *werr = nullptr;
     uint32_t *wst = nullptr;         // [nw][ST_STATW] visited nodes per level
-    uint32_t *done = nullptr;        // workgroups finished (the last one gathers; self-resetting)
-    CmpRes *res = nullptr, *res_dev = nullptr;   // host-mapped result record
-    uint64_t seq = 0;                // compares run (the result record's sequence number)
+    uint64_t *res = nullptr, *res_dev = nullptr;   // host-mapped: total, max per-wave count, first error
     DiffRec *rec = nullptr, *scratch = nullptr;
     uint64_t cap = 0;
 };
@@ -103,7 +100,6 @@ struct st_tree {
     uint64_t tiles_cap = 0;         // uint4 units
     uint32_t *tseg = nullptr, *tln = nullptr;
     TileInfo *tinfo = nullptr;
-    uint64_t *tpres = nullptr;      // per-window segment presence (k_rehash_prog)
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
@@ -615,7 +611,7 @@ extern "C" void st_destroy(st_tree *t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->tpres, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
@@ -776,18 +772,6 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // at most 256 nodes at level H-3 (H <= 6)
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
-// Full-rehash kernel for the fused geometry: k_rehash_prog (ST_REHASH=prog:
-// window levels hashed progressively while the segments are; class-ordered
-// tiles), or k_rehash_fused (levels after K1; length-ordered tiles).  Read
-// once per process, so the tile order and the kernel always agree.
-static bool use_prog() {
-    static const bool p = [] {
-        const char *e = getenv("ST_REHASH");
-        return e && !strcmp(e, "prog");
-    }();
-    return p;
-}
-
 static int ensure_tiles(st_tree *t) {
     if (t->tiles_valid) return ST_OK;
     if (!fused_geometry(t)) CHK(ensure_perm(t));
@@ -797,16 +781,12 @@ static int ensure_tiles(st_tree *t) {
         CHK(dalloc_t(t, &t->tln, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
-    if (fused_geometry(t) && use_prog() && !t->tpres) CHK(dalloc_t(t, &t->tpres, t->S / 64));
     Scratch sc(t);
     uint64_t *tsize = nullptr, *tbase = nullptr;
     CHK(sc.alloc(&tsize, ntiles + 1));
     CHK(sc.alloc(&tbase, ntiles + 1));
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
-    if (fused_geometry(t) && use_prog())   // window-local class order + presence (k_rehash_prog)
-        LAUNCH(t, "tile_build", k_tile_order_cls, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
-               tsize, t->tpres);
-    else if (fused_geometry(t))   // window-local order (k_rehash_fused)
+    if (fused_geometry(t))   // window-local order (k_rehash_fused)
         LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
                tsize);
     else
@@ -841,7 +821,6 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tseg = t->tseg;
     x.tln = t->tln;
     x.tiles = t->tiles;
-    x.pres = t->tpres;
     return x;
 }
 
@@ -908,12 +887,8 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            if (use_prog())
-                LAUNCH(t, "rehash_fused", (k_rehash_prog<false, false>), nwg, 1024, prog_lds_bytes(), d, tree_tiles(t),
-                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
-            else
-                LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                       (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
@@ -921,12 +896,8 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 32));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
-        if (use_prog())
-            LAUNCH(t, "rehash_fused", (k_rehash_prog<true, false>), nwg, 1024, prog_lds_bytes(), d, tree_tiles(t),
-                   (const TreeTiles *)nullptr, 0u, root0, lmin, st);
-        else
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                   (const TreeTiles *)nullptr, 0u, root0, lmin, st);
+        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+               (const TreeTiles *)nullptr, 0u, root0, lmin, st);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         CHK(tsync(t));
@@ -941,13 +912,9 @@ static int rehash_tiled(st_tree *t) {
                 fclose(f);
             }
         }
-        static const char *fnames[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
-                                         "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
-                                         "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
-        static const char *pnames[16] = {"start", "staged", "w0 no tiles", "all tiles", "copy-out", "h1 waves 0-2",
-                                         "root prefix", "w15 h1 done", "root done", "cnt won", "mail read",
-                                         "climb lvl 1", "climb lvl 2", "-", "-", "exit"};
-        const char *const *names = use_prog() ? pnames : fnames;
+        static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
+                                        "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
+                                        "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
         for (int k = 0; k < 16; k++) {
             std::vector<double> v;
             for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
@@ -1040,11 +1007,6 @@ struct IngestIn {
     uint32_t *seg_out;
     uint64_t n_rejected;
 };
-
-static int merge_mode() {
-    static const int v = getenv("ST_MERGE") ? atoi(getenv("ST_MERGE")) : 0;
-    return v;
-}
 
 static int ingest(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
@@ -1147,19 +1109,8 @@ static int ingest(st_tree *t, IngestIn &in) {
     MergeOut mo;
     mo.seg_off = out.o.seg_off; mo.seg_voff = out.o.seg_voff; mo.koff = out.o.koff; mo.voff = out.o.voff;
     mo.kheap = out.o.kheap; mo.vheap = out.o.vheap;
-    if (merge_mode() == 1) {   // A/B: the entry-by-entry walk
-        LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
-               (const BatchSums *)bx, (const SegSums *)sx, mo);
-    } else {
-        const uint64_t nspans = tot.v[3];
-        MergeSpan *spans = nullptr;
-        CHK(sc.alloc(&spans, nspans + 1));
-        LAUNCH(t, "merge_spans", k_merge_spans_build, grid_for(S + 1), 256, 0, ma, (const uint32_t *)mpos,
-               (const BatchSums *)bx, (const SegSums *)sx, mo, spans);
-        if (nspans)
-            LAUNCH(t, "merge_write", k_merge_spans_copy, grid_for(nspans * 64, 256, 8192), 256, 0, ma,
-                   (const MergeSpan *)spans, nspans, mo);
-    }
+    LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
+           (const BatchSums *)bx, (const SegSums *)sx, mo);
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
@@ -1716,12 +1667,8 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const uint32_t nwin = (uint32_t)(t->S / 4096);
     const uint64_t nwg = (uint64_t)nwin * n;
     if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
-    if (use_prog())
-        LAUNCH(t, "rehash_group", (k_rehash_prog<false, true>), (uint32_t)nwg, 1024, prog_lds_bytes(), view(t), h[0],
-               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
-    else
-        LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
-               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
+    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
+           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
     CHK(tsync(t));
     for (uint32_t i = 0; i < n; i++) {
         CHK(erec_after_rehash(trees[i]));
@@ -2256,25 +2203,13 @@ static int ensure_cmp_work(st_tree *t) {
     CHK(dalloc_t(t, &w.wbytes, w.nw));
     CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
     CHK(dalloc_t(t, &w.werr, w.nw));
-    CHK(dalloc_t(t, &w.done, 1));
-    HIPCHK(hipMemsetAsync(w.done, 0, 4, t->stream));
-    if (hipHostMalloc((void **)&w.res, sizeof(CmpRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         w.res = nullptr;
         g_err = "hipHostMalloc failed";
         return ST_EDEVICE;
     }
-    memset(w.res, 0, sizeof(CmpRes));
     HIPCHK(hipHostGetDevicePointer((void **)&w.res_dev, w.res, 0));
     return ST_OK;
-}
-
-// The walk's result record, once it carries `seq` and a valid check.
-static bool cmp_res_ready(const CmpRes *r, uint64_t seq, uint64_t *tot, uint64_t *mx, uint64_t *err) {
-    const volatile uint64_t *v = reinterpret_cast<const volatile uint64_t *>(r);
-    const uint64_t s0 = v[0], a = v[1], b = v[2], c = v[3], k = v[4];
-    if (s0 != seq || k != cmp_res_check(s0, a, b, c)) return false;
-    *tot = a; *mx = b; *err = c;
-    return true;
 }
 
 // record buffer >= cap records, scratch >= nw * R records
@@ -2340,10 +2275,8 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             CHK(sc.alloc(&stamps, (uint64_t)w.nw * 8));
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 64, t->stream));
         }
-        const uint64_t seq = ++w.seq;
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
-               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps, w.done, w.rec, w.cap,
-               w.res_dev, seq);
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 8);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
@@ -2362,18 +2295,11 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
                         v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
         }
-        // spin on the result record; after 5 ms a stream synchronisation
-        uint64_t ntot = 0, need = 0, e = 0;
-        bool ok = false;
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t i = 0; !(ok = cmp_res_ready(w.res, seq, &ntot, &need, &e)); i++) {
-            if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
-            __builtin_ia32_pause();
-        }
-        if (!ok) {
-            CHK(tsync(t));
-            if (!cmp_res_ready(w.res, seq, &ntot, &need, &e)) { g_err = "compare result record incomplete"; return ST_EDEVICE; }
-        }
+        w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
+        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4, 256, 0, w.nw, (const uint64_t *)w.wcnt,
+               (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
+        CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
+        const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
         if (e != ~0ull) {
             *status = ST_CORRUPTED;
             *clevel = (uint32_t)(e >> 56);
