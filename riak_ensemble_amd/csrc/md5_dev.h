@@ -134,11 +134,14 @@ __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
 
 // Keep the `valid` leading bytes of little-endian word w (0..4 valid), put
 // the 0x80 terminator right after them when they end inside this word.
+// Branch-free (selects only): lanes of a wave hold messages of different
+// lengths, and a per-lane branch per word would run every path.
 __device__ __forceinline__ uint32_t tail_word(uint32_t w, int valid) {
-    if (valid >= 4) return w;
-    if (valid < 0) return 0u;
-    uint32_t keep = valid == 0 ? 0u : (0xffffffffu >> (32 - 8 * valid));
-    return (w & keep) | (0x80u << (8 * valid));
+    const int v = valid < 0 ? -1 : (valid > 4 ? 4 : valid);
+    const uint32_t n = v < 0 ? 0u : (uint32_t)v;                    // bytes kept, 0..4
+    const uint32_t keep = (uint32_t)(0xffffffffull >> (32 - 8 * n));
+    const uint32_t term = (v >= 0 && v < 4) ? (0x80u << (8 * n)) : 0u;
+    return (w & keep) | term;
 }
 
 // Apply MD5 padding to block k of a `len`-byte message whose raw words
@@ -236,6 +239,42 @@ __device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t
         }
         if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
         compress(st, m);
+    }
+    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
+}
+
+// MD5 of an inner node's message (the present children's 17-byte entries,
+// at most 16 x 17 = 272 bytes) staged at a 16-byte aligned LDS address and
+// readable up to byte 320: at most 5 blocks, unrolled, each read with four
+// 16-byte LDS loads (the garbage past len is replaced by the padding).
+__device__ __forceinline__ void md5_lds_node(const uint8_t *p, uint32_t len, uint32_t out[4]) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    const uint32_t nblk = (len + 8) / 64 + 1;
+    uint32_t st[4];
+    init(st);
+    // block k + 1's reads are issued before block k is compressed
+    uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if ((uint32_t)k < nblk) {
+            uint32_t m[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+            if (k < 4 && (uint32_t)k + 1 < nblk) {
+                __asm__ volatile("" ::: "memory");   // only one block ahead (not all 20 reads hoisted: 80 VGPRs)
+                a = q[4 * k + 4]; b = q[4 * k + 5]; c = q[4 * k + 6]; d = q[4 * k + 7];
+            }
+            const int32_t rem = (int32_t)len - 64 * k;
+            if (k == 4 && __ballot(len != 272) == 0) {
+                // every lane of the wave holds a node with 16 children: the
+                // last block is 16 data bytes, the terminator, the bit length
+                m[4] = 0x80u;
+#pragma unroll
+                for (int w = 5; w < 16; w++) m[w] = 0u;
+                m[14] = 272u * 8u;
+            } else if (rem < 64) {
+                pad_block(m, rem, (uint32_t)k + 1 == nblk, len);
+            }
+            compress(st, m);
+        }
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }

@@ -1865,6 +1865,7 @@ struct TreeTiles {
     const TileInfo *tinfo;
     const uint32_t *tseg, *tln;
     const uint4 *tiles;
+    const uint64_t *pres;   // per-window segment presence bitmaps (tile build)
 };
 
 
@@ -1943,108 +1944,15 @@ __global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint
     tile_shape(ln, tl, (threadIdx.x & 63) == 0 && tl < ntiles, tinfo, tsize);
 }
 
-// ---------------------------------------------------------------------------
-// Fused full rehash (W == 16, H >= 3): K1 and the inner levels in ONE launch.
-//
-// One workgroup of 1024 threads per WINDOW = level-(H-2) subtree (4096
-// segments, 64 tiles built in window-local block-count order by
-// k_tile_order_window).  Phase 1 (K1): wave w hashes tiles w, w+16, w+32 and
-// w+48 of its window as one flat stream of MD5 blocks with two blocks in
-// flight (the loads of block f+2 are issued before block f is compressed),
-// and leaves each segment's entry in LDS in the node-block layout of
-// k_levels3_16.  Phase 2: the 4096 entries are copied to the slot arrays with
-// coalesced 16-B stores (one line-sized write per 8 entries instead of a
-// scattered 16-B + 2-B pair per segment).  Phase 3: levels H, H-1, H-2 of the
-// window from LDS (rehash/4, synctree.erl:515-535), then lane 0 climbs while
-// it is the last of 16 siblings to finish (cnt[slot] counts finished children
-// of inner node `slot`, levels 1..H-3; the last arriver resets it), hashing
-// the parent from global memory up to level lmin (1: the top hash; 2: a
-// segment-range partition stops at its level-2 entries).
-// Children come through generic pointers (LDS for phases 0-2, global for the
-// climb), so every level runs the same instructions.  Release/acquire fences
-// at agent scope around the counter make entries written by workgroups on
-// other XCDs (other L2s) visible to the climbing lane.
-// ent / tags point at LDS: the entries are read where the message needs them
-// (no 64-VGPR register copy of the node); reg must not overlap ent.
-__device__ __forceinline__ void node16_any(const uint4 *ent, const uint16_t *tags, uint8_t *reg, uint4 &e, uint32_t &tg) {
-    const uint4 *h = ent;
-    uint32_t t16[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) t16[j] = tags[j];
-    uint32_t pm = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) pm |= ((t16[j] >> 8) & 1u) << j;
-    const uint32_t np = __builtin_popcount(pm);
-    uint32_t dg[4];
-    // The path is chosen per WAVE, not per lane: a wave whose active lanes
-    // all hold nodes with 15 or 16 present children hashes from registers
-    // (md5_node16, the common case in big trees: an empty segment leaves its
-    // level-H parent with 15); otherwise every lane packs its present entries
-    // into its LDS region and hashes from there.  Lanes of one wave never
-    // split between the two paths (that would run both, one after the other).
-    if (__ballot(np < 15) == 0) {
-        uint32_t pf[16];
-        uint4 hr[16];   // one LDS round trip for the whole node
-#pragma unroll
-        for (int j = 0; j < 16; j++) { pf[j] = t16[j] & 0xffu; hr[j] = h[j]; }
-        if (__ballot(np == 15)) {
-            // one absent child ja: the entries after it move down one place
-            // (selects with compile-time indices, no register indexing)
-            const uint32_t ja = np == 15 ? (uint32_t)__builtin_ctz(~pm & 0xffffu) : 16u;
-#pragma unroll
-            for (int r = 0; r < 15; r++)
-                if ((uint32_t)r >= ja) { hr[r] = hr[r + 1]; pf[r] = pf[r + 1]; }
-            if (np == 15) { hr[15] = make_uint4(0, 0, 0, 0); pf[15] = 0x80u; }
-        }
-        stmd5::md5_node16<true>(pf, hr, dg, np);
-        tg = TAG_PRESENT;
-        e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-        return;
-    }
-    MsgWriter mw;
-    mw.init(reg);
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-        if (t16[j] & TAG_PRESENT) mw.entry(t16[j], h[j]);
-    const uint32_t len = mw.finish();
-    tg = len ? TAG_PRESENT : 0u;
-    e = make_uint4(0, 0, 0, 0);
-    if (!len) return;
-    stmd5::md5_lds(reg, len, dg);
-    e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
-}
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-#define RF_TILES 4   // tiles per wave: 64 tiles per window / 16 waves
-
-__device__ __forceinline__ void tile_block_load(const uint4 *tiles, uint64_t base, uint32_t R, uint32_t ln, uint32_t lane,
-                                                uint32_t k, uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
-    a = tile_row(tiles, base, lane, 4 * k, R, ln);
-    b = tile_row(tiles, base, lane, 4 * k + 1, R, ln);
-    c = tile_row(tiles, base, lane, 4 * k + 2, R, ln);
-    d = tile_row(tiles, base, lane, 4 * k + 3, R, ln);
-}
-
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
-// operations, not for its global stores (those are read by later kernels or,
-// for the climb, published by an explicit vmcnt wait before the counter).
+// operations, not for its global loads and stores.
 __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// LDS of k_rehash_fused: the k_levels3_16 node blocks, then one 272-byte
-// message region per level-H node (a node's message may not be packed over its
-// own entries: they are read from LDS while the message is written).
-#define MSG16 272
-__host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return levels3_16_lds_bytes() + 256 * MSG16 + 64; }
-
-// STAMP (diagnostic, ST_LEVEL_STAMPS=1): wall-clock stamps (100 MHz) per
-// workgroup at phase boundaries into stamps[blockIdx.x * 32 + k], the shader
-// clock (s_memtime) at the same points into [.. + 16 + k] (thread 0's
-// view: 0 start, 1 K1 done, 2/4/6 level H/H-1/H-2 hashed, 3/5 level H/H-1
-// barrier passed, 7 mailbox stored, 8/12 climb counter won, 9/13 mailboxes
-// read, 10/14 level 2/1 hashed, 11 level-2 mailbox stored, 15 exit).
+// Mailbox of one inner-node entry read by another workgroup (possibly on
+// another XCD, behind another L2): agent-scope atomics, coherent across XCDs
+// without a write-back of the writer's L2 or an invalidate of the reader's.
 __device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg) {
     __hip_atomic_store(&m->lo, ((unsigned long long)e.y << 32) | e.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&m->hi, ((unsigned long long)e.w << 32) | e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2058,281 +1966,15 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
     e = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// GROUP: the windows of many trees of one geometry in one launch (the
-// ensembles one GPU hosts, riak_ensemble_peer.erl:1845-1846): workgroup g
-// takes window g % nwin of tree group[g / nwin], each tree with its own slot
-// arrays, tiles, counters and mailboxes.
-template <bool STAMP, bool GROUP>
-__global__ void __launch_bounds__(1024) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
-                                                       uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
-#define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-                                                          stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
-    RF_STAMP(0);
-    const uint32_t gi = GROUP ? blockIdx.x / nwin : 0;
-    const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
-    // the tree's arrays, read where used (kernel arguments, or the group
-    // entry through the scalar cache): no long-lived pointer registers
-#define RFT(f) (GROUP ? group[gi].f : tt0.f)
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *A = lds;
-    uint8_t *At = A + 256 * NB16;
-    uint8_t *Bb = At + 256 * TB16;
-    uint8_t *Bt = Bb + 16 * NB16;
-    uint8_t *Cb = Bt + 16 * TB16;
-    uint8_t *Ct = Cb + NB16;
-    uint8_t *M = lds + levels3_16_lds_bytes();   // message regions
-    // wave-uniform values in scalar registers: the tile bookkeeping of the
-    // block stream below then runs on the scalar unit with scalar branches
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t H = t.H;
-    const uint64_t seg0 = root * 4096;
-
-    // ---- phase 1: K1 over this wave's tiles, one flat block stream
-    uint32_t Bq[RF_TILES], Rq[RF_TILES], RLq[RF_TILES], lnq[RF_TILES], liq[RF_TILES];
-    uint64_t bq[RF_TILES];
-    uint32_t T = 0;   // blocks in the wave's stream
-#pragma unroll
-    for (int q = 0; q < RF_TILES; q++) {
-        // snake order over the window's tiles (longest first): wave w takes
-        // w, 31 - w, 32 + w, 63 - w, which evens out the waves' block counts
-        const uint64_t tl = root * 64 + 16 * q + ((q & 1) ? 15 - wave : wave);
-        const TileInfo ti = RFT(tinfo)[tl];
-        Bq[q] = __builtin_amdgcn_readfirstlane(ti.B);
-        Rq[q] = __builtin_amdgcn_readfirstlane(ti.R);
-        RLq[q] = __builtin_amdgcn_readfirstlane(ti.R ? ti.R - 1 : 0);   // the last stored row (fetch clamp)
-        const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)ti.base),
-                       bhi = __builtin_amdgcn_readfirstlane((uint32_t)(ti.base >> 32));
-        bq[q] = ((uint64_t)bhi << 32) | blo;
-        liq[q] = (uint32_t)(RFT(tseg)[tl * 64 + lane] - seg0);
-        lnq[q] = RFT(tln)[tl * 64 + lane];
-        T += Bq[q];
-    }
-    auto pick = [&](const uint32_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
-    auto pick64 = [&](const uint64_t *v, uint32_t q) { return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3]; };
-    auto put_entry = [&](uint32_t li, uint32_t nb, const uint32_t st[4]) {
-        uint4 e = make_uint4(0, 0, 0, 0);
-        uint16_t tg = 0;
-        if (nb) { e = make_uint4(st[0], st[1], st[2], st[3]); tg = (uint16_t)TAG_PRESENT; }
-        *reinterpret_cast<uint4 *>(A + (li >> 4) * NB16 + (li & 15) * 16) = e;
-        *reinterpret_cast<uint16_t *>(At + (li >> 4) * TB16 + (li & 15) * 2) = tg;
-    };
-    {
-        // Two cursors walk the wave's tiles: the fetch cursor (lq, lk) two
-        // blocks ahead of the hash cursor (cq, ck).  Per-tile values are
-        // picked only when a cursor crosses into the next tile (wave-uniform:
-        // scalar registers and branches); per block the hash cursor costs one
-        // compare.
-        auto next_tile = [&](uint32_t q) {
-            while (q < RF_TILES && pick(Bq, q) == 0) q++;
-            return q;
-        };
-        uint32_t lq = next_tile(0), lk = 0, lL = 0, lB = 0;
-        uint64_t lbase = 0;
-        if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
-        // Always four loads per block (rows past the stored ones re-read the
-        // last stored row; hash_block replaces them), so the wait before a
-        // buffer is hashed leaves the other buffer's four loads in flight.
-        auto fetch = [&](uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
-            // row bases are wave-uniform (scalar address arithmetic); the lane
-            // offset is the only per-lane part of each load
-            const uint32_t r = 4 * lk, last = lL;
-            const uint4 *p = RFT(tiles) + lbase;
-            a = (p + (uint64_t)(r < last ? r : last) * 64)[lane];
-            b = (p + (uint64_t)(r + 1 < last ? r + 1 : last) * 64)[lane];
-            c = (p + (uint64_t)(r + 2 < last ? r + 2 : last) * 64)[lane];
-            d = (p + (uint64_t)(r + 3 < last ? r + 3 : last) * 64)[lane];
-            if (lq >= RF_TILES) return;   // past the stream: a dummy fetch (the loop's fixed load pattern)
-            if (++lk == lB) {
-                lk = 0;
-                lq = next_tile(lq + 1);
-                if (lq < RF_TILES) { lbase = pick64(bq, lq); lL = pick(RLq, lq); lB = pick(Bq, lq); }
-            }
-        };
-        // Ping-pong buffers, no register rotation: hashing buffer A waits only
-        // for A's loads (vmcnt leaves B's four in flight), then A is refilled
-        // with the block after B, and so on.
-        uint4 a0, a1, a2, a3, b0, b1, b2, b3;
-        fetch(a0, a1, a2, a3);
-        fetch(b0, b1, b2, b3);
-        uint32_t cq = next_tile(0), ck = 0, cB = 0, cR = 0, cnb = 0, cln = 0;
-        if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
-        uint32_t st[4];
-        stmd5::init(st);
-        auto hash_block = [&](const uint4 &x0, const uint4 &x1, const uint4 &x2, const uint4 &x3) {
-            const uint32_t r = 4 * ck;
-            if (r + 3 >= cR) {   // rows past the stored ones (a tile's last block or two)
-                const uint4 y0 = r >= cR ? tile_synth(r, cln) : x0, y1 = r + 1 >= cR ? tile_synth(r + 1, cln) : x1,
-                            y2 = r + 2 >= cR ? tile_synth(r + 2, cln) : x2, y3 = tile_synth(r + 3, cln);
-                const uint32_t m[16] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
-                                        y2.x, y2.y, y2.z, y2.w, y3.x, y3.y, y3.z, y3.w};
-                if (ck < cnb) stmd5::compress<true>(st, m);
-            } else {             // the common case: the loaded registers feed the compression as they are
-                const uint32_t m[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
-                                        x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
-                if (ck < cnb) stmd5::compress<true>(st, m);
-            }
-            if (++ck == cB) {
-                put_entry(pick(liq, cq), cnb, st);
-                stmd5::init(st);
-                ck = 0;
-                cq = next_tile(cq + 1);
-                if (cq < RF_TILES) { cB = pick(Bq, cq); cR = pick(Rq, cq); cln = pick(lnq, cq); cnb = ln_blocks(cln); }
-            }
-        };
-        // Every iteration issues both refills (dummies past the end), so the
-        // compiler's wait before each hash counts the other buffer's four
-        // loads as still in flight on every path.
-        for (uint32_t f = 0; f < T; f += 2) {
-            hash_block(a0, a1, a2, a3);
-            fetch(a0, a1, a2, a3);
-            if (f + 1 < T) hash_block(b0, b1, b2, b3);
-            fetch(b0, b1, b2, b3);
-        }
-#pragma unroll
-        for (int q0 = 0; q0 < RF_TILES; q0++)
-            if (Bq[q0] == 0) put_entry(liq[q0], 0, st);   // a tile of empty segments
-    }
-    lds_barrier();
-
-    RF_STAMP(1);
-    // ---- phase 2: the window's segment entries to the slot arrays, coalesced,
-    // by waves 4..15 while waves 0..3 hash level H (phase 3) from the same LDS
-    // The md5 words go out WRITE-THROUGH (sc1 buffer stores): the lines leave
-    // the XCD's L2 during the launch instead of being written back, dirty, at
-    // its end (~B / 6 TB/s added to the kernel boundary for B dirty bytes:
-    // 16.8 MB here).
-    if (tid >= 256) {
-        const uint64_t c0 = t.base[H + 1] + seg0;
-        const uint64_t nbytes = (t.base[H + 1] + t.S) * 16;
-        const __amdgpu_buffer_rsrc_t md5r = __builtin_amdgcn_make_buffer_rsrc(
-            GROUP ? group[gi].md5 : t.md5, (short)0, (int)(nbytes < 0xffffffffull ? nbytes : 0xffffffffull), 0x00020000);
-        for (uint32_t i = tid - 256; i < 4096; i += 768) {
-            const uint4 e = *reinterpret_cast<const uint4 *>(A + (i >> 4) * NB16 + (i & 15) * 16);
-            const u32x4 v = {e.x, e.y, e.z, e.w};
-            __builtin_amdgcn_raw_buffer_store_b128(v, md5r, (int)((c0 + i) * 16), 0, 16 /* sc1 */);
-            (GROUP ? group[gi].tag : t.tag)[c0 + i] = *reinterpret_cast<const uint16_t *>(At + (i >> 4) * TB16 + (i & 15) * 2);
-        }
-    }
-
-    // ---- phase 3: the window's levels H, H-1, H-2 from LDS; then the levels
-    // above the windows (H-3 .. lmin) by the launch's LAST window of the tree:
-    // one counter per tree (cnt[0], one arrival per window), then the last
-    // arriver reads every window root's mailbox and hashes the upper levels a
-    // lane per node (16 nodes at H = 5) -- one counter and one mailbox round
-    // trip for all of them.  Every level runs the one node16_any call site
-    // below (the unrolled node hash stays hot in the instruction cache).
-    uint32_t l = H;
-    uint64_t b = root * 256 + tid;
-    const uint8_t *ent = A + (tid & 255) * NB16, *tgs = At + (tid & 255) * TB16;
-    uint8_t *reg = M + (tid & 255) * MSG16;
-    uint8_t *nxE = Bb + ((tid & 255) >> 4) * NB16 + (tid & 15) * 16;
-    uint8_t *nxT = Bt + ((tid & 255) >> 4) * TB16 + (tid & 15) * 2;
-    bool act = tid < 256;
-    const uint32_t nw = GROUP ? nwin : gridDim.x;   // this launch's windows of the tree
-    uint64_t nlo = 0, nn = 0;                        // upper levels: this launch's nodes [nlo, nlo + nn)
-    __shared__ uint32_t s_last;
-#pragma unroll 1
-    for (uint32_t phase = 0;; phase++) {
-        if (act) {
-            uint4 e;
-            uint32_t tg;
-            node16_any(reinterpret_cast<const uint4 *>(ent), reinterpret_cast<const uint16_t *>(tgs), reg, e, tg);
-            RF_STAMP(phase <= 2 ? 2 + 2 * phase : (l == 2 ? 10 : 14));
-            const uint64_t slot = t.base[l] + b;
-            if (tg) (GROUP ? group[gi].md5 : t.md5)[slot] = e;
-            (GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
-            if (l == 1) { (GROUP ? group[gi].md5 : t.md5)[0] = e; (GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
-            if (phase == 2) {
-                if (l > lmin) mail_put(RFT(mail) + slot, e, tg);   // read by the tree's last window
-            } else if (l > lmin) {
-                *reinterpret_cast<uint4 *>(nxE) = e;
-                *reinterpret_cast<uint16_t *>(nxT) = (uint16_t)tg;
-            }
-        }
-        if (l <= lmin) break;
-        if (phase == 2) {
-            if (tid == 0) {
-                // this window's mailbox store has completed (agent-coherent)
-                // before the counter moves; no L2 write-back / invalidate
-                __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                RF_STAMP(7);
-                uint32_t *c = RFT(cnt);
-                const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_last = old + 1 == nw;
-                if (old + 1 == nw) {
-                    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    RF_STAMP(8);
-                }
-            }
-            __syncthreads();
-            if (!s_last) break;
-            // level H-3: the children are the window roots, from their mailboxes
-            l--;
-            nlo = (GROUP ? 0 : root0) >> 4;
-            nn = nw >> 4;
-            act = tid < nn;
-            b = nlo + tid;
-            ent = A + (tid & 255) * NB16;
-            tgs = At + (tid & 255) * TB16;
-            nxE = Bb + ((tid & 255) >> 4) * NB16 + (tid & 15) * 16;
-            nxT = Bt + ((tid & 255) >> 4) * TB16 + (tid & 15) * 2;
-            if (act) {
-                const uint64_t cc = t.base[l + 1] + b * 16;
-                uint4 h[16];
-                uint16_t g[16];
-#pragma unroll
-                for (int j = 0; j < 16; j++) mail_get(RFT(mail) + cc + j, h[j], g[j]);
-#pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    *reinterpret_cast<uint4 *>(const_cast<uint8_t *>(ent) + j * 16) = h[j];
-                    *reinterpret_cast<uint16_t *>(const_cast<uint8_t *>(tgs) + j * 2) = g[j];
-                }
-                RF_STAMP(9);
-            }
-            continue;
-        }
-        lds_barrier();   // the next level reads this one's LDS entries only
-        if (phase < 2) RF_STAMP(3 + 2 * phase);
-        l--;
-        if (phase == 0) {          // level H-1: 16 nodes of the window
-            act = tid < 16;
-            b = root * 16 + tid;
-            ent = Bb + (tid & 15) * NB16;
-            tgs = Bt + (tid & 15) * TB16;
-            nxE = Cb + (tid & 15) * 16;
-            nxT = Ct + (tid & 15) * 2;
-        } else if (phase == 1) {   // level H-2: the window root
-            act = tid == 0;
-            b = root;
-            ent = Cb;
-            tgs = Ct;
-        } else {                   // above level H-3 (H = 6: levels 2, 1): from the previous level's outputs
-            const bool fromB = phase == 3;
-            nlo >>= 4;
-            nn = (nn + 15) >> 4;
-            act = tid < nn;
-            b = nlo + tid;
-            ent = (fromB ? Bb : Cb) + (tid & 15) * NB16;
-            tgs = (fromB ? Bt : Ct) + (tid & 15) * TB16;
-            nxE = (fromB ? Cb : Bb) + (tid & 15) * 16;
-            nxT = (fromB ? Ct : Bt) + (tid & 15) * 2;
-        }
-    }
-    if (STAMP && tid == 0) {
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        RF_STAMP(15);
-    }
-#undef RFT
-#undef RF_STAMP
-}
-
 // Window-local tile order (fused rehash): one workgroup per window of 4096
 // segments sorts them by stored rows (message length in 16-byte rows,
 // descending; LDS counting sort) into the window's 64 tiles:
 // tseg/tln[window*4096 + position]; tinfo[tile].B / .R and tsize[tile] from
-// tile_shape.
+// tile_shape; pres[window*64 + w]: the window's segment presence bitmap (the
+// fused rehash packs each entry at its rank among the present siblings).
 __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tln,
-                                                           TileInfo *__restrict__ tinfo, uint64_t *__restrict__ tsize) {
+                                                           TileInfo *__restrict__ tinfo, uint64_t *__restrict__ tsize,
+                                                           uint64_t *__restrict__ pres) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t pln[4096];
     const uint32_t tid = threadIdx.x;
@@ -2347,6 +1989,9 @@ __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *
         const uint32_t r = ln_rows(ln[k]) + (ln[k] != 0);   // present-but-empty values sort above absent
         bin[k] = 255u - (r > 255u ? 255u : r);
         atomicAdd(&hist[bin[k]], 1u);
+        // presence bitmap: bit j of word w = segment 64 w + j has entries
+        const unsigned long long bits = __ballot(ln[k] != 0);
+        if ((tid & 63) == 0) pres[blockIdx.x * 64 + k * 4 + (tid >> 6)] = bits;
     }
     __syncthreads();
     if (tid == 0) {

@@ -22,6 +22,7 @@
 
 #include "../../include/synctree_hip.h"
 #include "st_kernels.h"
+#include "rehash_win.h"
 #include "leveldb_fmt.h"
 #include "small_path.h"
 
@@ -100,6 +101,7 @@ struct st_tree {
     uint64_t tiles_cap = 0;         // uint4 units
     uint32_t *tseg = nullptr, *tln = nullptr;
     TileInfo *tinfo = nullptr;
+    uint64_t *tpres = nullptr;      // per-window segment presence bitmaps (fused rehash)
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
@@ -611,7 +613,7 @@ extern "C" void st_destroy(st_tree *t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->tpres, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
@@ -781,6 +783,7 @@ static int ensure_tiles(st_tree *t) {
         CHK(dalloc_t(t, &t->tln, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
+    if (fused_geometry(t) && !t->tpres) CHK(dalloc_t(t, &t->tpres, t->S / 64));
     Scratch sc(t);
     uint64_t *tsize = nullptr, *tbase = nullptr;
     CHK(sc.alloc(&tsize, ntiles + 1));
@@ -788,7 +791,7 @@ static int ensure_tiles(st_tree *t) {
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
     if (fused_geometry(t))   // window-local order (k_rehash_fused)
         LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
-               tsize);
+               tsize, t->tpres);
     else
         LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
                (const uint32_t *)t->seg_perm, t->tseg, t->tln, t->tinfo, tsize, ntiles);
@@ -821,6 +824,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tseg = t->tseg;
     x.tln = t->tln;
     x.tiles = t->tiles;
+    x.pres = t->tpres;
     return x;
 }
 
@@ -887,7 +891,7 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t lmin = t->partitioned ? 2u : 1u;
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
                    (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
             return ST_OK;
         }
@@ -896,7 +900,7 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 32));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
-        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
+        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false, 16>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
                (const TreeTiles *)nullptr, 0u, root0, lmin, st);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
@@ -913,8 +917,8 @@ static int rehash_tiled(st_tree *t) {
             }
         }
         static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
-                                        "H-2 hashed", "mail stored", "L2 cnt won", "L2 mail read", "L2 hashed",
-                                        "L2 mail stored", "L1 cnt won", "L1 mail read", "L1 hashed", "exit"};
+                                        "H-2 hashed", "mail stored", "cnt won", "mail read", "climb 1st hashed",
+                                        "-", "-", "-", "climb last hashed", "exit"};
         for (int k = 0; k < 16; k++) {
             std::vector<double> v;
             for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
@@ -924,7 +928,7 @@ static int rehash_tiled(st_tree *t) {
                     v[v.size() / 2], v.back());
         }
         // shader cycles and clock (s_memtime / s_memrealtime) over the hash intervals
-        const int iv[5][2] = {{1, 2}, {3, 4}, {5, 6}, {9, 10}, {13, 14}};
+        const int iv[5][2] = {{1, 2}, {3, 4}, {5, 6}, {9, 10}, {10, 14}};
         for (auto &q : iv) {
             double cyc = 0, us = 0;
             int m = 0;
@@ -1667,7 +1671,9 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const uint32_t nwin = (uint32_t)(t->S / 4096);
     const uint64_t nwg = (uint64_t)nwin * n;
     if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
-    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true>), (uint32_t)nwg, 1024, fused_lds_bytes(), view(t), h[0],
+    // 8 waves per window: two windows per CU (75 KB of LDS each), so one
+    // window's level chain overlaps another's K1
+    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(), view(t), h[0],
            (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
     CHK(tsync(t));
     for (uint32_t i = 0; i < n; i++) {
