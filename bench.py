@@ -190,9 +190,10 @@ def main():
         # block count, 2 x 4 B per segment; 16 B per 64-segment tile), the
         # 18-B entry (md5 + tag) written per segment and per inner node
         # (69,905 for W=16, H=5; their inputs stay in LDS, except the 16
-        # children read by each of the 17 climbing nodes).
+        # children read by each of the 17 climbing nodes), and the window's
+        # segment presence bitmap (1 bit per segment).
         inner_nodes = sum(16 ** l for l in range(5))
-        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
+        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
         seg_blocks += 349525   # inner-node MD5 blocks (full nodes: 5 each)
         k1_avg_ms = max(k1_ms / max(k1_n, 1), 1e-9)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
@@ -619,6 +620,20 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     stable = bool((allt.cpu().numpy() == before).all()) and int(before.reshape(-1, 18)[:, 0].sum()) == world * E
+    # the group launch alone (HIP events on trees[0]'s stream) and its roofline:
+    # per tree the same algorithmic bytes as the headline's launch
+    trees[0].set_timing(True)
+    trees[0].kernel_stats('*reset*')
+    for _ in range(reps):
+        synctree_hip.rehash_group(trees)
+    g_n, g_ms = trees[0].kernel_stats('rehash_group')
+    trees[0].set_timing(False)
+    g_avg = g_ms / max(g_n, 1)
+    S = trees[0].segments
+    inner = sum(16 ** lv for lv in range(trees[0].height))
+    tree_bytes = 17 * nk + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner * 18
+    g_gbs = E * tree_bytes / (g_avg / 1e3) / 1e9 if g_avg > 0 else 0.0
+    mem0 = trees[0].mem_stats()
     # per-tree rehash for comparison (rank-local, untimed for the headline)
     t0 = time.perf_counter()
     for t in trees[:32]:
@@ -631,6 +646,13 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     return {'keys_per_s': round(world * E * nk * reps / el, 1), 'ms_per_batch': round(el * 1e3 / reps, 3),
             'ensembles_per_gpu': E, 'ensembles_total': world * E, 'keys_per_ensemble': nk, 'ranks': world,
             'tops_allgather_stable': stable, 'load_s': round(load_s, 2),
+            'kernel_ms_per_batch': round(g_avg, 4),
+            'roofline': {'bound': 'hbm', 'achieved': round(g_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                         'frac': round(g_gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': E * tree_bytes,
+                         'bytes_per_tree': tree_bytes, 'tile_bytes_per_tree': mem0['tiles'],
+                         'kernel': K1_KERNEL + '<GROUP, 8 waves per window, two windows per CU>',
+                         'note': 'per tree: 17 B of value per key + 8 B tile metadata + 1/8 B presence per segment, '
+                                 '18-B entry written per segment and inner node; kernel time from HIP events'},
             'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
             'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '
                     'the rank\'s trees + st_tops_to_device + all_gather_into_tensor of every ensemble\'s top hash '
