@@ -244,23 +244,28 @@ __device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t
 }
 
 // MD5 of an inner node's message (the present children's 17-byte entries,
-// at most 16 x 17 = 272 bytes) staged at a 16-byte aligned LDS address and
-// readable up to byte 320: at most 5 blocks, unrolled, each read with four
-// 16-byte LDS loads (the garbage past len is replaced by the padding).
+// at most 16 x 17 = 272 bytes) staged at a 4-byte aligned LDS address and
+// readable up to byte 320: at most 5 blocks, unrolled; block k + 1's words
+// are read before block k is compressed (the garbage past len is replaced by
+// the padding).
 __device__ __forceinline__ void md5_lds_node(const uint8_t *p, uint32_t len, uint32_t out[4]) {
-    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
     const uint32_t nblk = (len + 8) / 64 + 1;
     uint32_t st[4];
     init(st);
-    // block k + 1's reads are issued before block k is compressed
-    uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    uint32_t nx[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) nx[w] = q[w];
 #pragma unroll
     for (int k = 0; k < 5; k++) {
         if ((uint32_t)k < nblk) {
-            uint32_t m[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+            uint32_t m[16];
+#pragma unroll
+            for (int w = 0; w < 16; w++) m[w] = nx[w];
             if (k < 4 && (uint32_t)k + 1 < nblk) {
-                __asm__ volatile("" ::: "memory");   // only one block ahead (not all 20 reads hoisted: 80 VGPRs)
-                a = q[4 * k + 4]; b = q[4 * k + 5]; c = q[4 * k + 6]; d = q[4 * k + 7];
+                __asm__ volatile("" ::: "memory");   // only one block ahead (not all 80 words hoisted)
+#pragma unroll
+                for (int w = 0; w < 16; w++) nx[w] = q[16 * (k + 1) + w];
             }
             const int32_t rem = (int32_t)len - 64 * k;
             if (k == 4 && __ballot(len != 272) == 0) {

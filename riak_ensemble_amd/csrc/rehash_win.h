@@ -29,17 +29,25 @@
 // NW = 16 (one window per CU, every wave in K1).
 #pragma once
 
-#define RW_MSG 272                          // one node's message: 16 x 17 bytes
-#define RW_MH 0                             // 256 level-H node messages
-#define RW_M1 (RW_MH + 256 * RW_MSG)        // 16 level-(H-1) node messages
-#define RW_M0 (RW_M1 + 16 * RW_MSG)         // the window root's message (+ slack to 320: a final block's reads)
-#define RW_PRES (RW_M0 + 320)               // 64 x u64 segment presence bitmap of the window
-#define RW_TI (RW_PRES + 512)               // the window's 64 TileInfo
-#define RW_MISC (RW_TI + 64 * 16)           // [0] last-arriver flag, [1] level-H arrivals, [2] root's children
-                                            // mask, [4 + m] H-1 node m's children mask (the climb's masks reuse RW_TI)
-#define RW_LDS (RW_MISC + 80)
-
-__host__ __device__ __forceinline__ uint32_t fused_lds_bytes() { return RW_LDS; }
+#define RW_MSG 272                          // one node's message at most: 16 x 17 bytes
+// LDS layout for `mhb` bytes of level-H messages (the window's 256 messages
+// packed at 4-byte aligned offsets, NOFF; the climb's up to 256 messages at
+// RW_MSG stride; the host passes the largest need of the launch's windows):
+//   MH [0, mhb + 80)   M1 16 x RW_MSG (the 64 tile descriptors while K1 runs)
+//   M0 320   PRES 64 x u64   NOFF 256 x u16 (4-byte units)   MISC 20 x u32
+// PRES + NOFF hold the climb's node masks (after the window's levels).
+struct RwLayout {
+    uint32_t m1, m0, pres, noff, misc, total;
+    __host__ __device__ explicit RwLayout(uint32_t mhb) {
+        m1 = (mhb + 80 + 15) & ~15u;   // a message's last block may read 72 bytes past its end
+        m0 = m1 + 16 * RW_MSG;
+        pres = m0 + 320;
+        noff = pres + 512;
+        misc = noff + 512;
+        total = misc + 80;
+    }
+};
+__host__ __device__ __forceinline__ uint32_t fused_lds_bytes(uint32_t mhb) { return RwLayout(mhb).total; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -102,7 +110,8 @@ __device__ __forceinline__ void rw_node(const uint8_t *msg, uint32_t len, uint4 
 // arrays, tiles, counters and mailboxes.
 template <bool STAMP, bool GROUP, int NW>
 __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
-                                                          uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps) {
+                                                          uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps,
+                                                          uint32_t mhb) {
 #define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
                                                           stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
     constexpr int NT = 64 / NW;   // tiles per wave
@@ -111,20 +120,23 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
     const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
 #define RFT(f) (GROUP ? group[gi].f : tt0.f)
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *MH = lds + RW_MH;
-    uint8_t *M1 = lds + RW_M1;
-    uint8_t *M0 = lds + RW_M0;
-    uint64_t *PRES = reinterpret_cast<uint64_t *>(lds + RW_PRES);
-    uint32_t *MISC = reinterpret_cast<uint32_t *>(lds + RW_MISC);
+    const RwLayout LY(mhb);
+    uint8_t *MH = lds;
+    uint8_t *M1 = lds + LY.m1;
+    uint8_t *M0 = lds + LY.m0;
+    uint64_t *PRES = reinterpret_cast<uint64_t *>(lds + LY.pres);
+    uint32_t *MISC = reinterpret_cast<uint32_t *>(lds + LY.misc);
+    uint16_t *NOFF = reinterpret_cast<uint16_t *>(lds + LY.noff);   // level-H message offsets, 4-byte units
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t H = t.H;
     const uint64_t seg0 = root * 4096;
 
     // ---- the window's tile descriptors and presence bitmap into LDS
-    TileInfo *TI = reinterpret_cast<TileInfo *>(lds + RW_TI);
+    TileInfo *TI = reinterpret_cast<TileInfo *>(lds + LY.m1);   // M1 is free until level H
     if (tid < 64) {
         TI[tid] = RFT(tinfo)[root * 64 + tid];
         PRES[tid] = RFT(pres)[root * 64 + tid];
+        reinterpret_cast<uint64_t *>(NOFF)[tid] = reinterpret_cast<const uint64_t *>(RFT(noff) + root * 256)[tid];
     }
     if (tid < 4) MISC[tid] = 0;
     lds_barrier();
@@ -191,7 +203,7 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
     // a segment's entry into its parent's message (absent segments: nothing)
     auto put_entry = [&](uint32_t li, const uint32_t st[4]) {
         const uint32_t n = li >> 4, j = li & 15;
-        const uint32_t o = n * RW_MSG + 17u * __builtin_popcount(rw_pres16(PRES, n) & ((1u << j) - 1u));
+        const uint32_t o = 4u * NOFF[n] + 17u * __builtin_popcount(rw_pres16(PRES, n) & ((1u << j) - 1u));
         rw_put17(MH + o, 0u, make_uint4(st[0], st[1], st[2], st[3]));
     };
     {
@@ -245,7 +257,7 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
             uint4 e = make_uint4(0, 0, 0, 0);
             uint16_t tg = 0;
             if ((p16 >> j) & 1u) {
-                e = rw_get16(MH, n * RW_MSG + 17u * __builtin_popcount(p16 & ((1u << j) - 1u)) + 1u);
+                e = rw_get16(MH, 4u * NOFF[n] + 17u * __builtin_popcount(p16 & ((1u << j) - 1u)) + 1u);
                 tg = (uint16_t)TAG_PRESENT;
             }
             const u32x4 v = {e.x, e.y, e.z, e.w};
@@ -271,12 +283,12 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
             const uint8_t *msg;
             uint32_t len;
             uint64_t b;
-            if (ph == 0) { msg = MH + tid * RW_MSG; len = 17u * __builtin_popcount(rw_pres16(PRES, tid)); b = root * 256 + tid; }
+            if (ph == 0) { msg = MH + 4u * NOFF[tid]; len = 17u * __builtin_popcount(rw_pres16(PRES, tid)); b = root * 256 + tid; }
             else if (ph == 1) { msg = M1 + tid * RW_MSG; len = 17u * __builtin_popcount(MISC[4 + tid]); b = root * 16 + tid; }
             else if (ph == 2) { msg = M0; len = 17u * __builtin_popcount(MISC[2]); b = root; }
             else {
                 msg = (ph == 3 ? MH : ph == 4 ? M1 : M0) + tid * RW_MSG;
-                len = 17u * __builtin_popcount(reinterpret_cast<const uint32_t *>(lds + RW_TI)[tid]);
+                len = 17u * __builtin_popcount(reinterpret_cast<const uint32_t *>(lds + LY.pres)[tid]);
                 b = nlo + tid;
             }
             rw_node(msg, len, e, tg);
@@ -331,7 +343,7 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
             // mailboxes: 16 lanes per node read one mailbox each (one round
             // trip, 5 registers a lane) and place the entry at its rank in the
             // node's message; the node's presence mask goes to CLM
-            uint32_t *CLM = reinterpret_cast<uint32_t *>(lds + RW_TI);   // climb masks (the tile descriptors are dead)
+            uint32_t *CLM = reinterpret_cast<uint32_t *>(lds + LY.pres);   // climb masks (PRES and NOFF are dead)
             for (uint64_t c0 = 0; c0 < nn * 16; c0 += NW * 64) {
                 const uint64_t ci = c0 + tid;   // child ci % 16 of this level's node ci / 16
                 uint4 h = make_uint4(0, 0, 0, 0);
@@ -352,7 +364,7 @@ __global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles t
             if (act) {
                 const uint32_t j = tid & 15;
                 if (tg) rw_put17((ph == 3 ? M1 : M0) + (tid >> 4) * RW_MSG + 17u * __builtin_popcount(sib & ((1u << j) - 1u)), 0u, e);
-                if (j == 0) reinterpret_cast<uint32_t *>(lds + RW_TI)[tid >> 4] = sib;
+                if (j == 0) reinterpret_cast<uint32_t *>(lds + LY.pres)[tid >> 4] = sib;
             }
             __syncthreads();
             nlo >>= 4;

@@ -907,6 +907,94 @@ __device__ __forceinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8
     }
 }
 
+// Exclusive prefix sum over the wave's lanes.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+// exchange_final of one segment pair staged in LDS (orddict_delta +
+// filter, riak_ensemble_util.erl:115-141, synctree.erl:434-449): ao / bo the
+// key offsets (relative, n + 1), avo / bvo the value offsets (relative),
+// ak / bk the key bytes, av / bv the values (vl: staged, else compared in
+// global memory), ur nA + nB union slots.  Writes the pair's records in
+// ascending key order to out[base..lim); returns their count.
+__device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint64_t a0, uint64_t b0,
+                                   uint32_t nA, uint32_t nB, const uint32_t *ao, const uint32_t *bo, const uint32_t *avo,
+                                   const uint32_t *bvo, const uint8_t *ak, const uint8_t *bk, const uint8_t *av,
+                                   const uint8_t *bv, bool vl, uint32_t *ur, DiffRec *out, uint64_t base, uint64_t lim) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nu_max = (uint32_t)(nA + nB);
+    for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+    wave_sync_lds();
+    uint64_t cnt = 0;
+    uint32_t mcarry = 0;
+    for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
+        const uint32_t i = c + lane;
+        bool eq = false, emit = false;
+        uint32_t rb = 0;
+        if (i < nA) {
+            rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
+            if (eq) {
+                if (vl) {
+                    emit = lds_bytes_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
+                } else {
+                    const uint64_t x = a0 + i, y = b0 + rb;
+                    emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
+                                     B.voff[y + 1] - B.voff[y]);
+                }
+            } else {
+                emit = filter != 1;
+            }
+        }
+        const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+        mcarry += (uint32_t)__popcll(__ballot(eq));
+        cnt += (uint32_t)__popcll(__ballot(emit));
+        if (emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
+    }
+    mcarry = 0;
+    for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
+        const uint32_t j = c + lane;
+        bool eq = false, emit = false;
+        uint32_t ra = 0;
+        if (j < nB) {
+            ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
+            emit = !eq && filter != 2;
+        }
+        const uint32_t m = mcarry + wave_prefix_count(eq, lane);
+        mcarry += (uint32_t)__popcll(__ballot(eq));
+        cnt += (uint32_t)__popcll(__ballot(emit));
+        if (emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
+    }
+    wave_sync_lds();
+    uint64_t pos = base;
+    for (uint32_t c = 0; c < nu_max && cnt; c += 64) {   // union slots in key order -> records
+        const uint32_t u = c + lane;
+        const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
+        const bool e = r != 0xffffffffu;
+        const uint64_t p = pos + wave_prefix_count(e, lane);
+        if (e && p < lim) {
+            DiffRec d;
+            const uint32_t kind = r >> 30, x = (r >> 15) & 0x7fffu, y = r & 0x7fffu;
+            d.kind = kind;
+            d.pad = 0;
+            d.seg = s;
+            d.a = kind == 2 ? ~0ull : a0 + x;
+            d.b = kind == 1 ? ~0ull : b0 + y;
+            out[p] = d;
+        }
+        pos += (uint32_t)__popcll(__ballot(e));
+    }
+    wave_sync_lds();
+    return cnt;
+}
+
 // exchange_final for one segment pair (orddict_delta + filter), one wave:
 // writes the pair's records in ascending key order to out[base..] (records
 // at or past lim are counted, not written: the host grows the buffer and
@@ -946,68 +1034,8 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             // one round trip: key bytes and value bytes of both sides
             wave_copy4(A.kheap + ka0, bytesA, ak, B.kheap + kb0, bytesB, bk, A.vheap + va0, vl ? (uint32_t)vA : 0u, av,
                        B.vheap + vb0, vl ? (uint32_t)vB : 0u, bv);
-            const uint32_t nu_max = (uint32_t)(nA + nB);
-            for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
-            wave_sync_lds();
-            uint64_t cnt = 0;
-            uint32_t mcarry = 0;
-            for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
-                const uint32_t i = c + lane;
-                bool eq = false, emit = false;
-                uint32_t rb = 0;
-                if (i < nA) {
-                    rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
-                    if (eq) {
-                        if (vl) {
-                            emit = lds_bytes_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
-                        } else {
-                            const uint64_t x = a0 + i, y = b0 + rb;
-                            emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
-                                             B.voff[y + 1] - B.voff[y]);
-                        }
-                    } else {
-                        emit = filter != 1;
-                    }
-                }
-                const uint32_t m = mcarry + wave_prefix_count(eq, lane);
-                mcarry += (uint32_t)__popcll(__ballot(eq));
-                cnt += (uint32_t)__popcll(__ballot(emit));
-                if (emit) ur[i + rb - m] = (eq ? 0u : (1u << 30)) | (i << 15) | rb;
-            }
-            mcarry = 0;
-            for (uint32_t c = 0; c < nB; c += 64) {   // B side: remote-only
-                const uint32_t j = c + lane;
-                bool eq = false, emit = false;
-                uint32_t ra = 0;
-                if (j < nB) {
-                    ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
-                    emit = !eq && filter != 2;
-                }
-                const uint32_t m = mcarry + wave_prefix_count(eq, lane);
-                mcarry += (uint32_t)__popcll(__ballot(eq));
-                cnt += (uint32_t)__popcll(__ballot(emit));
-                if (emit) ur[j + ra - m] = (2u << 30) | (ra << 15) | j;
-            }
-            wave_sync_lds();
-            uint64_t pos = base;
-            for (uint32_t c = 0; c < nu_max && cnt; c += 64) {   // union slots in key order -> records
-                const uint32_t u = c + lane;
-                const uint32_t r = u < nu_max ? ur[u] : 0xffffffffu;
-                const bool e = r != 0xffffffffu;
-                const uint64_t p = pos + wave_prefix_count(e, lane);
-                if (e && p < lim) {
-                    DiffRec d;
-                    const uint32_t kind = r >> 30, x = (r >> 15) & 0x7fffu, y = r & 0x7fffu;
-                    d.kind = kind;
-                    d.pad = 0;
-                    d.seg = s;
-                    d.a = kind == 2 ? ~0ull : a0 + x;
-                    d.b = kind == 1 ? ~0ull : b0 + y;
-                    out[p] = d;
-                }
-                pos += (uint32_t)__popcll(__ballot(e));
-            }
-            wave_sync_lds();
+            const uint64_t cnt = lds_merge_pair(A, B, s, filter, a0, b0, (uint32_t)nA, (uint32_t)nB, ao, bo, avo, bvo, ak, bk,
+                                                av, bv, vl, ur, out, base, lim);
             return cnt;
         }
         *algo_bytes -= (uint64_t)bytesA + bytesB;   // counted again below
@@ -1114,16 +1142,6 @@ struct CmpWalk {
 };
 #define CW_STAMP(c, k) do { if ((c).stamp && (threadIdx.x & 63) == 0) (c).stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x - v;
-}
 
 // Verify the listed items on both sides, then merge-join the listed segments.
 // Verification: a lane per (item, side); each message -- an inner node's
@@ -1340,52 +1358,69 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
 __global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
                                                    const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
                                                    uint64_t *res) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nw) return;
-    uint64_t above = 0;
-    for (uint32_t v0 = w + 1; v0 < nw; v0 += 1024) {   // 16 loads per lane in flight
-        uint64_t x[16];
+    // Every workgroup scans all nw wave counts in LDS (one round trip of
+    // L2-resident loads, nw <= 256 x CMP_GK): wave w's region goes after the
+    // regions of every higher wave, at total - (inclusive prefix through w).
+    constexpr uint32_t CMP_GK = 16;
+    __shared__ uint64_t part[256];
+    __shared__ uint64_t incl[256 * CMP_GK];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t K = (nw + 255) / 256;   // counts per thread (<= CMP_GK: nw <= 4096, checked by the host)
+    uint64_t loc[CMP_GK], sum = 0;
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-            const uint32_t v = v0 + u * 64 + lane;
-            x[u] = v < nw ? wcnt[v] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++) above += x[u];
+    for (uint32_t i = 0; i < CMP_GK; i++) {
+        const uint32_t v = tid * K + i;
+        loc[i] = (i < K && v < nw) ? wcnt[v] : 0;
+        sum += loc[i];
     }
-    for (int o = 32; o; o >>= 1) above += __shfl_xor(above, o, 64);
-    const uint64_t n = wcnt[w];
-    if (w == 0) {
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {   // inclusive scan of the per-thread sums
+        const uint64_t x = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    uint64_t run = part[tid] - sum;
+#pragma unroll
+    for (uint32_t i = 0; i < CMP_GK; i++) {
+        if (i < K) { run += loc[i]; incl[tid * K + i] = run; }
+    }
+    __syncthreads();
+    const uint64_t total = part[255];
+    if (blockIdx.x == 0) {   // the largest per-wave count and the first failed verification
         uint64_t mx = 0, em = ~0ull;
-        for (uint32_t v0 = 0; v0 < nw; v0 += 512) {
-            uint64_t x[8], y[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t v = v0 + u * 64 + lane;
-                x[u] = v < nw ? wcnt[v] : 0;
-                y[u] = v < nw ? werr[v] : ~0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                mx = x[u] > mx ? x[u] : mx;
-                em = y[u] < em ? y[u] : em;
-            }
+        for (uint32_t v = tid; v < nw; v += 256) {
+            const uint64_t x = wcnt[v], y = werr[v];
+            mx = x > mx ? x : mx;
+            em = y < em ? y : em;
         }
         for (int o = 32; o; o >>= 1) {
             const uint64_t x = __shfl_xor(mx, o, 64), y = __shfl_xor(em, o, 64);
             mx = x > mx ? x : mx;
             em = y < em ? y : em;
         }
-        if (lane == 0) {
-            res[0] = above + n;
+        __syncthreads();
+        if (lane == 0) { part[tid >> 6] = mx; incl[tid >> 6] = em; }
+        __syncthreads();
+        if (tid == 0) {
+            for (int q = 1; q < 4; q++) {
+                mx = part[q] > mx ? part[q] : mx;
+                em = incl[q] < em ? incl[q] : em;
+            }
+            res[0] = total;
             res[1] = mx;
             res[2] = em;
             __threadfence_system();
             res[3] = 1;   // the host spins on this word
-            __threadfence_system();
         }
+        __syncthreads();   // (no reader of part / incl below in workgroup 0 before this)
+        return;            // workgroup 0 copies nothing: its waves' regions are copied by the last workgroup
     }
+    // workgroups 1..: wave q copies the region of wave w = (blockIdx.x - 1) * 4 + q
+    const uint32_t w = (blockIdx.x - 1) * 4 + (tid >> 6);
+    if (w >= nw) return;
+    const uint64_t n = wcnt[w], above = total - incl[w];
     if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
     const DiffRec *src = scratch + (uint64_t)w * R;
     for (uint64_t k = lane; k < n; k += 64) out[above + k] = src[k];
@@ -1866,6 +1901,7 @@ struct TreeTiles {
     const uint32_t *tseg, *tln;
     const uint4 *tiles;
     const uint64_t *pres;   // per-window segment presence bitmaps (tile build)
+    const uint16_t *noff;   // per window: the 256 level-H message offsets in LDS, 4-byte units (tile build)
 };
 
 
@@ -1974,12 +2010,15 @@ __device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
 // fused rehash packs each entry at its rank among the present siblings).
 __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tln,
                                                            TileInfo *__restrict__ tinfo, uint64_t *__restrict__ tsize,
-                                                           uint64_t *__restrict__ pres) {
+                                                           uint64_t *__restrict__ pres, uint16_t *__restrict__ noff,
+                                                           uint32_t *__restrict__ mhmax) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t pln[4096];
+    __shared__ uint32_t ncnt[256];
     const uint32_t tid = threadIdx.x;
     const uint64_t seg0 = (uint64_t)blockIdx.x * 4096;
     hist[tid] = 0;
+    ncnt[tid] = 0;
     __syncthreads();
     uint32_t ln[16], bin[16];
 #pragma unroll
@@ -1992,12 +2031,27 @@ __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *
         // presence bitmap: bit j of word w = segment 64 w + j has entries
         const unsigned long long bits = __ballot(ln[k] != 0);
         if ((tid & 63) == 0) pres[blockIdx.x * 64 + k * 4 + (tid >> 6)] = bits;
+        if (ln[k]) atomicAdd(&ncnt[k * 16 + (tid >> 4)], 1u);
     }
     __syncthreads();
     if (tid == 0) {
         uint32_t acc = 0;
         for (int x = 0; x < 256; x++) { const uint32_t c = hist[x]; hist[x] = acc; acc += c; }
     }
+    // level-H node tid's message (17 B per present segment) at a 4-byte
+    // aligned offset in the fused rehash's LDS: exclusive scan of the sizes
+    const uint32_t nsz = (17u * ncnt[tid] + 3u) / 4u;
+    __syncthreads();
+    ncnt[tid] = nsz;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+        const uint32_t x = tid >= o ? ncnt[tid - o] : 0u;
+        __syncthreads();
+        ncnt[tid] += x;
+        __syncthreads();
+    }
+    noff[blockIdx.x * 256 + tid] = (uint16_t)(ncnt[tid] - nsz);
+    if (tid == 255) atomicMax(mhmax, 4u * ncnt[255]);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) {

@@ -102,6 +102,9 @@ struct st_tree {
     uint32_t *tseg = nullptr, *tln = nullptr;
     TileInfo *tinfo = nullptr;
     uint64_t *tpres = nullptr;      // per-window segment presence bitmaps (fused rehash)
+    uint16_t *tnoff = nullptr;      // per-window level-H message offsets (fused rehash LDS layout)
+    uint32_t *tmhmax = nullptr;     // the largest window's level-H message bytes (device word)
+    uint32_t mh_bytes = 0;          // ... as read back at the last tile build
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
@@ -613,7 +616,7 @@ extern "C" void st_destroy(st_tree *t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
-                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->tpres, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
+                  t->seg_perm, t->tiles, t->tseg, t->tln, t->tinfo, t->tpres, t->tnoff, t->tmhmax, t->lvl_cnt, t->cw.wcnt, t->cw.wbytes, t->cw.werr,
                   t->cw.wst, t->cw.rec, t->cw.scratch, t->mail};
     for (void *p : ps) dfree(t, p);
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
@@ -774,6 +777,14 @@ static uint64_t num_tiles(const st_tree *t) { return (t->S + 63) / 64; }
 // at most 256 nodes at level H-3 (H <= 6)
 static bool fused_geometry(const st_tree *t) { return t->W == 16 && t->H >= 3 && t->H <= 6; }
 
+// Level-H message bytes of the fused rehash's LDS: the largest window's
+// packed messages, and room for the climb's nodes (nwin / 16 of them, one
+// RW_MSG each) in the tree's last window.
+static uint32_t fused_mh_bytes(uint32_t mh, uint64_t nwin) {
+    const uint64_t climb = (nwin / 16) * RW_MSG;
+    return (uint32_t)std::max<uint64_t>(std::max<uint64_t>(mh, climb), 64);
+}
+
 static int ensure_tiles(st_tree *t) {
     if (t->tiles_valid) return ST_OK;
     if (!fused_geometry(t)) CHK(ensure_perm(t));
@@ -783,7 +794,12 @@ static int ensure_tiles(st_tree *t) {
         CHK(dalloc_t(t, &t->tln, ntiles * 64));
         CHK(dalloc_t(t, &t->tinfo, ntiles));
     }
-    if (fused_geometry(t) && !t->tpres) CHK(dalloc_t(t, &t->tpres, t->S / 64));
+    if (fused_geometry(t) && !t->tpres) {
+        CHK(dalloc_t(t, &t->tpres, t->S / 64));
+        CHK(dalloc_t(t, &t->tnoff, t->S / 16));
+        CHK(dalloc_t(t, &t->tmhmax, 4));
+    }
+    if (fused_geometry(t)) HIPCHK(hipMemsetAsync(t->tmhmax, 0, 4, t->stream));
     Scratch sc(t);
     uint64_t *tsize = nullptr, *tbase = nullptr;
     CHK(sc.alloc(&tsize, ntiles + 1));
@@ -791,14 +807,17 @@ static int ensure_tiles(st_tree *t) {
     HIPCHK(hipMemsetAsync(tsize + ntiles, 0, 8, t->stream));
     if (fused_geometry(t))   // window-local order (k_rehash_fused)
         LAUNCH(t, "tile_build", k_tile_order_window, (uint32_t)(t->S / 4096), 256, 0, view(t), t->tseg, t->tln, t->tinfo,
-               tsize, t->tpres);
+               tsize, t->tpres, t->tnoff, t->tmhmax);
     else
         LAUNCH(t, "tile_build", k_tile_order_global, grid_for(ntiles * 64, 256, 1u << 30), 256, 0, view(t),
                (const uint32_t *)t->seg_perm, t->tseg, t->tln, t->tinfo, tsize, ntiles);
     CHK(exclusive_scan<uint64_t>(t, tsize, tbase, ntiles + 1));
     uint64_t total = 0;
     HIPCHK(hipMemcpyAsync(&total, tbase + ntiles, 8, hipMemcpyDeviceToHost, t->stream));
+    uint32_t mh = 0;
+    if (fused_geometry(t)) HIPCHK(hipMemcpyAsync(&mh, t->tmhmax, 4, hipMemcpyDeviceToHost, t->stream));
     CHK(tsync(t));
+    t->mh_bytes = mh;
     if (total + 1 > t->tiles_cap) {
         dfree(t, t->tiles);
         t->tiles = nullptr;
@@ -825,6 +844,7 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tln = t->tln;
     x.tiles = t->tiles;
     x.pres = t->tpres;
+    x.noff = t->tnoff;
     return x;
 }
 
@@ -889,10 +909,11 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t nwg = t->partitioned ? (uint32_t)((t->part_hi - t->part_lo) / 4096) : (uint32_t)nroots;
         if (root0 + nwg > nroots || nwg == 0) { g_err = "rehash window range out of bounds"; return ST_EINVAL; }
         const uint32_t lmin = t->partitioned ? 2u : 1u;
+        const uint32_t mhb = fused_mh_bytes(t->mh_bytes, nroots);
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr);
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, tree_tiles(t),
+                   (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr, mhb);
             return ST_OK;
         }
         // diagnostic: per-phase wall-clock stamps (100 MHz) to stderr
@@ -900,8 +921,8 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 32));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
-        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false, 16>), nwg, 1024, fused_lds_bytes(), d, tree_tiles(t),
-               (const TreeTiles *)nullptr, 0u, root0, lmin, st);
+        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, tree_tiles(t),
+               (const TreeTiles *)nullptr, 0u, root0, lmin, st, mhb);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         CHK(tsync(t));
@@ -1671,10 +1692,14 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const uint32_t nwin = (uint32_t)(t->S / 4096);
     const uint64_t nwg = (uint64_t)nwin * n;
     if (nwg > 0x7fffffffull) { g_err = "group too large for one launch"; return ST_EINVAL; }
-    // 8 waves per window: two windows per CU (75 KB of LDS each), so one
-    // window's level chain overlaps another's K1
-    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(), view(t), h[0],
-           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr);
+    // 8 waves per window and LDS sized for the group's largest window: two
+    // (dense trees) or three (sparse trees, <= 53 KB) windows per CU, so one
+    // window's level chain overlaps other windows' K1
+    uint32_t mh = 0;
+    for (uint32_t i = 0; i < n; i++) mh = std::max(mh, trees[i]->mh_bytes);
+    const uint32_t mhb = fused_mh_bytes(mh, nwin);
+    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(mhb), view(t), h[0],
+           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr, mhb);
     CHK(tsync(t));
     for (uint32_t i = 0; i < n; i++) {
         CHK(erec_after_rehash(trees[i]));
@@ -2204,7 +2229,7 @@ static int ensure_cmp_work(st_tree *t) {
     CmpWork &w = t->cw;
     if (w.wcnt) return ST_OK;
     const uint32_t per_cu = std::max<uint32_t>(1, (160 * 1024) / (CMP_WPG * cmp_slice(t)));
-    w.nw = (uint32_t)std::max(1, t->ncu) * per_cu * CMP_WPG;
+    w.nw = std::min<uint32_t>((uint32_t)std::max(1, t->ncu) * per_cu * CMP_WPG, 4096);   // k_cmp_gather scans <= 4096
     CHK(dalloc_t(t, &w.wcnt, w.nw));
     CHK(dalloc_t(t, &w.wbytes, w.nw));
     CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
@@ -2302,7 +2327,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             }
         }
         w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
-        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4, 256, 0, w.nw, (const uint64_t *)w.wcnt,
+        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4 + 1, 256, 0, w.nw, (const uint64_t *)w.wcnt,
                (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
         CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
         const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
