@@ -639,42 +639,86 @@ struct MergeOut {
 // entries with consecutive threads on consecutive entries, writing each
 // surviving entry's new offsets and bytes; it also writes the new segment
 // offsets of its segments (and the terminal offsets, from the last segment).
+// Everything an entry needs besides its own offsets and bytes -- its
+// segment's bounds, merged sums, replace / reject flags, first key and value
+// offsets, and the segment's batch run (positions and run-relative sums) --
+// is staged in LDS once per workgroup, so an entry costs one round trip for
+// its offsets and one for its bytes instead of a chain of per-entry loads.
+#define MO_RUNCAP 512   // batch records of a workgroup's segments staged in LDS (more: read from global memory)
 __global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *pos, const BatchSums *bx,
                                                    const SegSums *sx, MergeOut o) {
-    __shared__ uint64_t so[257];
+    __shared__ uint64_t so[257], sb[257], kb0[257], vb0[257];
+    __shared__ SegSums sxs[256];
+    __shared__ uint8_t flg[256];                  // 1 = old run replaced, 2 = batch run rejected
+    __shared__ uint32_t rpos[MO_RUNCAP];
+    __shared__ uint32_t rbx[MO_RUNCAP + 1][6];    // batch sums relative to the workgroup's first record
+    const uint32_t tid = threadIdx.x;
     const uint64_t s0 = (uint64_t)blockIdx.x * 256;
     const uint64_t ns = a.S - s0 < 256 ? a.S - s0 : 256;
-    for (uint32_t i = threadIdx.x; i <= ns; i += 256) {
+    for (uint32_t i = tid; i <= ns; i += 256) {
         so[i] = a.seg_off ? a.seg_off[s0 + i] : 0;
+        sb[i] = a.bseg_off[s0 + i];
         if (i < ns || s0 + i == a.S) {
             const SegSums x = sx[s0 + i];
+            if (i < ns) sxs[i] = x;
             o.seg_off[s0 + i] = x.v[0];
             o.seg_voff[s0 + i] = x.v[2];
             if (s0 + i == a.S) { o.koff[x.v[0]] = x.v[1]; o.voff[x.v[0]] = x.v[2]; }
         }
+        if (i < ns)
+            flg[i] = (uint8_t)((a.seg_replace && a.seg_replace[s0 + i] ? 1u : 0u) | (a.seg_reject && a.seg_reject[s0 + i] ? 2u : 0u));
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i <= ns; i += 256) {   // first key / value offsets of each segment
+        kb0[i] = a.seg_off ? a.koff[so[i]] : 0;
+        vb0[i] = a.seg_off ? a.voff[so[i]] : 0;
+    }
+    const uint64_t j0w = sb[0], nbw = sb[ns] - sb[0];
+    const bool staged = nbw + 1 <= MO_RUNCAP;
+    if (staged) {
+        for (uint64_t j = tid; j <= nbw; j += 256) {
+            if (j < nbw) rpos[j] = pos[j0w + j];
+            const BatchSums &x = bx[j0w + j], &x0 = bx[j0w];
+#pragma unroll
+            for (int q = 0; q < 6; q++) rbx[j][q] = (uint32_t)(x.v[q] - x0.v[q]);
+        }
     }
     __syncthreads();
     const uint64_t e0 = so[0], e1 = so[ns];
-    for (uint64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+    for (uint64_t e = e0 + tid; e < e1; e += 256) {
         uint32_t lo = 0, hi = (uint32_t)ns;   // local segment: so[k] <= e < so[k+1]
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (so[mid] <= e) lo = mid; else hi = mid;
         }
-        const uint64_t s = s0 + lo, i0 = so[lo], li = e - i0;
-        if (a.seg_replace && a.seg_replace[s]) continue;
-        const SegSums base = sx[s];
+        const uint8_t f = flg[lo];
+        if (f & 1) continue;
+        const uint64_t i0 = so[lo], li = e - i0;
         const uint64_t okb = a.koff[e], ovb = a.voff[e];
         const uint64_t kl = a.koff[e + 1] - okb, vl = a.voff[e + 1] - ovb;
-        uint64_t nw = base.v[0] + li, nk = base.v[1] + (okb - a.koff[i0]), nv = base.v[2] + (ovb - a.voff[i0]);
-        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-        if (j0 != je && !(a.seg_reject && a.seg_reject[s])) {
-            const uint64_t k = bound_pos(pos, j0, je, li, true), k2 = bound_pos(pos, j0, je, li, false);
-            const BatchSums &B0 = bx[j0], &Bk = bx[k], &Bk2 = bx[k2];
-            if (Bk.v[BS_EQ] != Bk2.v[BS_EQ]) continue;   // overwritten or erased by the batch
-            nw += (Bk.v[BS_NE] - B0.v[BS_NE]) - (Bk2.v[BS_EQ] - B0.v[BS_EQ]);
-            nk += (Bk.v[BS_KN] - B0.v[BS_KN]) - (Bk2.v[BS_KE] - B0.v[BS_KE]);
-            nv += (Bk.v[BS_VN] - B0.v[BS_VN]) - (Bk2.v[BS_VE] - B0.v[BS_VE]);
+        const SegSums &base = sxs[lo];
+        uint64_t nw = base.v[0] + li, nk = base.v[1] + (okb - kb0[lo]), nv = base.v[2] + (ovb - vb0[lo]);
+        const uint64_t j0 = sb[lo], je = sb[lo + 1];
+        if (j0 != je && !(f & 2)) {
+            if (staged) {
+                const uint32_t r0 = (uint32_t)(j0 - j0w), re = (uint32_t)(je - j0w);
+                uint32_t k = r0, hk = re;   // upper bound: first pos > li
+                while (k < hk) { const uint32_t mid = (k + hk) >> 1; if (rpos[mid] <= li) k = mid + 1; else hk = mid; }
+                uint32_t k2 = r0, h2 = re;  // lower bound: first pos >= li
+                while (k2 < h2) { const uint32_t mid = (k2 + h2) >> 1; if (rpos[mid] < li) k2 = mid + 1; else h2 = mid; }
+                if (rbx[k][BS_EQ] != rbx[k2][BS_EQ]) continue;   // overwritten or erased by the batch
+                // (each run-relative difference is >= 0; the sum may not be: 64-bit wrap as above)
+                nw += (uint64_t)(rbx[k][BS_NE] - rbx[r0][BS_NE]) - (uint64_t)(rbx[k2][BS_EQ] - rbx[r0][BS_EQ]);
+                nk += (uint64_t)(rbx[k][BS_KN] - rbx[r0][BS_KN]) - (uint64_t)(rbx[k2][BS_KE] - rbx[r0][BS_KE]);
+                nv += (uint64_t)(rbx[k][BS_VN] - rbx[r0][BS_VN]) - (uint64_t)(rbx[k2][BS_VE] - rbx[r0][BS_VE]);
+            } else {
+                const uint64_t k = bound_pos(pos, j0, je, li, true), k2 = bound_pos(pos, j0, je, li, false);
+                const BatchSums &B0 = bx[j0], &Bk = bx[k], &Bk2 = bx[k2];
+                if (Bk.v[BS_EQ] != Bk2.v[BS_EQ]) continue;
+                nw += (Bk.v[BS_NE] - B0.v[BS_NE]) - (Bk2.v[BS_EQ] - B0.v[BS_EQ]);
+                nk += (Bk.v[BS_KN] - B0.v[BS_KN]) - (Bk2.v[BS_KE] - B0.v[BS_KE]);
+                nv += (Bk.v[BS_VN] - B0.v[BS_VN]) - (Bk2.v[BS_VE] - B0.v[BS_VE]);
+            }
         }
         o.koff[nw] = nk;
         o.voff[nw] = nv;
