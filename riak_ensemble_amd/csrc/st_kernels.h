@@ -866,7 +866,7 @@ __device__ __forceinline__ bool entry_differs(uint16_t ta, uint16_t tb, const ui
 #define CMP_KB 4096     // key bytes per side
 #define CMP_VB 6144     // value bytes per side (larger: values compared in global memory)
 __host__ __device__ __forceinline__ uint32_t cmp_merge_lds_bytes() {
-    return (CMP_CAP + 1) * 4 * 4 + 2 * CMP_CAP * 4 + CMP_KB * 2 + CMP_VB * 2;
+    return (CMP_CAP + 1) * 4 * 4 + 2 * CMP_CAP * 4 + CMP_KB * 2 + CMP_VB * 2 + 2 * CMP_CAP * 16;
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -891,16 +891,56 @@ __device__ __forceinline__ int lds_rec_cmp(const uint8_t *a, uint32_t la, const 
     return lds_bytes_cmp(a, (uint32_t)krec_order_len(a, la), b, (uint32_t)krec_order_len(b, lb));
 }
 
-// lower_bound of key k in the n staged keys (LDS); *eq: equal key found
-__device__ __forceinline__ uint32_t lds_lower_bound(const uint32_t *off, const uint8_t *kb, uint32_t n, const uint8_t *k,
-                                                    uint32_t kl, bool *eq) {
+// Order prefix of a key record staged in LDS: its first 12 order bytes
+// (krec_order_len) big-endian in x..z, zero-padded, and the order length in
+// w.  Two prefixes decide the order unless both order lengths exceed 12 and
+// the 12 bytes tie (pfx_cmp returns 2: compare the staged bytes).
+__device__ __forceinline__ uint4 lds_key_prefix(const uint8_t *p, uint32_t len) {
+    const uint32_t ol = (uint32_t)krec_order_len(p, len);
+    uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 12; k++)
+        if ((uint32_t)k < ol) w[k >> 2] |= (uint32_t)p[k] << (24 - 8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], ol);
+}
+__device__ __forceinline__ int pfx_cmp(const uint4 &x, const uint4 &y) {
+    if (x.x != y.x) return x.x < y.x ? -1 : 1;
+    if (x.y != y.y) return x.y < y.y ? -1 : 1;
+    if (x.z != y.z) return x.z < y.z ? -1 : 1;
+    if (x.w > 12 && y.w > 12) return 2;
+    return x.w == y.w ? 0 : (x.w < y.w ? -1 : 1);
+}
+
+// lower_bound of key k (prefix kp, staged bytes k / kl) in the n staged keys
+// of a segment (prefixes pk, offsets off, bytes kb); *eq: equal key found (a
+// step that meets an equal key lands on it: keys of a segment are unique).
+__device__ __forceinline__ uint32_t lds_lower_bound(const uint4 *pk, const uint32_t *off, const uint8_t *kb, uint32_t n,
+                                                    const uint4 &kp, const uint8_t *k, uint32_t kl, bool *eq) {
     uint32_t lo = 0, hi = n;
+    bool found = false;
     while (lo < hi) {
         const uint32_t m = (lo + hi) >> 1;
-        if (lds_rec_cmp(kb + off[m], off[m + 1] - off[m], k, kl) < 0) lo = m + 1; else hi = m;
+        int c = pfx_cmp(pk[m], kp);
+        if (c == 2) c = lds_rec_cmp(kb + off[m], off[m + 1] - off[m], k, kl);
+        found |= c == 0;
+        if (c < 0) lo = m + 1; else hi = m;
     }
-    *eq = lo < n && lds_rec_cmp(kb + off[lo], off[lo + 1] - off[lo], k, kl) == 0;
+    *eq = found;
     return lo;
+}
+
+// Equality of two byte strings staged in LDS: eight independent byte reads
+// per step (one LDS round trip), no early exit inside a step.
+__device__ __forceinline__ bool lds_bytes_eq(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
+    if (la != lb) return false;
+    for (uint32_t i = 0; i < la; i += 8) {
+        uint32_t d = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++)
+            if (i + k < la) d |= (uint32_t)(a[i + k] ^ b[i + k]);
+        if (d) return false;
+    }
+    return true;
 }
 
 __device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
@@ -972,10 +1012,13 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
 __device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint64_t a0, uint64_t b0,
                                    uint32_t nA, uint32_t nB, const uint32_t *ao, const uint32_t *bo, const uint32_t *avo,
                                    const uint32_t *bvo, const uint8_t *ak, const uint8_t *bk, const uint8_t *av,
-                                   const uint8_t *bv, bool vl, uint32_t *ur, DiffRec *out, uint64_t base, uint64_t lim) {
+                                   const uint8_t *bv, bool vl, uint32_t *ur, uint4 *pa, uint4 *pb, DiffRec *out,
+                                   uint64_t base, uint64_t lim) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nu_max = (uint32_t)(nA + nB);
     for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
+    for (uint32_t i = lane; i < nA; i += 64) pa[i] = lds_key_prefix(ak + ao[i], ao[i + 1] - ao[i]);
+    for (uint32_t j = lane; j < nB; j += 64) pb[j] = lds_key_prefix(bk + bo[j], bo[j + 1] - bo[j]);
     wave_sync_lds();
     uint64_t cnt = 0;
     uint32_t mcarry = 0;
@@ -984,10 +1027,10 @@ __device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t 
         bool eq = false, emit = false;
         uint32_t rb = 0;
         if (i < nA) {
-            rb = lds_lower_bound(bo, bk, (uint32_t)nB, ak + ao[i], ao[i + 1] - ao[i], &eq);
+            rb = lds_lower_bound(pb, bo, bk, (uint32_t)nB, pa[i], ak + ao[i], ao[i + 1] - ao[i], &eq);
             if (eq) {
                 if (vl) {
-                    emit = lds_bytes_cmp(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]) != 0;
+                    emit = !lds_bytes_eq(av + avo[i], avo[i + 1] - avo[i], bv + bvo[rb], bvo[rb + 1] - bvo[rb]);
                 } else {
                     const uint64_t x = a0 + i, y = b0 + rb;
                     emit = !bytes_eq(A.vheap + A.voff[x], A.voff[x + 1] - A.voff[x], B.vheap + B.voff[y],
@@ -1008,7 +1051,7 @@ __device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t 
         bool eq = false, emit = false;
         uint32_t ra = 0;
         if (j < nB) {
-            ra = lds_lower_bound(ao, ak, (uint32_t)nA, bk + bo[j], bo[j + 1] - bo[j], &eq);
+            ra = lds_lower_bound(pa, ao, ak, (uint32_t)nA, pb[j], bk + bo[j], bo[j + 1] - bo[j], &eq);
             emit = !eq && filter != 2;
         }
         const uint32_t m = mcarry + wave_prefix_count(eq, lane);
@@ -1063,6 +1106,8 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
         uint8_t *bk = ak + CMP_KB;
         uint8_t *av = bk + CMP_KB;
         uint8_t *bv = av + CMP_VB;
+        uint4 *pa = reinterpret_cast<uint4 *>(bv + CMP_VB);  // key order prefixes (16-B aligned)
+        uint4 *pb = pa + CMP_CAP;
         // one round trip: the four offset runs (+ both key bases, broadcast)
         const uint64_t ka0 = A.koff[a0], kb0 = B.koff[b0];
         for (uint64_t i = lane; i <= nA; i += 64) { ao[i] = (uint32_t)A.koff[a0 + i]; avo[i] = (uint32_t)(A.voff[a0 + i] - va0); }
@@ -1079,7 +1124,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             wave_copy4(A.kheap + ka0, bytesA, ak, B.kheap + kb0, bytesB, bk, A.vheap + va0, vl ? (uint32_t)vA : 0u, av,
                        B.vheap + vb0, vl ? (uint32_t)vB : 0u, bv);
             const uint64_t cnt = lds_merge_pair(A, B, s, filter, a0, b0, (uint32_t)nA, (uint32_t)nB, ao, bo, avo, bvo, ak, bk,
-                                                av, bv, vl, ur, out, base, lim);
+                                                av, bv, vl, ur, pa, pb, out, base, lim);
             return cnt;
         }
         *algo_bytes -= (uint64_t)bytesA + bytesB;   // counted again below
@@ -1131,7 +1176,7 @@ __host__ __device__ __forceinline__ uint32_t cmp_shared_bytes(uint32_t W) {
     return ((a > m ? a : m) + 15) & ~15u;
 }
 __host__ __device__ __forceinline__ uint32_t cmp_slice_bytes(uint32_t W) {
-    return cmp_shared_bytes(W) + CMP_LIST * 8 + ST_MAXLEV * 8;
+    return (cmp_shared_bytes(W) + CMP_LIST * 8 + ST_MAXLEV * 8 + 15) & ~15u;   // 16-B aligned wave slices
 }
 
 // Does the level-k entry `anc` differ between the trees under the filter (and,

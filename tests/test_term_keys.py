@@ -238,3 +238,32 @@ def test_equal_numbers_are_one_key(bulk):
     assert dev.get_batch([b0]) == [R.get(b0, ref)]
     dev.close()
     dev2.close()
+
+
+@pytest.mark.gpu
+def test_compare_long_common_key_prefixes():
+    """The compare merge-join orders keys by a 12-byte order prefix and falls
+    back to the staged bytes on a tie: binary keys sharing 11..40 leading
+    bytes, keys that are prefixes of other keys, and values differing only in
+    their last byte, against synctree_ref's local_compare."""
+    from riak_ensemble_amd import synctree_hip
+    W, S = 4, 16
+    stem = bytes(range(65, 105))
+    keys = []
+    for cut in (10, 11, 12, 13, 20, 40):
+        for tail in (b'', b'\x00', b'\x01', b'\xff', b'\x00\x00', b'ab'):
+            keys.append(stem[:cut] + tail)
+    keys = list(dict.fromkeys(keys))
+    vals = [_val(i) for i in range(len(keys))]
+    keys2 = keys[::2] + [stem[:12] + b'zz', stem + b'\x00\x01']
+    vals2 = [(v[:-1] + bytes([v[-1] ^ 1])) if i % 3 == 0 else v for i, v in enumerate(vals[::2])] + [_val(900), _val(901)]
+    ref, ref2 = _ref_tree(keys, vals, W, S), _ref_tree(keys2, vals2, W, S)
+    dev, dev2 = synctree_hip.DeviceTree(W, S), synctree_hip.DeviceTree(W, S)
+    dev.insert_batch(keys, vals)
+    dev2.insert_batch(keys2, vals2)
+    for a, b, ra, rb in ((dev, dev2, ref, ref2), (dev2, dev, ref2, ref)):
+        res = a.compare(b)
+        assert res[0] == 'ok'
+        assert [(k, v) for _, k, v in res[1]] == R.local_compare(ra, rb)
+    dev.close()
+    dev2.close()
