@@ -362,7 +362,7 @@ template <int MODE>
 __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *list, const uint32_t *list_cnt,
                                uint8_t *ok, uint32_t *fail) {
     const uint32_t L = t.H + 1;
-    const uint64_t n = list ? (uint64_t)*list_cnt : t.S;
+    const uint64_t n = (list && list_cnt) ? (uint64_t)*list_cnt : t.S;   // list without a count: a permutation of the segments
     for (uint64_t i = gtid(); i < n; i += gstride()) {
         const uint64_t s = list ? list[i] : i;
         const uint64_t slot = t.base[L] + s;
@@ -377,7 +377,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
                 const uint4 e = t.md5[eslot];
                 good = (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
             }
@@ -390,7 +390,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
                 const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
                 t.md5[slot] = e;
                 t.tag[slot] = TAG_PRESENT;
@@ -436,6 +436,16 @@ __device__ __forceinline__ uint32_t stage_inner(const DevTree &t, uint32_t l, ui
         for (int j = 0; j < 16; j++) {
             if (j0 + j < t.W) { tg[j] = t.tag[c0 + j0 + j]; h[j] = t.md5[c0 + j0 + j]; }
             else tg[j] = 0;
+        }
+        bool all = t.W == 16;
+#pragma unroll
+        for (int j = 0; j < 16; j++) all = all && (tg[j] & TAG_PRESENT);
+        if (all) {   // W = 16, every child present: the byte positions are compile-time constants
+            MsgWriter m16;
+            m16.init(reg);
+#pragma unroll
+            for (int j = 0; j < 16; j++) m16.entry(tg[j], h[j]);
+            return m16.finish();
         }
 #pragma unroll
         for (int j = 0; j < 16; j++)
@@ -1242,6 +1252,7 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t L1 = A.H + 1;
     const uint32_t SH = cmp_shared_bytes(A.W);
+    CW_STAMP(c, 8);
     for (uint32_t k0 = 0; k0 < 2 * n; k0 += 64) {
         const uint32_t k = k0 + lane;
         const bool act = k < 2 * n;
@@ -1267,6 +1278,7 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         // inner nodes: the child entries, loaded while the loads above are in flight
         uint32_t mlen = 0;
         if (inner) mlen = side ? stage_inner(B, l, b, c.shared + ioff) : stage_inner(A, l, b, c.shared + ioff);
+        CW_STAMP(c, 9);
         const uint32_t ssz = seg ? (uint32_t)(len + 64 + 15 < SH ? ((len + 64 + 15) & ~15ull) : SH + 16) : 0;
         const uint32_t soff = itot + wave_excl_scan(ssz);
         const bool sfit = seg && (et & TAG_PRESENT) && soff + ssz <= SH;
@@ -1286,6 +1298,7 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
             }
             wave_copy4(sp[0], ln[0], dp[0], sp[1], ln[1], dp[1], sp[2], ln[2], dp[2], sp[3], ln[3], dp[3]);
         }
+        CW_STAMP(c, 10);
         wave_sync_lds();
         CW_STAMP(c, 7);
         if (act) {
@@ -1294,9 +1307,10 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
                 ok = inner ? (mlen == 0) : empty;
             } else {
                 uint32_t d[4];
-                if (inner) stmd5::md5_lds(c.shared + ioff, mlen, d);
-                else if (sfit) stmd5::md5_lds(c.shared + soff, (uint32_t)len, d);
-                else stmd5::md5_global_pf((side ? B.vheap : A.vheap) + v0, len, d);
+                if (inner || sfit)   // one inlined chain for every staged message (branches would run one after another)
+                    stmd5::md5_lds(c.shared + (inner ? ioff : soff), inner ? mlen : (uint32_t)len, d);
+                else
+                    stmd5::md5_global_pf((side ? B.vheap : A.vheap) + v0, len, d);
                 ok = et == TAG_PRESENT && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
             }
             if (!ok) {
@@ -1338,7 +1352,7 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
     uint8_t *wl = lds + (uint64_t)wave * slice;
     const uint32_t H = A.H, L1 = H + 1, sh = A.shift, W = A.W;
     CmpWalk c;
-    c.stamp = stamps ? stamps + (uint64_t)w * 8 : nullptr;
+    c.stamp = stamps ? stamps + (uint64_t)w * 16 : nullptr;
     CW_STAMP(c, 0);
     c.shared = wl;
     c.list = reinterpret_cast<uint64_t *>(wl + cmp_shared_bytes(W));

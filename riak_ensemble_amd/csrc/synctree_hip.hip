@@ -997,9 +997,11 @@ static int rehash_all(st_tree *t, const uint8_t *mask) {
 // Verify every node marked in t->mark (levels 1..L); results in t->ok.
 static int verify_marked(st_tree *t, uint32_t L) {
     DevTree d = view(t);
-    if (L == t->H + 1)
+    if (L == t->H + 1) {   // segments in the length order of seg_perm: lanes of a wave hash alike-sized messages
+        CHK(ensure_perm(t));
         LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
-               (const uint32_t *)nullptr, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+               (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+    }
     const uint32_t lmax = L < t->H ? L : t->H;
     if (lmax >= 1) {
         const uint64_t nodes = t->base[lmax + 1] - t->base[1];
@@ -2303,23 +2305,24 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         Scratch sc(t);
         uint64_t *stamps = nullptr;
         if (stamp) {   // diagnostic: per-wave phase stamps (100 MHz) to stderr
-            CHK(sc.alloc(&stamps, (uint64_t)w.nw * 8));
-            HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 64, t->stream));
+            CHK(sc.alloc(&stamps, (uint64_t)w.nw * 16));
+            HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 128, t->stream));
         }
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
                filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
         if (stamp) {
-            std::vector<uint64_t> h((uint64_t)w.nw * 8);
+            std::vector<uint64_t> h((uint64_t)w.nw * 16);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
             CHK(tsync(t));
             uint64_t t0 = ~0ull;
-            for (uint32_t x = 0; x < w.nw; x++) t0 = std::min(t0, h[x * 8]);
-            static const char *nm[8] = {"start", "levels", "children", "verify", "merge", "end", "", "staged"};
-            for (int k = 0; k < 8; k++) {
+            for (uint32_t x = 0; x < w.nw; x++) t0 = std::min(t0, h[x * 16]);
+            static const char *nm[11] = {"start", "levels", "children", "verify", "merge", "end", "", "staged",
+                                         "flush", "inner", "values"};
+            for (int k = 0; k < 11; k++) {
                 if (k == 6) continue;
                 std::vector<double> v;
                 for (uint32_t x = 0; x < w.nw; x++)
-                    if (h[x * 8 + k]) v.push_back((h[x * 8 + k] - t0) / 100.0);
+                    if (h[x * 16 + k]) v.push_back((h[x * 16 + k] - t0) / 100.0);
                 if (v.empty()) continue;
                 std::sort(v.begin(), v.end());
                 fprintf(stderr, "cmp stamp %-9s n=%4zu min %7.2f med %7.2f p90 %7.2f max %7.2f us\n", nm[k], v.size(), v[0],
