@@ -109,7 +109,7 @@ __device__ __forceinline__ void rw_node(const uint8_t *msg, uint32_t len, uint4 
 // takes window g % nwin of tree group[g / nwin], each tree with its own slot
 // arrays, tiles, counters and mailboxes.
 template <bool STAMP, bool GROUP, int NW>
-__global__ void __launch_bounds__(NW * 64) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
+__global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
                                                           uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps,
                                                           uint32_t mhb) {
 #define RF_STAMP(k) do { if (STAMP && threadIdx.x == 0) { stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime(); \
