@@ -532,14 +532,18 @@ __global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *ou
     // if the key's path verified)
     __shared__ const uint8_t *gsrc[SB_MAX];
     __shared__ uint32_t glen[SB_MAX], gfound[SB_MAX];
-    for (uint32_t x = tid; x < n * L1; x += SB_VERIFY) {
-        if (tid >= SB_VERIFY) break;
-        const uint32_t i = x / L1, l = x % L1 + 1;
-        const uint64_t s = seg[i];
-        bool good;
-        if (l == L1) good = verify_segment_ov(t, ov, s);
-        else good = verify_inner_node(t, l, s >> (t.shift * (L1 - l)), dyn + tid * lane_region_bytes(t.W));
-        if (!good) atomicMin(&bad[i], l);
+    // Inner path nodes on threads [0, SB_VERIFY), the segments on wave 3: the
+    // segment MD5 (global memory) and the inner-node MD5 (LDS) in one wave
+    // would run one after the other, as two branches.
+    if (tid < SB_VERIFY) {
+        for (uint32_t x = tid; x < n * t.H; x += SB_VERIFY) {
+            const uint32_t i = x / t.H, l = x % t.H + 1;
+            if (!verify_inner_node(t, l, seg[i] >> (t.shift * (L1 - l)), dyn + tid * lane_region_bytes(t.W)))
+                atomicMin(&bad[i], l);
+        }
+    } else if (tid >= 192) {
+        for (uint32_t i = tid - 192; i < n; i += 64)
+            if (!verify_segment_ov(t, ov, seg[i])) atomicMin(&bad[i], L1);
     }
     __shared__ uint8_t gval[SB_MAX][SB_GVAL];   // values found, prefetched while the paths verify
     if (in.op == 0 && tid >= 128 && tid < 128 + n) {   // orddict_find (synctree.erl:342-348)
