@@ -1097,11 +1097,28 @@ __device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t 
 // at or past lim are counted, not written: the host grows the buffer and
 // runs the compare again) and returns their count.  Record kinds: 0 = {K,{A,B}}, 1 = {K,{A,'$none'}},
 // 2 = {K,{'$none',B}}.
-__device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, int filter, uint8_t *lds,
-                                   DiffRec *out, uint64_t base, uint64_t lim, uint64_t *algo_bytes) {
+// The CSR bounds of one segment pair (entry and value-byte ranges, both sides).
+struct SegPair {
+    uint64_t a0, a1, b0, b1, va0, va1, vb0, vb1;
+};
+__device__ __forceinline__ SegPair seg_pair(const DevTree &A, const DevTree &B, uint64_t s) {
+    SegPair p;
+    p.a0 = A.seg_off[s]; p.a1 = A.seg_off[s + 1]; p.b0 = B.seg_off[s]; p.b1 = B.seg_off[s + 1];
+    p.va0 = A.seg_voff[s]; p.va1 = A.seg_voff[s + 1]; p.vb0 = B.seg_voff[s]; p.vb1 = B.seg_voff[s + 1];
+    return p;
+}
+__device__ __forceinline__ SegPair shfl_pair(const SegPair &p, int j) {
+    SegPair q;
+    q.a0 = __shfl(p.a0, j, 64); q.a1 = __shfl(p.a1, j, 64); q.b0 = __shfl(p.b0, j, 64); q.b1 = __shfl(p.b1, j, 64);
+    q.va0 = __shfl(p.va0, j, 64); q.va1 = __shfl(p.va1, j, 64); q.vb0 = __shfl(p.vb0, j, 64); q.vb1 = __shfl(p.vb1, j, 64);
+    return q;
+}
+
+__device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, const SegPair &P, int filter,
+                                   uint8_t *lds, DiffRec *out, uint64_t base, uint64_t lim, uint64_t *algo_bytes) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t a0 = A.seg_off[s], a1 = A.seg_off[s + 1], b0 = B.seg_off[s], b1 = B.seg_off[s + 1];
-    const uint64_t va0 = A.seg_voff[s], va1 = A.seg_voff[s + 1], vb0 = B.seg_voff[s], vb1 = B.seg_voff[s + 1];
+    const uint64_t a0 = P.a0, a1 = P.a1, b0 = P.b0, b1 = P.b1;
+    const uint64_t va0 = P.va0, va1 = P.va1, vb0 = P.vb0, vb1 = P.vb1;
     const uint64_t nA = a1 - a0, nB = b1 - b0;
     // algorithmic bytes of this segment pair (bench roofline): per side the
     // offsets, key records, values and the parent's entry (key bytes added below)
@@ -1321,14 +1338,23 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         wave_sync_lds();
     }
     CW_STAMP(c, 3);
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t it = c.list[i];
-        if ((uint32_t)(it >> 56) != L1) continue;
+    // the listed segments' CSR bounds, 64 per round trip (lane i: the i-th
+    // item), handed to each merge-join by shuffles in list order
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint64_t it = i < n ? c.list[i] : 0;
+        const bool sg = i < n && (uint32_t)(it >> 56) == L1;
         const uint64_t sj = it & ((1ull << 56) - 1);
-        uint64_t by;
-        c.pos += seg_merge_wave(A, B, sj, c.filter, c.shared, c.scratch, c.rb + c.pos, c.lim, &by);
-        c.bytes += by;
-        wave_sync_lds();
+        SegPair p = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (sg) p = seg_pair(A, B, sj);
+        for (uint64_t m = __ballot(sg); m; m &= m - 1) {
+            const int j = __ffsll((long long)m) - 1;
+            uint64_t by;
+            c.pos += seg_merge_wave(A, B, __shfl(sj, j, 64), shfl_pair(p, j), c.filter, c.shared, c.scratch, c.rb + c.pos,
+                                    c.lim, &by);
+            c.bytes += by;
+            wave_sync_lds();
+        }
     }
     CW_STAMP(c, 4);
 }
@@ -1989,10 +2015,14 @@ __device__ __forceinline__ uint4 tile_row(const uint4 *tiles, uint64_t base, uin
 // (possibly on another XCD, behind another L2) reads: written and read with
 // agent-scope atomics, which are coherent across XCDs without a write-back of
 // the writer's L2 or an invalidate of the reader's.
+// A window root's entry for the tree's last window: the 16-byte MD5 and the
+// tag in three 64-bit words of 48 payload bits, each stamped with the launch's
+// epoch in its top 16 bits (TreeTiles::epoch, never 0; the mailboxes start
+// zeroed).  Every word is one atomic store, so a reader that sees the epoch in
+// all three has the whole entry, whatever order the stores become visible in.
 struct MailEntry {
-    unsigned long long lo, hi;
-    uint32_t tag, pad0;
-    uint64_t pad1;
+    unsigned long long w[3];
+    uint64_t pad;
 };
 
 struct TreeTiles {
@@ -2005,6 +2035,7 @@ struct TreeTiles {
     const uint4 *tiles;
     const uint64_t *pres;   // per-window segment presence bitmaps (tile build)
     const uint16_t *noff;   // per window: the 256 level-H message offsets in LDS, 4-byte units (tile build)
+    uint32_t epoch;         // this launch's mailbox epoch for the tree (1..65535, differs from its last launch)
 };
 
 
@@ -2092,17 +2123,32 @@ __device__ __forceinline__ void lds_barrier() {
 // Mailbox of one inner-node entry read by another workgroup (possibly on
 // another XCD, behind another L2): agent-scope atomics, coherent across XCDs
 // without a write-back of the writer's L2 or an invalidate of the reader's.
-__device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg) {
-    __hip_atomic_store(&m->lo, ((unsigned long long)e.y << 32) | e.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&m->hi, ((unsigned long long)e.w << 32) | e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&m->tag, tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t tg, uint32_t ep) {
+    const unsigned long long E = (unsigned long long)ep << 48;
+    const unsigned long long w0 = (unsigned long long)e.x | ((unsigned long long)(e.y & 0xffffu) << 32);
+    const unsigned long long w1 = (unsigned long long)(e.y >> 16) | ((unsigned long long)e.z << 16);
+    const unsigned long long w2 = (unsigned long long)e.w | ((unsigned long long)(tg & 0xffffu) << 32);
+    __hip_atomic_store(&m->w[0], w0 | E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&m->w[1], w1 | E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&m->w[2], w2 | E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg) {
-    const unsigned long long lo = __hip_atomic_load(&m->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long hi = __hip_atomic_load(&m->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tg = (uint16_t)__hip_atomic_load(&m->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    e = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+// Reads a mailbox written in this launch: each word is re-read until it
+// carries the epoch (bounded: a word that never does is taken as it is after
+// ~2^20 polls, so a defect cannot hang the GPU).
+__device__ __forceinline__ unsigned long long mail_word(unsigned long long *w, uint32_t ep) {
+    unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t it = 0; (uint32_t)(v >> 48) != ep && it < (1u << 20); it++) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return v;
+}
+__device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg, uint32_t ep) {
+    const unsigned long long w0 = mail_word(&m->w[0], ep), w1 = mail_word(&m->w[1], ep), w2 = mail_word(&m->w[2], ep);
+    e = make_uint4((uint32_t)w0, (uint32_t)((w0 >> 32) & 0xffffu) | ((uint32_t)w1 << 16), (uint32_t)(w1 >> 16),
+                   (uint32_t)w2);
+    tg = (uint16_t)(w2 >> 32);
 }
 
 // Window-local tile order (fused rehash): one workgroup per window of 4096

@@ -108,6 +108,7 @@ struct st_tree {
     bool tiles_valid = false;
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
+    uint32_t mail_epoch = 0;        // epoch of the last fused launch over this tree (MailEntry)
     // segment-range partition (st_set_partition): owned segments [part_lo, part_hi)
     bool partitioned = false;
     uint64_t part_lo = 0, part_hi = 0;
@@ -845,12 +846,20 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tiles = t->tiles;
     x.pres = t->tpres;
     x.noff = t->tnoff;
+    x.epoch = t->mail_epoch;
     return x;
+}
+// A fused launch's mailbox epoch for tree t: 1..65535, never the epoch of
+// the tree's previous launch (whose words its mailboxes still hold).
+static TreeTiles launch_tiles(st_tree *t) {
+    t->mail_epoch = t->mail_epoch % 65535u + 1u;
+    return tree_tiles(t);
 }
 
 static int ensure_lvl_cnt(st_tree *t) {
     if (t->lvl_cnt || t->H < 3) return ST_OK;
     CHK(dalloc_t(t, &t->mail, t->base[t->H - 1]));
+    HIPCHK(hipMemsetAsync(t->mail, 0, t->base[t->H - 1] * sizeof(MailEntry), t->stream));   // epoch 0: never a launch's
     CHK(dalloc_t(t, &t->lvl_cnt, t->base[t->H - 2]));
     HIPCHK(hipMemsetAsync(t->lvl_cnt, 0, t->base[t->H - 2] * 4, t->stream));
     return ST_OK;
@@ -912,7 +921,7 @@ static int rehash_tiled(st_tree *t) {
         const uint32_t mhb = fused_mh_bytes(t->mh_bytes, nroots);
         static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
         if (!stamp) {
-            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, tree_tiles(t),
+            LAUNCH(t, "rehash_fused", (k_rehash_fused<false, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, launch_tiles(t),
                    (const TreeTiles *)nullptr, 0u, root0, lmin, (uint64_t *)nullptr, mhb);
             return ST_OK;
         }
@@ -921,7 +930,7 @@ static int rehash_tiled(st_tree *t) {
         uint64_t *st = nullptr;
         CHK(sc.alloc(&st, (uint64_t)nwg * 32));
         HIPCHK(hipMemsetAsync(st, 0, (uint64_t)nwg * 32 * 8, t->stream));
-        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, tree_tiles(t),
+        LAUNCH(t, "rehash_fused", (k_rehash_fused<true, false, 16>), nwg, 1024, fused_lds_bytes(mhb), d, launch_tiles(t),
                (const TreeTiles *)nullptr, 0u, root0, lmin, st, mhb);
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
@@ -1686,7 +1695,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     // every window of every tree in ONE launch of the fused kernel (K1 +
     // levels + top per tree): the trees' tails overlap each other's K1
     std::vector<TreeTiles> h(n);
-    for (uint32_t i = 0; i < n; i++) h[i] = tree_tiles(trees[i]);
+    for (uint32_t i = 0; i < n; i++) h[i] = launch_tiles(trees[i]);
     Scratch sc(t);
     TreeTiles *dtt = nullptr;
     CHK(sc.alloc(&dtt, n));
