@@ -77,8 +77,8 @@ def _free_port():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--steps', type=int, default=200)   # 200 x ~66 us: a timed region of ~13 ms, so host jitter does not dominate
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--keys', type=int, default=10_000_000)
     ap.add_argument('--no-cpu', action='store_true', help='skip the CPU baseline legs')
     ap.add_argument('--no-extras', action='store_true', help='skip every leg but the headline rehash')
