@@ -184,28 +184,39 @@ def main():
         S = 1 << 20
         seg_of = _segment_histogram(tree, keys_h)
         seg_blocks = int(md5_blocks(seg_of[seg_of > 0] * 17).sum())
-        # Algorithmic bytes of one rehash launch (k_rehash_fused = K1 + the
-        # inner levels): every segment's hash input (its values, 17 B per key;
-        # MD5 padding is computed, not data), the tile metadata (segment id +
-        # block count, 2 x 4 B per segment; 16 B per 64-segment tile), the
-        # 18-B entry (md5 + tag) written per segment and per inner node
-        # (69,905 for W=16, H=5; their inputs stay in LDS, except the 16
-        # children read by each of the 17 climbing nodes), and the window's
-        # segment presence bitmap (1 bit per segment).
+        # Algorithmic bytes of one rehash launch: every value
+        # byte the hash reads (17 B per key; MD5 padding is computed, not
+        # data) + one 17-byte entry <<0, MD5>> per PRESENT node written
+        # (non-empty segments + present inner nodes, counted on this tree).
+        # The kernel's own bookkeeping (tile metadata, presence bits, the
+        # 18-B slot writes of absent segments) is traffic, not algorithm: it
+        # is reported separately (bytes_incl_metadata).
+        present_inner = _present_inner(tree)
+        nonempty = int((seg_of > 0).sum())
+        k1_bytes = 17 * n + 17 * (nonempty + present_inner)
         inner_nodes = sum(16 ** l for l in range(5))
-        k1_bytes = 17 * n + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
+        meta_bytes = 17 * n + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
         seg_blocks += 349525   # inner-node MD5 blocks (full nodes: 5 each)
         k1_avg_ms = max(k1_ms / max(k1_n, 1), 1e-9)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
         t_valu = seg_blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
+        cold = _bench_cold_l3(tree, torch, dev, k1_bytes, k1_avg_ms)
         roof = {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
                 'traffic': pmc['traffic_bytes'] if pmc and pmc.get('traffic_bytes') else None,
                 'kernel': K1_KERNEL + ' (K1 segment_hash + levels 5..1 + top, one launch)',
                 'kernel_avg_ms': round(k1_avg_ms, 4),
                 'kernel_time_source': 'HIP events on the library stream around every launch (%d launches)' % k1_n,
-                'bytes_per_launch': k1_bytes, 'tile_bytes_per_launch': 64 * seg_blocks,
+                'bytes_per_launch': k1_bytes,
+                'bytes_formula': '17 B x %d keys (values) + 17 B x (%d non-empty segments + %d present inner nodes) '
+                                 '(SURVEY §8(d))' % (n, nonempty, present_inner),
+                'bytes_incl_metadata': meta_bytes,
+                'cold_l3': {'frac': cold['frac'], 'kernel_avg_ms': cold['kernel_avg_ms'],
+                            'achieved': cold['achieved_GBps'],
+                            'what': 'same launch after a 1 GiB read (the 256 MiB Infinity Cache flushed): tiles '
+                                    'from HBM'},
+                'tile_bytes_per_launch': 64 * seg_blocks,
                 'md5_blocks_per_launch': seg_blocks, 't_min_hbm_us': round(t_hbm * 1e6, 2),
                 'valu': {'t_min_us': round(t_valu * 1e6, 2), 'frac': round(t_valu / (k1_avg_ms / 1e3), 4),
                          'simd_cycles_per_block': round(MD5_SIMD_CYCLES_PER_BLOCK, 2),
@@ -222,7 +233,6 @@ def main():
                'roofline': roof,
                'rehash_top_hash': top0.hex(), 'tops_allgather_ok': tops_ok}
         if not args.no_extras:
-            out['cold_l3'] = _bench_cold_l3(tree, torch, dev, k1_bytes, k1_avg_ms)
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, dev_index, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_d, vals_d, n, dev_index, torch)
             out['leveldb'] = _bench_leveldb(synctree_hip, tree, dev_index, torch)
@@ -367,6 +377,16 @@ def _bench_repair(tree, keys_h, torch, reps=10):
             'what': 'repair path: delete one segment node + full rehash/1 (tile rebuild included), median of %d, '
                     'wall incl. the C-ABI calls; tile_bytes = the device copy of every value the tiled '
                     'layout keeps (the headline rehash reads it)' % reps}
+
+
+def _present_inner(tree):
+    """Present inner nodes (levels 1..H) of a device tree: the entries its
+    parents hold for them (st_level_entries of levels 2..H+1 give the
+    children's presence; a node is present iff one of its children is)."""
+    n = 0
+    for lvl in range(2, tree.height + 2):
+        n += int(tree.level_entries(lvl)[0].reshape(-1, tree.width).any(1).sum())
+    return n
 
 
 def _segment_histogram(tree, keys_h):
@@ -636,8 +656,17 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     trees[0].set_timing(False)
     g_avg = g_ms / max(g_n, 1)
     S = trees[0].segments
-    inner = sum(16 ** lv for lv in range(trees[0].height))
-    tree_bytes = 17 * nk + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner * 18
+    H = trees[0].height
+    # SURVEY §8(d) bytes per tree: 17 B per key (values) + a 17-B entry per
+    # present node (non-empty segments + present inner nodes), counted on a
+    # sample of the trees (Poisson occupancy: every tree has the same
+    # expectation; the sample's spread is a few hundred nodes)
+    samp = trees[:4]
+    nonempty = [int(t.level_entries(H + 1)[0].sum()) for t in samp]
+    pinner = [_present_inner(t) for t in samp]
+    tree_bytes = int(17 * nk + 17 * (sum(nonempty) + sum(pinner)) / len(samp))
+    inner = sum(16 ** lv for lv in range(H))
+    meta_bytes = 17 * nk + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner * 18
     g_gbs = E * tree_bytes / (g_avg / 1e3) / 1e9 if g_avg > 0 else 0.0
     mem0 = trees[0].mem_stats()
     # per-tree rehash for comparison (rank-local, untimed for the headline)
@@ -655,10 +684,13 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
             'kernel_ms_per_batch': round(g_avg, 4),
             'roofline': {'bound': 'hbm', 'achieved': round(g_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(g_gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': E * tree_bytes,
-                         'bytes_per_tree': tree_bytes, 'tile_bytes_per_tree': mem0['tiles'],
-                         'kernel': K1_KERNEL + '<GROUP, 8 waves per window, two windows per CU>',
-                         'note': 'per tree: 17 B of value per key + 8 B tile metadata + 1/8 B presence per segment, '
-                                 '18-B entry written per segment and inner node; kernel time from HIP events'},
+                         'bytes_per_tree': tree_bytes, 'bytes_per_tree_incl_metadata': meta_bytes,
+                         'tile_bytes_per_tree': mem0['tiles'],
+                         'sample_nonempty_segments': nonempty, 'sample_present_inner': pinner,
+                         'kernel': K1_KERNEL + '<GROUP, 8 waves per window, 6 waves per SIMD>',
+                         'note': 'SURVEY §8(d): per tree 17 B of value per key + a 17-B entry per present node '
+                                 '(non-empty segments + present inner nodes, mean of %d sampled trees); kernel time '
+                                 'from HIP events on trees[0]\'s stream' % len(samp)},
             'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
             'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '
                     'the rank\'s trees + st_tops_to_device + all_gather_into_tensor of every ensemble\'s top hash '

@@ -9,9 +9,22 @@
  * riak_ensemble_amd/synctree.py.
  *
  * Conventions:
- *  - Trees are device-resident; a handle is used by one caller at a time
- *    (like the owning gen_server, src/riak_ensemble_peer_tree.erl:58-59);
- *    different handles may be used concurrently (each has its own stream).
+ *  - Trees are device-resident and each handle is owned by one lock, like
+ *    the gen_server that owns a tree (src/riak_ensemble_peer_tree.erl:58-59):
+ *    every entry point holds the handle's lock for the whole call, so calls
+ *    on one handle from different threads run one after the other, and
+ *    different handles run concurrently (each has its own stream).  A call
+ *    that reads a SECOND tree (st_compare*, st_exchange_apply/plan) holds
+ *    both locks, taken in address order, and drains its device work before
+ *    releasing them: the remote tree is read only through its owner's lock,
+ *    as the reference reads it only through the remote peer_tree process
+ *    (src/riak_ensemble_exchange.erl:72-81, peer_tree.erl:155-157).
+ *    st_rehash_group / st_tops_to_device lock every tree of the group.
+ *  - Device work is enqueued asynchronously where the call returns nothing
+ *    that depends on it (st_rehash); a device error of such work is
+ *    reported (ST_EDEVICE) by the first call that waits for it (st_sync,
+ *    st_top_hash, any read), and the tree then refuses every read with
+ *    ST_EDEVICE until a full st_rehash completes without error.
  *  - Corruption is a VALUE, not an error: ST_CORRUPTED plus the (Level,
  *    Bucket) of the first node on the root->leaf path whose hash does not
  *    match its parent's entry, exactly like {corrupted, Level, Bucket}
@@ -350,6 +363,15 @@ int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint
  * kernel ("segment_hash", "level_rehash", "key_segment", "tree_compare"...). */
 int st_set_timing(st_tree *t, int enabled);
 int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *total_ms);
+
+/* Fault injection for tests (no reference counterpart; the reference's
+ * equivalent is rt_intercept, test/synctree_intercepts.erl).
+ * ST_DBG_SKIP_MAIL: the next fused rehash launches of this tree do not store
+ * the mailbox entry of window `value` (a level-(Height-2) subtree; -1 = off),
+ * so the launch's climb never sees it: the bounded wait then reports
+ * ST_EDEVICE instead of hashing a stale entry into the top hash. */
+#define ST_DBG_SKIP_MAIL 1
+int st_debug_knob(st_tree *t, int knob, int64_t value);
 
 #ifdef __cplusplus
 }

@@ -106,7 +106,9 @@ _SIGS = {
                                      u64p]),
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
+    'st_debug_knob': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
 }
+ST_DBG_SKIP_MAIL = 1
 
 EXPORTED = sorted(_SIGS)
 _lib = None

@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
         } else if (ph == 2) {   // the window root: mailbox, counter; the last window climbs
             if (tid == 0) {
                 const uint64_t slot = t.base[l] + root;
-                mail_put(RFT(mail) + slot, e, tg, RFT(epoch));   // read by the tree's last window
+                if (root != RFT(skip_root)) mail_put(RFT(mail) + slot, e, tg, RFT(epoch));   // read by the tree's last window
                 // this window's mailbox stores have completed (agent-coherent)
                 // before the counter moves; no L2 write-back / invalidate
                 __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -348,7 +348,8 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
                 const uint64_t ci = c0 + tid;   // child ci % 16 of this level's node ci / 16
                 uint4 h = make_uint4(0, 0, 0, 0);
                 uint16_t g = 0;
-                if (ci < nn * 16) mail_get(RFT(mail) + t.base[l] + nlo * 16 + ci, h, g, RFT(epoch));
+                if (ci < nn * 16 && !mail_get(RFT(mail) + t.base[l] + nlo * 16 + ci, h, g, RFT(epoch)))
+                    raise_derr(RFT(err), ST_DERR_MAIL);
                 const unsigned long long pb = __ballot(ci < nn * 16 && (g & TAG_PRESENT));
                 const uint32_t sib = (uint32_t)(pb >> (16 * ((tid & 63) >> 4))) & 0xffffu, j = tid & 15;
                 if (g & TAG_PRESENT) rw_put17(MH + (ci >> 4) * RW_MSG + 17u * __builtin_popcount(sib & ((1u << j) - 1u)), g & 0xffu, h);

@@ -2035,8 +2035,11 @@ struct TreeTiles {
     const uint4 *tiles;
     const uint64_t *pres;   // per-window segment presence bitmaps (tile build)
     const uint16_t *noff;   // per window: the 256 level-H message offsets in LDS, 4-byte units (tile build)
+    uint32_t *err;          // the tree's device-error word (host-mapped): set when a mailbox wait times out
     uint32_t epoch;         // this launch's mailbox epoch for the tree (1..65535, differs from its last launch)
+    uint32_t skip_root;     // fault injection (st_debug_knob ST_DBG_SKIP_MAIL): this window stores no mailbox; ~0u = none
 };
+#define ST_DERR_MAIL 1u     // TreeTiles::err bit: a window root's mailbox entry did not arrive
 
 
 // One workgroup per tile: write the tile's stored rows (row r of lane j at
@@ -2134,21 +2137,33 @@ __device__ __forceinline__ void mail_put(MailEntry *m, const uint4 &e, uint32_t 
 }
 
 // Reads a mailbox written in this launch: each word is re-read until it
-// carries the epoch (bounded: a word that never does is taken as it is after
-// ~2^20 polls, so a defect cannot hang the GPU).
-__device__ __forceinline__ unsigned long long mail_word(unsigned long long *w, uint32_t ep) {
-    unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t it = 0; (uint32_t)(v >> 48) != ep && it < (1u << 20); it++) {
+// carries the epoch.  The wait is bounded (2^18 polls, a fraction of a
+// second; a hand-off that works takes microseconds) so a defect cannot hang
+// the GPU, and a word that never carries the epoch is an ERROR, not a value:
+// mail_get returns false and the caller sets the tree's error word, which
+// the host reports as ST_EDEVICE (the climb's hashes are then discarded).
+__device__ __forceinline__ bool mail_word(unsigned long long *w, uint32_t ep, unsigned long long &v) {
+    v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t it = 0; (uint32_t)(v >> 48) != ep && it < (1u << 18); it++) {
         __builtin_amdgcn_s_sleep(1);
         v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return v;
+    return (uint32_t)(v >> 48) == ep;
 }
-__device__ __forceinline__ void mail_get(MailEntry *m, uint4 &e, uint16_t &tg, uint32_t ep) {
-    const unsigned long long w0 = mail_word(&m->w[0], ep), w1 = mail_word(&m->w[1], ep), w2 = mail_word(&m->w[2], ep);
+__device__ __forceinline__ bool mail_get(MailEntry *m, uint4 &e, uint16_t &tg, uint32_t ep) {
+    unsigned long long w0 = 0, w1 = 0, w2 = 0;
+    bool ok = mail_word(&m->w[0], ep, w0);
+    if (ok) ok = mail_word(&m->w[1], ep, w1);   // after a timeout no further waiting
+    if (ok) ok = mail_word(&m->w[2], ep, w2);
     e = make_uint4((uint32_t)w0, (uint32_t)((w0 >> 32) & 0xffffu) | ((uint32_t)w1 << 16), (uint32_t)(w1 >> 16),
                    (uint32_t)w2);
     tg = (uint16_t)(w2 >> 32);
+    return ok;
+}
+// Raise a bit of a tree's device-error word (host-mapped, read by the host
+// after its next stream synchronisation).  A vector store at system scope.
+__device__ __forceinline__ void raise_derr(uint32_t *err, uint32_t bit) {
+    if (err) __hip_atomic_store(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Window-local tile order (fused rehash): one workgroup per window of 4096

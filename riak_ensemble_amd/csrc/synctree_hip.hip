@@ -125,6 +125,16 @@ struct st_tree {
     SmallRes sres;                                    // the last call's validated results
     uint32_t small_seq = 0;   // sequence number of the last k_small call
     std::atomic<uint64_t> sync_epoch{0};   // host synchronisations of `stream` (tsync; block reuse)
+    // the handle's owner lock (one caller at a time, like the tree's
+    // gen_server, riak_ensemble_peer_tree.erl:58-59); recursive: entry points
+    // call one another
+    std::recursive_mutex mu;
+    // device-error word in host-mapped memory (ST_DERR_*, set by kernels,
+    // checked after every synchronisation) and the poisoned state it leaves:
+    // reads refuse with ST_EDEVICE until a full rehash completes cleanly
+    uint32_t *derr = nullptr, *derr_dev = nullptr;
+    bool poisoned = false;
+    uint32_t dbg_skip_mail = ~0u;   // st_debug_knob(ST_DBG_SKIP_MAIL)
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -240,8 +250,74 @@ static int tsync(st_tree *t) {
         return ST_EDEVICE;
     }
     t->sync_epoch.fetch_add(1, std::memory_order_release);
+    // every kernel enqueued before has completed: its device-error word is final
+    if (t->derr && __atomic_load_n(t->derr, __ATOMIC_ACQUIRE)) {
+        const uint32_t w = __atomic_exchange_n(t->derr, 0u, __ATOMIC_ACQ_REL);
+        t->poisoned = true;
+        g_err = std::string("device error 0x") + std::to_string(w) +
+                ((w & ST_DERR_MAIL) ? ": fused rehash: a window root's mailbox entry never arrived (bounded wait "
+                                      "timed out); the tree's upper levels are invalid until a clean full rehash"
+                                    : "");
+        return ST_EDEVICE;
+    }
     return ST_OK;
 }
+
+// Reads of a tree whose last device work failed are refused (ST_EDEVICE)
+// until a full rehash completes cleanly.
+static int alive(const st_tree *t) {
+    if (!t->poisoned) return ST_OK;
+    g_err = "tree is in error after a failed device launch (rehash it)";
+    return ST_EDEVICE;
+}
+
+// Entry-point guards.  ENTER: the handle's owner lock for the whole call (+
+// its device, + refuse a poisoned tree); ENTER_ANY: the same without the
+// poison check (rehash, sync, destroy, stats).
+#define ENTER_ANY(t)                                                \
+    if (!(t)) { g_err = "NULL tree"; return ST_EINVAL; }            \
+    std::lock_guard<std::recursive_mutex> enter_lk_((t)->mu);       \
+    CHK(use_device(t))
+#define ENTER(t)   \
+    ENTER_ANY(t);  \
+    CHK(alive(t))
+
+// Two trees read by one call (compare / exchange): both owner locks, taken in
+// address order (no lock-order deadlock between two exchanges A->B and B->A),
+// and the local stream drained before they are released, so no device work
+// that reads the remote tree's buffers outlives the remote's lock (the
+// remote's owner may free or replace them as soon as it runs again).
+struct PairLock {
+    st_tree *a, *b;
+    std::unique_lock<std::recursive_mutex> l1, l2;
+    PairLock(st_tree *x, st_tree *y) : a(x), b(y) {
+        st_tree *lo = x < y ? x : y, *hi = x < y ? y : x;
+        l1 = std::unique_lock<std::recursive_mutex>(lo->mu);
+        if (hi != lo) l2 = std::unique_lock<std::recursive_mutex>(hi->mu);
+    }
+    PairLock(const PairLock &) = delete;
+    ~PairLock() {
+        if (a != b && hipStreamQuery(a->stream) != hipSuccess) (void)hipStreamSynchronize(a->stream);
+    }
+};
+#define ENTER_PAIR(x, y)                                                             \
+    if (!(x) || !(y)) { g_err = "NULL tree"; return ST_EINVAL; }                     \
+    PairLock enter_pl_(x, y);                                                        \
+    CHK(use_device(x));                                                              \
+    CHK(alive(x));                                                                   \
+    CHK(alive(y))
+
+// Every tree of a group call, locked in address order (duplicates once).
+struct GroupLock {
+    std::vector<std::unique_lock<std::recursive_mutex>> ls;
+    GroupLock(st_tree **trees, uint32_t n) {
+        std::vector<st_tree *> v(trees, trees + n);
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (st_tree *u : v)
+            if (u) ls.emplace_back(u->mu);
+    }
+};
 
 // Stream-ordered scratch buffers freed when the scope ends, on every return
 // path (error returns from LAUNCH / HIPCHK / CHK included).  release() hands a
@@ -586,6 +662,14 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
         st_destroy(t);
         return ST_EDEVICE;
     }
+    // the device-error word: fine-grained host memory the kernels store into
+    if (hipHostMalloc((void **)&t->derr, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&t->derr_dev, t->derr, 0) != hipSuccess) {
+        g_err = "hipHostMalloc (mapped) failed";
+        st_destroy(t);
+        return ST_EDEVICE;
+    }
+    memset(t->derr, 0, 64);
     if ((r = dalloc_t(t, &t->md5, t->nslots)) || (r = dalloc_t(t, &t->tag, t->nslots)) ||
         (r = dalloc_t(t, &t->mark, t->nslots)) || (r = dalloc_t(t, &t->ok, t->nslots)) ||
         (r = dalloc_t(t, &t->flag, 4)) || (r = dalloc_t(t, &t->cnt64, 2)) ||
@@ -614,6 +698,9 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
 
 extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
+    // wait for a call still running on the handle (a caller must not use it
+    // after destroy; this only orders destroy after calls already inside)
+    { std::lock_guard<std::recursive_mutex> g(t->mu); }
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);   // nothing of this tree is pending after this
     void *ps[] = {t->erec, t->md5, t->tag, t->mark, t->ok, t->flag, t->cnt64, t->seg_off, t->seg_voff, t->koff, t->voff, t->kheap, t->vheap,
@@ -627,6 +714,7 @@ extern "C" void st_destroy(st_tree *t) {
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
     if (t->pin) (void)hipHostFree(t->pin);
+    if (t->derr) (void)hipHostFree(t->derr);
     if (t->sout) (void)hipHostFree(t->sout);
     if (t->sreq) (void)hipHostFree(t->sreq);
     if (t->cw.res) (void)hipHostFree(t->cw.res);
@@ -637,24 +725,39 @@ extern "C" void st_destroy(st_tree *t) {
 }
 
 extern "C" int st_set_stream(st_tree *t, void *s) {
-    CHK(use_device(t));
+    ENTER_ANY(t);
     CHK(tsync(t));
     t->stream = s ? (hipStream_t)s : t->own_stream;
     return ST_OK;
 }
 
 extern "C" int st_sync(st_tree *t) {
+    ENTER_ANY(t);
     CHK(tsync(t));
     return ST_OK;
 }
 
-extern "C" uint32_t st_height(const st_tree *t) { return t->H; }
+extern "C" uint32_t st_height(const st_tree *t) { return t->H; }   // geometry: immutable after st_create
 extern "C" uint64_t st_width(const st_tree *t) { return t->W; }
 extern "C" uint64_t st_segments(const st_tree *t) { return t->S; }
-extern "C" uint64_t st_num_entries(st_tree *t) { return t->n; }
+extern "C" uint64_t st_num_entries(st_tree *t) {
+    std::lock_guard<std::recursive_mutex> g(t->mu);
+    return t->n;
+}
+
+extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
+    ENTER_ANY(t);
+    if (knob == ST_DBG_SKIP_MAIL) {
+        t->dbg_skip_mail = value < 0 ? ~0u : (uint32_t)value;
+        return ST_OK;
+    }
+    g_err = "unknown debug knob";
+    return ST_EINVAL;
+}
 
 static uint64_t num_tiles(const st_tree *t);
 extern "C" int st_mem_stats(st_tree *t, uint64_t out[6]) {
+    ENTER_ANY(t);
     out[0] = t->nslots * (sizeof(uint4) + sizeof(uint16_t) + 2);   // md5, tag, mark, ok
     out[1] = (t->S + 1) * 16 + t->cap_n * 16 + t->cap_k + t->cap_v;
     out[2] = t->tiles_cap * sizeof(uint4) + (t->tseg ? num_tiles(t) * (64 * 8 + sizeof(TileInfo)) : 0);
@@ -668,11 +771,13 @@ extern "C" int st_mem_stats(st_tree *t, uint64_t out[6]) {
 }
 
 extern "C" int st_set_timing(st_tree *t, int enabled) {
+    ENTER_ANY(t);
     t->timing = enabled != 0;
     return ST_OK;
 }
 
 extern "C" int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *total_ms) {
+    ENTER_ANY(t);
     CHK(tsync(t));
     for (auto &p : t->pending) {
         float ms = 0.f;
@@ -846,7 +951,9 @@ static TreeTiles tree_tiles(const st_tree *t) {
     x.tiles = t->tiles;
     x.pres = t->tpres;
     x.noff = t->tnoff;
+    x.err = t->derr_dev;
     x.epoch = t->mail_epoch;
+    x.skip_root = t->dbg_skip_mail;
     return x;
 }
 // A fused launch's mailbox epoch for tree t: 1..65535, never the epoch of
@@ -1387,7 +1494,7 @@ static int upload_values(st_tree *t, uint64_t n, const uint8_t *vheap, const uin
 extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                                const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel,
                                uint64_t *cbucket) {
-    CHK(use_device(t));
+    ENTER(t);
     if (n == 0) return ST_OK;
     if (n <= SB_MAX) {   // per-key latency path: one launch, one sync
         HostRecords hr;
@@ -1437,7 +1544,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
 
 extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                                int on_device, uint64_t *n_corrupted) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (n_corrupted) *n_corrupted = 0;
     if (n == 0) return ST_OK;
@@ -1488,7 +1595,7 @@ extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, cons
 }
 
 extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     uint64_t koff[2] = {0, klen};
     uint8_t *krec = nullptr, *dv = nullptr, *bop = nullptr;
@@ -1518,7 +1625,7 @@ extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
 
 extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
                                 const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (segment >= t->S) { g_err = "segment out of range"; return ST_EINVAL; }
     HostRecords hr;
@@ -1593,7 +1700,7 @@ static void set_entry_host(uint16_t &tag, uint4 &m, const uint8_t *h17) {
 
 extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint32_t n, const uint64_t *children,
                               const uint8_t *hashes17) {
-    CHK(use_device(t));
+    ENTER(t);
     if (level < 1 || level > t->H) { g_err = "inner level out of range"; return ST_EINVAL; }
     if (bucket >= t->base[level + 1] - t->base[level]) { g_err = "bucket out of range"; return ST_EINVAL; }
     std::vector<uint16_t> tags(t->W, 0);
@@ -1616,6 +1723,7 @@ extern "C" int st_store_inner(st_tree *t, uint32_t level, uint64_t bucket, uint3
 }
 
 extern "C" int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket) {
+    ENTER(t);
     if (level == 0) return st_store_top(t, nullptr, 0);
     if (level == t->H + 1) CHK(st_store_segment(t, bucket, 0, nullptr, nullptr, nullptr, nullptr, nullptr));
     else CHK(st_store_inner(t, level, bucket, 0, nullptr, nullptr));
@@ -1625,7 +1733,7 @@ extern "C" int st_delete_node(st_tree *t, uint32_t level, uint64_t bucket) {
 }
 
 extern "C" int st_store_top(st_tree *t, const uint8_t *hash17, int also_record) {
-    CHK(use_device(t));
+    ENTER(t);
     uint16_t tg = 0;
     uint4 m = make_uint4(0, 0, 0, 0);
     if (hash17) set_entry_host(tg, m, hash17);
@@ -1641,7 +1749,7 @@ extern "C" int st_store_top(st_tree *t, const uint8_t *hash17, int also_record) 
 }
 
 extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
-    CHK(use_device(t));
+    ENTER(t);
     uint16_t tg = 0;
     uint4 m = make_uint4(0, 0, 0, 0);
     if (hash17) set_entry_host(tg, m, hash17);
@@ -1654,7 +1762,8 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 
 // ------------------------------------------------------------------ rehash / verify
 extern "C" int st_rehash(st_tree *t, int upper) {
-    CHK(use_device(t));
+    ENTER_ANY(t);
+    if (upper) CHK(alive(t));   // only a full rehash recomputes every level of a tree in error
     FLUSH(t);
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
     if (t->partitioned && upper) {
@@ -1665,6 +1774,10 @@ extern "C" int st_rehash(st_tree *t, int upper) {
     else CHK(rehash_all(t, nullptr));
     CHK(erec_after_rehash(t));
     t->fresh = false;
+    if (t->poisoned) {   // a tree in error becomes readable again once this rehash completed cleanly
+        CHK(tsync(t));
+        t->poisoned = false;
+    }
     return ST_OK;
 }
 
@@ -1675,6 +1788,9 @@ extern "C" int st_rehash(st_tree *t, int upper) {
 // §8d config 4: many ensembles per GPU).
 extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     if (n == 0) return ST_OK;
+    for (uint32_t i = 0; i < n; i++)
+        if (!trees[i]) { g_err = "NULL tree"; return ST_EINVAL; }
+    GroupLock glk(trees, n);
     st_tree *t = trees[0];
     CHK(use_device(t));
     for (uint32_t i = 0; i < n; i++) {
@@ -1711,17 +1827,25 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const uint32_t mhb = fused_mh_bytes(mh, nwin);
     LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(mhb), view(t), h[0],
            (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr, mhb);
-    CHK(tsync(t));
+    // every tree's device-error word is checked (tsync): a tree whose climb
+    // timed out is left in error (ST_EDEVICE returned), the others are clean
+    int first = ST_OK;
+    if (hipStreamSynchronize(t->stream) != hipSuccess) CHK(tsync(t));   // a launch fault: report it
     for (uint32_t i = 0; i < n; i++) {
         CHK(erec_after_rehash(trees[i]));
-        CHK(tsync(trees[i]));
-        trees[i]->fresh = false;
+        const int r = tsync(trees[i]);
+        if (r == ST_OK) {
+            trees[i]->fresh = false;
+            trees[i]->poisoned = false;
+        } else if (first == ST_OK) {
+            first = r;
+        }
     }
-    return ST_OK;
+    return first;
 }
 
 extern "C" int st_verify(st_tree *t, int upper, int *ok) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     const uint32_t maxd = upper ? t->H : t->H + 1;
     if (maxd == 0) { g_err = "verify_upper at Height 0 crashes in the reference"; return ST_EINVAL; }
@@ -1752,7 +1876,7 @@ static void entry_to_h17(uint16_t tg, const uint4 &m, uint8_t *out) {
 }
 
 extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
-    CHK(use_device(t));
+    ENTER(t);
     uint16_t tg = 0;
     uint4 m;
     HIPCHK(hipMemcpyAsync(&tg, t->tag, 2, hipMemcpyDeviceToHost, t->stream));
@@ -1764,7 +1888,7 @@ extern "C" int st_top_hash(st_tree *t, uint8_t out17[17], int *present) {
 }
 
 extern "C" int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (seg_lo == 0 && seg_hi == t->S) { t->partitioned = false; return ST_OK; }
     const uint64_t l2 = t->W == 16 && t->H >= 4 ? t->S / 16 : 0;
@@ -1780,7 +1904,7 @@ extern "C" int st_set_partition(st_tree *t, uint64_t seg_lo, uint64_t seg_hi) {
 }
 
 extern "C" int st_combine_upper(st_tree *t, const uint8_t *present16, const uint8_t *hashes17) {
-    CHK(use_device(t));
+    ENTER(t);
     if (t->W != 16 || t->H < 2) { g_err = "combine needs width 16 and height >= 2"; return ST_EINVAL; }
     uint16_t tg[16];
     uint4 m[16];
@@ -1799,7 +1923,7 @@ extern "C" int st_combine_upper(st_tree *t, const uint8_t *present16, const uint
 }
 
 extern "C" int st_level_entries(st_tree *t, uint32_t level, uint8_t *present, uint8_t *hashes17) {
-    CHK(use_device(t));
+    ENTER(t);
     if (level < 1 || level > t->H + 1) { g_err = "level out of range"; return ST_EINVAL; }
     const uint64_t n = t->base[level + 1] - t->base[level];
     std::vector<uint16_t> tg(n);
@@ -1919,7 +2043,7 @@ __global__ void k_u32_to_u64(const uint32_t *a, uint64_t n, uint64_t *b) {
 // get/2 path: no result block.
 extern "C" int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, uint8_t *vout, uint32_t vcap,
                        uint32_t *vlen, uint32_t *clevel, uint64_t *cbucket) {
-    CHK(use_device(t));
+    ENTER(t);
     const uint64_t koff[2] = {0, klen};
     HostRecords hr;
     CHK(pack_records(1, &ktype, kbytes, koff, hr));
@@ -1959,6 +2083,7 @@ extern "C" int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_
 // do_insert (peer_tree.erl:224-234).
 extern "C" int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, const uint8_t *value,
                           uint32_t vlen, uint32_t *clevel, uint64_t *cbucket) {
+    ENTER(t);
     const uint64_t koff[2] = {0, klen}, voff[2] = {0, vlen};
     int32_t st = ST_OK;
     CHK(st_insert_batch(t, 1, &ktype, kbytes, koff, value, voff, &st, clevel, cbucket));
@@ -1967,7 +2092,7 @@ extern "C" int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
 
 extern "C" int st_get_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                             st_result **out) {
-    CHK(use_device(t));
+    ENTER(t);
     *out = nullptr;
     if (n >= 1 && n <= SB_MAX) {   // per-key latency path: one launch, one sync
         HostRecords hr;
@@ -2184,13 +2309,13 @@ static int node_images(st_tree *t, uint32_t level, uint64_t n, const uint64_t *b
 }
 
 extern "C" int st_exchange_get_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     return node_images(t, level, n, buckets, out, true);
 }
 
 extern "C" int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint64_t *buckets, st_result **out) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (level == 0) {
         st_result *res = new_result(n);
@@ -2215,7 +2340,7 @@ extern "C" int st_fetch_batch(st_tree *t, uint32_t level, uint64_t n, const uint
 
 extern "C" int st_segment_of_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
                                    const uint64_t *koff, uint64_t *segments_out) {
-    CHK(use_device(t));
+    ENTER(t);
     if (n == 0) return ST_OK;
     uint8_t *krec = nullptr;
     uint64_t *dko = nullptr;
@@ -2363,7 +2488,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
 
 extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
                                  uint64_t *cbucket, int *cside) {
-    CHK(use_device(local));
+    ENTER_PAIR(local, remote);
     CHK(flush_overlay(local));
     CHK(flush_overlay(remote));
     CompareOut co;
@@ -2380,7 +2505,7 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
 // peer_tree:insert gen_server call per diff.
 static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *n_diffs, uint64_t *n_applied,
                          uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
-    CHK(use_device(local));
+    ENTER_PAIR(local, remote);
     CHK(flush_overlay(local));
     CHK(flush_overlay(remote));
     *n_diffs = 0;
@@ -2468,7 +2593,7 @@ extern "C" int st_exchange_plan(st_tree *local, st_tree *remote, uint64_t *n_dif
 
 extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
                           uint64_t *cbucket, int *cside) {
-    CHK(use_device(local));
+    ENTER_PAIR(local, remote);
     CHK(flush_overlay(local));
     CHK(flush_overlay(remote));
     *out = nullptr;
@@ -2531,7 +2656,7 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
 // The last compare's frontier: visited nodes per level (levels 1..H+1) and
 // the algorithmic bytes of its final-level segment pairs (bench roofline).
 extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_levels, uint64_t *seg_bytes) {
-    CHK(use_device(local));
+    ENTER(local);
     CmpWork &w = local->cw;
     if (!w.wcnt) { g_err = "no compare has run on this tree"; return ST_EINVAL; }
     std::vector<uint32_t> st((uint64_t)w.nw * ST_STATW);
@@ -2557,6 +2682,7 @@ extern "C" int st_compare_stats(st_tree *local, uint64_t *visited, uint32_t max_
 // (SMALL_ATOM_UTF8_EXT / ATOM_UTF8_EXT only).
 extern "C" int st_set_etf_atoms(st_tree *t, int utf8) {
     if (!t) { g_err = "NULL tree"; return ST_EINVAL; }
+    std::lock_guard<std::recursive_mutex> g(t->mu);
     t->flags = utf8 ? (t->flags | ST_FLAG_ATOM_UTF8) : (t->flags & ~ST_FLAG_ATOM_UTF8);
     return ST_OK;
 }
@@ -2579,8 +2705,12 @@ extern "C" int st_key_record(uint8_t ktype, const uint8_t *bytes, uint64_t len, 
 // (18 bytes per tree: present, hash17), for an RCCL all-gather.
 extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
     if (n == 0) return ST_OK;
+    for (uint32_t i = 0; i < n; i++)
+        if (!trees[i]) { g_err = "NULL tree"; return ST_EINVAL; }
+    GroupLock glk(trees, n);
     st_tree *t = trees[0];
     CHK(use_device(t));
+    for (uint32_t i = 0; i < n; i++) CHK(alive(trees[i]));
     std::vector<TreeTiles> h(n);
     for (uint32_t i = 0; i < n; i++) {
         if (trees[i]->device != t->device) { g_err = "trees on different devices"; return ST_EINVAL; }
@@ -2652,7 +2782,7 @@ static int snapshot_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, 
 
 extern "C" int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, st_kv **out) {
     *out = nullptr;
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (t->partitioned) { g_err = "snapshot of a partitioned tree (one partition is not a synctree)"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
@@ -2681,7 +2811,7 @@ extern "C" int st_snapshot_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t 
 
 extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t *n_records,
                                           uint64_t *key_bytes, uint64_t *value_bytes) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (t->partitioned) { g_err = "snapshot of a partitioned tree"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }
@@ -2699,7 +2829,7 @@ extern "C" int st_snapshot_leveldb_device(st_tree *t, const uint8_t *tree_id, ui
 extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t id_len, uint64_t n,
                                   const uint8_t *kheap, const uint64_t *koff, const uint8_t *vheap,
                                   const uint64_t *voff, uint64_t *n_loaded, uint64_t *n_skipped) {
-    CHK(use_device(t));
+    ENTER(t);
     FLUSH(t);
     if (t->partitioned) { g_err = "restore into a partitioned tree"; return ST_EINVAL; }
     if (id_len && !tree_id) { g_err = "tree_id is NULL"; return ST_EINVAL; }

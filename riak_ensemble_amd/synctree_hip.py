@@ -404,6 +404,10 @@ class DeviceTree:
     def set_stream(self, stream_handle):
         _lib.check(self.L.st_set_stream(self.h, ctypes.c_void_p(stream_handle)), 'st_set_stream')
 
+    def debug_knob(self, knob, value):
+        """Fault injection for tests (st_debug_knob)."""
+        _lib.check(self.L.st_debug_knob(self.h, knob, int(value)), 'st_debug_knob')
+
 
 # ---------------------------------------------------------------------------
 # The backend behaviour (synctree_ets.erl:22-66) over a DeviceTree state.

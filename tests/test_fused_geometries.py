@@ -71,3 +71,42 @@ def test_group_rehash_mixed_density():
     for dev, ora in pairs:
         _level_parity(dev, ora)
         dev.close()
+
+
+@pytest.mark.parametrize('segments,skip', [(1 << 20, 37), (1 << 16, 15)])
+def test_mailbox_timeout_is_a_device_error(segments, skip):
+    """A window root's mailbox entry that never arrives (fault injection:
+    st_debug_knob ST_DBG_SKIP_MAIL) must not become a stale entry hashed into
+    the top hash: the bounded wait raises the tree's device-error word, the
+    call that waits for the launch reports ST_EDEVICE, reads are refused, and
+    a clean full rehash makes the tree readable again with the right hashes."""
+    from riak_ensemble_amd import _lib
+    dev, ora = _pair(segments, 100_000, workload.SEED ^ 0xB0B ^ segments)
+    dev.rehash()
+    _level_parity(dev, ora)
+    dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, skip)
+    dev.rehash()                      # asynchronous: the launch is enqueued
+    with pytest.raises(_lib.DeviceError, match='mailbox'):
+        dev.sync()                    # the call that waits reports it
+    with pytest.raises(_lib.DeviceError):
+        dev.top_hash()                # no top hash from a tree in error
+    with pytest.raises(_lib.DeviceError):
+        dev.level_entries(2)
+    dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, -1)
+    dev.rehash()                      # a clean full rehash clears the error
+    dev.sync()
+    _level_parity(dev, ora)
+    # the same through the group rehash: only the faulted tree is in error
+    other, ora2 = _pair(segments, 50_000, workload.SEED ^ 0xB0C ^ segments)
+    dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, skip)
+    with pytest.raises(_lib.DeviceError, match='mailbox'):
+        synctree_hip.rehash_group([other, dev])
+    _level_parity(other, ora2)
+    with pytest.raises(_lib.DeviceError):
+        dev.top_hash()
+    dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, -1)
+    synctree_hip.rehash_group([other, dev])
+    _level_parity(dev, ora)
+    _level_parity(other, ora2)
+    dev.close()
+    other.close()
