@@ -83,6 +83,7 @@ def parse():
     ap.add_argument('--no-cpu', action='store_true', help='skip the CPU baseline legs')
     ap.add_argument('--no-extras', action='store_true', help='skip every leg but the headline rehash')
     ap.add_argument('--no-pmc', action='store_true', help='skip the rocprofv3 PMC traffic passes')
+    ap.add_argument('--no-cold', action='store_true', help='skip the cold-L3 launches (isolated kernel traces)')
     ap.add_argument('--ensembles', type=int, default=512,
                     help='config-4 leg: ensembles (trees) per GPU (4096 over 8 GPUs = 512)')
     ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
@@ -201,7 +202,8 @@ def main():
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
         t_valu = seg_blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
-        cold = _bench_cold_l3(tree, torch, dev, k1_bytes, k1_avg_ms)
+        cold = {'frac': None, 'kernel_avg_ms': None, 'achieved_GBps': None} if args.no_cold else \
+            _bench_cold_l3(tree, torch, dev, k1_bytes, k1_avg_ms)
         roof = {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(achieved_gbs / HBM_PEAK_GBS, 4),
                 'traffic': pmc['traffic_bytes'] if pmc and pmc.get('traffic_bytes') else None,
