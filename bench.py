@@ -88,7 +88,8 @@ def parse():
                     help='config-4 leg: ensembles (trees) per GPU (4096 over 8 GPUs = 512)')
     ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
     ap.add_argument('--part-keys', type=int, default=100_000_000, help='config-5 leg: keys in the partitioned tree')
-    ap.add_argument('--part-batches', type=int, default=5, help='config-5 leg: timed write batches')
+    ap.add_argument('--part-batches', type=int, default=30,
+                    help='config-5 leg: timed write batches (enough to cross a delta fold at the default limit)')
     ap.add_argument('--part-batch-keys', type=int, default=1_000_000, help='config-5 leg: keys per write batch')
     ap.add_argument('--pmc-probe', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -730,23 +731,30 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         k = torch.cat([_dev_keys_at(seed, old, dev, torch), _dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
         seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
         batches.append((k.contiguous(), _dev_values(seq, dev, torch).contiguous()))
-    # one warm-up batch, then K timed
+    # one warm-up batch, then K timed: each batch timed on its own (a device
+    # synchronisation around it) so the batches that fold the delta into the
+    # base CSR show; the reported rate is the amortised one (all K batches)
     k, v = batches[0]
     pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
     pt.combine()
     torch.cuda.synchronize()
+    folds0 = pt.tree.delta_stats()[2]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    per = []
     t0 = time.perf_counter()
     for j in range(1, K + 1):
         k, v = batches[j]
+        tb = time.perf_counter()
         pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
         pt.combine()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        per.append(time.perf_counter() - tb)
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    dl_n, dl_new, folds = pt.tree.delta_stats()
     top = pt.top_hash()
     same = True
     if dist:
@@ -755,15 +763,20 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         el = float(t.item())
         tops = parallel.gather_tops(dist, [top], device=coll_dev)
         same = all(x == top for x in tops)
+    per.sort()
     entries = pt.tree.num_entries()
     pt.tree.close()
     return {'batch_keys_per_s': round(K * B / el, 1), 'ms_per_batch': round(el * 1e3 / K, 4), 'batches': K,
+            'ms_per_batch_median': round(per[len(per) // 2] * 1e3, 4), 'ms_per_batch_max': round(per[-1] * 1e3, 4),
+            'delta_folds_in_timed_batches': folds - folds0, 'delta_entries_after': dl_n,
             'batch_keys': B, 'tree_keys': N, 'ranks': world, 'entries_on_rank0': entries,
             'tops_agree_across_ranks': same, 'load_s': round(load_s, 3),
             'what': 'config5: %d-key tree partitioned by segment range over %d rank(s); per batch: insert/3 of %d keys '
                     '(50%% overwrites Seq+1, 50%% new; verify + dirty-path rehash) on every rank, all-gather of the '
-                    'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits)'
-                    % (N, world, B)}
+                    'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits); a batch '
+                    'merges into the streaming delta CSR, which folds into the base past a quarter of the tree: '
+                    'ms_per_batch is the mean over all timed batches, folds included (median = a batch without a '
+                    'fold, max = one with)' % (N, world, B)}
 
 
 class _SoloGroup:

@@ -371,7 +371,19 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * so the launch's climb never sees it: the bounded wait then reports
  * ST_EDEVICE instead of hashing a stale entry into the top hash. */
 #define ST_DBG_SKIP_MAIL 1
+/* ST_DBG_DELTA_LIMIT: fold the streaming delta into the base CSR once it
+ * holds more than `value` entries (0 = auto: a quarter of the tree, at least
+ * 2^20; -1 = never use the delta: every batch rewrites the base CSR). */
+#define ST_DBG_DELTA_LIMIT 2
 int st_debug_knob(st_tree *t, int knob, int64_t value);
+
+/* The streaming-insert delta (no reference counterpart): a
+ * batch of insert/3 much smaller than the tree merges into a delta CSR whose
+ * entries overlay the base CSR's segments (a segment's content is the merged
+ * view), so a batch does not rewrite the whole tree; every call but a
+ * streaming insert first folds the delta into the base.  out[0] = entries in
+ * the delta, out[1] = of them new keys of the tree, out[2] = folds so far. */
+int st_delta_stats(st_tree *t, uint64_t out[3]);
 
 #ifdef __cplusplus
 }

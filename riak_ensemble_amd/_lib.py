@@ -107,8 +107,9 @@ _SIGS = {
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
     'st_debug_knob': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
+    'st_delta_stats': (ctypes.c_int, [ctypes.c_void_p, u64p]),
 }
-ST_DBG_SKIP_MAIL = 1
+ST_DBG_SKIP_MAIL, ST_DBG_DELTA_LIMIT = 1, 2
 
 EXPORTED = sorted(_SIGS)
 _lib = None

@@ -284,6 +284,7 @@ __global__ void k_snap_entries(DevTree t, uint64_t n, uint64_t sb, const uint64_
 
 // ---------------------------------------------------------------------------
 // Restore: binary_to_term of the records on the device.
+#define DK_DEPTH 48   // open tuples / lists of one restored key (deeper keys: ST_EINVAL)
 //
 // bad = malformed bytes (the reference's binary_to_term raises and fetch/3
 // answers Default: the node is absent); dom = a well-formed term the device
@@ -377,15 +378,24 @@ struct DEtf {
         if (!bad && p != e) bad = true;   // trailing bytes: binary_to_term/1 raises badarg
         return !bad;
     }
-    // Key term -> device key record (tag byte + payload; integers as
-    // sign-flipped big-endian, Latin-1 atoms converted to UTF-8).  dst NULL:
+    // Key term -> device key record (term_key.h): the plain form for int64,
+    // atom and binary keys (integers as sign-flipped big-endian, Latin-1
+    // atoms converted to UTF-8), the term record [SK][ETF][Seg][etf_len]
+    // [seg_len] for every other key the host accepts (tuples, lists,
+    // floats, integers outside int64, nested atoms / binaries).  dst NULL:
     // only the record length.
     __device__ bool key(uint8_t *dst, uint32_t &rlen) {
         if (!need(1)) return false;
         const uint32_t tg = *p;
-        if (tg == 97 || tg == 98 || tg == 110) {
+        if (tg == 97 || tg == 98 || tg == 110 || tg == 111) {
+            const uint8_t *t0 = p;
             int64_t v;
-            if (!integer(v)) return false;
+            if (tg == 111 || !integer(v)) {   // a bignum beyond int64: a term record
+                if (bad) return false;
+                p = t0;
+                dom = false;
+                return term_key(dst, rlen);
+            }
             if (dst) {
                 const uint64_t u = (uint64_t)v ^ 0x8000000000000000ull;
                 dst[0] = KEYTAG_INT;
@@ -415,6 +425,7 @@ struct DEtf {
             rlen = o;
             return true;
         }
+        if (tg != 109) return term_key(dst, rlen);
         const uint8_t *b;
         uint32_t len;
         if (!binary(b, len)) return false;
@@ -423,6 +434,211 @@ struct DEtf {
             for (uint32_t i = 0; i < len; i++) dst[1 + i] = b[i];
         }
         rlen = 1 + len;
+        return true;
+    }
+
+    // ---- term records (term_key.h, restated for the device: an explicit
+    // stack instead of recursion, DK_DEPTH open tuples / lists at most)
+    __device__ void sk_put(uint8_t *dst, uint32_t &o, uint32_t b) {
+        if (dst) dst[o] = (uint8_t)b;
+        o++;
+    }
+    __device__ void sk_int64(uint8_t *dst, uint32_t &o, int64_t v) {
+        const uint64_t u = (uint64_t)v ^ 0x8000000000000000ull;
+        sk_put(dst, o, KEYTAG_INT);
+        for (int i = 7; i >= 0; i--) sk_put(dst, o, (uint32_t)(u >> (8 * i)) & 0xFF);
+    }
+    // |v| = mag[0..n) little-endian; the SK of the integer (int64 form when it fits)
+    __device__ void sk_bigmag(uint8_t *dst, uint32_t &o, bool neg, const uint8_t *le, uint32_t n, uint32_t shift_bytes,
+                              uint64_t lo64) {
+        // n significant little-endian bytes (le[n-1] != 0) followed by shift_bytes zero bytes below them
+        const uint32_t tot = n + shift_bytes;
+        const bool fits = tot < 8 || (tot == 8 && (le[n - 1] < 0x80 || (neg && le[n - 1] == 0x80 && lo64 == 0x8000000000000000ull)));
+        if (tot == 0) { sk_int64(dst, o, 0); return; }
+        if (fits) { sk_int64(dst, o, neg ? (int64_t)(0 - lo64) : (int64_t)lo64); return; }
+        if (tot > 255) { dom = true; return; }   // beyond the record's one-byte length (host alike)
+        sk_put(dst, o, neg ? KEYTAG_NUMLO : KEYTAG_NUMHI);
+        sk_put(dst, o, neg ? 255 - tot : tot);
+        for (uint32_t i = 0; i < n; i++) sk_put(dst, o, neg ? (uint32_t)(uint8_t)~le[n - 1 - i] : le[n - 1 - i]);
+        for (uint32_t i = 0; i < shift_bytes; i++) sk_put(dst, o, neg ? 0xFF : 0x00);
+    }
+    __device__ void sk_escaped(uint8_t *dst, uint32_t &o, uint32_t tag, const uint8_t *b, uint32_t n, bool latin) {
+        sk_put(dst, o, tag);
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t c = b[i];
+            if (latin && c >= 0x80) { sk_put(dst, o, 0xC0 | (c >> 6)); sk_put(dst, o, 0x80 | (c & 0x3F)); continue; }
+            sk_put(dst, o, c);
+            if (c == 0) sk_put(dst, o, 0xFF);
+        }
+        sk_put(dst, o, 0);
+        sk_put(dst, o, 1);
+    }
+    __device__ void sk_float(uint8_t *dst, uint32_t &o, double v) {
+        const double two63 = 9223372036854775808.0;
+        if (v >= -two63 && v < two63) {
+            const double f = floor(v);
+            const double r = v - f;
+            sk_int64(dst, o, (int64_t)f);
+            if (r == 0.0) return;   // integral (and -0.0): the SK of the equal integer
+            const uint64_t bits = (uint64_t)__double_as_longlong(r);
+            sk_put(dst, o, SK_FLOAT);
+            for (int i = 7; i >= 0; i--) sk_put(dst, o, (uint32_t)(bits >> (8 * i)) & 0xFF);
+            return;
+        }
+        int ex;
+        const double m = frexp(fabs(v), &ex);                 // |v| = m * 2^ex, m in [0.5, 1)
+        const uint64_t mant = (uint64_t)ldexp(m, 53);         // 53-bit integer
+        const uint32_t shift = (uint32_t)(ex - 53);           // >= 11 here
+        const uint64_t x = mant << (shift & 7);               // <= 60 bits
+        uint8_t le[8];
+        uint32_t n = 0;
+        for (uint64_t y = x; y; y >>= 8) le[n++] = (uint8_t)y;
+        sk_bigmag(dst, o, v < 0, le, n, shift >> 3, 0);
+    }
+    // One term at p (a key, not in the plain domain) -> its term record.
+    __device__ bool term_key(uint8_t *dst, uint32_t &rlen) {
+        const uint8_t *t0 = p;
+        uint32_t o = 0;
+        uint32_t kind[DK_DEPTH], rem[DK_DEPTH];   // open containers: 0 tuple, 1 list, 2 list tail
+        int sp = 0;
+        bool top = true, big = false;
+        uint64_t big_lo = 0;
+        for (;;) {
+            const uint32_t tg = u8();
+            if (bad) return false;
+            bool opened = false;
+            switch (tg) {
+            case 97: sk_int64(dst, o, (int64_t)u8()); break;
+            case 98: sk_int64(dst, o, (int64_t)(int32_t)u32()); break;
+            case 110: case 111: {
+                const uint32_t n = tg == 110 ? u8() : u32();
+                const uint32_t sign = u8();
+                if (!need(n)) return false;
+                uint32_t m = n;
+                while (m && p[m - 1] == 0) m--;   // significant magnitude bytes
+                uint64_t lo = 0;
+                for (uint32_t i = 0; i < 8 && i < n; i++) lo |= (uint64_t)p[i] << (8 * i);
+                sk_bigmag(dst, o, sign != 0 && m, p, m, 0, lo);
+                if (top && !(m < 8 || (m == 8 && (p[7] < 0x80 || (sign && lo == 0x8000000000000000ull))))) {
+                    big = true;   // ensure_binary(Integer) = <<Key:64>>: the low 64 bits, two's complement
+                    big_lo = sign ? 0 - lo : lo;
+                }
+                p += n;
+                break;
+            }
+            case 70: {
+                if (!need(8)) return false;
+                uint64_t b = 0;
+                for (int i = 0; i < 8; i++) b = (b << 8) | p[i];
+                p += 8;
+                const double v = __longlong_as_double((long long)b);
+                if (!isfinite(v)) { bad = true; return false; }   // binary_to_term refuses non-finite floats
+                sk_float(dst, o, v);
+                break;
+            }
+            case 100: case 115: case 118: case 119: {
+                const uint32_t n = (tg == 100 || tg == 118) ? u16() : u8();
+                if (!need(n)) return false;
+                sk_escaped(dst, o, KEYTAG_ATOM, p, n, tg == 100 || tg == 115);
+                p += n;
+                break;
+            }
+            case 109: {
+                const uint32_t n = u32();
+                if (!need(n)) return false;
+                sk_escaped(dst, o, KEYTAG_BINARY, p, n, false);
+                p += n;
+                break;
+            }
+            case 104: case 105: {
+                const uint32_t n = tg == 104 ? u8() : u32();
+                if (bad) return false;
+                sk_put(dst, o, KEYTAG_TUPLE);
+                for (int i = 3; i >= 0; i--) sk_put(dst, o, (n >> (8 * i)) & 0xFF);
+                if (n) {
+                    if (sp == DK_DEPTH) { dom = true; return false; }
+                    kind[sp] = 0; rem[sp] = n; sp++;
+                    opened = true;
+                }
+                break;
+            }
+            case 106: sk_put(dst, o, KEYTAG_NIL); break;
+            case 107: {
+                const uint32_t n = u16();
+                if (!need(n)) return false;
+                sk_put(dst, o, KEYTAG_LIST);
+                for (uint32_t i = 0; i < n; i++) sk_int64(dst, o, p[i]);
+                p += n;
+                sk_put(dst, o, SK_LIST_END);
+                break;
+            }
+            case 108: {
+                const uint32_t n = u32();
+                if (bad) return false;
+                if (n == 0) { dom = true; return false; }   // never written by term_to_binary
+                if (sp == DK_DEPTH) { dom = true; return false; }
+                sk_put(dst, o, KEYTAG_LIST);
+                kind[sp] = 1; rem[sp] = n; sp++;
+                opened = true;
+                break;
+            }
+            default:
+                other(tg);   // pids, ports, refs, funs, maps, bitstrings, FLOAT_EXT: outside the key domain
+                return false;
+            }
+            if (dom) return false;
+            top = false;
+            if (opened) continue;
+            // the term is complete: close the containers it completes
+            while (sp > 0) {
+                const int q = sp - 1;
+                if (kind[q] == 2) { sp--; continue; }   // a list's improper tail ends the list
+                if (--rem[q]) break;                    // more elements
+                if (kind[q] == 0) { sp--; continue; }   // a tuple ends
+                if (!need(1)) return false;             // a list's elements ended: its tail
+                const uint32_t t = *p;
+                if (t == 106) { p++; sk_put(dst, o, SK_LIST_END); sp--; continue; }
+                if (t == 108) {                         // the tail is a list: the same list goes on
+                    p++;
+                    rem[q] = u32();
+                    if (bad) return false;
+                    if (rem[q] == 0) { dom = true; return false; }
+                    break;
+                }
+                if (t == 107) {                         // a string tail: small integers, then []
+                    p++;
+                    const uint32_t n = u16();
+                    if (!need(n)) return false;
+                    for (uint32_t i = 0; i < n; i++) sk_int64(dst, o, p[i]);
+                    p += n;
+                    sk_put(dst, o, SK_LIST_END);
+                    sp--;
+                    continue;
+                }
+                sk_put(dst, o, t == 109 ? SK_TAIL_HIGH : SK_TAIL_LOW);   // improper tail: compared as a term
+                kind[q] = 2;
+                break;
+            }
+            if (sp == 0) break;
+        }
+        // [SK][ETF = 131 ++ the term's bytes][Seg][etf_len u16 LE][seg_len u16 LE]
+        const uint32_t etf_len = 1 + (uint32_t)(p - t0);
+        if (etf_len > 0xFFFE) { dom = true; return false; }
+        if (dst) {
+            dst[o] = 131;
+            for (uint32_t i = 1; i < etf_len; i++) dst[o + i] = t0[i - 1];
+        }
+        uint32_t r = o + etf_len;
+        if (big) {
+            if (dst) for (int i = 0; i < 8; i++) dst[r + i] = (uint8_t)(big_lo >> (8 * (7 - i)));
+            r += 8;
+        }
+        const uint32_t seg_len = big ? 8u : 0xFFFFu;
+        if (dst) {
+            dst[r] = (uint8_t)(etf_len & 0xFF); dst[r + 1] = (uint8_t)(etf_len >> 8);
+            dst[r + 2] = (uint8_t)(seg_len & 0xFF); dst[r + 3] = (uint8_t)(seg_len >> 8);
+        }
+        rlen = r + 4;
         return true;
     }
 };
@@ -576,12 +792,8 @@ __global__ void k_rest_segments(DevTree t, const unsigned long long *recof, cons
             in.tuple2();
             in.key(kheap + kp, kl);
             in.binary(v, len);
-            if (j) {   // strictly ascending in term order (memcmp, then length)
-                const uint64_t m = pl < kl ? pl : kl;
-                int c = 0;
-                for (uint64_t q = 0; q < m && !c; q++) c = (int)kheap[pk + q] - (int)kheap[kp + q];
-                if (c > 0 || (c == 0 && pl >= kl)) rst_dom(ctr, sb + s);
-            }
+            if (j && rec_cmp(kheap + pk, pl, kheap + kp, kl) >= 0)   // strictly ascending in Erlang term order
+                rst_dom(ctr, sb + s);
             koff[e] = kp;
             voff[e] = vp;
             for (uint32_t q = 0; q < len; q++) vheap[vp + q] = v[q];

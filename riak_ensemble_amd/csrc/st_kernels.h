@@ -537,6 +537,16 @@ struct MergeArgs {
     const uint64_t *bvoff;
     const uint8_t *bvheap;
     uint64_t S;
+    // optional per-entry payload carried with the entries (the delta CSR's
+    // base positions, delta.h): aux of the old entries, baux of the sorted
+    // batch records; NULL when the CSR has none
+    const uint2 *aux;
+    uint2 *baux;
+    // the delta's base CSR (delta.h): when set, k_merge_pos also computes
+    // every batch record's base position into baux and counts the records
+    // that are new keys of the tree (in neither the delta nor the base)
+    const uint64_t *b_seg_off, *b_koff, *b_voff;
+    const uint8_t *b_kheap;
 };
 
 // Running sums of the merge: per sorted batch record (BatchSums: eq = kept and
@@ -559,7 +569,7 @@ struct USum {
     }
 };
 typedef USum<6> BatchSums;   // eq, ne, ke, kn, ve, vn
-typedef USum<3> SegSums;     // count, key bytes, value bytes
+typedef USum<4> SegSums;     // count, key bytes, value bytes, new keys of the tree (delta merges)
 enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 
 // ---------------------------------------------------------------------------
@@ -590,8 +600,11 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
         tot.v[0] = nold;
         tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
         tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
-        uint64_t lo = 0;
+        tot.v[3] = 0;
+        uint64_t lo = 0, blo = 0;
         bool changed = false;
+        const uint64_t bb0 = a.b_seg_off ? a.b_seg_off[s] : 0, nb = a.b_seg_off ? a.b_seg_off[s + 1] - bb0 : 0;
+        const uint64_t bv0 = a.b_seg_off ? a.b_voff[bb0] : 0;
         for (uint64_t j = j0; j < je; j++) {
             BatchSums f(0);
             if (rej) { pos[j] = 0; bs[j] = f; continue; }
@@ -620,6 +633,20 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
             }
             bs[j] = f;
             changed |= kept;
+            if (a.b_seg_off) {   // the record's place in the base run (ascending: the search resumes)
+                uint64_t bhi = nb;
+                while (blo < bhi) {
+                    const uint64_t mid = (blo + bhi) >> 1, e2 = bb0 + mid;
+                    if (rec_cmp(a.b_kheap + a.b_koff[e2], a.b_koff[e2 + 1] - a.b_koff[e2], kb, kl) < 0) blo = mid + 1; else bhi = mid;
+                }
+                const uint64_t e2 = bb0 + blo;
+                const bool beq = blo < nb && rec_cmp(a.b_kheap + a.b_koff[e2], a.b_koff[e2 + 1] - a.b_koff[e2], kb, kl) == 0;
+                uint2 x;
+                x.x = (uint32_t)(a.b_voff[e2] - bv0) | (beq ? 0x80000000u : 0u);
+                x.y = beq ? (uint32_t)(a.b_voff[e2 + 1] - a.b_voff[e2]) : 0u;
+                a.baux[j] = x;
+                if (ne && !eq && !beq) tot.v[3] += 1;
+            }
             tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
             tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
             tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
@@ -643,6 +670,7 @@ struct MergeOut {
     uint64_t *seg_off, *seg_voff;   // S + 1
     uint64_t *koff, *voff;          // n_new + 1
     uint8_t *kheap, *vheap;
+    uint2 *aux;                     // n_new (NULL: no payload)
 };
 
 // Old entries: a workgroup per 256 consecutive segments walks their old
@@ -732,6 +760,7 @@ __global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *
         }
         o.koff[nw] = nk;
         o.voff[nw] = nv;
+        if (o.aux) o.aux[nw] = a.aux[e];
         copy_bytes(o.kheap + nk, a.kheap + okb, kl);
         copy_bytes(o.vheap + nv, a.vheap + ovb, vl);
     }
@@ -759,6 +788,7 @@ __global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const
         const uint64_t bk = a.bv.koff[bi], bv = a.bvoff[bi];
         o.koff[nw] = nk;
         o.voff[nw] = nv;
+        if (o.aux) o.aux[nw] = a.baux[j];
         copy_bytes(o.kheap + nk, a.bv.kheap + bk, a.bv.koff[bi + 1] - bk);
         copy_bytes(o.vheap + nv, a.bvheap + bv, a.bvoff[bi + 1] - bv);
     }

@@ -25,6 +25,7 @@
 #include "rehash_win.h"
 #include "leveldb_fmt.h"
 #include "small_path.h"
+#include "delta.h"
 
 static thread_local std::string g_err;
 static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past a range
@@ -64,6 +65,8 @@ struct CsrSet {
     uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
     uint8_t *kheap = nullptr, *vheap = nullptr;
     uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
+    uint2 *aux = nullptr;   // the delta's per-entry base positions (delta.h); none in the base CSR
+    uint64_t cap_aux = 0;
 };
 
 struct st_tree {
@@ -93,6 +96,11 @@ struct st_tree {
     // retired previous CSR kept as the next merge's output buffers (csr_take)
     uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
     CsrSet spare;
+    // streaming-insert delta (delta.h): entries inserted since the last
+    // fold, their CSR and its spare; dl_new = delta entries that are new keys
+    CsrSet dl, dl_spare;
+    uint64_t dl_n = 0, dl_new = 0, dl_folds = 0;
+    uint64_t dl_limit = 0;   // fold threshold in entries (0: auto, ~0: no delta; st_debug_knob)
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -135,6 +143,9 @@ struct st_tree {
     uint32_t *derr = nullptr, *derr_dev = nullptr;
     bool poisoned = false;
     uint32_t dbg_skip_mail = ~0u;   // st_debug_knob(ST_DBG_SKIP_MAIL)
+    // device work that reads ANOTHER tree's buffers (compare / exchange) may
+    // still be in flight on this tree's stream (cleared by a completed wait)
+    bool reads_remote = false;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -250,6 +261,7 @@ static int tsync(st_tree *t) {
         return ST_EDEVICE;
     }
     t->sync_epoch.fetch_add(1, std::memory_order_release);
+    t->reads_remote = false;
     // every kernel enqueued before has completed: its device-error word is final
     if (t->derr && __atomic_load_n(t->derr, __ATOMIC_ACQUIRE)) {
         const uint32_t w = __atomic_exchange_n(t->derr, 0u, __ATOMIC_ACQ_REL);
@@ -297,7 +309,7 @@ struct PairLock {
     }
     PairLock(const PairLock &) = delete;
     ~PairLock() {
-        if (a != b && hipStreamQuery(a->stream) != hipSuccess) (void)hipStreamSynchronize(a->stream);
+        if (a != b && a->reads_remote) (void)tsync(a);
     }
 };
 #define ENTER_PAIR(x, y)                                                             \
@@ -352,7 +364,8 @@ struct Scratch {
 static const uint64_t CSR_KEEP_SPARE = 16ull << 20;
 
 static void csr_free(st_tree *t, CsrSet &c) {
-    for (void *p : {(void *)c.seg_off, (void *)c.seg_voff, (void *)c.koff, (void *)c.voff, (void *)c.kheap, (void *)c.vheap})
+    for (void *p : {(void *)c.seg_off, (void *)c.seg_voff, (void *)c.koff, (void *)c.voff, (void *)c.kheap, (void *)c.vheap,
+                    (void *)c.aux})
         dfree(t, p);
     c = CsrSet();
 }
@@ -710,6 +723,8 @@ extern "C" void st_destroy(st_tree *t) {
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
                     (void *)t->spare.kheap, (void *)t->spare.vheap})
         dfree(t, p);
+    csr_free(t, t->dl);
+    csr_free(t, t->dl_spare);
     dfree(t, t->ov.idx);
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
@@ -742,7 +757,7 @@ extern "C" uint64_t st_width(const st_tree *t) { return t->W; }
 extern "C" uint64_t st_segments(const st_tree *t) { return t->S; }
 extern "C" uint64_t st_num_entries(st_tree *t) {
     std::lock_guard<std::recursive_mutex> g(t->mu);
-    return t->n;
+    return t->n + t->dl_new;   // base entries + the delta's new keys
 }
 
 extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
@@ -751,8 +766,20 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
         t->dbg_skip_mail = value < 0 ? ~0u : (uint32_t)value;
         return ST_OK;
     }
+    if (knob == ST_DBG_DELTA_LIMIT) {
+        t->dl_limit = value < 0 ? ~0ull : (uint64_t)value;
+        return ST_OK;
+    }
     g_err = "unknown debug knob";
     return ST_EINVAL;
+}
+
+extern "C" int st_delta_stats(st_tree *t, uint64_t out[3]) {
+    ENTER_ANY(t);
+    out[0] = t->dl_n;
+    out[1] = t->dl_new;
+    out[2] = t->dl_folds;
+    return ST_OK;
 }
 
 static uint64_t num_tiles(const st_tree *t);
@@ -1094,11 +1121,16 @@ static int rehash_tiled(st_tree *t) {
 // block-count order (k_segment_hash_perm), then the marked inner nodes:
 // W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the per-level
 // kernels above; other geometries: one k_level_hash launch per level.
-static int rehash_all(st_tree *t, const uint8_t *mask) {
+// dv: the segments are the merged views of the base CSR and this delta (delta.h).
+static int rehash_all(st_tree *t, const uint8_t *mask, const DeltaView *dv) {
     if (!mask) return rehash_tiled(t);
     DevTree d = view(t);
     CHK(ensure_perm(t));
-    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
+    if (dv)
+        LAUNCH(t, "segment_hash", k_segment_hash_merged<MODE_STORE>, grid_for(t->S), 256, 0, d, *dv,
+               (const uint32_t *)t->seg_perm, mask, (uint8_t *)nullptr);
+    else
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
@@ -1111,12 +1143,17 @@ static int rehash_all(st_tree *t, const uint8_t *mask) {
 }
 
 // Verify every node marked in t->mark (levels 1..L); results in t->ok.
-static int verify_marked(st_tree *t, uint32_t L) {
+// dv: segments are merged views with this delta (delta.h).
+static int verify_marked(st_tree *t, uint32_t L, const DeltaView *dv = nullptr) {
     DevTree d = view(t);
     if (L == t->H + 1) {   // segments in the length order of seg_perm: lanes of a wave hash alike-sized messages
         CHK(ensure_perm(t));
-        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
-               (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+        if (dv)
+            LAUNCH(t, "segment_verify", k_segment_hash_merged<MODE_VERIFY>, grid_for(t->S), 256, 0, d, *dv,
+                   (const uint32_t *)t->seg_perm, (const uint8_t *)t->mark, t->ok);
+        else
+            LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
+                   (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
     }
     const uint32_t lmax = L < t->H ? L : t->H;
     if (lmax >= 1) {
@@ -1149,85 +1186,133 @@ struct IngestIn {
     uint32_t *clevel_out;
     uint32_t *seg_out;
     uint64_t n_rejected;
+    // presorted: the records are already in segment order with unique keys
+    // ascending within each segment, seg_given their segments and
+    // bseg_given the S + 1 run bounds (the delta folded into the base)
+    bool presorted;
+    const uint64_t *bseg_given;
 };
 
-static int ingest(st_tree *t, IngestIn &in) {
-    const uint64_t n = in.n, S = t->S;
-    in.n_rejected = 0;
-    if (n == 0) return ST_OK;
-    DevTree d = view(t);
-    Scratch sc(t);
-    uint32_t *seg = nullptr, *sseg = nullptr, *idx = nullptr, *perm = nullptr, *mpos = nullptr;
+// The batch in merge order: segment per record (seg), sorted segments
+// (sseg), sorted record order (perm), run bounds per segment (bseg_off), and
+// the last writer of every key (keep).
+struct BatchPrep {
+    uint32_t *seg = nullptr, *sseg = nullptr, *perm = nullptr;
     uint64_t *bseg_off = nullptr;
-    uint8_t *keep = nullptr, *reject = nullptr, *dirty = nullptr;
-    CHK(sc.alloc(&seg, n));
-    CHK(sc.alloc(&sseg, n));
-    CHK(sc.alloc(&idx, n));
-    CHK(sc.alloc(&perm, n));
-    CHK(sc.alloc(&bseg_off, S + 1));
-    CHK(sc.alloc(&keep, n));
-    if (in.seg_given) {
-        HIPCHK(hipMemcpyAsync(seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
-    } else {
-        LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, seg);
+    uint8_t *keep = nullptr;
+};
+
+static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
+    const uint64_t n = in.n, S = t->S;
+    CHK(sc.alloc(&bp.keep, n));
+    if (in.presorted) {
+        bp.seg = bp.sseg = const_cast<uint32_t *>(in.seg_given);
+        bp.bseg_off = const_cast<uint64_t *>(in.bseg_given);
+        CHK(sc.alloc(&bp.perm, n));
+        LAUNCH(t, "iota", k_iota, grid_for(n), 256, 0, bp.perm, n);
+        HIPCHK(hipMemsetAsync(bp.keep, 1, n, t->stream));
+        if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
+        return ST_OK;
     }
-    if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
+    uint32_t *idx = nullptr;
+    CHK(sc.alloc(&bp.seg, n));
+    CHK(sc.alloc(&bp.sseg, n));
+    CHK(sc.alloc(&idx, n));
+    CHK(sc.alloc(&bp.perm, n));
+    CHK(sc.alloc(&bp.bseg_off, S + 1));
+    if (in.seg_given) {
+        HIPCHK(hipMemcpyAsync(bp.seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
+    } else {
+        LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, bp.seg);
+    }
+    if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
     LAUNCH(t, "iota", k_iota, grid_for(n), 256, 0, idx, n);
     if (S > 1) {
         unsigned end_bit = 0;
         while ((1ull << end_bit) < S) end_bit++;
         size_t bytes = 0;
-        HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream));
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, bp.seg, bp.sseg, idx, bp.perm, (size_t)n, 0u, end_bit, t->stream));
         uint8_t *tmp = nullptr;
         CHK(sc.bytes(&tmp, bytes));
         TimedLaunch tl(t, "radix_sort");
-        HIPCHK(rocprim::radix_sort_pairs(tmp, bytes, seg, sseg, idx, perm, (size_t)n, 0u, end_bit, t->stream));
+        HIPCHK(rocprim::radix_sort_pairs(tmp, bytes, bp.seg, bp.sseg, idx, bp.perm, (size_t)n, 0u, end_bit, t->stream));
     } else {
-        HIPCHK(hipMemcpyAsync(sseg, seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
-        HIPCHK(hipMemcpyAsync(perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
+        HIPCHK(hipMemcpyAsync(bp.sseg, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
+        HIPCHK(hipMemcpyAsync(bp.perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
     }
     if (n < S)
-        LAUNCH(t, "run_bounds", k_run_bounds_search, grid_for(S + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
+        LAUNCH(t, "run_bounds", k_run_bounds_search, grid_for(S + 1), 256, 0, (const uint32_t *)bp.sseg, n, S, bp.bseg_off);
     else
-        LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)sseg, n, S, bseg_off);
-    if (t->partitioned) LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bseg_off, S, t->part_lo, t->part_hi);
+        LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)bp.sseg, n, S, bp.bseg_off);
+    if (t->partitioned)
+        LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bp.bseg_off, S, t->part_lo, t->part_hi);
     BatchView bv{in.krec, in.koff};
-    LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, perm, (const uint64_t *)bseg_off, S, keep);
+    LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, bp.perm, (const uint64_t *)bp.bseg_off, S, bp.keep);
+    return ST_OK;
+}
 
-    // path verification of touched segments (insert semantics)
+// Path verification of the touched segments (insert semantics): rejects[S]
+// = first failing level of each touched segment's root->segment path.
+static int verify_batch_paths(st_tree *t, const BatchPrep &bp, Scratch &sc, uint8_t **reject, const DeltaView *dv) {
+    const uint64_t S = t->S;
+    CHK(sc.alloc(reject, S));
+    if (t->fresh) {
+        HIPCHK(hipMemsetAsync(*reject, 0, S, t->stream));
+        return ST_OK;
+    }
+    DevTree d = view(t);
+    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+    LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
+           (const uint64_t *)nullptr, S, t->mark);
+    CHK(verify_marked(t, t->H + 1, dv));
+    LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
+           (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, *reject, (uint32_t *)nullptr);
+    return ST_OK;
+}
+
+static MergeArgs merge_args(const uint64_t *seg_off, const uint64_t *koff, const uint8_t *kheap, const uint64_t *voff,
+                            const uint8_t *vheap, const IngestIn &in, const BatchPrep &bp, const uint8_t *reject, uint64_t S) {
+    MergeArgs ma;
+    ma.seg_off = seg_off;
+    ma.koff = koff;
+    ma.kheap = kheap;
+    ma.voff = voff;
+    ma.vheap = vheap;
+    ma.perm = bp.perm;
+    ma.bseg_off = bp.bseg_off;
+    ma.keep = bp.keep;
+    ma.bop = in.bop;
+    ma.seg_reject = reject;
+    ma.seg_replace = in.seg_replace;
+    ma.bv = BatchView{in.krec, in.koff};
+    ma.bvoff = in.voff;
+    ma.bvheap = in.vheap;
+    ma.S = S;
+    ma.aux = nullptr;
+    ma.baux = nullptr;
+    ma.b_seg_off = ma.b_koff = ma.b_voff = nullptr;
+    ma.b_kheap = nullptr;
+    return ma;
+}
+
+static int flush_delta(st_tree *t);
+
+// The batch merged into the base CSR (a whole new CSR).
+static int ingest_direct(st_tree *t, IngestIn &in) {
+    const uint64_t n = in.n, S = t->S;
+    Scratch sc(t);
+    BatchPrep bp;
+    CHK(batch_prepare(t, in, sc, bp));
+    uint8_t *reject = nullptr, *dirty = nullptr;
+    uint32_t *mpos = nullptr;
     if (in.verify_rehash) {
-        CHK(sc.alloc(&reject, S));
-        if (t->fresh) {
-            HIPCHK(hipMemsetAsync(reject, 0, S, t->stream));
-        } else {
-            HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
-            LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
-                   (const uint64_t *)nullptr, S, t->mark);
-            CHK(verify_marked(t, t->H + 1));
-            LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bseg_off,
-                   (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
-        }
-        if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)seg, n,
+        CHK(verify_batch_paths(t, bp, sc, &reject, nullptr));
+        if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
                                   (const uint8_t *)reject, in.clevel_out);
     }
 
     // merge (k_merge_pos / k_merge_old / k_merge_new): count, scan, write
-    MergeArgs ma;
-    ma.seg_off = t->seg_off;
-    ma.koff = t->koff;
-    ma.kheap = t->kheap;
-    ma.voff = t->voff;
-    ma.vheap = t->vheap;
-    ma.perm = perm;
-    ma.bseg_off = bseg_off;
-    ma.keep = keep;
-    ma.bop = in.bop;
-    ma.seg_reject = reject;
-    ma.seg_replace = in.seg_replace;
-    ma.bv = bv;
-    ma.bvoff = in.voff;
-    ma.bvheap = in.vheap;
-    ma.S = S;
+    MergeArgs ma = merge_args(t->seg_off, t->koff, t->kheap, t->voff, t->vheap, in, bp, reject, S);
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *ss = nullptr, *sx = nullptr;
     CHK(sc.alloc(&ss, S + 1));
@@ -1251,10 +1336,10 @@ static int ingest(st_tree *t, IngestIn &in) {
     HIPCHK(hipMemsetAsync(out.o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
     MergeOut mo;
     mo.seg_off = out.o.seg_off; mo.seg_voff = out.o.seg_voff; mo.koff = out.o.koff; mo.voff = out.o.voff;
-    mo.kheap = out.o.kheap; mo.vheap = out.o.vheap;
+    mo.kheap = out.o.kheap; mo.vheap = out.o.vheap; mo.aux = nullptr;
     LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
-    LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)sseg, n, (const uint32_t *)mpos,
+    LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     const uint64_t tot_k = tot.v[1], tot_v = tot.v[2];
     // swap in the new CSR (the old one becomes the spare set, in stream order)
@@ -1268,12 +1353,201 @@ static int ingest(st_tree *t, IngestIn &in) {
     if (in.verify_rehash) {
         // dirty-path rehash: segments whose content changed and their ancestors
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
-        d = view(t);
-        LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
-        CHK(rehash_all(t, t->mark));
+        LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
+        CHK(rehash_all(t, t->mark, nullptr));
     }
     t->fresh = false;
     return ST_OK;
+}
+
+// ------------------------------------------------------------------ the delta CSR (delta.h)
+// A streaming batch (insert semantics, a batch small next to the tree)
+// merges into the delta instead of the base CSR; the delta is folded into the
+// base when it exceeds its limit, and before any call but a streaming insert.
+
+static DeltaView delta_view(const st_tree *t) {
+    DeltaView v;
+    v.seg_off = t->dl.seg_off;
+    v.voff = t->dl.voff;
+    v.vheap = t->dl.vheap;
+    v.aux = t->dl.aux;
+    return v;
+}
+
+// An empty delta CSR (every run empty) as the first streaming batch's "old" delta.
+static int ensure_delta(st_tree *t) {
+    if (t->dl.seg_off) return ST_OK;
+    CsrSet &c = t->dl;
+    CHK(dalloc_t(t, &c.seg_off, t->S + 1));
+    CHK(dalloc_t(t, &c.seg_voff, t->S + 1));
+    CHK(dalloc_t(t, &c.koff, 1));
+    CHK(dalloc_t(t, &c.voff, 1));
+    CHK(dalloc_t(t, &c.aux, 1));
+    CHK(dalloc(t, (void **)&c.kheap, HEAP_SLACK));
+    CHK(dalloc(t, (void **)&c.vheap, HEAP_SLACK));
+    c.cap_n = 1; c.cap_k = HEAP_SLACK; c.cap_v = HEAP_SLACK; c.cap_aux = 1;
+    HIPCHK(hipMemsetAsync(c.seg_off, 0, (t->S + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(c.seg_voff, 0, (t->S + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(c.koff, 0, 8, t->stream));
+    HIPCHK(hipMemsetAsync(c.voff, 0, 8, t->stream));
+    HIPCHK(hipMemsetAsync(c.kheap, 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(c.vheap, 0, HEAP_SLACK, t->stream));
+    t->dl_n = 0;
+    t->dl_new = 0;
+    return ST_OK;
+}
+
+// Output buffers of a delta merge: the delta's spare set, grown as needed.
+static int delta_take(st_tree *t, uint64_t n1, uint64_t kb, uint64_t vb, CsrSet &o) {
+    CsrSet &sp = t->dl_spare;
+    if (!sp.seg_off) CHK(dalloc_t(t, &sp.seg_off, t->S + 1));
+    if (!sp.seg_voff) CHK(dalloc_t(t, &sp.seg_voff, t->S + 1));
+    auto grow = [&](auto *&p, uint64_t &cap, uint64_t want, uint64_t unit) -> int {
+        if (cap >= want && p) return ST_OK;
+        dfree(t, p);
+        p = nullptr;
+        cap = 0;
+        const uint64_t w = want + want / 4 + 64;
+        CHK(dalloc(t, (void **)&p, w * unit));
+        cap = w;
+        return ST_OK;
+    };
+    CHK(grow(sp.koff, sp.cap_n, n1, 8));
+    if (!sp.voff || sp.cap_aux < n1) {   // voff and aux share the entry capacity of koff
+        dfree(t, sp.voff); dfree(t, sp.aux);
+        sp.voff = nullptr; sp.aux = nullptr; sp.cap_aux = 0;
+        CHK(dalloc_t(t, &sp.voff, sp.cap_n));
+        CHK(dalloc_t(t, &sp.aux, sp.cap_n));
+        sp.cap_aux = sp.cap_n;
+    }
+    CHK(grow(sp.kheap, sp.cap_k, kb, 1));
+    CHK(grow(sp.vheap, sp.cap_v, vb, 1));
+    o = sp;
+    sp = CsrSet();
+    return ST_OK;
+}
+
+static void delta_install(st_tree *t, const CsrSet &o) {
+    csr_free(t, t->dl_spare);
+    t->dl_spare = t->dl;
+    t->dl = o;
+}
+
+// Streaming batch size that goes to the delta: small next to the (owned
+// part of the) tree.
+static bool delta_eligible(const st_tree *t, const IngestIn &in) {
+    if (!in.verify_rehash || in.seg_given || in.bop || in.seg_replace || in.presorted || t->fresh || t->n == 0) return false;
+    if (t->dl_limit == ~0ull) return false;   // disabled (st_debug_knob)
+    const double own = t->partitioned ? (double)(t->part_hi - t->part_lo) / (double)t->S : 1.0;
+    return (double)in.n * own * 32.0 <= (double)t->n;
+}
+
+static uint64_t delta_limit(const st_tree *t) {
+    if (t->dl_limit) return t->dl_limit;
+    return std::max<uint64_t>(t->n / 4, 1u << 20);
+}
+
+static int ingest_delta(st_tree *t, IngestIn &in) {
+    const uint64_t n = in.n, S = t->S;
+    CHK(ensure_delta(t));
+    CHK(ensure_perm(t));   // the base's block-count order: valid until the next compaction
+    Scratch sc(t);
+    BatchPrep bp;
+    CHK(batch_prepare(t, in, sc, bp));
+    const DeltaView old = delta_view(t);
+    uint8_t *reject = nullptr, *dirty = nullptr;
+    CHK(verify_batch_paths(t, bp, sc, &reject, &old));
+    if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
+                              (const uint8_t *)reject, in.clevel_out);
+    // merge the batch into the delta (the base is not touched); the count
+    // pass also places every record in its segment's base run (baux) and
+    // counts the records that are new keys of the tree (SegSums v[3])
+    uint2 *baux = nullptr;
+    CHK(sc.alloc(&baux, n));
+    DevTree d = view(t);
+    MergeArgs ma = merge_args(t->dl.seg_off, t->dl.koff, t->dl.kheap, t->dl.voff, t->dl.vheap, in, bp, reject, S);
+    ma.aux = t->dl.aux;
+    ma.baux = baux;
+    ma.b_seg_off = t->seg_off; ma.b_koff = t->koff; ma.b_voff = t->voff; ma.b_kheap = t->kheap;
+    BatchSums *bs = nullptr, *bx = nullptr;
+    SegSums *ss = nullptr, *sx = nullptr;
+    uint32_t *mpos = nullptr;
+    CHK(sc.alloc(&ss, S + 1));
+    CHK(sc.alloc(&sx, S + 1));
+    CHK(sc.alloc(&dirty, S));
+    CHK(sc.alloc(&mpos, n));
+    CHK(sc.alloc(&bs, n + 1));
+    CHK(sc.alloc(&bx, n + 1));
+    HIPCHK(hipMemsetAsync(ss + S, 0, sizeof(SegSums), t->stream));
+    HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
+    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty);
+    CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
+    CHK(exclusive_scan<SegSums>(t, ss, sx, S + 1));
+    SegSums tot(0);
+    CHK(d2h(t, &tot, sx + S, sizeof(SegSums)));
+    const uint64_t n_new = tot.v[0];
+    CsrSet o;
+    CHK(delta_take(t, n_new + 1, tot.v[1] + HEAP_SLACK, tot.v[2] + HEAP_SLACK, o));
+    bool installed = false;
+    struct Back {   // a failed merge returns the taken set to the spare slot
+        st_tree *t; CsrSet &o; bool &done;
+        ~Back() { if (!done) { csr_free(t, t->dl_spare); t->dl_spare = o; } }
+    } back{t, o, installed};
+    HIPCHK(hipMemsetAsync(o.kheap + tot.v[1], 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
+    MergeOut mo;
+    mo.seg_off = o.seg_off; mo.seg_voff = o.seg_voff; mo.koff = o.koff; mo.voff = o.voff;
+    mo.kheap = o.kheap; mo.vheap = o.vheap; mo.aux = o.aux;
+    LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
+           (const BatchSums *)bx, (const SegSums *)sx, mo);
+    LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, (const uint32_t *)mpos,
+           (const BatchSums *)bx, (const SegSums *)sx, mo);
+    delta_install(t, o);
+    installed = true;
+    t->dl_n = n_new;
+    t->dl_new += tot.v[3];   // keys of the tree = base entries + delta entries that replace none
+    t->tiles_valid = false;
+    // dirty-path rehash over the merged views
+    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+    LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
+    const DeltaView nv = delta_view(t);
+    CHK(rehash_all(t, t->mark, &nv));
+    t->fresh = false;
+    if (t->dl_n > delta_limit(t)) CHK(flush_delta(t));
+    return ST_OK;
+}
+
+// Fold the delta into the base CSR (one full merge; hashes unchanged: the
+// merged views are the tree's content already).
+static int flush_delta(st_tree *t) {
+    if (!t->dl_n) return ST_OK;
+    const uint64_t n = t->dl_n;
+    Scratch sc(t);
+    uint32_t *seg = nullptr;
+    CHK(sc.alloc(&seg, n));
+    LAUNCH(t, "delta_fold", k_delta_entry_seg, grid_for(t->S), 256, 0, (const uint64_t *)t->dl.seg_off, t->S, seg);
+    IngestIn in{};
+    in.n = n; in.krec = t->dl.kheap; in.koff = t->dl.koff; in.vheap = t->dl.vheap; in.voff = t->dl.voff;
+    in.seg_given = seg; in.presorted = true; in.bseg_given = t->dl.seg_off;
+    in.verify_rehash = false;
+    CHK(ingest_direct(t, in));
+    // the delta is empty again (its buffers stay for the next streaming batch)
+    HIPCHK(hipMemsetAsync(t->dl.seg_off, 0, (t->S + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(t->dl.seg_voff, 0, (t->S + 1) * 8, t->stream));
+    HIPCHK(hipMemsetAsync(t->dl.koff, 0, 8, t->stream));
+    HIPCHK(hipMemsetAsync(t->dl.voff, 0, 8, t->stream));
+    t->dl_n = 0;
+    t->dl_new = 0;
+    t->dl_folds++;
+    return ST_OK;
+}
+
+static int ingest(st_tree *t, IngestIn &in) {
+    in.n_rejected = 0;
+    if (in.n == 0) return ST_OK;
+    if (delta_eligible(t, in)) return ingest_delta(t, in);
+    CHK(flush_delta(t));
+    return ingest_direct(t, in);
 }
 
 // ------------------------------------------------------------------ overlay (small_path.h)
@@ -1328,7 +1602,14 @@ static int flush_overlay(st_tree *t) {
     return ST_OK;
 }
 
-#define FLUSH(t) CHK(flush_overlay(t))
+// Every entry point that reads segments: the small inserts' overlay and the
+// streaming delta folded into the base CSR first.
+static int flush_all(st_tree *t) {
+    CHK(flush_overlay(t));
+    CHK(flush_delta(t));
+    return ST_OK;
+}
+#define FLUSH(t) CHK(flush_all(t))
 
 static int ensure_small(st_tree *t) {
     if (!t->ov.idx) {
@@ -1408,6 +1689,7 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
         small_lds_bytes((uint32_t)t->W) > 160 * 1024)
         return ST_OK;
+    CHK(flush_delta(t));   // k_small reads the base CSR
     CHK(ensure_small(t));
     if (++t->small_seq == 0) t->small_seq = 1;
     const uint32_t seq = t->small_seq;
@@ -1510,7 +1792,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
             return ST_OK;
         }
     }
-    FLUSH(t);
+    CHK(flush_overlay(t));   // the delta stays: a streaming batch may go to it (ingest)
     uint8_t *krec = nullptr, *dv = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr;
     uint32_t *dcl = nullptr, *dseg = nullptr;
@@ -1545,7 +1827,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
 extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                                int on_device, uint64_t *n_corrupted) {
     ENTER(t);
-    FLUSH(t);
+    CHK(flush_overlay(t));   // the delta stays: a streaming batch may go to it (ingest)
     if (n_corrupted) *n_corrupted = 0;
     if (n == 0) return ST_OK;
     const int64_t *dkeys = keys;
@@ -1771,7 +2053,7 @@ extern "C" int st_rehash(st_tree *t, int upper) {
         return ST_EINVAL;
     }
     if (upper) CHK(rehash_levels(t, t->H, nullptr));
-    else CHK(rehash_all(t, nullptr));
+    else CHK(rehash_all(t, nullptr, nullptr));
     CHK(erec_after_rehash(t));
     t->fresh = false;
     if (t->poisoned) {   // a tree in error becomes readable again once this rehash completed cleanly
@@ -1803,7 +2085,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
             if (trees[j] == u) { g_err = "a tree appears twice in the group"; return ST_EINVAL; }
     }
     for (uint32_t i = 0; i < n; i++) {
-        CHK(flush_overlay(trees[i]));
+        CHK(flush_all(trees[i]));
         CHK(ensure_tiles(trees[i]));
         CHK(ensure_lvl_cnt(trees[i]));
         CHK(tsync(trees[i]));
@@ -2442,6 +2724,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             CHK(sc.alloc(&stamps, (uint64_t)w.nw * 16));
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 128, t->stream));
         }
+        A->reads_remote = true;   // until the gather's completion word is seen
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
                filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
         if (stamp) {
@@ -2467,6 +2750,7 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4 + 1, 256, 0, w.nw, (const uint64_t *)w.wcnt,
                (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
         CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
+        A->reads_remote = false;   // the gather wrote its word last: the walk over B has completed
         const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
         if (e != ~0ull) {
             *status = ST_CORRUPTED;
@@ -2489,8 +2773,8 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
 extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, uint64_t *n_diffs, uint32_t *clevel,
                                  uint64_t *cbucket, int *cside) {
     ENTER_PAIR(local, remote);
-    CHK(flush_overlay(local));
-    CHK(flush_overlay(remote));
+    CHK(flush_all(local));
+    CHK(flush_all(remote));
     CompareOut co;
     int status = ST_OK;
     CHK(compare_core(local, remote, filter, co, clevel, cbucket, cside, &status));
@@ -2506,8 +2790,8 @@ extern "C" int st_compare_device(st_tree *local, st_tree *remote, int filter, ui
 static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *n_diffs, uint64_t *n_applied,
                          uint64_t *n_rejected, int *crashed, uint32_t *clevel, uint64_t *cbucket, int *cside) {
     ENTER_PAIR(local, remote);
-    CHK(flush_overlay(local));
-    CHK(flush_overlay(remote));
+    CHK(flush_all(local));
+    CHK(flush_all(remote));
     *n_diffs = 0;
     *n_applied = 0;
     *n_rejected = 0;
@@ -2535,6 +2819,7 @@ static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *
     CHK(sc.alloc(&ko, n + 1));
     CHK(sc.alloc(&vo, n + 1));
     HIPCHK(hipMemsetAsync(fb, 0xff, 8, t->stream));
+    t->reads_remote = true;
     LAUNCH(t, "diff_apply", k_diff_apply_select, grid_for(n), 256, 0, da, db, co.rec, n, take, fb);
     LAUNCH(t, "diff_apply", k_diff_apply_lengths, grid_for(n + 1), 256, 0, db, co.rec, n, (const uint8_t *)take,
            (const unsigned long long *)fb, one, kl, vl);
@@ -2558,6 +2843,7 @@ static int exchange_core(st_tree *local, st_tree *remote, bool apply, uint64_t *
         CHK(sc.alloc(&bko, m + 1));
         CHK(sc.alloc(&bvo, m + 1));
         CHK(sc.alloc(&dcl, m));
+        t->reads_remote = true;
         LAUNCH(t, "diff_apply", k_diff_apply_gather, grid_for(n + 1), 256, 0, db, co.rec, n, (const uint64_t *)pos,
                (const uint64_t *)ko, (const uint64_t *)vo, kh, bko, vh, bvo);
         IngestIn in{};
@@ -2594,8 +2880,8 @@ extern "C" int st_exchange_plan(st_tree *local, st_tree *remote, uint64_t *n_dif
 extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result **out, uint32_t *clevel,
                           uint64_t *cbucket, int *cside) {
     ENTER_PAIR(local, remote);
-    CHK(flush_overlay(local));
-    CHK(flush_overlay(remote));
+    CHK(flush_all(local));
+    CHK(flush_all(remote));
     *out = nullptr;
     CompareOut co;
     int status = ST_OK;
@@ -2630,6 +2916,7 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
     if ((r = sc.alloc(&kl, n + 1)) || (r = sc.alloc(&al, n + 1)) || (r = sc.alloc(&bl, n + 1)) || (r = sc.alloc(&ko, n + 1)) ||
         (r = sc.alloc(&ao, n + 1)) || (r = sc.alloc(&bo, n + 1)) || (r = sc.alloc(&kind, n)) || (r = sc.alloc(&seg, n)))
         return fail(r);
+    t->reads_remote = true;
     hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, da, db, co.rec, n, kl, al, bl);
     if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, al, ao, n + 1)) ||
         (r = exclusive_scan<uint64_t>(t, bl, bo, n + 1)))

@@ -404,6 +404,12 @@ class DeviceTree:
     def set_stream(self, stream_handle):
         _lib.check(self.L.st_set_stream(self.h, ctypes.c_void_p(stream_handle)), 'st_set_stream')
 
+    def delta_stats(self):
+        """(entries in the streaming delta, of them new keys, folds so far)."""
+        v = (ctypes.c_uint64 * 3)()
+        _lib.check(self.L.st_delta_stats(self.h, v), 'st_delta_stats')
+        return tuple(int(x) for x in v)
+
     def debug_knob(self, knob, value):
         """Fault injection for tests (st_debug_knob)."""
         _lib.check(self.L.st_debug_knob(self.h, knob, int(value)), 'st_debug_knob')

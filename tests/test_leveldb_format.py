@@ -224,7 +224,8 @@ def test_restore_rejects_out_of_domain_nodes():
         [(LR.db_key(b'', 0, 0), LR.term_to_binary(b'\x00' * 16))],             # 16-byte top hash
         [(LR.db_key(b'', 2, 0), LR.term_to_binary([(99, b'\x00' * 17)]))],    # child outside node {2,0}
         [(LR.db_key(b'', 6, 3), LR.term_to_binary([(2, b'a'), (1, b'b')]))],  # not an orddict
-        [(LR.db_key(b'', 6, 3), LR.term_to_binary([(1 << 70, b'a')]))],       # key beyond int64
+        [(LR.db_key(b'', 6, 3), bytes([131, 108, 0, 0, 0, 1, 104, 2, 116, 0, 0, 0, 0,
+                                       109, 0, 0, 0, 1, 97, 106]))],               # a map key #{} (outside the key domain)
         [(LR.db_key(b'', 6, 3), LR.term_to_binary([(1, 5)]))],                # non-binary value
     ]
     for recs in bad:
@@ -328,3 +329,31 @@ def test_checkpoint_into_tracks_corrupt_and_rehash():
     d = S.rehash(d)
     S.checkpoint_into(d, db, b'c')
     assert db == LR.tree_records(o.modstate.db, b'c')
+
+
+@pytest.mark.gpu
+def test_restore_term_keys_roundtrip():
+    """Segments with term_to_binary keys -- tuples, lists, strings, floats,
+    integers beyond int64, nested atoms and binaries -- decode on the device
+    (synctree_leveldb:fetch/3 reopens any record it can decode,
+    synctree_leveldb.erl:111-123): the restored tree equals the tree the
+    oracle's synctree_leveldb DB was written from, record for record."""
+    from test_term_keys import distinct_terms
+    from riak_ensemble_amd import synctree as S
+    keys = distinct_terms(1500, 31) + [(1 << 64) + 5, -(1 << 70), 5.5, -2.0 ** 80, (1.5, 'a'), 'atom', b'bin', 7,
+                                       [104, 105], [], (), ((), [[]]), ('a\u0000b', b'\x00\xff')]
+    rng = random.Random(3)
+    vals = [rng.randbytes(rng.choice([0, 8, 17])) for _ in keys]
+    o, d = _pair(keys, vals)
+    recs = list(LR.tree_records(o.modstate.db, b'tree-7').items())
+    fresh = S.new()
+    loaded, skipped = fresh.modstate.restore_leveldb(recs, b'tree-7')
+    assert (loaded, skipped) == (len(recs), 0)
+    assert fresh.modstate.top_hash() == d.modstate.top_hash() == R.top_hash(o)
+    assert fresh.modstate.snapshot_leveldb(b'tree-7') == d.modstate.snapshot_leveldb(b'tree-7')
+    assert dict(fresh.modstate.snapshot_leveldb(b'tree-7')) == dict(recs)
+    assert fresh.modstate.compare(d.modstate) == ('ok', [])
+    assert fresh.modstate.get_batch(keys[::3]) == vals[::3]
+    assert fresh.modstate.verify() is True
+    fresh.modstate.rehash()
+    assert fresh.modstate.top_hash() == d.modstate.top_hash()

@@ -14,7 +14,7 @@ import bench  # noqa: E402
 from riak_ensemble_amd import synctree_hip  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
-K = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 B = 1_000_000
 dev = torch.device('cuda', 0)
 t = synctree_hip.DeviceTree()
@@ -38,7 +38,7 @@ t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
 names = ['key_segment', 'iota', 'radix_sort', 'run_bounds', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
-         'segment_hash', 'level_rehash', 'pack_int64']
+         'segment_hash', 'level_rehash', 'pack_int64', 'delta_aux', 'delta_count', 'delta_fold']
 t.set_timing(True)
 t.kernel_stats('*reset*')
 t0 = time.perf_counter()
@@ -60,5 +60,5 @@ for j in range(1, K + 1):
     k, v = batches[j]
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
-print('wall %.3f ms/batch (timing off), entries %d' % ((time.perf_counter() - t0) / K * 1e3, t.num_entries()))
+print('wall %.3f ms/batch (timing off), entries %d, delta (entries, new keys, folds) %s' % ((time.perf_counter() - t0) / K * 1e3, t.num_entries(), t.delta_stats()))
 t.close()

@@ -11,5 +11,5 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/group -o run -- python3 $R/tools/group_time.py 512 1000000 5 > $OUT/group.txt 2> $OUT/group.err
 cat $OUT/group.txt
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/config5 -o run -- python3 $R/tools/part_breakdown.py 100000000 5 > $OUT/config5.txt 2> $OUT/config5.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/config5 -o run -- python3 $R/tools/part_breakdown.py 100000000 30 > $OUT/config5.txt 2> $OUT/config5.err
 cat $OUT/config5.txt
