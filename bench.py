@@ -726,7 +726,7 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     load_s = time.perf_counter() - t0
     rng = np.random.default_rng(5)
     batches = []
-    for j in range(K + 1):
+    for j in range(2 * K + 1):
         old = torch.from_numpy(rng.integers(0, N, B // 2)).to(dev)          # overwrites: Seq + 1 of a loaded key
         k = torch.cat([_dev_keys_at(seed, old, dev, torch), _dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
         seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
@@ -754,7 +754,26 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    # the same workload with the streaming delta on: K more
+    # batches merge into the delta (folded past a quarter of the tree)
+    from riak_ensemble_amd import _lib
+    pt.tree.debug_knob(_lib.ST_DBG_DELTA_LIMIT, 0)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dper = []
+    t1 = time.perf_counter()
+    for j in range(K + 1, 2 * K + 1):
+        k, v = batches[j]
+        tb = time.perf_counter()
+        pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
+        pt.combine()
+        torch.cuda.synchronize()
+        dper.append(time.perf_counter() - tb)
+    el_delta = time.perf_counter() - t1
     dl_n, dl_new, folds = pt.tree.delta_stats()
+    pt.tree.debug_knob(_lib.ST_DBG_DELTA_LIMIT, -1)
+    dper.sort()
     top = pt.top_hash()
     same = True
     if dist:
@@ -768,7 +787,12 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     pt.tree.close()
     return {'batch_keys_per_s': round(K * B / el, 1), 'ms_per_batch': round(el * 1e3 / K, 4), 'batches': K,
             'ms_per_batch_median': round(per[len(per) // 2] * 1e3, 4), 'ms_per_batch_max': round(per[-1] * 1e3, 4),
-            'delta_folds_in_timed_batches': folds - folds0, 'delta_entries_after': dl_n,
+            'delta_mode': {'ms_per_batch': round(el_delta * 1e3 / K, 4), 'ms_per_batch_median': round(dper[len(dper) // 2] * 1e3, 4),
+                           'ms_per_batch_max': round(dper[-1] * 1e3, 4), 'folds': folds - folds0, 'delta_entries_after': dl_n,
+                           'what': 'the next %d batches with the streaming delta on (st_debug_knob ST_DBG_DELTA_LIMIT '
+                                   '= auto): each merges into a delta CSR and hashes merged views; folded into the '
+                                   'base past a quarter of the tree (mean incl. folds); rank-local, not max over '
+                                   'ranks' % K},
             'batch_keys': B, 'tree_keys': N, 'ranks': world, 'entries_on_rank0': entries,
             'tops_agree_across_ranks': same, 'load_s': round(load_s, 3),
             'what': 'config5: %d-key tree partitioned by segment range over %d rank(s); per batch: insert/3 of %d keys '

@@ -371,9 +371,10 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * so the launch's climb never sees it: the bounded wait then reports
  * ST_EDEVICE instead of hashing a stale entry into the top hash. */
 #define ST_DBG_SKIP_MAIL 1
-/* ST_DBG_DELTA_LIMIT: fold the streaming delta into the base CSR once it
- * holds more than `value` entries (0 = auto: a quarter of the tree, at least
- * 2^20; -1 = never use the delta: every batch rewrites the base CSR). */
+/* ST_DBG_DELTA_LIMIT: use the streaming delta (st_delta_stats) and fold it
+ * into the base CSR once it holds more than `value` entries (0 = auto: a
+ * quarter of the tree, at least 2^20); -1 = no delta (the default: every
+ * batch merges into the base CSR, which measured faster). */
 #define ST_DBG_DELTA_LIMIT 2
 int st_debug_knob(st_tree *t, int knob, int64_t value);
 

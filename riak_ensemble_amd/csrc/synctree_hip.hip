@@ -100,7 +100,7 @@ struct st_tree {
     // fold, their CSR and its spare; dl_new = delta entries that are new keys
     CsrSet dl, dl_spare;
     uint64_t dl_n = 0, dl_new = 0, dl_folds = 0;
-    uint64_t dl_limit = 0;   // fold threshold in entries (0: auto, ~0: no delta; st_debug_knob)
+    uint64_t dl_limit = ~0ull;   // fold threshold in entries (~0: no delta, the default; 0: auto; st_debug_knob)
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -760,6 +760,7 @@ extern "C" uint64_t st_num_entries(st_tree *t) {
     return t->n + t->dl_new;   // base entries + the delta's new keys
 }
 
+static int flush_delta(st_tree *t);
 extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
     ENTER_ANY(t);
     if (knob == ST_DBG_SKIP_MAIL) {
@@ -767,6 +768,7 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
         return ST_OK;
     }
     if (knob == ST_DBG_DELTA_LIMIT) {
+        if (value < 0) CHK(flush_delta(t));   // turning the delta off folds what it holds
         t->dl_limit = value < 0 ? ~0ull : (uint64_t)value;
         return ST_OK;
     }

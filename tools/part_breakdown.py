@@ -1,7 +1,7 @@
 """Config-5 batch breakdown: a 100M-key tree (one partition = the whole
 range), then per-kernel times (HIP events on the library's stream,
 st_kernel_stats) over 5 timed 1M-key batches (50 % overwrites, 50 % new).
-Usage: python tools/part_breakdown.py [tree_keys] [batches]"""
+Usage: python tools/part_breakdown.py [tree_keys] [batches] [delta]"""
 import os
 import sys
 import time
@@ -18,6 +18,9 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 B = 1_000_000
 dev = torch.device('cuda', 0)
 t = synctree_hip.DeviceTree()
+if len(sys.argv) > 3 and sys.argv[3] == 'delta':   # the streaming delta on
+    from riak_ensemble_amd import _lib  # noqa: E402
+    t.debug_knob(_lib.ST_DBG_DELTA_LIMIT, 0)
 seed = 0x5EED0005
 for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
