@@ -672,6 +672,7 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     meta_bytes = 17 * nk + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner * 18
     g_gbs = E * tree_bytes / (g_avg / 1e3) / 1e9 if g_avg > 0 else 0.0
     mem0 = trees[0].mem_stats()
+    perkey = _bench_perkey_multi(trees, synctree_hip, torch)
     # per-tree rehash for comparison (rank-local, untimed for the headline)
     t0 = time.perf_counter()
     for t in trees[:32]:
@@ -695,9 +696,76 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
                                  '(non-empty segments + present inner nodes, mean of %d sampled trees); kernel time '
                                  'from HIP events on trees[0]\'s stream' % len(samp)},
             'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
+            'per_key_multi': perkey,
             'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '
                     'the rank\'s trees + st_tops_to_device + all_gather_into_tensor of every ensemble\'s top hash '
                     '(keys generated on device: splitmix64 masked to 63 bits)' % (E, nk, world, world * E)}
+
+
+def _bench_perkey_multi(trees, synctree_hip, torch, rounds=40):
+    """The per-key path of many ensembles at once (SURVEY §8f rank 4 in the
+    config-4 shape): one insert/3 into EVERY tree per st_insert1_multi call
+    (one device launch, a workgroup per tree), R rounds of new keys; then
+    get/2 of the same keys per st_get1_multi call (values checked).  Beside
+    it, st_insert1 on one tree (one launch per key).  Host arrays prepared
+    before the timed loop (ctypes call, no Python packing inside it)."""
+    import ctypes
+    from riak_ensemble_amd import _lib
+    L = _lib.load()
+    E = len(trees)
+    arr = (ctypes.c_void_p * E)(*[t.h.value for t in trees])
+    rng = np.random.default_rng(404)
+    kt = np.zeros(E, np.uint8)                                   # ST_KEY_INT
+    ko = (np.arange(E + 1, dtype=np.uint64) * 8)
+    vo = (np.arange(E + 1, dtype=np.uint64) * 17)
+    rounds_k = [rng.integers(0, 1 << 62, E, dtype=np.int64) for _ in range(rounds)]
+    rounds_v = []
+    for r in range(rounds):
+        v = np.zeros((E, 17), np.uint8)
+        v[:, 8] = 9
+        v[:, 9:17] = np.array(np.arange(E) + r * E, '>u8').view(np.uint8).reshape(-1, 8)
+        rounds_v.append(v)
+    kh = [np.ascontiguousarray(k.astype('>i8')).view(np.uint8) for k in rounds_k]
+    st = np.zeros(E, np.int32)
+    p = lambda a: ctypes.c_void_p(a.ctypes.data)   # noqa: E731
+
+    def ins(r):
+        _lib.check(L.st_insert1_multi(arr, E, p(kt), p(kh[r]), p(ko), p(rounds_v[r]), p(vo), p(st), None, None),
+                   'st_insert1_multi')
+        assert not st.any()
+    ins(0)                                                      # warm-up (per-tree request slots)
+    torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    for r in range(1, rounds):
+        tb = time.perf_counter()
+        ins(r)
+        lat.append(time.perf_counter() - tb)
+    el = time.perf_counter() - t0
+    lat.sort()
+    # gets of the last round's keys, values checked
+    vout = np.zeros(E * 17 + 64, np.uint8)
+    vof = np.zeros(E + 1, np.uint64)
+    tg = time.perf_counter()
+    _lib.check(L.st_get1_multi(arr, E, p(kt), p(kh[rounds - 1]), p(ko), p(vout), len(vout), p(vof), p(st), None, None),
+               'st_get1_multi')
+    get_s = time.perf_counter() - tg
+    assert not st.any() and (vout[:E * 17].reshape(E, 17) == rounds_v[rounds - 1]).all(), 'multi get values differ'
+    # one tree, one launch per key
+    t1 = trees[0]
+    one = []
+    for r in range(50):
+        tb = time.perf_counter()
+        assert t1.insert1(int(rng.integers(0, 1 << 62)), bytes(rounds_v[0][r % E])) is None
+        one.append(time.perf_counter() - tb)
+    one.sort()
+    return {'inserts_per_s': round(E * (rounds - 1) / el, 1), 'trees_per_launch': E,
+            'ms_per_launch_median': round(lat[len(lat) // 2] * 1e3, 4), 'ms_per_launch_max': round(lat[-1] * 1e3, 4),
+            'get_ms_per_launch': round(get_s * 1e3, 4),
+            'single_tree_insert1_us_median': round(one[len(one) // 2] * 1e6, 1),
+            'what': 'st_insert1_multi: one insert/3 into each of the %d trees per call (one k_small_multi launch, '
+                    'a workgroup per tree), %d calls; latency = one call (every tree answered); st_get1_multi of '
+                    'the last round checked; single_tree = st_insert1 on one tree (ctypes included)' % (E, rounds - 1)}
 
 
 def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
@@ -797,10 +865,9 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
             'tops_agree_across_ranks': same, 'load_s': round(load_s, 3),
             'what': 'config5: %d-key tree partitioned by segment range over %d rank(s); per batch: insert/3 of %d keys '
                     '(50%% overwrites Seq+1, 50%% new; verify + dirty-path rehash) on every rank, all-gather of the '
-                    'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits); a batch '
-                    'merges into the streaming delta CSR, which folds into the base past a quarter of the tree: '
-                    'ms_per_batch is the mean over all timed batches, folds included (median = a batch without a '
-                    'fold, max = one with)' % (N, world, B)}
+                    'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits); each batch '
+                    'is merged into the segment CSR (the default; delta_mode is the opt-in streaming delta); '
+                    'ms_per_batch is the mean over the timed batches' % (N, world, B)}
 
 
 class _SoloGroup:

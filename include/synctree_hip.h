@@ -268,6 +268,21 @@ int st_get1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, uin
 int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, const uint8_t *value, uint32_t vlen,
                uint32_t *clevel, uint64_t *cbucket);
 
+/* The per-key path of many trees at once (many peer trees of one node
+ * taking puts / gets together, riak_ensemble_peer_tree.erl:224-246): request
+ * i is insert/3 (or get/2) of key i into trees[i]; trees may repeat.  The
+ * requests of each tree are served in request order (the semantics of the
+ * per-tree calls one after the other), and the batches of all trees run in
+ * ONE device launch (a workgroup per tree, <= 16 keys per tree a launch;
+ * more keys: further launches).  Per-request outputs as st_insert1 /
+ * st_get1; get values packed in request order into vout with
+ * voff_out[n+1] (ST_EINVAL if vcap is too small).  Trees on one device. */
+int st_insert1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                     const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel, uint64_t *cbucket);
+int st_get1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                  uint8_t *vout, uint64_t vcap, uint64_t *voff_out, int32_t *status, uint32_t *clevel,
+                  uint64_t *cbucket);
+
 /* exchange_get/3 (synctree.erl:231-237) at one level for n buckets, each
  * verified root->node (verified_hashes, synctree.erl:288-298).  Level 0
  * (bucket 0) is answered as [{0, TopHash}] by the caller from st_top_hash.

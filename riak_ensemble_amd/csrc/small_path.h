@@ -482,7 +482,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
 //     one thread per distinct node, a barrier per level (update_path,
 //     synctree.erl:201-209).
 // `out` is mapped pinned host memory: the host reads it after the stream sync.
-__global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *out) {
+__device__ __forceinline__ void small_body(const SmallReq *req, SmallOut *out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     // the request (host memory) into LDS: one round trip, dword per thread
     __shared__ __attribute__((aligned(16))) SmallReq rq;
@@ -859,4 +859,18 @@ __global__ void k_erec_emptied(DevTree t, const uint8_t *krec, const uint64_t *k
     if (threadIdx.x != 0) return;
     const uint64_t s = record_segment(krec + koff[0], koff[1] - koff[0], t.S - 1);
     if (t.seg_off[s] == t.seg_off[s + 1]) erec[t.base[t.H + 1] + s] = 1;
+}
+
+__global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *out) { small_body(req, out); }
+
+// Many trees' per-key batches in ONE launch (st_insert1_multi / st_get1_multi):
+// workgroup b serves items[b], one tree's batch of <= SB_MAX keys (its own
+// request slot and result block; no two items of a launch share a tree).
+struct SmallItem {
+    const SmallReq *req;
+    SmallOut *out;
+};
+__global__ void __launch_bounds__(256) k_small_multi(const SmallItem *items) {
+    const SmallItem it = items[blockIdx.x];
+    small_body(it.req, it.out);
 }

@@ -146,6 +146,9 @@ struct st_tree {
     // device work that reads ANOTHER tree's buffers (compare / exchange) may
     // still be in flight on this tree's stream (cleared by a completed wait)
     bool reads_remote = false;
+    // work enqueued on `stream` that the call did not wait for (st_rehash):
+    // another stream's launch over this tree synchronises it first
+    bool async_pending = false;
     // timing
     bool timing = false;
     std::vector<Pending> pending;
@@ -262,6 +265,7 @@ static int tsync(st_tree *t) {
     }
     t->sync_epoch.fetch_add(1, std::memory_order_release);
     t->reads_remote = false;
+    t->async_pending = false;
     // every kernel enqueued before has completed: its device-error word is final
     if (t->derr && __atomic_load_n(t->derr, __ATOMIC_ACQUIRE)) {
         const uint32_t w = __atomic_exchange_n(t->derr, 0u, __ATOMIC_ACQ_REL);
@@ -1623,6 +1627,7 @@ static int ensure_small(st_tree *t) {
         HIPCHK(hipMemsetAsync(t->ov.heap + cap, 0, HEAP_SLACK, t->stream));
         HIPCHK(hipMemsetAsync(t->ov.used, 0, 8, t->stream));
         t->ov.cap = cap;
+        t->async_pending = true;   // another stream's k_small_multi waits for these
     }
     if (!t->sout) {
         // fine-grained (coherent) host memory for the result block and the
@@ -1679,13 +1684,12 @@ static bool small_collect(st_tree *t, uint32_t seq, uint32_t n, int op) {
     return true;
 }
 
-// One get/2 (op 0) or insert/3 (op 1) batch through k_small when it fits:
-// returns ST_OK with *served = 1 and t->sres filled (get values in
-// t->sout->vbytes), or *served = 0 (the caller takes the bulk path).  Host
-// pointers, records packed by the caller.
-static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, const uint8_t *vheap, const uint64_t *voff,
-                      int *served) {
-    *served = 0;
+// Fill t's next request slot for one get/2 (op 0) or insert/3 (op 1) batch of
+// k_small; *ok = 0 when the batch does not fit the kernel (the caller takes
+// the bulk path).  Host pointers, records packed by the caller.
+static int small_prepare(st_tree *t, int op, uint64_t n, const HostRecords &hr, const uint8_t *vheap, const uint64_t *voff,
+                         int *ok, SmallItem *item) {
+    *ok = 0;
     const uint64_t kbytes = hr.off[n];
     const uint64_t vbytes = op == 1 ? voff[n] - voff[0] : 0;
     if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
@@ -1712,21 +1716,50 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
         for (uint64_t i = 0; i <= n; i++) in.voff[i] = (uint32_t)(voff[i] - voff[0]);
         memcpy(in.vb, vheap + voff[0], vbytes);
     }
+    item->req = t->sreq_dev + seq % SMALL_SLOTS;
+    item->out = t->sout_dev;
+    *ok = 1;
+    return ST_OK;
+}
+
+// After the host validated a served batch's results (t->sres).
+static void small_served(st_tree *t, int op) {
+    if (op == 1) {
+        t->n += t->sres.new_entries;
+        t->ov_pending = true;
+        t->fresh = false;
+        t->tiles_valid = false;
+        t->perm_valid = false;
+    }
+}
+
+// One get/2 (op 0) or insert/3 (op 1) batch through k_small when it fits:
+// returns ST_OK with *served = 1 and t->sres filled (get values in
+// t->sout->vbytes), or *served = 0 (the caller takes the bulk path).  Host
+// pointers, records packed by the caller.
+static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, const uint8_t *vheap, const uint64_t *voff,
+                      int *served) {
+    *served = 0;
+    int ok = 0;
+    SmallItem item;
+    CHK(small_prepare(t, op, n, hr, vheap, voff, &ok, &item));
+    if (!ok) return ST_OK;
+    const uint32_t seq = t->small_seq;
     std::atomic_thread_fence(std::memory_order_release);   // the request is in memory before the launch
-    LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), (const SmallReq *)(t->sreq_dev + seq % SMALL_SLOTS),
-           t->sout_dev);
+    LAUNCH(t, "small", k_small, 1, 256, small_lds_bytes((uint32_t)t->W), item.req, item.out);
     // spin on the result records; after 5 ms (a faulted or very slow kernel)
     // a stream synchronisation, after which every write of the kernel is visible
-    bool ok = false;
+    bool done = false;
     const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 0; !(ok = small_collect(t, seq, (uint32_t)n, op)); i++) {
+    for (uint32_t i = 0; !(done = small_collect(t, seq, (uint32_t)n, op)); i++) {
         if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
         __builtin_ia32_pause();
     }
-    if (!ok) {
+    if (!done) {
         CHK(tsync(t));
         if (!small_collect(t, seq, (uint32_t)n, op)) { g_err = "small-batch kernel results incomplete"; return ST_EDEVICE; }
     }
+    static const int sdbg = getenv("ST_SMALL_STAMPS") ? atoi(getenv("ST_SMALL_STAMPS")) : 0;
     if (sdbg) {   // diagnostic: phase times (µs from kernel start) to stderr
         CHK(tsync(t));
         const uint64_t *st = t->sout->stamp;
@@ -1738,14 +1771,222 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
     }
     if (t->sres.retry) return ST_OK;
     *served = 1;
-    if (op == 1) {
-        t->n += t->sres.new_entries;
-        t->ov_pending = true;
-        t->fresh = false;
-        t->tiles_valid = false;
-        t->perm_valid = false;
+    small_served(t, op);
+    return ST_OK;
+}
+
+// ------------------------------------------------------------------ per-key requests of many trees
+// The per-key path of many ensembles at once (every
+// peer tree of a node takes puts at the same time, riak_ensemble_peer_tree.erl:
+// 224-234): the requests of each tree (in order, <= SB_MAX keys a round)
+// become one k_small batch, and the batches of all trees run in ONE launch of
+// k_small_multi, a workgroup per tree.  Same results as the per-tree calls in
+// request order.  Each calling thread keeps its own host-mapped item array.
+static thread_local SmallItem *t_items = nullptr, *t_items_dev = nullptr;
+static thread_local uint32_t t_items_cap = 0;
+
+static int items_reserve(uint32_t n) {
+    if (n <= t_items_cap) return ST_OK;
+    if (t_items) (void)hipHostFree(t_items);
+    t_items = t_items_dev = nullptr;
+    t_items_cap = 0;
+    const uint32_t cap = std::max<uint32_t>(n, 256);
+    if (hipHostMalloc((void **)&t_items, cap * sizeof(SmallItem), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&t_items_dev, t_items, 0) != hipSuccess) {
+        t_items = nullptr;
+        g_err = "hipHostMalloc (mapped) failed";
+        return ST_EDEVICE;
+    }
+    t_items_cap = cap;
+    return ST_OK;
+}
+
+// op 0: get/2 (values into vout at voff_out), op 1: insert/3.
+static int small_multi(int op, st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                       const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel, uint64_t *cbucket,
+                       uint8_t *vout, uint64_t vcap, uint64_t *voff_out) {
+    if (n == 0) {
+        if (voff_out) voff_out[0] = 0;
+        return ST_OK;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (!trees[i]) { g_err = "NULL tree"; return ST_EINVAL; }
+    GroupLock glk(trees, n);
+    // requests per tree, in request order
+    std::vector<st_tree *> order;
+    std::unordered_map<st_tree *, std::vector<uint32_t>> reqs;
+    for (uint32_t i = 0; i < n; i++) {
+        auto &v = reqs[trees[i]];
+        if (v.empty()) order.push_back(trees[i]);
+        v.push_back(i);
+    }
+    for (st_tree *u : order) {
+        CHK(use_device(u));
+        CHK(alive(u));
+        if (u->device != trees[0]->device) { g_err = "trees on different devices"; return ST_EINVAL; }
+    }
+    std::vector<uint64_t> vlen(n, 0);             // get: value length of request i (status ST_OK)
+    std::vector<std::vector<uint8_t>> vals(op == 0 ? n : 0);
+    std::unordered_map<st_tree *, size_t> next;   // the tree's next request (index into reqs[u])
+    st_tree *t0 = trees[0];
+    hipStream_t s0 = t0->stream;
+    for (;;) {
+        // this round: the next <= SB_MAX requests of every tree with requests left
+        struct Part { st_tree *t; std::vector<uint32_t> idx; uint32_t seq; bool small; };
+        std::vector<Part> parts;
+        for (st_tree *u : order) {
+            auto &v = reqs[u];
+            size_t &k = next[u];
+            if (k == v.size()) continue;
+            Part pt{u, {}, 0, false};
+            uint64_t kb = 0, vb = 0;
+            while (k < v.size() && pt.idx.size() < SB_MAX) {
+                const uint32_t i = v[k];
+                const uint64_t kl = koff[i + 1] - koff[i] + 16, vl = op == 1 ? voff[i + 1] - voff[i] : 0;
+                if (!pt.idx.empty() && (kb + kl > SB_KB || vb + vl > SB_VB)) break;
+                kb += kl;
+                vb += vl;
+                pt.idx.push_back(i);
+                k++;
+            }
+            parts.push_back(std::move(pt));
+        }
+        if (parts.empty()) break;
+        CHK(items_reserve((uint32_t)parts.size()));
+        uint32_t m = 0;
+        size_t lds = 0;
+        for (Part &pt : parts) {
+            st_tree *u = pt.t;
+            const uint64_t c = pt.idx.size();
+            std::vector<uint8_t> kt(c);
+            std::vector<uint64_t> ko(c + 1, 0), vo(c + 1, 0);
+            std::vector<uint8_t> kh, vh;
+            for (uint64_t j = 0; j < c; j++) {
+                const uint32_t i = pt.idx[j];
+                kt[j] = ktype[i];
+                kh.insert(kh.end(), kheap + koff[i], kheap + koff[i + 1]);
+                ko[j + 1] = kh.size();
+                if (op == 1) vh.insert(vh.end(), vheap + voff[i], vheap + voff[i + 1]);
+                vo[j + 1] = vh.size();
+            }
+            HostRecords hr;
+            CHK(pack_records(c, kt.data(), kh.data(), ko.data(), hr));
+            int ok = 0;
+            SmallItem it;
+            CHK(small_prepare(u, op, c, hr, vh.data(), vo.data(), &ok, &it));
+            if (!ok) continue;   // served below through the per-tree bulk path
+            if (u->stream != s0 && u->async_pending) CHK(tsync(u));   // its own work first (e.g. an st_rehash)
+            pt.small = true;
+            pt.seq = u->small_seq;
+            lds = std::max<size_t>(lds, small_lds_bytes((uint32_t)u->W));
+            t_items[m++] = it;
+        }
+        if (m) {
+            std::atomic_thread_fence(std::memory_order_release);   // requests and items are in memory before the launch
+            hipLaunchKernelGGL(k_small_multi, dim3(m), dim3(256), lds, s0, (const SmallItem *)t_items_dev);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) { g_err = std::string("launch small_multi: ") + hipGetErrorString(e); return ST_EDEVICE; }
+        }
+        // collect every served batch (spin; after 5 ms a synchronisation of the launch stream)
+        const auto tw = std::chrono::steady_clock::now();
+        std::vector<char> got(parts.size(), 0);
+        size_t left = m;
+        bool synced = false;
+        while (left) {
+            for (size_t p = 0; p < parts.size(); p++) {
+                if (!parts[p].small || got[p]) continue;
+                if (small_collect(parts[p].t, parts[p].seq, (uint32_t)parts[p].idx.size(), op)) { got[p] = 1; left--; }
+            }
+            if (!left) break;
+            if (synced) { g_err = "small-batch kernel results incomplete"; return ST_EDEVICE; }
+            if (std::chrono::steady_clock::now() - tw > std::chrono::milliseconds(5)) {
+                if (hipStreamSynchronize(s0) != hipSuccess) { g_err = "hipStreamSynchronize (small_multi)"; return ST_EDEVICE; }
+                synced = true;
+            }
+            __builtin_ia32_pause();
+        }
+        // outputs; batches the kernel did not serve (retry) or could not take go through the bulk path
+        for (Part &pt : parts) {
+            st_tree *u = pt.t;
+            const uint64_t c = pt.idx.size();
+            if (pt.small && !u->sres.retry) {
+                small_served(u, op);
+                for (uint64_t j = 0; j < c; j++) {
+                    const uint32_t i = pt.idx[j];
+                    status[i] = u->sres.status[j];
+                    if (clevel) clevel[i] = u->sres.clevel[j];
+                    if (cbucket) cbucket[i] = u->sres.cbucket[j];
+                    if (op == 0 && status[i] == ST_OK) {
+                        const uint32_t a = u->sres.voff[j], b = u->sres.voff[j + 1];
+                        vals[i].assign((const uint8_t *)u->sout->vbytes + a, (const uint8_t *)u->sout->vbytes + b);
+                    }
+                }
+                continue;
+            }
+            std::vector<uint8_t> kt(c);
+            std::vector<uint64_t> ko(c + 1, 0), vo(c + 1, 0);
+            std::vector<uint8_t> kh, vh;
+            for (uint64_t j = 0; j < c; j++) {
+                const uint32_t i = pt.idx[j];
+                kt[j] = ktype[i];
+                kh.insert(kh.end(), kheap + koff[i], kheap + koff[i + 1]);
+                ko[j + 1] = kh.size();
+                if (op == 1) vh.insert(vh.end(), vheap + voff[i], vheap + voff[i + 1]);
+                vo[j + 1] = vh.size();
+            }
+            kh.push_back(0);
+            vh.push_back(0);
+            if (op == 1) {
+                std::vector<int32_t> st(c);
+                std::vector<uint32_t> cl(c);
+                std::vector<uint64_t> cb(c);
+                CHK(st_insert_batch(u, c, kt.data(), kh.data(), ko.data(), vh.data(), vo.data(), st.data(), cl.data(), cb.data()));
+                for (uint64_t j = 0; j < c; j++) {
+                    status[pt.idx[j]] = st[j];
+                    if (clevel) clevel[pt.idx[j]] = cl[j];
+                    if (cbucket) cbucket[pt.idx[j]] = cb[j];
+                }
+            } else {
+                st_result *res = nullptr;
+                CHK(st_get_batch(u, c, kt.data(), kh.data(), ko.data(), &res));
+                for (uint64_t j = 0; j < c; j++) {
+                    const uint32_t i = pt.idx[j];
+                    status[i] = res->status[j];
+                    if (clevel) clevel[i] = res->clevel[j];
+                    if (cbucket) cbucket[i] = res->cbucket[j];
+                    if (status[i] == ST_OK) {
+                        const uint64_t e = res->eoff[j];
+                        vals[i].assign(res->aheap + res->aoff[e], res->aheap + res->aoff[e + 1]);
+                    }
+                }
+                st_free_result(res);
+            }
+        }
+    }
+    if (op == 0) {   // the values, packed in request order
+        uint64_t o = 0;
+        voff_out[0] = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t l = status[i] == ST_OK ? vals[i].size() : 0;
+            if (o + l > vcap) { g_err = "value buffer too small"; voff_out[i + 1] = o + l; return ST_EINVAL; }
+            if (l) memcpy(vout + o, vals[i].data(), l);
+            o += l;
+            voff_out[i + 1] = o;
+        }
     }
     return ST_OK;
+}
+
+extern "C" int st_insert1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                                const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel,
+                                uint64_t *cbucket) {
+    return small_multi(1, trees, n, ktype, kheap, koff, vheap, voff, status, clevel, cbucket, nullptr, 0, nullptr);
+}
+
+extern "C" int st_get1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
+                             uint8_t *vout, uint64_t vcap, uint64_t *voff_out, int32_t *status, uint32_t *clevel,
+                             uint64_t *cbucket) {
+    return small_multi(0, trees, n, ktype, kheap, koff, nullptr, nullptr, status, clevel, cbucket, vout, vcap, voff_out);
 }
 
 // ------------------------------------------------------------------ writes
@@ -2058,6 +2299,7 @@ extern "C" int st_rehash(st_tree *t, int upper) {
     else CHK(rehash_all(t, nullptr, nullptr));
     CHK(erec_after_rehash(t));
     t->fresh = false;
+    t->async_pending = true;
     if (t->poisoned) {   // a tree in error becomes readable again once this rehash completed cleanly
         CHK(tsync(t));
         t->poisoned = false;

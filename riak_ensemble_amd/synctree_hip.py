@@ -463,6 +463,55 @@ def rehash_group(trees):
     _lib.check(L.st_rehash_group(arr, len(trees)), 'st_rehash_group')
 
 
+def insert1_multi(trees, keys, values):
+    """insert/3 of keys[i] -> values[i] into trees[i] for every i, as ONE device
+    launch over all the trees (st_insert1_multi).  Returns per request None or
+    ('corrupted', Level, Bucket)."""
+    n = len(trees)
+    if n == 0:
+        return []
+    for v in values:
+        if not isinstance(v, (bytes, bytearray)):
+            raise TypeError('function_clause: synctree values are binaries (synctree.erl:190)')
+    L = trees[0].L
+    arr = (ctypes.c_void_p * n)(*[t.h.value for t in trees])
+    kt, kh, ko = terms.pack_keys(keys)
+    vh, vo = terms.pack_values(values)
+    st = np.zeros(n, np.int32)
+    cl = np.zeros(n, np.uint32)
+    cb = np.zeros(n, np.uint64)
+    _lib.check(L.st_insert1_multi(arr, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vh), _ptr(vo), _ptr(st), _ptr(cl),
+                                  _ptr(cb)), 'st_insert1_multi')
+    return [None if st[i] == _lib.ST_OK else (terms.CORRUPTED, int(cl[i]), int(cb[i])) for i in range(n)]
+
+
+def get1_multi(trees, keys, vcap=1 << 20):
+    """get/2 of keys[i] in trees[i] for every i, as ONE device launch
+    (st_get1_multi): the value, 'notfound' or ('corrupted', L, B) per request."""
+    n = len(trees)
+    if n == 0:
+        return []
+    L = trees[0].L
+    arr = (ctypes.c_void_p * n)(*[t.h.value for t in trees])
+    kt, kh, ko = terms.pack_keys(keys)
+    vout = np.zeros(vcap, np.uint8)
+    vo = np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.int32)
+    cl = np.zeros(n, np.uint32)
+    cb = np.zeros(n, np.uint64)
+    _lib.check(L.st_get1_multi(arr, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vout), vcap, _ptr(vo), _ptr(st), _ptr(cl),
+                               _ptr(cb)), 'st_get1_multi')
+    out = []
+    for i in range(n):
+        if st[i] == _lib.ST_OK:
+            out.append(bytes(vout[int(vo[i]):int(vo[i + 1])]))
+        elif st[i] == _lib.ST_NOTFOUND:
+            out.append(terms.NOTFOUND)
+        else:
+            out.append((terms.CORRUPTED, int(cl[i]), int(cb[i])))
+    return out
+
+
 def tops_to_device(trees, dev_ptr):
     """Top-hash records (18 B each: present, hash17) of `trees` into device
     memory at dev_ptr (st_tops_to_device), e.g. a torch uint8 tensor to

@@ -167,3 +167,69 @@ def test_single_key_entry_points():
     with pytest.raises(TypeError):
         dev.insert1(k0, 'not a binary')
     dev.close()
+
+
+@pytest.mark.gpu
+def test_per_key_requests_of_many_trees_in_one_launch():
+    """st_insert1_multi / st_get1_multi: per-key insert/3 and get/2 requests
+    of many trees (riak_ensemble_peer_tree.erl:224-246, every peer tree of a
+    node taking puts at once) served by ONE launch over all the trees, a
+    workgroup per tree -- the same results as the per-tree calls in request
+    order, checked against one C restatement per tree: statuses (including
+    {corrupted, L, B} from a corrupted segment), gets, top hashes."""
+    import oracle_c as C
+    from riak_ensemble_amd import synctree_hip, workload
+    rng = np.random.default_rng(2024)
+    geoms = [(16, 1 << 16), (16, 1 << 20), (4, 4096)]
+    T, n0 = 24, 20_000
+    devs, oras, keys = [], [], []
+    for i in range(T):
+        W, S = geoms[i % 3]
+        k = workload.keys_int63(n0, workload.SEED ^ (0x3000 + i))
+        v = workload.obj_hash_values(n0)
+        d = synctree_hip.DeviceTree(W, S)
+        assert d.insert_int64(k, v) == 0
+        o = C.OTree(W, S).bulk_load_int64(k, v)
+        devs.append(d); oras.append(o); keys.append([int(x) for x in k])
+    # one corrupted segment in tree 5: requests into it are refused
+    victim = keys[5][11]
+    devs[5].corrupt(victim)
+    oras[5].corrupt(victim)
+    same = [k for k in keys[5] if oras[5].segment_of(k) == oras[5].segment_of(victim) and k != victim][:2]
+    seq = 10 ** 6
+    for r in range(12):
+        m = int(rng.integers(40, 160))
+        tix = [int(x) for x in rng.integers(0, T, m)]
+        tix[:4] = [3, 3, 3, 3] * 1               # a tree repeated within the launch
+        if r % 3 == 0:
+            tix += [7] * 20                       # more than 16 requests for one tree: two launches
+        ks, vs = [], []
+        for t in tix:
+            if rng.random() < 0.5:
+                ks.append(keys[t][int(rng.integers(0, len(keys[t])))])
+            else:
+                nk = int(rng.integers(0, 1 << 62))
+                keys[t].append(nk)
+                ks.append(nk)
+            seq += 1
+            vs.append(bytes([0]) + (3).to_bytes(8, 'big') + seq.to_bytes(8, 'big'))
+        if r == 4:
+            tix += [5, 5]
+            ks += same
+            vs += [b'\x00' * 17, b'\x00' * 17]
+        got = synctree_hip.insert1_multi([devs[t] for t in tix], ks, vs)
+        exp = []
+        for t, k, v in zip(tix, ks, vs):
+            res = oras[t].insert(k, v)
+            exp.append(None if res is oras[t] else res)
+        assert got == exp, r
+        if r == 4:
+            assert exp[-1] is not None and exp[-1][0] == 'corrupted'
+        probe_t = [int(x) for x in rng.integers(0, T, 200)]
+        probe_k = [keys[t][int(rng.integers(0, len(keys[t])))] for t in probe_t]
+        assert synctree_hip.get1_multi([devs[t] for t in probe_t], probe_k) == \
+            [oras[t].get(k) for t, k in zip(probe_t, probe_k)], r
+        for t in range(T):
+            assert devs[t].top_hash() == oras[t].top_hash(), (r, t)
+    for d in devs:
+        d.close()

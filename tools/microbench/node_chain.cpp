@@ -1,0 +1,84 @@
+// Diagnostic microbenchmark: latency of one inner-node hash (16 children =
+// 272-byte message, 5 MD5 blocks) as the fused rehash's level chain runs it,
+// one wave, lanes 0..A-1 active.  Variants:
+//   A  stmd5::md5_lds_node from LDS (the kernel's call)
+//   B  the 68 message words loaded from LDS into registers first, then the
+//      5 compressions (md5_node16-like, no LDS traffic inside the chain)
+//   C  compress<false> x 5 on register words only (the floor)
+// Build: hipcc -O3 --offload-arch=gfx950 -I riak_ensemble_amd/csrc tools/microbench/node_chain.cpp
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "md5_dev.h"
+
+template <int V>
+__global__ void __launch_bounds__(64) k(int n, int active, uint32_t *sink, unsigned long long *cyc) {
+    __shared__ __attribute__((aligned(16))) uint8_t msg[64 * 320];
+    const int lane = threadIdx.x;
+    uint8_t *my = msg + lane * 320;
+    for (int i = 0; i < 320; i++) my[i] = (uint8_t)(i * 7 + lane);
+    __syncthreads();
+    uint32_t d[4] = {1, 2, 3, 4};
+    const unsigned long long t0 = clock64();
+    if (lane < active) {
+        for (int r = 0; r < n; r++) {
+            if (V == 0) {
+                stmd5::md5_lds_node(my, 272, d);
+            } else if (V == 1) {
+                const uint32_t *q = reinterpret_cast<const uint32_t *>(my);
+                uint32_t w[80];
+#pragma unroll
+                for (int i = 0; i < 68; i++) w[i] = q[i];
+                w[68] = 0x80u;
+#pragma unroll
+                for (int i = 69; i < 80; i++) w[i] = 0u;
+                w[78] = 272u * 8u;
+                uint32_t st[4];
+                stmd5::init(st);
+#pragma unroll
+                for (int b = 0; b < 5; b++) stmd5::compress(st, w + 16 * b);
+                d[0] = st[0]; d[1] = st[1]; d[2] = st[2]; d[3] = st[3];
+            } else {
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) w[i] = d[i & 3] + i;
+                uint32_t st[4];
+                stmd5::init(st);
+#pragma unroll
+                for (int b = 0; b < 5; b++) { stmd5::compress(st, w); w[b] ^= st[0]; }
+                d[0] = st[0]; d[1] = st[1]; d[2] = st[2]; d[3] = st[3];
+            }
+            reinterpret_cast<uint32_t *>(my)[r & 63] = d[0];   // next message depends on this digest
+        }
+    }
+    const unsigned long long t1 = clock64();
+    sink[lane] = d[0] ^ d[1] ^ d[2] ^ d[3];
+    if (lane == 0) cyc[0] = t1 - t0;
+}
+
+template <int V>
+void run(uint32_t *s, unsigned long long *c, int active) {
+    const int n = 200;
+    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, s, c);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, s, c);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    unsigned long long cyc;
+    hipMemcpy(&cyc, c, 8, hipMemcpyDeviceToHost);
+    printf("variant %c active %2d: %7.3f us per node (event), %7.0f shader cycles per node, %6.0f per block\n",
+           "ABC"[V], active, ms * 1e3 / n, (double)cyc / n, (double)cyc / n / 5);
+}
+
+int main() {
+    uint32_t *s;
+    unsigned long long *c;
+    hipMalloc(&s, 4096);
+    hipMalloc(&c, 64);
+    for (int active : {1, 16, 64}) { run<0>(s, c, active); run<1>(s, c, active); run<2>(s, c, active); }
+    return 0;
+}
