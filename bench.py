@@ -462,6 +462,22 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
     t0 = time.perf_counter()
     res = tree_a.compare(tb)
     dt_host = time.perf_counter() - t0
+    # the records returned to host memory by the C ABI alone (st_compare ->
+    # st_result, freed; no Python decoding), as a NIF would take them
+    import ctypes
+    from riak_ensemble_amd import _lib
+    L = _lib.load()
+    rp = ctypes.POINTER(_lib.StResult)()
+    cl, cb, cs = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_int()
+    c_times = []
+    for _ in range(reps):
+        tc = time.perf_counter()
+        _lib.check(L.st_compare(tree_a.h, tb.h, _lib.ST_FILTER_ALL, ctypes.byref(rp), ctypes.byref(cl), ctypes.byref(cb),
+                                ctypes.byref(cs)), 'st_compare')
+        c_times.append(time.perf_counter() - tc)
+        assert rp.contents.n_entries == nd
+        L.st_free_result(rp)
+    c_times.sort()
     assert res[0] == 'ok' and len(res[1]) == len(segs)
     # (B's bumped FIRST byte is the ?H_OBJ_NONE prefix: the reference exchange
     # would crash in valid_obj_hash on these diffs, and so does ours)
@@ -495,7 +511,11 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
                          'frac': round(gbs / HBM_PEAK_GBS, 6), 'bytes_per_compare': int(algo),
                          'note': 'latency-bound: ~1 MB of algorithmic traffic per compare; the bound that binds is '
                                  'the dependent chain frontier -> verify/merge -> scan -> write'},
-            'ms_per_compare_incl_d2h_records': round(dt_host * 1e3, 4),
+            'ms_per_compare_records_to_host_c': round(c_times[len(c_times) // 2] * 1e3, 4),
+            'ms_per_compare_records_to_host_c_what': 'st_compare through ctypes: compare + the ordered diff records '
+                                                     '(keys, both values, kinds, segments) in host memory; median of '
+                                                     '%d calls' % reps,
+            'ms_per_compare_incl_python_decode': round(dt_host * 1e3, 4),
             'exchange_apply_ms': round(dt_apply * 1e3, 4),
             'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
                               'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),

@@ -124,6 +124,9 @@ struct st_tree {
     CmpWork cw;
     // small pinned host buffer for scalar results (one D2H per call)
     uint64_t *pin = nullptr;
+    // pinned host staging for result records (st_compare), grown on demand
+    uint8_t *rpin = nullptr;
+    uint64_t rpin_cap = 0;
     // per-key latency path (small_path.h): overlay of segments changed by
     // small inserts, and the mapped pinned result block of k_small
     Overlay ov{nullptr, nullptr, nullptr, 0};
@@ -616,6 +619,20 @@ static int d2h(st_tree *t, void *dst, const void *src, uint64_t bytes) {
     CHK(tsync(t));
     return ST_OK;
 }
+// the tree's pinned staging buffer, at least `bytes` (contents not kept)
+static int rpin_reserve(st_tree *t, uint64_t bytes) {
+    if (bytes <= t->rpin_cap) return ST_OK;
+    uint64_t cap = t->rpin_cap ? t->rpin_cap : 65536;
+    while (cap < bytes) cap *= 2;
+    if (t->rpin) { CHK(tsync(t)); (void)hipHostFree(t->rpin); t->rpin = nullptr; t->rpin_cap = 0; }
+    if (hipHostMalloc((void **)&t->rpin, cap, hipHostMallocDefault) != hipSuccess) {
+        t->rpin = nullptr;
+        g_err = "hipHostMalloc (staging) failed";
+        return ST_ENOMEM;
+    }
+    t->rpin_cap = cap;
+    return ST_OK;
+}
 static int h2d(st_tree *t, void *dst, const void *src, uint64_t bytes) {
     if (!bytes) return ST_OK;
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, t->stream));
@@ -733,6 +750,7 @@ extern "C" void st_destroy(st_tree *t) {
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
     if (t->pin) (void)hipHostFree(t->pin);
+    if (t->rpin) (void)hipHostFree(t->rpin);
     if (t->derr) (void)hipHostFree(t->derr);
     if (t->sout) (void)hipHostFree(t->sout);
     if (t->sreq) (void)hipHostFree(t->sreq);
@@ -3151,34 +3169,51 @@ extern "C" int st_compare(st_tree *local, st_tree *remote, int filter, st_result
         *out = res;
         return ST_OK;
     }
+    // The records to host memory with two synchronisations: the lengths of
+    // every key and value as ONE array [keys | local values | remote values]
+    // (n + 1 each, the last 0) and ONE scan, so the three offset arrays are
+    // windows of the scan and the three heaps are ranges of one buffer; the
+    // scan comes back in one copy (the heap sizes), then the heaps, segments
+    // and kinds in one more.
     DevTree da = view(local), db = view(remote);
     Scratch sc(t);
-    uint64_t *kl = nullptr, *al = nullptr, *bl = nullptr, *ko = nullptr, *ao = nullptr, *bo = nullptr, *seg = nullptr;
-    uint8_t *kind = nullptr, *kh = nullptr, *ah = nullptr, *bh = nullptr;
+    const uint64_t m = n + 1, m3 = 3 * m;
+    uint64_t *len = nullptr, *off = nullptr;
+    uint8_t *D = nullptr;
     int r = ST_OK;
     auto fail = [&](int rc) { st_free_result(res); return rc; };
-    if ((r = sc.alloc(&kl, n + 1)) || (r = sc.alloc(&al, n + 1)) || (r = sc.alloc(&bl, n + 1)) || (r = sc.alloc(&ko, n + 1)) ||
-        (r = sc.alloc(&ao, n + 1)) || (r = sc.alloc(&bo, n + 1)) || (r = sc.alloc(&kind, n)) || (r = sc.alloc(&seg, n)))
-        return fail(r);
+    if ((r = sc.alloc(&len, m3)) || (r = sc.alloc(&off, m3))) return fail(r);
     t->reads_remote = true;
-    hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, da, db, co.rec, n, kl, al, bl);
-    if ((r = exclusive_scan<uint64_t>(t, kl, ko, n + 1)) || (r = exclusive_scan<uint64_t>(t, al, ao, n + 1)) ||
-        (r = exclusive_scan<uint64_t>(t, bl, bo, n + 1)))
-        return fail(r);
-    if ((r = d2h(t, res->koff, ko, (n + 1) * 8)) || (r = d2h(t, res->aoff, ao, (n + 1) * 8)) ||
-        (r = d2h(t, res->boff, bo, (n + 1) * 8)))
-        return fail(r);
-    const uint64_t kb = res->koff[n], ab = res->aoff[n], bb = res->boff[n];
-    if ((r = sc.bytes(&kh, kb + 16)) || (r = sc.bytes(&ah, ab + 16)) || (r = sc.bytes(&bh, bb + 16))) return fail(r);
-    hipLaunchKernelGGL(k_diff_gather, dim3(grid_for(n)), dim3(256), 0, t->stream, da, db, co.rec, n, (const uint64_t *)ko, kh,
-                       (const uint64_t *)ao, ah, (const uint64_t *)bo, bh, kind, seg);
+    hipLaunchKernelGGL(k_diff_lengths, dim3(grid_for(m)), dim3(256), 0, t->stream, da, db, co.rec, n, len, len + m, len + 2 * m);
+    if ((r = exclusive_scan<uint64_t>(t, len, off, m3)) || (r = rpin_reserve(t, m3 * 8))) return fail(r);
+    HIPCHK(hipMemcpyAsync(t->rpin, off, m3 * 8, hipMemcpyDeviceToHost, t->stream));
+    if ((r = tsync(t))) return fail(r);
+    const uint64_t *S = reinterpret_cast<const uint64_t *>(t->rpin);
+    const uint64_t kb = S[n], ab = S[2 * m - 1] - S[m], bb = S[m3 - 1] - S[2 * m];
+    for (uint64_t i = 0; i <= n; i++) {
+        res->koff[i] = S[i];
+        res->aoff[i] = S[m + i] - S[m];
+        res->boff[i] = S[2 * m + i] - S[2 * m];
+    }
+    const uint64_t hb = (S[m3 - 1] + 7) & ~7ull;   // the three heaps, back to back
+    if ((r = sc.bytes(&D, hb + 9 * n + 16))) return fail(r);
+    uint64_t *dseg = reinterpret_cast<uint64_t *>(D + hb);
+    uint8_t *dkind = D + hb + 8 * n;
+    hipLaunchKernelGGL(k_diff_gather, dim3(grid_for(n)), dim3(256), 0, t->stream, da, db, co.rec, n, (const uint64_t *)off, D,
+                       (const uint64_t *)(off + m), D, (const uint64_t *)(off + 2 * m), D, dkind, dseg);
     if (hipGetLastError() != hipSuccess) { g_err = "launch diff_gather"; return fail(ST_EDEVICE); }
+    if ((r = rpin_reserve(t, hb + 9 * n))) return fail(r);
+    HIPCHK(hipMemcpyAsync(t->rpin, D, hb + 9 * n, hipMemcpyDeviceToHost, t->stream));
+    if ((r = tsync(t))) return fail(r);
     res->kheap = (uint8_t *)malloc(kb + 1);
     res->aheap = (uint8_t *)malloc(ab + 1);
     res->bheap = (uint8_t *)malloc(bb + 1);
-    if ((r = d2h(t, res->kheap, kh, kb)) || (r = d2h(t, res->aheap, ah, ab)) || (r = d2h(t, res->bheap, bh, bb)) ||
-        (r = d2h(t, res->kind, kind, n)) || (r = d2h(t, res->seg, seg, n * 8)))
-        return fail(r);
+    if (!res->kheap || !res->aheap || !res->bheap) { g_err = "malloc"; return fail(ST_ENOMEM); }
+    memcpy(res->kheap, t->rpin, kb);
+    memcpy(res->aheap, t->rpin + kb, ab);
+    memcpy(res->bheap, t->rpin + kb + ab, bb);
+    memcpy(res->seg, t->rpin + hb, 8 * n);
+    memcpy(res->kind, t->rpin + hb + 8 * n, n);
     records_to_keys(res, n);
     *out = res;
     return ST_OK;

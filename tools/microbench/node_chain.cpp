@@ -5,13 +5,15 @@
 //   B  the 68 message words loaded from LDS into registers first, then the
 //      5 compressions (md5_node16-like, no LDS traffic inside the chain)
 //   C  compress<false> x 5 on register words only (the floor)
+//   D  A with the message length a run-time value (as in the kernel)
+//   E  D for ONE node per launch (instruction cache cold, as at level H)
 // Build: hipcc -O3 --offload-arch=gfx950 -I riak_ensemble_amd/csrc tools/microbench/node_chain.cpp
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "md5_dev.h"
 
 template <int V>
-__global__ void __launch_bounds__(64) k(int n, int active, uint32_t *sink, unsigned long long *cyc) {
+__global__ void __launch_bounds__(64) k(int n, int active, uint32_t len, uint32_t *sink, unsigned long long *cyc) {
     __shared__ __attribute__((aligned(16))) uint8_t msg[64 * 320];
     const int lane = threadIdx.x;
     uint8_t *my = msg + lane * 320;
@@ -23,6 +25,8 @@ __global__ void __launch_bounds__(64) k(int n, int active, uint32_t *sink, unsig
         for (int r = 0; r < n; r++) {
             if (V == 0) {
                 stmd5::md5_lds_node(my, 272, d);
+            } else if (V >= 3) {
+                stmd5::md5_lds_node(my, len, d);
             } else if (V == 1) {
                 const uint32_t *q = reinterpret_cast<const uint32_t *>(my);
                 uint32_t w[80];
@@ -57,13 +61,13 @@ __global__ void __launch_bounds__(64) k(int n, int active, uint32_t *sink, unsig
 
 template <int V>
 void run(uint32_t *s, unsigned long long *c, int active) {
-    const int n = 200;
-    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, s, c);
+    const int n = V == 4 ? 1 : 200;
+    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, 272u, s, c);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
     hipEventRecord(a);
-    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, s, c);
+    hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, 272u, s, c);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -71,7 +75,7 @@ void run(uint32_t *s, unsigned long long *c, int active) {
     unsigned long long cyc;
     hipMemcpy(&cyc, c, 8, hipMemcpyDeviceToHost);
     printf("variant %c active %2d: %7.3f us per node (event), %7.0f shader cycles per node, %6.0f per block\n",
-           "ABC"[V], active, ms * 1e3 / n, (double)cyc / n, (double)cyc / n / 5);
+           "ABCDE"[V], active, ms * 1e3 / n, (double)cyc / n, (double)cyc / n / 5);
 }
 
 int main() {
@@ -79,6 +83,9 @@ int main() {
     unsigned long long *c;
     hipMalloc(&s, 4096);
     hipMalloc(&c, 64);
-    for (int active : {1, 16, 64}) { run<0>(s, c, active); run<1>(s, c, active); run<2>(s, c, active); }
+    run<0>(s, c, 64);   // warm-up (clocks)
+    for (int active : {1, 16, 64}) {
+        run<0>(s, c, active); run<1>(s, c, active); run<2>(s, c, active); run<3>(s, c, active); run<4>(s, c, active);
+    }
     return 0;
 }
