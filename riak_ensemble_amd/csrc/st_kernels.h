@@ -1275,6 +1275,7 @@ __device__ __forceinline__ bool cmp_visited(const DevTree &A, const DevTree &B, 
 // records of a wave that overflowed R.  No same-address atomics on the
 // success path.
 #define ST_STATW (ST_MAXLEV + 2)
+#define CMP_SPEC 5   // frontier levels loaded up front (2..6: H <= 6)
 
 struct CmpWalk {
     uint8_t *shared;       // lane regions / merge area
@@ -1300,6 +1301,9 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
     const uint32_t L1 = A.H + 1;
     const uint32_t SH = cmp_shared_bytes(A.W);
     CW_STAMP(c, 8);
+    // the first 32 items' segment bounds (lane 2i: item i's local side, 2i + 1
+    // its remote side), kept for the merge-joins (no second round trip)
+    uint64_t kv0 = 0, kvl = 0, ks0 = 0, ks1 = 0;
     for (uint32_t k0 = 0; k0 < 2 * n; k0 += 64) {
         const uint32_t k = k0 + lane;
         const bool act = k < 2 * n;
@@ -1319,8 +1323,11 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
             if (side) { et = B.tag[eslot]; e = B.md5[eslot]; } else { et = A.tag[eslot]; e = A.md5[eslot]; }
         }
         if (seg) {
-            if (side) { v0 = B.seg_voff[b]; len = B.seg_voff[b + 1] - v0; empty = B.seg_off[b] == B.seg_off[b + 1]; }
-            else      { v0 = A.seg_voff[b]; len = A.seg_voff[b + 1] - v0; empty = A.seg_off[b] == A.seg_off[b + 1]; }
+            uint64_t s0, s1;
+            if (side) { v0 = B.seg_voff[b]; len = B.seg_voff[b + 1] - v0; s0 = B.seg_off[b]; s1 = B.seg_off[b + 1]; }
+            else      { v0 = A.seg_voff[b]; len = A.seg_voff[b + 1] - v0; s0 = A.seg_off[b]; s1 = A.seg_off[b + 1]; }
+            empty = s0 == s1;
+            if (k0 == 0) { kv0 = v0; kvl = len; ks0 = s0; ks1 = s1; }
         }
         // inner nodes: the child entries, loaded while the loads above are in flight
         uint32_t mlen = 0;
@@ -1376,7 +1383,15 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         const bool sg = i < n && (uint32_t)(it >> 56) == L1;
         const uint64_t sj = it & ((1ull << 56) - 1);
         SegPair p = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (sg) p = seg_pair(A, B, sj);
+        if (i0 == 0 && n <= 32) {   // every item's bounds are in the phase-1 registers
+            const int la = (int)(2 * (lane & 31)), lb = la + 1;
+            p.a0 = __shfl(ks0, la, 64); p.a1 = __shfl(ks1, la, 64);
+            p.va0 = __shfl(kv0, la, 64); p.va1 = p.va0 + __shfl(kvl, la, 64);
+            p.b0 = __shfl(ks0, lb, 64); p.b1 = __shfl(ks1, lb, 64);
+            p.vb0 = __shfl(kv0, lb, 64); p.vb1 = p.vb0 + __shfl(kvl, lb, 64);
+        } else if (sg) {
+            p = seg_pair(A, B, sj);
+        }
         for (uint64_t m = __ballot(sg); m; m &= m - 1) {
             const int j = __ffsll((long long)m) - 1;
             uint64_t by;
@@ -1450,6 +1465,31 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         }
         for (uint64_t c0 = h0 + ((h1 - h0 - 1) & ~63ull);; c0 -= 64) {
             const uint64_t c1 = c0 + 64 < h1 ? c0 + 64 : h1;   // level-H nodes [c0, c1)
+            // H <= CMP_SPEC + 1: the entries of every level 2..H under these
+            // nodes are loaded up front (a lane per node, index clamped), so the
+            // frontier costs one memory round trip instead of one per level;
+            // only the flags chain through the levels
+            const bool spec = H <= CMP_SPEC + 1;
+            uint32_t dmask = 0;
+            if (spec) {
+                uint16_t ta[CMP_SPEC], tb[CMP_SPEC];
+                uint4 xa[CMP_SPEC], xb[CMP_SPEC];
+#pragma unroll
+                for (uint32_t i = 0; i < CMP_SPEC; i++) {
+                    if (2 + i > H) break;
+                    const uint32_t up = sh * (H - 2 - i);
+                    const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
+                    const uint64_t slot = A.base[2 + i] + (lo + lane <= hi ? lo + lane : hi);
+                    ta[i] = A.tag[slot]; tb[i] = B.tag[slot]; xa[i] = A.md5[slot]; xb[i] = B.md5[slot];
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < CMP_SPEC; i++) {
+                    if (2 + i > H) break;
+                    const uint64_t b = (c0 >> (sh * (H - 2 - i))) + lane;
+                    const bool d = entry_differs(ta[i], tb[i], xa[i], xb[i], filter) && (i != 0 || (b >= lo2 && b < hi2));
+                    dmask |= (uint32_t)d << (2 + i);
+                }
+            }
             bool f = true;       // this lane's node flag at the previous level (level 1: the root)
             for (uint32_t l = 2; l <= H; l++) {
                 const uint32_t up = sh * (H - l);
@@ -1458,7 +1498,7 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
                 const uint64_t plo = lo >> sh;
                 const uint32_t plane = (uint32_t)((b >> sh) - plo);
                 const bool fp = __shfl((int)f, (int)(plane < 64 ? plane : 0), 64) != 0;
-                f = b <= hi && fp && cmp_entry_in(A, B, filter, l, b, lo2, hi2);
+                f = b <= hi && fp && (spec ? ((dmask >> l) & 1u) != 0 : cmp_entry_in(A, B, filter, l, b, lo2, hi2));
                 const bool owned = f && (b << up) >= c0 && (b << up) < c1;
                 if (n + 64 > CMP_LIST) { cmp_flush(A, B, c, n); n = 0; }
                 const uint32_t n0 = n;

@@ -7,6 +7,8 @@
 //   C  compress<false> x 5 on register words only (the floor)
 //   D  A with the message length a run-time value (as in the kernel)
 //   E  D for ONE node per launch (instruction cache cold, as at level H)
+//   F  stmd5::md5_lds_node_rolled (block loop rolled), run-time length
+//   G  F for ONE node per launch
 // Build: hipcc -O3 --offload-arch=gfx950 -I riak_ensemble_amd/csrc tools/microbench/node_chain.cpp
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -25,8 +27,10 @@ __global__ void __launch_bounds__(64) k(int n, int active, uint32_t len, uint32_
         for (int r = 0; r < n; r++) {
             if (V == 0) {
                 stmd5::md5_lds_node(my, 272, d);
-            } else if (V >= 3) {
+            } else if (V == 3 || V == 4) {
                 stmd5::md5_lds_node(my, len, d);
+            } else if (V >= 5) {
+                stmd5::md5_lds_node_rolled(my, len, d);
             } else if (V == 1) {
                 const uint32_t *q = reinterpret_cast<const uint32_t *>(my);
                 uint32_t w[80];
@@ -61,7 +65,7 @@ __global__ void __launch_bounds__(64) k(int n, int active, uint32_t len, uint32_
 
 template <int V>
 void run(uint32_t *s, unsigned long long *c, int active) {
-    const int n = V == 4 ? 1 : 200;
+    const int n = (V == 4 || V == 6) ? 1 : 200;
     hipLaunchKernelGGL(k<V>, dim3(1), dim3(64), 0, 0, n, active, 272u, s, c);
     hipEvent_t a, b;
     hipEventCreate(&a);
@@ -75,7 +79,7 @@ void run(uint32_t *s, unsigned long long *c, int active) {
     unsigned long long cyc;
     hipMemcpy(&cyc, c, 8, hipMemcpyDeviceToHost);
     printf("variant %c active %2d: %7.3f us per node (event), %7.0f shader cycles per node, %6.0f per block\n",
-           "ABCDE"[V], active, ms * 1e3 / n, (double)cyc / n, (double)cyc / n / 5);
+           "ABCDEFG"[V], active, ms * 1e3 / n, (double)cyc / n, (double)cyc / n / 5);
 }
 
 int main() {
@@ -86,6 +90,7 @@ int main() {
     run<0>(s, c, 64);   // warm-up (clocks)
     for (int active : {1, 16, 64}) {
         run<0>(s, c, active); run<1>(s, c, active); run<2>(s, c, active); run<3>(s, c, active); run<4>(s, c, active);
+        run<5>(s, c, active); run<6>(s, c, active);
     }
     return 0;
 }
