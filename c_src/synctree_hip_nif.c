@@ -389,6 +389,101 @@ static ERL_NIF_TERM nif_rehash_group(ErlNifEnv *env, int argc, const ERL_NIF_TER
     return rc == ST_OK ? A_OK : err(env);
 }
 
+/* The requests of many trees: a list of {Ref, {Type, KeyBin}} (with_values
+ * 0) or {Ref, {Type, KeyBin}, Value} (1) -> the trees and the packed keys. */
+static int pack_multi(ErlNifEnv *env, ERL_NIF_TERM list, int with_values, st_tree ***trees, packed *p) {
+    unsigned n;
+    if (!enif_get_list_length(env, list, &n)) return 0;
+    st_tree **ts = enif_alloc(sizeof(st_tree *) * ((size_t)n + 1));
+    ERL_NIF_TERM *keys = enif_alloc(sizeof(ERL_NIF_TERM) * ((size_t)n + 1));
+    int ok = ts && keys;
+    ERL_NIF_TERM h, t = list;
+    for (unsigned i = 0; ok && i < n; i++) {
+        const ERL_NIF_TERM *e;
+        int a;
+        ok = enif_get_list_cell(env, t, &h, &t) && enif_get_tuple(env, h, &a, &e) && a == 2 + with_values &&
+             get_tree(env, e[0], &ts[i]);
+        if (ok) keys[i] = with_values ? enif_make_tuple2(env, e[1], e[2]) : e[1];
+    }
+    if (ok) ok = pack(env, enif_make_list_from_array(env, keys, n), with_values, p);
+    enif_free(keys);
+    if (!ok) {
+        enif_free(ts);
+        return 0;
+    }
+    *trees = ts;
+    return 1;
+}
+
+/* insert_multi([{Ref, {Type, KeyBin}, Value}]) -> [ok | {corrupted, L, B}]:
+ * insert/3 of each request into its tree (synctree.erl:189-209; the puts of
+ * many peer trees, riak_ensemble_peer_tree.erl:224-234), a tree's requests in
+ * list order, every tree's batch in one device launch.  DIRTY. */
+static ERL_NIF_TERM nif_insert_multi(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    st_tree **ts;
+    packed p;
+    (void)argc;
+    if (!pack_multi(env, argv[0], 1, &ts, &p)) return enif_make_badarg(env);
+    int32_t *st = enif_alloc(4 * ((size_t)p.n + 1));
+    uint32_t *cl = enif_alloc(4 * ((size_t)p.n + 1));
+    uint64_t *cb = enif_alloc(8 * ((size_t)p.n + 1));
+    ERL_NIF_TERM res;
+    if (st_insert1_multi(ts, p.n, p.kt, p.kh, p.ko, p.vh, p.vo, st, cl, cb) < 0) res = err(env);
+    else res = status_list(env, p.n, st, cl, cb);
+    enif_free(st);
+    enif_free(cl);
+    enif_free(cb);
+    enif_free(ts);
+    packed_free(&p);
+    return res;
+}
+
+/* get_multi([{Ref, {Type, KeyBin}}]) -> [Value | notfound | {corrupted, L, B}]
+ * (synctree:get/2, synctree.erl:213-227, of many trees in one launch).  A
+ * value buffer that turns out too small is doubled and the (read-only) call
+ * run again.  DIRTY. */
+static ERL_NIF_TERM nif_get_multi(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    st_tree **ts;
+    packed p;
+    (void)argc;
+    if (!pack_multi(env, argv[0], 0, &ts, &p)) return enif_make_badarg(env);
+    int32_t *st = enif_alloc(4 * ((size_t)p.n + 1));
+    uint32_t *cl = enif_alloc(4 * ((size_t)p.n + 1));
+    uint64_t *cb = enif_alloc(8 * ((size_t)p.n + 1));
+    uint64_t *vo = enif_alloc(8 * ((size_t)p.n + 2));
+    uint64_t cap = 64 * ((uint64_t)p.n + 16);
+    uint8_t *vout = NULL;
+    int rc = ST_EINVAL;
+    for (int attempt = 0; attempt < 16; attempt++, cap *= 2) {
+        enif_free(vout);
+        vout = enif_alloc((size_t)cap);
+        if (!vout) break;
+        rc = st_get1_multi(ts, p.n, p.kt, p.kh, p.ko, vout, cap, vo, st, cl, cb);
+        if (rc != ST_EINVAL || !strstr(st_last_error(), "too small")) break;
+    }
+    ERL_NIF_TERM res;
+    if (rc < 0) {
+        res = err(env);
+    } else {
+        res = enif_make_list(env, 0);
+        for (unsigned i = p.n; i-- > 0;) {
+            ERL_NIF_TERM v;
+            if (st[i] == ST_CORRUPTED) v = corrupted(env, cl[i], cb[i]);
+            else if (st[i] == ST_NOTFOUND) v = A_NOTFOUND;
+            else v = bin_term(env, vout + vo[i], vo[i + 1] - vo[i]);
+            res = enif_make_list_cell(env, v, res);
+        }
+    }
+    enif_free(vout);
+    enif_free(vo);
+    enif_free(st);
+    enif_free(cl);
+    enif_free(cb);
+    enif_free(ts);
+    packed_free(&p);
+    return res;
+}
+
 /* ------------------------------------------------------------ reads */
 
 /* One node of a result block as the orddict the ETS backend holds:
@@ -647,6 +742,8 @@ static ErlNifFunc funcs[] = {
     {"height", 1, nif_height, 0},
     {"insert_batch", 2, nif_insert_batch, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"insert", 3, nif_insert, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"insert_multi", 1, nif_insert_multi, ERL_NIF_DIRTY_JOB_CPU_BOUND},
+    {"get_multi", 1, nif_get_multi, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"corrupt", 2, nif_corrupt, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"store", 2, nif_store, ERL_NIF_DIRTY_JOB_CPU_BOUND},
     {"set_record_top", 2, nif_set_record_top, 0},

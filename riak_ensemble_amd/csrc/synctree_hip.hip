@@ -2987,8 +2987,11 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 128, t->stream));
         }
         A->reads_remote = true;   // until the gather's completion word is seen
+        // ST_CMP_STAGED=1: the first pair of a short list merge-joined from the
+        // verification's staging (st_kernels.h CMP_FM_*; A/B knob, off by default)
+        static const uint32_t opts = getenv("ST_CMP_STAGED") && atoi(getenv("ST_CMP_STAGED")) ? 1u : 0u;
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
-               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps, opts);
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 16);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));

@@ -50,6 +50,7 @@ ERL_NIF_TERM enif_make_badarg(ErlNifEnv *env);
 ERL_NIF_TERM enif_make_tuple2(ErlNifEnv *env, ERL_NIF_TERM e1, ERL_NIF_TERM e2);
 ERL_NIF_TERM enif_make_tuple3(ErlNifEnv *env, ERL_NIF_TERM e1, ERL_NIF_TERM e2, ERL_NIF_TERM e3);
 ERL_NIF_TERM enif_make_list(ErlNifEnv *env, unsigned cnt, ...);
+ERL_NIF_TERM enif_make_list_from_array(ErlNifEnv *env, const ERL_NIF_TERM arr[], unsigned cnt);
 ERL_NIF_TERM enif_make_list_cell(ErlNifEnv *env, ERL_NIF_TERM head, ERL_NIF_TERM tail);
 ERL_NIF_TERM enif_make_uint(ErlNifEnv *env, unsigned i);
 ERL_NIF_TERM enif_make_uint64(ErlNifEnv *env, ErlNifUInt64 i);
