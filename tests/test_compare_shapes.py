@@ -95,7 +95,7 @@ def test_compare_many_diff_segments_per_wave():
     """Every segment differs (a wave lists more than 32 items: no staged
     pair), then one differing segment per 50 (one or two a wave)."""
     rng = np.random.default_rng(5)
-    S = 16384
+    S = 65536
     keys = [int(x) for x in rng.choice(1 << 40, 60_000, replace=False)]
     vals = [bytes(_rand_bin(rng, 17, 17)) for _ in keys]
     o = C.OTree(16, S)
