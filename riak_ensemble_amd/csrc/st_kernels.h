@@ -1534,19 +1534,47 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
     c.stage_pair = (opts & 1u) != 0;
     c.errmin = ~0ull;
     for (uint32_t l = lane; l < ST_STATW; l += 64) c.cnt[l] = 0;
-    bool topdiff;
-    {
-        const uint16_t ta = A.tag[0], tb = B.tag[0];
-        topdiff = ta != tb;
-        if (!topdiff && (ta & TAG_PRESENT)) {
-            const uint4 x = A.md5[0], y = B.md5[0];
-            topdiff = x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
-        }
-    }
     const uint64_t nH = A.base[L1] - A.base[H];   // level-H nodes
     const uint64_t P = (nH + nw - 1) / nw;
     const uint64_t h0 = (uint64_t)w * P < nH ? (uint64_t)w * P : nH;
     const uint64_t h1 = h0 + P < nH ? h0 + P : nH;
+    // H <= CMP_SPEC + 1: the entries of every level 2..H under a chunk of 64
+    // level-H nodes are loaded up front (a lane per node, index clamped), so
+    // the frontier costs one memory round trip instead of one per level; only
+    // the flags chain through the levels.  The first chunk's loads go out with
+    // the top entries' (one round trip for both).
+    const bool spec = H <= CMP_SPEC + 1;
+    uint16_t sta[CMP_SPEC], stb[CMP_SPEC];
+    uint4 sxa[CMP_SPEC], sxb[CMP_SPEC];
+    auto spec_load = [&](uint64_t c0, uint64_t c1) {
+#pragma unroll
+        for (uint32_t i = 0; i < CMP_SPEC; i++) {
+            if (2 + i > H) break;
+            const uint32_t up = sh * (H - 2 - i);
+            const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
+            const uint64_t slot = A.base[2 + i] + (lo + lane <= hi ? lo + lane : hi);
+            sta[i] = A.tag[slot]; stb[i] = B.tag[slot]; sxa[i] = A.md5[slot]; sxb[i] = B.md5[slot];
+        }
+    };
+    auto spec_mask = [&](uint64_t c0) {
+        uint32_t dm = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < CMP_SPEC; i++) {
+            if (2 + i > H) break;
+            const uint64_t b = (c0 >> (sh * (H - 2 - i))) + lane;
+            const bool d = entry_differs(sta[i], stb[i], sxa[i], sxb[i], filter) && (i != 0 || (b >= lo2 && b < hi2));
+            dm |= (uint32_t)d << (2 + i);
+        }
+        return dm;
+    };
+    const uint64_t cfirst = h1 > h0 ? h0 + ((h1 - h0 - 1) & ~63ull) : 0;
+    if (spec && h1 > h0) spec_load(cfirst, cfirst + 64 < h1 ? cfirst + 64 : h1);
+    bool topdiff;
+    {
+        const uint16_t ta = A.tag[0], tb = B.tag[0];
+        const uint4 x = A.md5[0], y = B.md5[0];
+        topdiff = ta != tb || ((ta & TAG_PRESENT) && (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w));
+    }
     uint32_t n = 0;
     wave_sync_lds();
     if (topdiff && H == 0) {   // one segment under the top hash (segments = 1): wave 0
@@ -1561,32 +1589,12 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
             cmp_append(c.list, n, lane == 0, (1ull << 56));
             if (lane == 0) c.cnt[1] += 1;
         }
-        for (uint64_t c0 = h0 + ((h1 - h0 - 1) & ~63ull);; c0 -= 64) {
+        for (uint64_t c0 = cfirst;; c0 -= 64) {
             const uint64_t c1 = c0 + 64 < h1 ? c0 + 64 : h1;   // level-H nodes [c0, c1)
-            // H <= CMP_SPEC + 1: the entries of every level 2..H under these
-            // nodes are loaded up front (a lane per node, index clamped), so the
-            // frontier costs one memory round trip instead of one per level;
-            // only the flags chain through the levels
-            const bool spec = H <= CMP_SPEC + 1;
             uint32_t dmask = 0;
             if (spec) {
-                uint16_t ta[CMP_SPEC], tb[CMP_SPEC];
-                uint4 xa[CMP_SPEC], xb[CMP_SPEC];
-#pragma unroll
-                for (uint32_t i = 0; i < CMP_SPEC; i++) {
-                    if (2 + i > H) break;
-                    const uint32_t up = sh * (H - 2 - i);
-                    const uint64_t lo = c0 >> up, hi = (c1 - 1) >> up;
-                    const uint64_t slot = A.base[2 + i] + (lo + lane <= hi ? lo + lane : hi);
-                    ta[i] = A.tag[slot]; tb[i] = B.tag[slot]; xa[i] = A.md5[slot]; xb[i] = B.md5[slot];
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < CMP_SPEC; i++) {
-                    if (2 + i > H) break;
-                    const uint64_t b = (c0 >> (sh * (H - 2 - i))) + lane;
-                    const bool d = entry_differs(ta[i], tb[i], xa[i], xb[i], filter) && (i != 0 || (b >= lo2 && b < hi2));
-                    dmask |= (uint32_t)d << (2 + i);
-                }
+                if (c0 != cfirst) spec_load(c0, c1);
+                dmask = spec_mask(c0);
             }
             bool f = true;       // this lane's node flag at the previous level (level 1: the root)
             for (uint32_t l = 2; l <= H; l++) {
