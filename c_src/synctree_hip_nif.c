@@ -440,8 +440,8 @@ static ERL_NIF_TERM nif_insert_multi(ErlNifEnv *env, int argc, const ERL_NIF_TER
 
 /* get_multi([{Ref, {Type, KeyBin}}]) -> [Value | notfound | {corrupted, L, B}]
  * (synctree:get/2, synctree.erl:213-227, of many trees in one launch).  A
- * value buffer that turns out too small is doubled and the (read-only) call
- * run again.  DIRTY. */
+ * value buffer that turns out too small (ST_ERANGE) is resized to the bytes
+ * the call reports in vo[n] and the (read-only) call run once more.  DIRTY. */
 static ERL_NIF_TERM nif_get_multi(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     st_tree **ts;
     packed p;
@@ -452,14 +452,13 @@ static ERL_NIF_TERM nif_get_multi(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     uint64_t *cb = enif_alloc(8 * ((size_t)p.n + 1));
     uint64_t *vo = enif_alloc(8 * ((size_t)p.n + 2));
     uint64_t cap = 64 * ((uint64_t)p.n + 16);
-    uint8_t *vout = NULL;
-    int rc = ST_EINVAL;
-    for (int attempt = 0; attempt < 16; attempt++, cap *= 2) {
+    uint8_t *vout = enif_alloc((size_t)cap);
+    int rc = vout ? st_get1_multi(ts, p.n, p.kt, p.kh, p.ko, vout, cap, vo, st, cl, cb) : ST_ENOMEM;
+    if (rc == ST_ERANGE) {   /* a concurrent put may grow a value again: at most one more try */
+        cap = vo[p.n] + vo[p.n] / 4 + 64;
         enif_free(vout);
         vout = enif_alloc((size_t)cap);
-        if (!vout) break;
-        rc = st_get1_multi(ts, p.n, p.kt, p.kh, p.ko, vout, cap, vo, st, cl, cb);
-        if (rc != ST_EINVAL || !strstr(st_last_error(), "too small")) break;
+        rc = vout ? st_get1_multi(ts, p.n, p.kt, p.kh, p.ko, vout, cap, vo, st, cl, cb) : ST_ENOMEM;
     }
     ERL_NIF_TERM res;
     if (rc < 0) {

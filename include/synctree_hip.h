@@ -61,6 +61,7 @@ extern "C" {
 #define ST_EINVAL (-1)   /* bad argument / geometry (reference: crash) */
 #define ST_EDEVICE (-2)  /* HIP runtime error */
 #define ST_ENOMEM (-3)
+#define ST_ERANGE (-4)   /* output buffer too small: the size needed is in the call's size out-param */
 
 #define ST_KEY_INT 0
 #define ST_KEY_ATOM 1
@@ -276,7 +277,9 @@ int st_insert1(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint32_t klen, 
  * ONE device launch (a workgroup per tree, <= 16 keys per tree a launch;
  * more keys: further launches).  Per-request outputs as st_insert1 /
  * st_get1; get values packed in request order into vout with
- * voff_out[n+1] (ST_EINVAL if vcap is too small).  Trees on one device. */
+ * voff_out[n+1].  If vcap is too small: ST_ERANGE with nothing copied and
+ * voff_out[n] = the bytes needed (the reads happened: retry with that
+ * capacity).  Trees on one device. */
 int st_insert1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,
                      const uint8_t *vheap, const uint64_t *voff, int32_t *status, uint32_t *clevel, uint64_t *cbucket);
 int st_get1_multi(st_tree **trees, uint32_t n, const uint8_t *ktype, const uint8_t *kheap, const uint64_t *koff,

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('ST_LIB') or os.path.join(_HERE, 'libsynctree_hip.so')
 
 ST_OK, ST_NOTFOUND, ST_CORRUPTED = 0, 1, 2
-ST_EINVAL, ST_EDEVICE, ST_ENOMEM = -1, -2, -3
+ST_EINVAL, ST_EDEVICE, ST_ENOMEM, ST_ERANGE = -1, -2, -3, -4
 ST_KEY_INT, ST_KEY_ATOM, ST_KEY_BINARY, ST_KEY_TERM = 0, 1, 2, 3
 ST_FILTER_ALL, ST_FILTER_LOCAL_ONLY, ST_FILTER_REMOTE_ONLY = 0, 1, 2
 ST_DIFF_BOTH, ST_DIFF_LOCAL_ONLY, ST_DIFF_REMOTE_ONLY = 0, 1, 2
@@ -146,6 +146,6 @@ def check(rc, what=''):
     if rc in (ST_OK, ST_NOTFOUND, ST_CORRUPTED):
         return rc
     msg = '%s failed (%d): %s' % (what, rc, last_error())
-    if rc == ST_EINVAL:
+    if rc in (ST_EINVAL, ST_ERANGE):
         raise ValueError(msg)
     raise DeviceError(msg)

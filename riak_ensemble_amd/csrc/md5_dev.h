@@ -284,40 +284,6 @@ __device__ __forceinline__ void md5_lds_node(const uint8_t *p, uint32_t len, uin
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
 
-// md5_lds_node with the block loop rolled (one compression body in the
-// code, ~1/5 of the unrolled form's instruction bytes): for chains that run
-// once per launch, where the unrolled form's first pass is instruction-fetch
-// bound.  Lanes with fewer blocks keep their state (select, not a branch).
-__device__ __forceinline__ void md5_lds_node_rolled(const uint8_t *p, uint32_t len, uint32_t out[4]) {
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
-    const uint32_t nblk = (len + 8) / 64 + 1;
-    const uint32_t kmax = __builtin_amdgcn_readfirstlane(nblk) | 0u;
-    uint32_t nmax = nblk;
-    for (int o = 32; o; o >>= 1) { const uint32_t x = __shfl_xor(nmax, o); nmax = x > nmax ? x : nmax; }
-    nmax = __builtin_amdgcn_readfirstlane(nmax);
-    (void)kmax;
-    uint32_t st[4];
-    init(st);
-    uint32_t nx[16];
-#pragma unroll
-    for (int w = 0; w < 16; w++) nx[w] = q[w];
-#pragma unroll 1
-    for (uint32_t k = 0; k < nmax; k++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int w = 0; w < 16; w++) m[w] = nx[w];
-        if (k + 1 < nmax) {
-#pragma unroll
-            for (int w = 0; w < 16; w++) nx[w] = q[16 * (k + 1) + w];
-        }
-        const int32_t rem = (int32_t)len - 64 * (int32_t)k;
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        uint32_t t4[4] = {st[0], st[1], st[2], st[3]};
-        compress(t4, m);
-        if (k < nblk) { st[0] = t4[0]; st[1] = t4[1]; st[2] = t4[2]; st[3] = t4[3]; }
-    }
-    out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
-}
 
 // The state after the first nfull (complete) blocks of an LDS message: the
 // prefix a later md5_lds_resume continues from.

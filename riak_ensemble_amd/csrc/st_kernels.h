@@ -1284,7 +1284,6 @@ struct CmpWalk {
     DiffRec *scratch;
     uint64_t rb, lim, pos, bytes;
     int filter;
-    bool stage_pair;       // the staged first pair of a short list (CMP_FM_*)
     uint64_t errmin;       // this lane's first failed verification (err_code), ~0 if none
     uint64_t *stamp;       // diagnostic: this wave's 8 phase stamps, or null
 };
@@ -1297,15 +1296,6 @@ struct CmpWalk {
 // wave, coalesced) -- is staged in the shared LDS area first, so every lane
 // runs the same md5_lds chain; runs that do not fit are hashed from global
 // memory.
-// The first listed segment pair's merge-join staged alongside the
-// verification (cmp_flush, a list of <= 32 items): its key and value offsets
-// load with the value runs, its key bytes load into registers before the MD5
-// chains and land in LDS after them, and its values are the runs the
-// verification staged -- so its merge-join waits on no memory of its own.
-// Pairs of <= 63 entries and <= CMP_FM_KB key bytes a side.
-#define CMP_FM_N 63
-#define CMP_FM_KB 1024
-#define CMP_FMB (4 * 256 + 512 + 2 * 1024 + 2 * (CMP_FM_KB + 16))   // offsets, union slots, prefixes, key bytes
 
 __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, CmpWalk &c, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1315,14 +1305,6 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
     // the first 32 items' segment bounds (lane 2i: item i's local side, 2i + 1
     // its remote side), kept for the merge-joins (no second round trip)
     uint64_t kv0 = 0, kvl = 0, ks0 = 0, ks1 = 0;
-    // the staged first pair (CMP_FM_*): wave-uniform state
-    bool fm = false;
-    uint32_t fj = 0, fnA = 0, fnB = 0, fkbA = 0, fkbB = 0, fsoA = 0, fsoB = 0;
-    uint8_t *FM = c.shared + SH0 - CMP_FMB;
-    uint32_t *fao = reinterpret_cast<uint32_t *>(FM), *fbo = fao + 64, *favo = fbo + 64, *fbvo = favo + 64;
-    uint32_t *fur = fbvo + 64;
-    uint4 *fpa = reinterpret_cast<uint4 *>(fur + 128), *fpb = fpa + 64;
-    uint8_t *fak = reinterpret_cast<uint8_t *>(fpb + 64), *fbk = fak + CMP_FM_KB + 16;
     for (uint32_t k0 = 0; k0 < 2 * n; k0 += 64) {
         const uint32_t k = k0 + lane;
         const bool act = k < 2 * n;
@@ -1352,24 +1334,7 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         uint32_t mlen = 0;
         if (inner) mlen = side ? stage_inner(B, l, b, c.shared + ioff) : stage_inner(A, l, b, c.shared + ioff);
         CW_STAMP(c, 9);
-        // the first segment pair of a short list: its key and value offsets,
-        // loaded with the value runs below (registers until the runs land)
-        uint64_t fka = 0, fva = 0, fkb = 0, fvb = 0;
-        if (k0 == 0 && n <= 32 && c.stage_pair) {
-            const uint64_t sm = __ballot(seg && side == 0);
-            if (sm) {
-                fj = (uint32_t)(__ffsll((long long)sm) - 1);   // lane of its local side; fj + 1 its remote side
-                const uint64_t a0 = __shfl(ks0, fj, 64), b0 = __shfl(ks0, fj + 1, 64);
-                fnA = (uint32_t)(__shfl(ks1, fj, 64) - a0);
-                fnB = (uint32_t)(__shfl(ks1, fj + 1, 64) - b0);
-                fm = fnA <= CMP_FM_N && fnB <= CMP_FM_N && itot + CMP_FMB <= SH0;   // the inner regions stay below the pair's area
-                if (fm) {
-                    if (lane <= fnA) { fka = A.koff[a0 + lane]; fva = A.voff[a0 + lane]; }
-                    if (lane <= fnB) { fkb = B.koff[b0 + lane]; fvb = B.voff[b0 + lane]; }
-                }
-            }
-        }
-        const uint32_t SH = fm ? SH0 - CMP_FMB : SH0;   // the staging area below the pair's
+        const uint32_t SH = SH0;
         const uint32_t ssz = seg ? (uint32_t)(len + 64 + 15 < SH ? ((len + 64 + 15) & ~15ull) : SH + 16) : 0;
         const uint32_t soff = itot + wave_excl_scan(ssz);
         const bool sfit = seg && (et & TAG_PRESENT) && soff + ssz <= SH;
@@ -1390,37 +1355,6 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
             wave_copy4(sp[0], ln[0], dp[0], sp[1], ln[1], dp[1], sp[2], ln[2], dp[2], sp[3], ln[3], dp[3]);
         }
         CW_STAMP(c, 10);
-        // the staged pair: offsets to LDS (relative), key bytes into registers
-        // (their loads stay in flight under the MD5 chains below)
-        uint32_t fx[2][5] = {{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}};
-        uint32_t fmis[2] = {0, 0};
-        if (fm) {
-            const bool stA = __shfl((int)sfit, fj, 64) != 0, stB = __shfl((int)sfit, fj + 1, 64) != 0;
-            const uint64_t ka0 = __shfl(fka, 0, 64), kb0 = __shfl(fkb, 0, 64);
-            fkbA = (uint32_t)(__shfl(fka, fnA, 64) - ka0);
-            fkbB = (uint32_t)(__shfl(fkb, fnB, 64) - kb0);
-            fm = (stA || fnA == 0) && (stB || fnB == 0) && fkbA <= CMP_FM_KB && fkbB <= CMP_FM_KB;
-            if (fm) {
-                fsoA = __shfl(soff, fj, 64);
-                fsoB = __shfl(soff, fj + 1, 64);
-                const uint64_t va0 = __shfl(kv0, fj, 64), vb0 = __shfl(kv0, fj + 1, 64);
-                if (lane <= fnA) { fao[lane] = (uint32_t)(fka - ka0); favo[lane] = (uint32_t)(fva - va0); }
-                if (lane <= fnB) { fbo[lane] = (uint32_t)(fkb - kb0); fbvo[lane] = (uint32_t)(fvb - vb0); }
-                const uint8_t *kp[2] = {A.kheap + ka0, B.kheap + kb0};
-                const uint32_t kn[2] = {fkbA, fkbB};
-#pragma unroll
-                for (int r = 0; r < 2; r++) {
-                    const uintptr_t a = reinterpret_cast<uintptr_t>(kp[r]);
-                    fmis[r] = (uint32_t)(a & 3);
-                    const uint32_t *w = reinterpret_cast<const uint32_t *>(a - fmis[r]);
-#pragma unroll
-                    for (int u = 0; u < 5; u++) {
-                        const uint32_t idx = u * 64 + lane;
-                        fx[r][u] = (4 * idx < kn[r] + fmis[r]) ? w[idx] : 0u;
-                    }
-                }
-            }
-        }
         wave_sync_lds();
         CW_STAMP(c, 7);
         if (act) {
@@ -1440,37 +1374,9 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
                 if (ec < c.errmin) c.errmin = ec;
             }
         }
-        if (fm && k0 == 0) {   // the staged pair's key bytes land
-            uint8_t *kd[2] = {fak, fbk};
-            const uint32_t kn[2] = {fkbA, fkbB};
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-#pragma unroll
-                for (int u = 0; u < 5; u++) {
-                    const uint32_t idx = u * 64 + lane;
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int p = (int)(4 * idx + q) - (int)fmis[r];
-                        if (p >= 0 && (uint32_t)p < kn[r]) kd[r][p] = (uint8_t)(fx[r][u] >> (8 * q));
-                    }
-                }
-            }
-        }
         wave_sync_lds();
     }
     CW_STAMP(c, 3);
-    uint64_t fmask = 0;   // the staged pair's item, skipped by the loop below
-    if (fm) {
-        const uint64_t it = c.list[fj >> 1];
-        const uint64_t s = it & ((1ull << 56) - 1);
-        const uint64_t a0 = __shfl(ks0, fj, 64), b0 = __shfl(ks0, fj + 1, 64);
-        const uint64_t vA = __shfl(kvl, fj, 64), vB = __shfl(kvl, fj + 1, 64);
-        c.pos += lds_merge_pair(A, B, s, c.filter, a0, b0, fnA, fnB, fao, fbo, favo, fbvo, fak, fbk, c.shared + fsoA,
-                                c.shared + fsoB, true, fur, fpa, fpb, c.scratch, c.rb + c.pos, c.lim);
-        c.bytes += 2 * (16 + 16 + 18) + 16 * (uint64_t)(fnA + fnB + 2) + vA + vB + fkbA + fkbB;
-        fmask = 1ull << (fj >> 1);
-        wave_sync_lds();
-    }
     // the listed segments' CSR bounds, 64 per round trip (lane i: the i-th
     // item), handed to each merge-join by shuffles in list order
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
@@ -1488,7 +1394,7 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         } else if (sg) {
             p = seg_pair(A, B, sj);
         }
-        for (uint64_t m = __ballot(sg) & (i0 == 0 ? ~fmask : ~0ull); m; m &= m - 1) {
+        for (uint64_t m = __ballot(sg); m; m &= m - 1) {
             const int j = __ffsll((long long)m) - 1;
             uint64_t by;
             c.pos += seg_merge_wave(A, B, __shfl(sj, j, 64), shfl_pair(p, j), c.filter, c.shared, c.scratch, c.rb + c.pos,
@@ -1511,8 +1417,7 @@ __device__ __forceinline__ void cmp_append(uint64_t *list, uint32_t &n, bool f, 
 
 __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2, uint32_t nw,
                                                  uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *wcnt,
-                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps,
-                                                 uint32_t opts) {
+                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t w = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -1531,7 +1436,6 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
     c.pos = 0;
     c.bytes = 0;
     c.filter = filter;
-    c.stage_pair = (opts & 1u) != 0;
     c.errmin = ~0ull;
     for (uint32_t l = lane; l < ST_STATW; l += 64) c.cnt[l] = 0;
     const uint64_t nH = A.base[L1] - A.base[H];   // level-H nodes

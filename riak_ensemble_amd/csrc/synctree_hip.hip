@@ -486,9 +486,13 @@ struct TimedLaunch {
     }
 };
 
+// Every launch leaves work on the tree's stream that the call may not wait
+// for: async_pending tells a launch on ANOTHER stream over this tree
+// (k_small_multi) to synchronise it first; tsync clears it.
 #define LAUNCH(t, name, kern, grid, block, shmem, ...)                            \
     do {                                                                          \
         TimedLaunch tl_(t, name);                                                 \
+        (t)->async_pending = true;                                                \
         hipLaunchKernelGGL(kern, dim3(grid), dim3(block), shmem, (t)->stream, __VA_ARGS__); \
         hipError_t e_ = hipGetLastError();                                        \
         if (e_ != hipSuccess) {                                                   \
@@ -1713,6 +1717,11 @@ static int small_prepare(st_tree *t, int op, uint64_t n, const HostRecords &hr, 
     if (n == 0 || n > SB_MAX || kbytes > SB_KB || vbytes > SB_VB || t->W > 32 || t->partitioned ||
         small_lds_bytes((uint32_t)t->W) > 160 * 1024)
         return ST_OK;
+    // a launch the tree did not wait for (st_rehash returns before its
+    // kernel ends): its device error must be seen before k_small reads the
+    // upper levels it wrote (st_rehash's error is reported by the next call
+    // that waits, and that is this one)
+    if (t->async_pending) CHK(tsync(t));
     CHK(flush_delta(t));   // k_small reads the base CSR
     CHK(ensure_small(t));
     if (++t->small_seq == 0) t->small_seq = 1;
@@ -1792,6 +1801,8 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
         fprintf(stderr, "\n");
         memset((void *)t->sout->stamp, 0, sizeof(t->sout->stamp));
     }
+    // the results came after every earlier launch on the stream (stream order)
+    t->async_pending = false;
     if (t->sres.retry) return ST_OK;
     *served = 1;
     small_served(t, op);
@@ -1987,11 +1998,17 @@ static int small_multi(int op, st_tree **trees, uint32_t n, const uint8_t *ktype
         }
     }
     if (op == 0) {   // the values, packed in request order
+        uint64_t need = 0;
+        for (uint32_t i = 0; i < n; i++) need += status[i] == ST_OK ? vals[i].size() : 0;
+        if (need > vcap) {
+            voff_out[n] = need;
+            g_err = "value buffer too small (" + std::to_string(need) + " bytes needed)";
+            return ST_ERANGE;
+        }
         uint64_t o = 0;
         voff_out[0] = 0;
         for (uint32_t i = 0; i < n; i++) {
             const uint64_t l = status[i] == ST_OK ? vals[i].size() : 0;
-            if (o + l > vcap) { g_err = "value buffer too small"; voff_out[i + 1] = o + l; return ST_EINVAL; }
             if (l) memcpy(vout + o, vals[i].data(), l);
             o += l;
             voff_out[i + 1] = o;
@@ -2992,11 +3009,8 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 128, t->stream));
         }
         A->reads_remote = true;   // until the gather's completion word is seen
-        // ST_CMP_STAGED=1: the first pair of a short list merge-joined from the
-        // verification's staging (st_kernels.h CMP_FM_*; A/B knob, off by default)
-        static const uint32_t opts = getenv("ST_CMP_STAGED") && atoi(getenv("ST_CMP_STAGED")) ? 1u : 0u;
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
-               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps, opts);
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 16);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));

@@ -499,8 +499,13 @@ def get1_multi(trees, keys, vcap=1 << 20):
     st = np.zeros(n, np.int32)
     cl = np.zeros(n, np.uint32)
     cb = np.zeros(n, np.uint64)
-    _lib.check(L.st_get1_multi(arr, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vout), vcap, _ptr(vo), _ptr(st), _ptr(cl),
-                               _ptr(cb)), 'st_get1_multi')
+    rc = L.st_get1_multi(arr, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vout), vcap, _ptr(vo), _ptr(st), _ptr(cl), _ptr(cb))
+    if rc == _lib.ST_ERANGE:   # too small: the call reported the bytes needed in vo[n]
+        vcap = int(vo[n])
+        vout = np.zeros(max(vcap, 1), np.uint8)
+        rc = L.st_get1_multi(arr, n, _ptr(kt), _ptr(kh), _ptr(ko), _ptr(vout), vcap, _ptr(vo), _ptr(st), _ptr(cl),
+                             _ptr(cb))
+    _lib.check(rc, 'st_get1_multi')
     out = []
     for i in range(n):
         if st[i] == _lib.ST_OK:

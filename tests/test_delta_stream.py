@@ -107,16 +107,21 @@ def test_variable_keys_and_values_through_delta():
     dev.close()
 
 
-def test_corrupted_segment_rejects_streamed_keys():
+@pytest.mark.parametrize('delta', [True, False], ids=['delta', 'default_merge'])
+def test_corrupted_segment_rejects_streamed_keys(delta):
     """A corrupted segment (corrupt/2, synctree.erl:241-247) met by a streamed
-    batch: its keys are refused with {corrupted, Level, Bucket} and the rest go
-    to the delta, as sequential insert/3 calls would do."""
+    batch: its keys are refused with {corrupted, Level, Bucket} and the rest
+    are inserted, as sequential insert/3 calls would do.  With the delta
+    enabled (ST_DBG_DELTA_LIMIT 0 = auto limit) the batch lands in the delta;
+    with the default merge (delta off) nothing does."""
     S, n0 = 1 << 16, 200_000
     keys = workload.keys_int63(n0 + 5000, workload.SEED ^ 0xC0)
     vals = _obj(range(n0 + 5000))
     dev, ora = synctree_hip.DeviceTree(16, S), C.OTree(16, S)
     assert dev.insert_int64(keys[:n0], vals[:n0]) == 0
     ora.bulk_load_int64(keys[:n0], vals[:n0])
+    if delta:
+        dev.debug_knob(_lib.ST_DBG_DELTA_LIMIT, 0)
     # one streamed batch first (the delta holds entries), then corrupt a key's segment
     assert dev.insert_int64(keys[n0:n0 + 2000], vals[n0:n0 + 2000]) == 0
     ora.insert_int64_seq(keys[n0:n0 + 2000], vals[n0:n0 + 2000])
@@ -134,7 +139,10 @@ def test_corrupted_segment_rejects_streamed_keys():
         exp.append(None if r is ora else r)
     assert any(e is not None for e in exp)
     assert dev.insert_batch(bk, bv) == exp
-    assert dev.delta_stats()[0] > 0                           # the streamed batch went to the delta
+    if delta:
+        assert dev.delta_stats()[0] > 0                       # the streamed batch went to the delta
+    else:
+        assert dev.delta_stats()[0] == 0                      # default: merged into the base
     assert dev.top_hash() == ora.top_hash()
     _levels(dev, ora)
     assert dev.get_batch(bk[:50]) == [ora.get(k) for k in bk[:50]]

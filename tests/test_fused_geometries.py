@@ -92,6 +92,15 @@ def test_mailbox_timeout_is_a_device_error(segments, skip):
         dev.top_hash()                # no top hash from a tree in error
     with pytest.raises(_lib.DeviceError):
         dev.level_entries(2)
+    # the per-key path right after a faulted rehash: k_small must not read
+    # the invalid upper levels (get/2, insert/3 report the device error)
+    probe = int(workload.keys_int63(1, workload.SEED ^ 0xB0B ^ segments)[0])
+    for op in (lambda: dev.get1(probe), lambda: dev.insert1(probe, b'x' * 17)):
+        dev.rehash()
+        with pytest.raises(_lib.DeviceError):
+            op()
+        with pytest.raises(_lib.DeviceError):
+            dev.get1(probe)           # and the tree stays in error
     dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, -1)
     dev.rehash()                      # a clean full rehash clears the error
     dev.sync()

@@ -227,8 +227,10 @@ def test_per_key_requests_of_many_trees_in_one_launch():
             assert exp[-1] is not None and exp[-1][0] == 'corrupted'
         probe_t = [int(x) for x in rng.integers(0, T, 200)]
         probe_k = [keys[t][int(rng.integers(0, len(keys[t])))] for t in probe_t]
-        assert synctree_hip.get1_multi([devs[t] for t in probe_t], probe_k) == \
-            [oras[t].get(k) for t, k in zip(probe_t, probe_k)], r
+        want = [oras[t].get(k) for t, k in zip(probe_t, probe_k)]
+        assert synctree_hip.get1_multi([devs[t] for t in probe_t], probe_k) == want, r
+        if r == 0:   # a value buffer too small: ST_ERANGE reports the size, the retry gets it all
+            assert synctree_hip.get1_multi([devs[t] for t in probe_t], probe_k, vcap=16) == want
         for t in range(T):
             assert devs[t].top_hash() == oras[t].top_hash(), (r, t)
     for d in devs:
