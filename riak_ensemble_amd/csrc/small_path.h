@@ -67,7 +67,7 @@ struct SmallRes {
 struct SmallOut {
     uint4 hdr;
     uint4 rec[SB_MAX];
-    uint64_t stamp[8];         // diagnostic phase stamps (100 MHz), in.dbg only; read after a stream sync
+    uint64_t stamp[16];        // diagnostic phase stamps, in.dbg only, read after a stream sync: [k] wall (100 MHz), [8 + k] shader clock
     uint8_t vbytes[SB_OUT_VB]; // get: key i's value at the sum of the earlier keys' vlen
 };
 
@@ -125,7 +125,7 @@ __device__ __forceinline__ uint64_t record_segment(const uint8_t *p, uint64_t le
         for (int w = 3; w < 16; w++) m[w] = 0u;
         m[14] = 64u;
         stmd5::init(d);
-        stmd5::compress(d, m);
+        stmd5::compress_lat(d, m);
     } else {
         const uint8_t *sp;
         uint64_t sl;
@@ -223,8 +223,8 @@ __host__ __device__ __forceinline__ uint32_t small_lds_bytes(uint32_t W) {
 // the path's slot entries committed; a corrupted path commits nothing
 // ({corrupted, L, B}, :193-194); the overlay space of the discarded record is
 // reclaimed at the next flush.
-#define SB_STAMP(k) do { if (in.dbg && threadIdx.x == 0) out->stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define SB_STAMPW(k) do { if (in.dbg && (threadIdx.x & 63) == 0) out->stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SB_STAMP(k) do { if (in.dbg && threadIdx.x == 0) { out->stamp[k] = __builtin_amdgcn_s_memrealtime(); out->stamp[8 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define SB_STAMPW(k) do { if (in.dbg && (threadIdx.x & 63) == 0) { out->stamp[k] = __builtin_amdgcn_s_memrealtime(); out->stamp[8 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
 #define S1_VBUF 4096   // value bytes of a segment hashed from LDS (larger: bulk path)
 #define S1_PATH 192    // path child entries (H x W <= 192 for W <= 32, S <= 2^31)
 // LDS flags between the waves of the one-key insert (workgroup scope)
@@ -279,7 +279,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
             else good = verify_inner_node(t, l, s >> (t.shift * (L1 - l)), dyn + lane * lane_region_bytes(W));
             if (!good) atomicMin(&bad[0], l);
         }
-        if (lane == 0 && in.dbg) out->stamp[2] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && in.dbg) { out->stamp[2] = __builtin_amdgcn_s_memrealtime(); out->stamp[10] = __builtin_amdgcn_s_memtime(); }
     } else if (wave == 1) {
         // path nodes' child entries (level l node b_l, children base[l+1] +
         // b_l*W + j); lanes 1..H: level `lane`'s node message with the path
@@ -384,7 +384,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
             wave_sync_lds();
         }
         if (lane == 0) lds_flag_set(&s1_plan_ready);
-        if (lane == 0 && in.dbg) out->stamp[3] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && in.dbg) { out->stamp[3] = __builtin_amdgcn_s_memrealtime(); out->stamp[11] = __builtin_amdgcn_s_memtime(); }
         if (!s1_retry && lane == 0) {
             uint32_t d[4];
             stmd5::md5_lds(vbuf, s1_vb, d);   // the new segment hash
@@ -402,7 +402,7 @@ __device__ __forceinline__ void small_insert_one(const DevTree &t, const Overlay
                 e = make_uint4(d[0], d[1], d[2], d[3]);
                 s1_new[l] = e;
             }
-            if (in.dbg) out->stamp[4] = __builtin_amdgcn_s_memrealtime();
+            if (in.dbg) { out->stamp[4] = __builtin_amdgcn_s_memrealtime(); out->stamp[12] = __builtin_amdgcn_s_memtime(); }
         }
     } else {
         // wave 3: the segment's new overlay record (header, offset tables,

@@ -1784,6 +1784,11 @@ static int small_call(st_tree *t, int op, uint64_t n, const HostRecords &hr, con
         fprintf(stderr, "small op=%d n=%llu:", op, (unsigned long long)n);
         for (int k = 1; k < 8; k++)
             if (st[k]) fprintf(stderr, " %d:%.2f", k, (st[k] - st[0]) / 100.0);
+        // the shader clock over the kernel: cycles / wall between stamp 0 and the last
+        int kl = 0;
+        for (int k = 1; k < 8; k++)
+            if (st[k] && st[8 + k]) kl = k;
+        if (kl && st[kl] > st[0]) fprintf(stderr, " | %.2f GHz", (double)(st[8 + kl] - st[8]) / ((st[kl] - st[0]) * 10.0));
         fprintf(stderr, "\n");
         memset((void *)t->sout->stamp, 0, sizeof(t->sout->stamp));
     }

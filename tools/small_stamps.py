@@ -16,3 +16,16 @@ for k in keys[:5]:
     t.get_batch([int(k)])
 for k in keys[:5]:
     t.insert_batch([int(k)], [bytes(17)])
+# the clock an insert finds: after 100 ms idle, and right behind a 10M-key-class
+# load of work (20 rehashes of this tree queued just before)
+import time
+import sys as _s
+for label in ('idle', 'busy'):
+    for k in keys[5:10]:
+        if label == 'idle':
+            time.sleep(0.1)
+        else:
+            for _ in range(20):
+                t.rehash()
+        print('--- %s' % label, file=_s.stderr, flush=True)
+        t.insert_batch([int(k)], [bytes(17)])
