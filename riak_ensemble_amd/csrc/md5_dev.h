@@ -132,6 +132,35 @@ __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
+// The latency form as ONE out-of-line copy per kernel (STMD5_NOINLINE, the
+// default): the per-key and compare kernels run their MD5 chains once per
+// launch on a cold instruction cache, and every inlined compression is ~2.5 KB
+// of code (k_small carried 11 copies, k_cmp_walk 8).  Twenty scalar arguments
+// and a four-word result stay in registers (the AMDGPU calling convention
+// passes up to 32 VGPR arguments); the call costs ~30 instructions a block.
+struct St4 { uint32_t a, b, c, d; };
+__device__ __noinline__ St4 compress_ool(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t m0, uint32_t m1,
+                                         uint32_t m2, uint32_t m3, uint32_t m4, uint32_t m5, uint32_t m6, uint32_t m7,
+                                         uint32_t m8, uint32_t m9, uint32_t m10, uint32_t m11, uint32_t m12,
+                                         uint32_t m13, uint32_t m14, uint32_t m15) {
+    uint32_t st[4] = {a, b, c, d};
+    const uint32_t m[16] = {m0, m1, m2, m3, m4, m5, m6, m7, m8, m9, m10, m11, m12, m13, m14, m15};
+    compress(st, m);
+    return St4{st[0], st[1], st[2], st[3]};
+}
+#ifndef STMD5_NOINLINE
+#define STMD5_NOINLINE 1
+#endif
+__device__ __forceinline__ void compress_lat(uint32_t st[4], const uint32_t m[16]) {
+#if STMD5_NOINLINE
+    const St4 r = compress_ool(st[0], st[1], st[2], st[3], m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], m[10],
+                               m[11], m[12], m[13], m[14], m[15]);
+    st[0] = r.a; st[1] = r.b; st[2] = r.c; st[3] = r.d;
+#else
+    compress(st, m);
+#endif
+}
+
 // Keep the `valid` leading bytes of little-endian word w (0..4 valid), put
 // the 0x80 terminator right after them when they end inside this word.
 // Branch-free (selects only): lanes of a wave hold messages of different
@@ -156,6 +185,33 @@ __device__ __forceinline__ void pad_block(uint32_t m[16], int64_t rem, bool last
         m[14] = (uint32_t)(len << 3);
         m[15] = (uint32_t)(len >> 29);
     }
+}
+
+// compress_lat with the MD5 padding of block k of a `len`-byte message applied
+// first (rem = len - 64k; a no-op for rem >= 64): the padding's selects live
+// in the one out-of-line copy too.
+__device__ __noinline__ St4 compress_pad_ool(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t m0, uint32_t m1,
+                                             uint32_t m2, uint32_t m3, uint32_t m4, uint32_t m5, uint32_t m6, uint32_t m7,
+                                             uint32_t m8, uint32_t m9, uint32_t m10, uint32_t m11, uint32_t m12,
+                                             uint32_t m13, uint32_t m14, uint32_t m15, int32_t rem, uint32_t last,
+                                             uint32_t len_lo, uint32_t len_hi) {
+    uint32_t st[4] = {a, b, c, d};
+    uint32_t m[16] = {m0, m1, m2, m3, m4, m5, m6, m7, m8, m9, m10, m11, m12, m13, m14, m15};
+    if (rem < 64) pad_block(m, rem, last != 0, ((uint64_t)len_hi << 32) | len_lo);
+    compress(st, m);
+    return St4{st[0], st[1], st[2], st[3]};
+}
+__device__ __forceinline__ void compress_pad_lat(uint32_t st[4], uint32_t m[16], int64_t rem, bool last, uint64_t len) {
+#if STMD5_NOINLINE
+    const int32_t r = rem > 64 ? 64 : (int32_t)rem;
+    const St4 x = compress_pad_ool(st[0], st[1], st[2], st[3], m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9],
+                                   m[10], m[11], m[12], m[13], m[14], m[15], r, last ? 1u : 0u, (uint32_t)len,
+                                   (uint32_t)(len >> 32));
+    st[0] = x.a; st[1] = x.b; st[2] = x.c; st[3] = x.d;
+#else
+    if (rem < 64) pad_block(m, rem, last, len);
+    compress(st, m);
+#endif
 }
 
 __device__ __forceinline__ void load_block_global(const uint8_t *p, uint32_t m[16]) {
@@ -187,7 +243,7 @@ __device__ __forceinline__ void md5_global(const uint8_t *p, uint64_t len, uint3
             }
             pad_block(m, rem, k + 1 == nblk, len);
         }
-        compress(st, m);
+        compress_lat(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
@@ -210,8 +266,12 @@ __device__ __forceinline__ void md5_global_pf(const uint8_t *p, uint64_t len, ui
         for (int w = 0; w < 16; w++) m[w] = nx[w];
         const int64_t rem = (int64_t)len - (int64_t)(64 * k);
         if (rem - 64 > 0) load_block_global(p + 64 * (k + 1), nx);
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        compress<TPUT>(st, m);
+        if (TPUT) {
+            if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
+            compress<true>(st, m);
+        } else {
+            compress_pad_lat(st, m, rem, k + 1 == nblk, len);
+        }
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
@@ -237,8 +297,7 @@ __device__ __forceinline__ void md5_lds(const uint8_t *p, uint32_t len, uint32_t
 #pragma unroll
             for (int w = 0; w < 16; w++) nx[w] = pw[16 * (k + 1) + w];
         }
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        compress(st, m);
+        compress_pad_lat(st, m, rem, k + 1 == nblk, len);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
@@ -294,7 +353,7 @@ __device__ __forceinline__ void md5_lds_prefix(const uint8_t *p, uint32_t nfull,
         uint32_t m[16];
 #pragma unroll
         for (int w = 0; w < 16; w++) m[w] = pw[16 * k + w];
-        compress(st, m);
+        compress_lat(st, m);
     }
 }
 
@@ -310,8 +369,7 @@ __device__ __forceinline__ void md5_lds_resume(const uint8_t *p, uint32_t len, u
 #pragma unroll
         for (int w = 0; w < 16; w++) m[w] = pw[16 * k + w];
         const int32_t rem = (int32_t)len - (int32_t)(64 * k);
-        if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
-        compress(st, m);
+        compress_pad_lat(st, m, rem, k + 1 == nblk, len);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
@@ -406,7 +464,7 @@ __device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[
     for (int k = 0; k < 5; k++) {
         uint32_t m[16];
         node16_block(k, pf, h, m, n);
-        compress(st, m);
+        compress_lat(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }

@@ -125,7 +125,7 @@ __device__ __forceinline__ uint64_t record_segment(const uint8_t *p, uint64_t le
         for (int w = 3; w < 16; w++) m[w] = 0u;
         m[14] = 64u;
         stmd5::init(d);
-        stmd5::compress(d, m);
+        stmd5::compress_lat(d, m);
     } else {
         const uint8_t *sp;
         uint64_t sl;

@@ -427,8 +427,7 @@ struct MsgWriter {
 // trip per 16 children, not one per child).
 __device__ __forceinline__ uint32_t stage_inner(const DevTree &t, uint32_t l, uint64_t b, uint8_t *reg) {
     const uint64_t c0 = t.base[l + 1] + b * t.W;
-    MsgWriter mw;
-    mw.init(reg);
+    uint32_t len = 0;
     for (uint32_t j0 = 0; j0 < t.W; j0 += 16) {
         uint32_t tg[16];
         uint4 h[16];
@@ -447,11 +446,23 @@ __device__ __forceinline__ uint32_t stage_inner(const DevTree &t, uint32_t l, ui
             for (int j = 0; j < 16; j++) m16.entry(tg[j], h[j]);
             return m16.finish();
         }
+        // some child absent: each present entry at 17 x its rank, byte stores
+        // (compact code: these kernels run it once per launch, cold)
+        uint32_t pres = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) pres |= (tg[j] & TAG_PRESENT) ? (1u << j) : 0u;
 #pragma unroll
         for (int j = 0; j < 16; j++)
-            if (tg[j] & TAG_PRESENT) mw.entry(tg[j], h[j]);
+            if ((pres >> j) & 1u) {
+                uint8_t *q = reg + len + 17u * (uint32_t)__builtin_popcount(pres & ((1u << j) - 1u));
+                const uint32_t w4[4] = {h[j].x, h[j].y, h[j].z, h[j].w};
+                q[0] = (uint8_t)tg[j];
+#pragma unroll
+                for (int x = 0; x < 16; x++) q[1 + x] = (uint8_t)(w4[x >> 2] >> (8 * (x & 3)));
+            }
+        len += 17u * (uint32_t)__builtin_popcount(pres);
     }
-    return mw.finish();
+    return len;
 }
 
 // Bytes of LDS per lane for inner-node staging (odd dword stride).
@@ -988,11 +999,14 @@ __device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
     return (uint32_t)__popcll(bal & ((1ull << lane) - 1));
 }
 
-// Wave-cooperative copy of up to 4 byte runs from global memory into LDS:
-// dword loads (the run's first word aligned down; heaps keep >= 64 bytes of
-// slack past their end), every load of an iteration in flight together, so
-// runs up to 1 KB cost one memory round trip.
-__device__ __forceinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t *d0, const uint8_t *s1, uint32_t n1,
+// Wave-cooperative copy of up to 4 byte runs from global memory into LDS
+// (destinations 4-byte aligned): a lane per destination dword, the two source
+// dwords it straddles loaded (the run's first word aligned down; nothing read
+// past the run's last dword) and joined with one v_alignbyte, one ds_write_b32
+// per dword (byte stores only for a run's last partial dword).  Every load of
+// an iteration is in flight together, so runs up to 1 KB cost one memory
+// round trip.  One out-of-line copy per kernel (instruction-cache footprint).
+__device__ __noinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t *d0, const uint8_t *s1, uint32_t n1,
                                            uint8_t *d1, const uint8_t *s2, uint32_t n2, uint8_t *d2, const uint8_t *s3,
                                            uint32_t n3, uint8_t *d3) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1002,8 +1016,8 @@ __device__ __forceinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8
     uint32_t mx = n0 > n1 ? n0 : n1;
     mx = mx > n2 ? mx : n2;
     mx = mx > n3 ? mx : n3;
-    for (uint32_t q0 = 0; q0 < mx + 3; q0 += 1024) {
-        uint32_t x[4][4];
+    for (uint32_t q0 = 0; q0 < mx; q0 += 1024) {
+        uint32_t lo[4][4], hi[4][4];
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const uintptr_t a = reinterpret_cast<uintptr_t>(src[r]);
@@ -1011,20 +1025,26 @@ __device__ __forceinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8
             const uint32_t *w = reinterpret_cast<const uint32_t *>(a - mis);
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const uint32_t idx = q0 / 4 + u * 64 + lane;
-                x[r][u] = (4 * idx < len[r] + mis) ? w[idx] : 0u;
+                const uint32_t q = q0 / 4 + u * 64 + lane;
+                lo[r][u] = 4 * q < len[r] ? w[q] : 0u;
+                hi[r][u] = mis && 4 * (q + 1) < len[r] + mis ? w[q + 1] : 0u;
             }
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(src[r]) & 3);
+            uint32_t *dw = reinterpret_cast<uint32_t *>(dst[r]);
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const uint32_t idx = q0 / 4 + u * 64 + lane;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int p = (int)(4 * idx + k) - (int)mis;
-                    if (p >= 0 && (uint32_t)p < len[r]) dst[r][p] = (uint8_t)(x[r][u] >> (8 * k));
+                const uint32_t q = q0 / 4 + u * 64 + lane;
+                const uint32_t v = __builtin_amdgcn_alignbyte(hi[r][u], lo[r][u], mis);
+                if (4 * q + 4 <= len[r]) {
+                    dw[q] = v;
+                } else if (4 * q < len[r]) {
+                    const uint32_t nb = len[r] - 4 * q;   // 1..3
+                    dst[r][4 * q] = (uint8_t)v;
+                    if (nb > 1) dst[r][4 * q + 1] = (uint8_t)(v >> 8);
+                    if (nb > 2) dst[r][4 * q + 2] = (uint8_t)(v >> 16);
                 }
             }
         }
