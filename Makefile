@@ -5,7 +5,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -shared --offload-arch=$(ARCH) -Wall -Wno-unused-result
 LIB := riak_ensemble_amd/libsynctree_hip.so
 SRC := riak_ensemble_amd/csrc/synctree_hip.hip
-DEPS := $(SRC) riak_ensemble_amd/csrc/small_path.h riak_ensemble_amd/csrc/st_kernels.h riak_ensemble_amd/csrc/rehash_win.h riak_ensemble_amd/csrc/md5_dev.h riak_ensemble_amd/csrc/leveldb_fmt.h riak_ensemble_amd/csrc/term_key.h riak_ensemble_amd/csrc/delta.h include/synctree_hip.h
+DEPS := $(SRC) riak_ensemble_amd/csrc/small_path.h riak_ensemble_amd/csrc/st_kernels.h riak_ensemble_amd/csrc/rehash_win.h riak_ensemble_amd/csrc/md5_dev.h riak_ensemble_amd/csrc/leveldb_fmt.h riak_ensemble_amd/csrc/term_key.h riak_ensemble_amd/csrc/pages.h include/synctree_hip.h
 
 all: $(LIB) oracle
 

@@ -89,7 +89,7 @@ def parse():
     ap.add_argument('--ensemble-keys', type=int, default=1_000_000, help='config-4 leg: keys per ensemble')
     ap.add_argument('--part-keys', type=int, default=100_000_000, help='config-5 leg: keys in the partitioned tree')
     ap.add_argument('--part-batches', type=int, default=30,
-                    help='config-5 leg: timed write batches (enough to cross a delta fold at the default limit)')
+                    help='config-5 leg: timed write batches')
     ap.add_argument('--part-batch-keys', type=int, default=1_000_000, help='config-5 leg: keys per write batch')
     ap.add_argument('--pmc-probe', action='store_true', help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -819,14 +819,14 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         k = torch.cat([_dev_keys_at(seed, old, dev, torch), _dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
         seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
         batches.append((k.contiguous(), _dev_values(seq, dev, torch).contiguous()))
-    # one warm-up batch, then K timed: each batch timed on its own (a device
-    # synchronisation around it) so the batches that fold the delta into the
-    # base CSR show; the reported rate is the amortised one (all K batches)
+    # one warm-up batch (it builds the pages), then K timed: each batch timed
+    # on its own (a device synchronisation around it) so the batches that
+    # rebuild the pages show; the reported rate is the amortised one (all K)
     k, v = batches[0]
     pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
     pt.combine()
     torch.cuda.synchronize()
-    folds0 = pt.tree.delta_stats()[2]
+    ps0 = pt.tree.page_stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -842,10 +842,11 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    # the same workload with the streaming delta on: K more
-    # batches merge into the delta (folded past a quarter of the tree)
+    ps1 = pt.tree.page_stats()
+    # the same workload with the pages off: K more batches,
+    # each merged into the canonical CSR (the whole CSR rewritten)
     from riak_ensemble_amd import _lib
-    pt.tree.debug_knob(_lib.ST_DBG_DELTA_LIMIT, 0)
+    pt.tree.debug_knob(_lib.ST_DBG_PAGES, -1)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -859,8 +860,7 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         torch.cuda.synchronize()
         dper.append(time.perf_counter() - tb)
     el_delta = time.perf_counter() - t1
-    dl_n, dl_new, folds = pt.tree.delta_stats()
-    pt.tree.debug_knob(_lib.ST_DBG_DELTA_LIMIT, -1)
+    pt.tree.debug_knob(_lib.ST_DBG_PAGES, 0)
     dper.sort()
     top = pt.top_hash()
     same = True
@@ -875,18 +875,21 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     pt.tree.close()
     return {'batch_keys_per_s': round(K * B / el, 1), 'ms_per_batch': round(el * 1e3 / K, 4), 'batches': K,
             'ms_per_batch_median': round(per[len(per) // 2] * 1e3, 4), 'ms_per_batch_max': round(per[-1] * 1e3, 4),
-            'delta_mode': {'ms_per_batch': round(el_delta * 1e3 / K, 4), 'ms_per_batch_median': round(dper[len(dper) // 2] * 1e3, 4),
-                           'ms_per_batch_max': round(dper[-1] * 1e3, 4), 'folds': folds - folds0, 'delta_entries_after': dl_n,
-                           'what': 'the next %d batches with the streaming delta on (st_debug_knob ST_DBG_DELTA_LIMIT '
-                                   '= auto): each merges into a delta CSR and hashes merged views; folded into the '
-                                   'base past a quarter of the tree (mean incl. folds); rank-local, not max over '
-                                   'ranks' % K},
+            'pages': {'batches': ps1[1] - ps0[1], 'page_builds': ps1[2] - ps0[2],
+                      'moved_entry_slots': ps1[4] - ps0[4],
+                      'what': 'st_page_stats over the timed batches: batches through the pages, page rebuilds '
+                              '(append region full), entry slots of segments moved to new pages'},
+            'csr_merge_mode': {'ms_per_batch': round(el_delta * 1e3 / K, 4), 'ms_per_batch_median': round(dper[len(dper) // 2] * 1e3, 4),
+                               'ms_per_batch_max': round(dper[-1] * 1e3, 4),
+                               'what': 'the next %d batches with the pages off (st_debug_knob ST_DBG_PAGES = -1; the first '
+                                       'folds the pages): each merged into the canonical CSR, rewriting every entry; '
+                                       'rank-local, not max over ranks' % K},
             'batch_keys': B, 'tree_keys': N, 'ranks': world, 'entries_on_rank0': entries,
             'tops_agree_across_ranks': same, 'load_s': round(load_s, 3),
             'what': 'config5: %d-key tree partitioned by segment range over %d rank(s); per batch: insert/3 of %d keys '
                     '(50%% overwrites Seq+1, 50%% new; verify + dirty-path rehash) on every rank, all-gather of the '
                     'level-2 entries, level 1 + top (keys generated on device: splitmix64 masked to 63 bits); each batch '
-                    'is merged into the segment CSR (the default; delta_mode is the opt-in streaming delta); '
+                    'rewrites the tails of the segments it touches in the paged layout (DESIGN.md 3.3); '
                     'ms_per_batch is the mean over the timed batches' % (N, world, B)}
 
 

@@ -389,20 +389,22 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * so the launch's climb never sees it: the bounded wait then reports
  * ST_EDEVICE instead of hashing a stale entry into the top hash. */
 #define ST_DBG_SKIP_MAIL 1
-/* ST_DBG_DELTA_LIMIT: use the streaming delta (st_delta_stats) and fold it
- * into the base CSR once it holds more than `value` entries (0 = auto: a
- * quarter of the tree, at least 2^20); -1 = no delta (the default: every
- * batch merges into the base CSR, which measured faster). */
-#define ST_DBG_DELTA_LIMIT 2
+/* ST_DBG_PAGES: streaming insert batches in the paged segment layout with
+ * `value` percent of slack per page (0 = the default, 25 %); -1 = off (every
+ * batch merges into the canonical CSR; the pages are folded first). */
+#define ST_DBG_PAGES 2
 int st_debug_knob(st_tree *t, int knob, int64_t value);
 
-/* The streaming-insert delta (no reference counterpart): a
- * batch of insert/3 much smaller than the tree merges into a delta CSR whose
- * entries overlay the base CSR's segments (a segment's content is the merged
- * view), so a batch does not rewrite the whole tree; every call but a
- * streaming insert first folds the delta into the base.  out[0] = entries in
- * the delta, out[1] = of them new keys of the tree, out[2] = folds so far. */
-int st_delta_stats(st_tree *t, uint64_t out[3]);
+/* The paged segment layout of streaming insert batches (no reference
+ * counterpart: the reference's backend stores each touched segment's
+ * orddict, synctree.erl:201-209, :468-485).  An insert batch
+ * small next to the tree rewrites only the tails of the segments it touches
+ * inside per-segment pages with slack; every other call folds the pages back
+ * into the canonical CSR first.  out[0] = pages in use, out[1] = batches
+ * through the pages, out[2] = page builds (the first batch's, and rebuilds
+ * when moved segments fill the append region), out[3] = folds, out[4] =
+ * entry slots of the segments moved to new pages. */
+int st_page_stats(st_tree *t, uint64_t out[5]);
 
 #ifdef __cplusplus
 }

@@ -107,12 +107,12 @@ _SIGS = {
     'st_set_timing': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_kernel_stats': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, u64p, ctypes.POINTER(ctypes.c_double)]),
     'st_debug_knob': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
-    'st_delta_stats': (ctypes.c_int, [ctypes.c_void_p, u64p]),
+    'st_page_stats': (ctypes.c_int, [ctypes.c_void_p, u64p]),
     'st_insert1_multi': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 8),
     'st_get1_multi': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4),
 }
-ST_DBG_SKIP_MAIL, ST_DBG_DELTA_LIMIT = 1, 2
+ST_DBG_SKIP_MAIL, ST_DBG_PAGES = 1, 2
 
 EXPORTED = sorted(_SIGS)
 _lib = None

@@ -189,7 +189,7 @@ __global__ void k_snap_sizes(DevTree t, uint32_t idlen, uint64_t R, const uint64
                     }
                 if (cnt) { p = 1; vl = 7 + body; }
             } else {
-                const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
+                const uint64_t e0 = t.seg_off[b], e1 = t.seg_end[b];
                 if (e1 > e0) { p = 1; vl = 7 + eo[e1] - eo[e0]; }
             }
             // an empty node the backend holds as [] (a raw store of [], or the
@@ -252,7 +252,7 @@ __global__ void k_snap_write(DevTree t, const uint8_t *id, uint32_t idlen, uint6
             v[0] = 106;
             continue;
         }
-        const uint64_t e0 = t.seg_off[b], e1 = t.seg_off[b + 1];
+        const uint64_t e0 = t.seg_off[b], e1 = t.seg_end[b];
         if (e1 == e0) { v[1] = 106; continue; }   // []
         v[1] = 108; v = etf_u32be(v + 2, (uint32_t)(e1 - e0));
         v[eo[e1] - eo[e0]] = 106;

@@ -166,7 +166,7 @@ __device__ __forceinline__ SegView seg_view(const DevTree &t, const Overlay &ov,
         v.ko64 = v.vo64 = nullptr;
     } else {
         v.e0 = t.seg_off[s];
-        v.n = t.seg_off[s + 1] - v.e0;
+        v.n = t.seg_end[s] - v.e0;
         v.kh = t.kheap;
         v.vh = t.vheap;
         v.ko64 = t.koff;
@@ -858,7 +858,7 @@ __global__ void k_ov_terminate(uint64_t n, const uint64_t *ktot, const uint64_t 
 __global__ void k_erec_emptied(DevTree t, const uint8_t *krec, const uint64_t *koff, uint8_t *erec) {
     if (threadIdx.x != 0) return;
     const uint64_t s = record_segment(krec + koff[0], koff[1] - koff[0], t.S - 1);
-    if (t.seg_off[s] == t.seg_off[s + 1]) erec[t.base[t.H + 1] + s] = 1;
+    if (t.seg_off[s] == t.seg_end[s]) erec[t.base[t.H + 1] + s] = 1;
 }
 
 __global__ void __launch_bounds__(256) k_small(const SmallReq *req, SmallOut *out) { small_body(req, out); }

@@ -36,8 +36,16 @@ struct DevTree {
     uint64_t base[ST_MAXLEV + 2];
     uint4 *md5;
     uint16_t *tag;
+    // segment s: entries [seg_off[s], seg_end[s]) of koff/voff (each entry's
+    // key and value end at the next entry's offsets; entry seg_end[s] holds
+    // the ends of the last one), values [seg_voff[s], seg_vend[s]).  The
+    // canonical CSR is gap-free (seg_end = seg_off + 1, seg_vend = seg_voff +
+    // 1); the paged layout of streaming batches (pages.h) leaves slack after
+    // every segment's page.
     const uint64_t *seg_off;
+    const uint64_t *seg_end;
     const uint64_t *seg_voff;
+    const uint64_t *seg_vend;
     const uint64_t *koff;
     const uint8_t *kheap;
     const uint64_t *voff;
@@ -367,7 +375,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
         const uint64_t s = list ? list[i] : i;
         const uint64_t slot = t.base[L] + s;
         if (mask && !mask[slot]) continue;
-        const uint64_t e0 = t.seg_off[s], e1 = t.seg_off[s + 1];
+        const uint64_t e0 = t.seg_off[s], e1 = t.seg_end[s];
         const uint64_t eslot = (L == 1) ? 0 : slot;
         if (MODE == MODE_VERIFY) {
             const uint16_t et = t.tag[eslot];
@@ -377,7 +385,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_vend[s] - v0, d);
                 const uint4 e = t.md5[eslot];
                 good = (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
             }
@@ -390,7 +398,7 @@ __global__ void k_segment_hash(DevTree t, const uint8_t *mask, const uint32_t *l
             } else {
                 uint32_t d[4];
                 const uint64_t v0 = t.seg_voff[s];
-                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+                stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_vend[s] - v0, d);
                 const uint4 e = make_uint4(d[0], d[1], d[2], d[3]);
                 t.md5[slot] = e;
                 t.tag[slot] = TAG_PRESENT;
@@ -531,8 +539,9 @@ __global__ void k_level_hash(DevTree t, uint32_t lmin, uint32_t lmax, const uint
 // synctree.erl:206, applied per segment with last-writer-wins).
 
 struct MergeArgs {
-    // old tree
+    // old tree (canonical CSR or pages: segment s = entries [seg_off[s], seg_end[s]))
     const uint64_t *seg_off;
+    const uint64_t *seg_end;
     const uint64_t *koff;
     const uint8_t *kheap;
     const uint64_t *voff;
@@ -548,16 +557,6 @@ struct MergeArgs {
     const uint64_t *bvoff;
     const uint8_t *bvheap;
     uint64_t S;
-    // optional per-entry payload carried with the entries (the delta CSR's
-    // base positions, delta.h): aux of the old entries, baux of the sorted
-    // batch records; NULL when the CSR has none
-    const uint2 *aux;
-    uint2 *baux;
-    // the delta's base CSR (delta.h): when set, k_merge_pos also computes
-    // every batch record's base position into baux and counts the records
-    // that are new keys of the tree (in neither the delta nor the base)
-    const uint64_t *b_seg_off, *b_koff, *b_voff;
-    const uint8_t *b_kheap;
 };
 
 // Running sums of the merge: per sorted batch record (BatchSums: eq = kept and
@@ -580,7 +579,7 @@ struct USum {
     }
 };
 typedef USum<6> BatchSums;   // eq, ne, ke, kn, ve, vn
-typedef USum<4> SegSums;     // count, key bytes, value bytes, new keys of the tree (delta merges)
+typedef USum<4> SegSums;     // count, key bytes, value bytes, new keys of the tree
 enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 
 // ---------------------------------------------------------------------------
@@ -603,7 +602,7 @@ enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty) {
     for (uint64_t s = gtid(); s < a.S; s += gstride()) {
         const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
-        uint64_t nold = a.seg_off ? a.seg_off[s + 1] - i0 : 0;
+        uint64_t nold = a.seg_off ? a.seg_end[s] - i0 : 0;
         const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
         const bool rej = a.seg_reject && a.seg_reject[s];
         if (a.seg_replace && a.seg_replace[s]) nold = 0;
@@ -612,10 +611,8 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
         tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
         tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
         tot.v[3] = 0;
-        uint64_t lo = 0, blo = 0;
+        uint64_t lo = 0;
         bool changed = false;
-        const uint64_t bb0 = a.b_seg_off ? a.b_seg_off[s] : 0, nb = a.b_seg_off ? a.b_seg_off[s + 1] - bb0 : 0;
-        const uint64_t bv0 = a.b_seg_off ? a.b_voff[bb0] : 0;
         for (uint64_t j = j0; j < je; j++) {
             BatchSums f(0);
             if (rej) { pos[j] = 0; bs[j] = f; continue; }
@@ -644,20 +641,7 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
             }
             bs[j] = f;
             changed |= kept;
-            if (a.b_seg_off) {   // the record's place in the base run (ascending: the search resumes)
-                uint64_t bhi = nb;
-                while (blo < bhi) {
-                    const uint64_t mid = (blo + bhi) >> 1, e2 = bb0 + mid;
-                    if (rec_cmp(a.b_kheap + a.b_koff[e2], a.b_koff[e2 + 1] - a.b_koff[e2], kb, kl) < 0) blo = mid + 1; else bhi = mid;
-                }
-                const uint64_t e2 = bb0 + blo;
-                const bool beq = blo < nb && rec_cmp(a.b_kheap + a.b_koff[e2], a.b_koff[e2 + 1] - a.b_koff[e2], kb, kl) == 0;
-                uint2 x;
-                x.x = (uint32_t)(a.b_voff[e2] - bv0) | (beq ? 0x80000000u : 0u);
-                x.y = beq ? (uint32_t)(a.b_voff[e2 + 1] - a.b_voff[e2]) : 0u;
-                a.baux[j] = x;
-                if (ne && !eq && !beq) tot.v[3] += 1;
-            }
+            if (ne && !eq) tot.v[3] += 1;   // a new key of the tree
             tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
             tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
             tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
@@ -681,7 +665,6 @@ struct MergeOut {
     uint64_t *seg_off, *seg_voff;   // S + 1
     uint64_t *koff, *voff;          // n_new + 1
     uint8_t *kheap, *vheap;
-    uint2 *aux;                     // n_new (NULL: no payload)
 };
 
 // Old entries: a workgroup per 256 consecutive segments walks their old
@@ -771,7 +754,6 @@ __global__ void __launch_bounds__(256) k_merge_old(MergeArgs a, const uint32_t *
         }
         o.koff[nw] = nk;
         o.voff[nw] = nv;
-        if (o.aux) o.aux[nw] = a.aux[e];
         copy_bytes(o.kheap + nk, a.kheap + okb, kl);
         copy_bytes(o.vheap + nv, a.vheap + ovb, vl);
     }
@@ -799,7 +781,6 @@ __global__ void k_merge_new(MergeArgs a, const uint32_t *sseg, uint64_t n, const
         const uint64_t bk = a.bv.koff[bi], bv = a.bvoff[bi];
         o.koff[nw] = nk;
         o.voff[nw] = nv;
-        if (o.aux) o.aux[nw] = a.baux[j];
         copy_bytes(o.kheap + nk, a.bv.kheap + bk, a.bv.koff[bi + 1] - bk);
         copy_bytes(o.vheap + nv, a.bvheap + bv, a.bvoff[bi + 1] - bv);
     }
@@ -831,7 +812,7 @@ __global__ void k_count_nonzero(const uint32_t *v, uint64_t n, unsigned long lon
 __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t n, uint64_t *found) {
     for (uint64_t i = gtid(); i < n; i += gstride()) {
         const uint64_t s = seg[i];
-        uint64_t lo = t.seg_off[s], hi = t.seg_off[s + 1];
+        uint64_t lo = t.seg_off[s], hi = t.seg_end[s];
         const uint8_t *k = bv.kheap + bv.koff[i];
         const uint64_t kl = bv.koff[i + 1] - bv.koff[i];
         while (lo < hi) {
@@ -839,7 +820,7 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
             if (rec_cmp(t.kheap + t.koff[m], t.koff[m + 1] - t.koff[m], k, kl) < 0) lo = m + 1; else hi = m;
         }
         uint64_t r = ~0ull;
-        if (lo < t.seg_off[s + 1] && rec_cmp(t.kheap + t.koff[lo], t.koff[lo + 1] - t.koff[lo], k, kl) == 0) r = lo;
+        if (lo < t.seg_end[s] && rec_cmp(t.kheap + t.koff[lo], t.koff[lo + 1] - t.koff[lo], k, kl) == 0) r = lo;
         found[i] = r;
     }
 }
@@ -883,10 +864,10 @@ __device__ __forceinline__ bool verify_segment(const DevTree &t, uint64_t s) {
     const uint64_t slot = t.base[L] + s;
     const uint64_t eslot = (L == 1) ? 0 : slot;
     const uint16_t et = t.tag[eslot];
-    if (!(et & TAG_PRESENT)) return t.seg_off[s] == t.seg_off[s + 1];
+    if (!(et & TAG_PRESENT)) return t.seg_off[s] == t.seg_end[s];
     uint32_t d[4];
     const uint64_t v0 = t.seg_voff[s];
-    stmd5::md5_global_pf(t.vheap + v0, t.seg_voff[s + 1] - v0, d);
+    stmd5::md5_global_pf(t.vheap + v0, t.seg_vend[s] - v0, d);
     const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
 }
@@ -1153,8 +1134,8 @@ struct SegPair {
 };
 __device__ __forceinline__ SegPair seg_pair(const DevTree &A, const DevTree &B, uint64_t s) {
     SegPair p;
-    p.a0 = A.seg_off[s]; p.a1 = A.seg_off[s + 1]; p.b0 = B.seg_off[s]; p.b1 = B.seg_off[s + 1];
-    p.va0 = A.seg_voff[s]; p.va1 = A.seg_voff[s + 1]; p.vb0 = B.seg_voff[s]; p.vb1 = B.seg_voff[s + 1];
+    p.a0 = A.seg_off[s]; p.a1 = A.seg_end[s]; p.b0 = B.seg_off[s]; p.b1 = B.seg_end[s];
+    p.va0 = A.seg_voff[s]; p.va1 = A.seg_vend[s]; p.vb0 = B.seg_voff[s]; p.vb1 = B.seg_vend[s];
     return p;
 }
 __device__ __forceinline__ SegPair shfl_pair(const SegPair &p, int j) {
@@ -1345,8 +1326,8 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         }
         if (seg) {
             uint64_t s0, s1;
-            if (side) { v0 = B.seg_voff[b]; len = B.seg_voff[b + 1] - v0; s0 = B.seg_off[b]; s1 = B.seg_off[b + 1]; }
-            else      { v0 = A.seg_voff[b]; len = A.seg_voff[b + 1] - v0; s0 = A.seg_off[b]; s1 = A.seg_off[b + 1]; }
+            if (side) { v0 = B.seg_voff[b]; len = B.seg_vend[b] - v0; s0 = B.seg_off[b]; s1 = B.seg_end[b]; }
+            else      { v0 = A.seg_voff[b]; len = A.seg_vend[b] - v0; s0 = A.seg_off[b]; s1 = A.seg_end[b]; }
             empty = s0 == s1;
             if (k0 == 0) { kv0 = v0; kvl = len; ks0 = s0; ks1 = s1; }
         }
@@ -1790,8 +1771,8 @@ __global__ void k_entry_gather(DevTree t, const uint64_t *idx, uint64_t n, const
 
 #define PERM_BINS 256
 __device__ __forceinline__ uint32_t perm_bin(const DevTree &t, uint64_t s) {
-    if (t.seg_off[s] == t.seg_off[s + 1]) return PERM_BINS - 1;
-    const uint64_t blocks = (t.seg_voff[s + 1] - t.seg_voff[s] + 8) / 64 + 1;
+    if (t.seg_off[s] == t.seg_end[s]) return PERM_BINS - 1;
+    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1;
     return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
 }
 
@@ -1854,14 +1835,14 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
         const uint64_t s = perm[i];
         const uint64_t slot = t.base[L1] + s;
         if (mask && !mask[slot]) continue;
-        if (t.seg_off[s] == t.seg_off[s + 1]) {
+        if (t.seg_off[s] == t.seg_end[s]) {
             t.tag[slot] = 0;
             if (L1 == 1) t.tag[0] = 0;
             continue;
         }
         uint32_t dg[4];
         const uint64_t v0 = t.seg_voff[s];
-        stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_voff[s + 1] - v0, dg);
+        stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_vend[s] - v0, dg);
         const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;
@@ -2208,7 +2189,7 @@ __global__ void __launch_bounds__(256) k_tile_order_global(DevTree t, const uint
     uint32_t s = 0xffffffffu, ln = 0;
     if (i < t.S) {
         s = perm[i];
-        if (t.seg_off[s] != t.seg_off[s + 1]) ln = (uint32_t)(t.seg_voff[s + 1] - t.seg_voff[s] + 1);
+        if (t.seg_off[s] != t.seg_end[s]) ln = (uint32_t)(t.seg_vend[s] - t.seg_voff[s] + 1);
     }
     if (tl < ntiles) {
         tseg[i] = s;
@@ -2288,7 +2269,7 @@ __global__ void __launch_bounds__(256) k_tile_order_window(DevTree t, uint32_t *
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const uint64_t s = seg0 + k * 256 + tid;
-        ln[k] = t.seg_off[s] != t.seg_off[s + 1] ? (uint32_t)(t.seg_voff[s + 1] - t.seg_voff[s] + 1) : 0u;
+        ln[k] = t.seg_off[s] != t.seg_end[s] ? (uint32_t)(t.seg_vend[s] - t.seg_voff[s] + 1) : 0u;
         const uint32_t r = ln_rows(ln[k]) + (ln[k] != 0);   // present-but-empty values sort above absent
         bin[k] = 255u - (r > 255u ? 255u : r);
         atomicAdd(&hist[bin[k]], 1u);

@@ -25,7 +25,7 @@
 #include "rehash_win.h"
 #include "leveldb_fmt.h"
 #include "small_path.h"
-#include "delta.h"
+#include "pages.h"
 
 static thread_local std::string g_err;
 static const uint64_t HEAP_SLACK = 256;   // md5_global over-reads <= 64 B past a range
@@ -65,8 +65,18 @@ struct CsrSet {
     uint64_t *seg_off = nullptr, *seg_voff = nullptr, *koff = nullptr, *voff = nullptr;
     uint8_t *kheap = nullptr, *vheap = nullptr;
     uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
-    uint2 *aux = nullptr;   // the delta's per-entry base positions (delta.h); none in the base CSR
-    uint64_t cap_aux = 0;
+};
+
+// The paged segment layout of streaming insert batches (pages.h): page
+// metadata, entry slots and heaps with an append region after the pages.
+struct Pages {
+    bool on = false;
+    PageMeta m{};
+    uint64_t *koff = nullptr, *voff = nullptr;
+    uint8_t *kheap = nullptr, *vheap = nullptr;
+    uint64_t cap_e = 0, cap_k = 0, cap_v = 0;   // allocated entry slots / heap bytes
+    uint64_t use_e = 0, use_k = 0, use_v = 0;   // the append region starts here
+    uint64_t batches = 0, builds = 0, folds = 0, reloc_e = 0;
 };
 
 struct st_tree {
@@ -96,11 +106,11 @@ struct st_tree {
     // retired previous CSR kept as the next merge's output buffers (csr_take)
     uint64_t cap_n = 0, cap_k = 0, cap_v = 0;
     CsrSet spare;
-    // streaming-insert delta (delta.h): entries inserted since the last
-    // fold, their CSR and its spare; dl_new = delta entries that are new keys
-    CsrSet dl, dl_spare;
-    uint64_t dl_n = 0, dl_new = 0, dl_folds = 0;
-    uint64_t dl_limit = ~0ull;   // fold threshold in entries (~0: no delta, the default; 0: auto; st_debug_knob)
+    // streaming insert batches go to the paged layout (pages.h) while
+    // pg_slack >= 0 (percent of slack per page; st_debug_knob ST_DBG_PAGES);
+    // any other call folds it back into the CSR first
+    Pages pg;
+    int pg_slack = 25;
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -371,8 +381,7 @@ struct Scratch {
 static const uint64_t CSR_KEEP_SPARE = 16ull << 20;
 
 static void csr_free(st_tree *t, CsrSet &c) {
-    for (void *p : {(void *)c.seg_off, (void *)c.seg_voff, (void *)c.koff, (void *)c.voff, (void *)c.kheap, (void *)c.vheap,
-                    (void *)c.aux})
+    for (void *p : {(void *)c.seg_off, (void *)c.seg_voff, (void *)c.koff, (void *)c.voff, (void *)c.kheap, (void *)c.vheap})
         dfree(t, p);
     c = CsrSet();
 }
@@ -440,6 +449,8 @@ struct CsrTaken {
     void install() { csr_install(t, o); installed = true; }
 };
 
+// The tree as kernels see it: the canonical CSR, or the paged layout while
+// streaming batches are in it (pages.h).
 static DevTree view(const st_tree *t) {
     DevTree d;
     memset(&d, 0, sizeof(d));
@@ -451,8 +462,21 @@ static DevTree view(const st_tree *t) {
     for (int i = 0; i < ST_MAXLEV + 2; i++) d.base[i] = t->base[i];
     d.md5 = t->md5;
     d.tag = t->tag;
+    if (t->pg.on) {
+        d.seg_off = t->pg.m.beg;
+        d.seg_end = t->pg.m.end;
+        d.seg_voff = t->pg.m.vbeg;
+        d.seg_vend = t->pg.m.vend;
+        d.koff = t->pg.koff;
+        d.kheap = t->pg.kheap;
+        d.voff = t->pg.voff;
+        d.vheap = t->pg.vheap;
+        return d;
+    }
     d.seg_off = t->seg_off;
+    d.seg_end = t->seg_off + 1;
     d.seg_voff = t->seg_voff;
+    d.seg_vend = t->seg_voff + 1;
     d.koff = t->koff;
     d.kheap = t->kheap;
     d.voff = t->voff;
@@ -734,6 +758,7 @@ extern "C" int st_create(uint64_t width, uint64_t segments, int device, st_tree 
     return ST_OK;
 }
 
+static void pages_free(st_tree *t, Pages &g);
 extern "C" void st_destroy(st_tree *t) {
     if (!t) return;
     // wait for a call still running on the handle (a caller must not use it
@@ -748,8 +773,7 @@ extern "C" void st_destroy(st_tree *t) {
     for (void *p : {(void *)t->spare.seg_off, (void *)t->spare.seg_voff, (void *)t->spare.koff, (void *)t->spare.voff,
                     (void *)t->spare.kheap, (void *)t->spare.vheap})
         dfree(t, p);
-    csr_free(t, t->dl);
-    csr_free(t, t->dl_spare);
+    pages_free(t, t->pg);
     dfree(t, t->ov.idx);
     dfree(t, t->ov.heap);
     dfree(t, t->ov.used);
@@ -783,30 +807,32 @@ extern "C" uint64_t st_width(const st_tree *t) { return t->W; }
 extern "C" uint64_t st_segments(const st_tree *t) { return t->S; }
 extern "C" uint64_t st_num_entries(st_tree *t) {
     std::lock_guard<std::recursive_mutex> g(t->mu);
-    return t->n + t->dl_new;   // base entries + the delta's new keys
+    return t->n;
 }
 
-static int flush_delta(st_tree *t);
+static int pages_fold(st_tree *t);
 extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
     ENTER_ANY(t);
     if (knob == ST_DBG_SKIP_MAIL) {
         t->dbg_skip_mail = value < 0 ? ~0u : (uint32_t)value;
         return ST_OK;
     }
-    if (knob == ST_DBG_DELTA_LIMIT) {
-        if (value < 0) CHK(flush_delta(t));   // turning the delta off folds what it holds
-        t->dl_limit = value < 0 ? ~0ull : (uint64_t)value;
+    if (knob == ST_DBG_PAGES) {
+        if (value < 0) CHK(pages_fold(t));   // pages off: streaming batches merge into the CSR
+        t->pg_slack = value < 0 ? -1 : value == 0 ? 25 : (int)std::min<int64_t>(value, 400);
         return ST_OK;
     }
     g_err = "unknown debug knob";
     return ST_EINVAL;
 }
 
-extern "C" int st_delta_stats(st_tree *t, uint64_t out[3]) {
+extern "C" int st_page_stats(st_tree *t, uint64_t out[5]) {
     ENTER_ANY(t);
-    out[0] = t->dl_n;
-    out[1] = t->dl_new;
-    out[2] = t->dl_folds;
+    out[0] = t->pg.on ? 1 : 0;
+    out[1] = t->pg.batches;
+    out[2] = t->pg.builds;
+    out[3] = t->pg.folds;
+    out[4] = t->pg.reloc_e;
     return ST_OK;
 }
 
@@ -816,7 +842,8 @@ extern "C" int st_mem_stats(st_tree *t, uint64_t out[6]) {
     out[0] = t->nslots * (sizeof(uint4) + sizeof(uint16_t) + 2);   // md5, tag, mark, ok
     out[1] = (t->S + 1) * 16 + t->cap_n * 16 + t->cap_k + t->cap_v;
     out[2] = t->tiles_cap * sizeof(uint4) + (t->tseg ? num_tiles(t) * (64 * 8 + sizeof(TileInfo)) : 0);
-    out[3] = t->spare.koff ? (t->S + 1) * 16 + t->spare.cap_n * 16 + t->spare.cap_k + t->spare.cap_v : 0;
+    out[3] = (t->spare.koff ? (t->S + 1) * 16 + t->spare.cap_n * 16 + t->spare.cap_k + t->spare.cap_v : 0) +
+             (t->pg.koff ? t->S * 56 + t->pg.cap_e * 16 + t->pg.cap_k + t->pg.cap_v : 0);
     out[4] = t->ov.idx ? t->S * 8 + t->ov.cap : 0;
     std::lock_guard<std::mutex> g(g_mem_mu);
     uint64_t c = 0;
@@ -1145,20 +1172,15 @@ static int rehash_tiled(st_tree *t) {
 }
 
 // Full (mask == NULL) or dirty-path (mask: marked segments + ancestors) rehash.
-// The dirty path hashes the marked segments straight from the CSR in
-// block-count order (k_segment_hash_perm), then the marked inner nodes:
-// W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the per-level
-// kernels above; other geometries: one k_level_hash launch per level.
-// dv: the segments are the merged views of the base CSR and this delta (delta.h).
-static int rehash_all(st_tree *t, const uint8_t *mask, const DeltaView *dv) {
+// The dirty path hashes the marked segments straight from the CSR (or the
+// pages) in block-count order (k_segment_hash_perm), then the marked inner
+// nodes: W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the
+// per-level kernels above; other geometries: one k_level_hash launch per level.
+static int rehash_all(st_tree *t, const uint8_t *mask) {
     if (!mask) return rehash_tiled(t);
     DevTree d = view(t);
     CHK(ensure_perm(t));
-    if (dv)
-        LAUNCH(t, "segment_hash", k_segment_hash_merged<MODE_STORE>, grid_for(t->S), 256, 0, d, *dv,
-               (const uint32_t *)t->seg_perm, mask, (uint8_t *)nullptr);
-    else
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
+    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
@@ -1171,17 +1193,12 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const DeltaView *dv) {
 }
 
 // Verify every node marked in t->mark (levels 1..L); results in t->ok.
-// dv: segments are merged views with this delta (delta.h).
-static int verify_marked(st_tree *t, uint32_t L, const DeltaView *dv = nullptr) {
+static int verify_marked(st_tree *t, uint32_t L) {
     DevTree d = view(t);
     if (L == t->H + 1) {   // segments in the length order of seg_perm: lanes of a wave hash alike-sized messages
         CHK(ensure_perm(t));
-        if (dv)
-            LAUNCH(t, "segment_verify", k_segment_hash_merged<MODE_VERIFY>, grid_for(t->S), 256, 0, d, *dv,
-                   (const uint32_t *)t->seg_perm, (const uint8_t *)t->mark, t->ok);
-        else
-            LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
-                   (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
+               (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
     }
     const uint32_t lmax = L < t->H ? L : t->H;
     if (lmax >= 1) {
@@ -1214,11 +1231,6 @@ struct IngestIn {
     uint32_t *clevel_out;
     uint32_t *seg_out;
     uint64_t n_rejected;
-    // presorted: the records are already in segment order with unique keys
-    // ascending within each segment, seg_given their segments and
-    // bseg_given the S + 1 run bounds (the delta folded into the base)
-    bool presorted;
-    const uint64_t *bseg_given;
 };
 
 // The batch in merge order: segment per record (seg), sorted segments
@@ -1233,15 +1245,6 @@ struct BatchPrep {
 static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
     const uint64_t n = in.n, S = t->S;
     CHK(sc.alloc(&bp.keep, n));
-    if (in.presorted) {
-        bp.seg = bp.sseg = const_cast<uint32_t *>(in.seg_given);
-        bp.bseg_off = const_cast<uint64_t *>(in.bseg_given);
-        CHK(sc.alloc(&bp.perm, n));
-        LAUNCH(t, "iota", k_iota, grid_for(n), 256, 0, bp.perm, n);
-        HIPCHK(hipMemsetAsync(bp.keep, 1, n, t->stream));
-        if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
-        return ST_OK;
-    }
     uint32_t *idx = nullptr;
     CHK(sc.alloc(&bp.seg, n));
     CHK(sc.alloc(&bp.sseg, n));
@@ -1281,7 +1284,7 @@ static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
 
 // Path verification of the touched segments (insert semantics): rejects[S]
 // = first failing level of each touched segment's root->segment path.
-static int verify_batch_paths(st_tree *t, const BatchPrep &bp, Scratch &sc, uint8_t **reject, const DeltaView *dv) {
+static int verify_batch_paths(st_tree *t, const BatchPrep &bp, Scratch &sc, uint8_t **reject) {
     const uint64_t S = t->S;
     CHK(sc.alloc(reject, S));
     if (t->fresh) {
@@ -1292,20 +1295,20 @@ static int verify_batch_paths(st_tree *t, const BatchPrep &bp, Scratch &sc, uint
     HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
     LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
            (const uint64_t *)nullptr, S, t->mark);
-    CHK(verify_marked(t, t->H + 1, dv));
+    CHK(verify_marked(t, t->H + 1));
     LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
            (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, *reject, (uint32_t *)nullptr);
     return ST_OK;
 }
 
-static MergeArgs merge_args(const uint64_t *seg_off, const uint64_t *koff, const uint8_t *kheap, const uint64_t *voff,
-                            const uint8_t *vheap, const IngestIn &in, const BatchPrep &bp, const uint8_t *reject, uint64_t S) {
+static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPrep &bp, const uint8_t *reject, uint64_t S) {
     MergeArgs ma;
-    ma.seg_off = seg_off;
-    ma.koff = koff;
-    ma.kheap = kheap;
-    ma.voff = voff;
-    ma.vheap = vheap;
+    ma.seg_off = d.seg_off;
+    ma.seg_end = d.seg_end;
+    ma.koff = d.koff;
+    ma.kheap = d.kheap;
+    ma.voff = d.voff;
+    ma.vheap = d.vheap;
     ma.perm = bp.perm;
     ma.bseg_off = bp.bseg_off;
     ma.keep = bp.keep;
@@ -1316,14 +1319,8 @@ static MergeArgs merge_args(const uint64_t *seg_off, const uint64_t *koff, const
     ma.bvoff = in.voff;
     ma.bvheap = in.vheap;
     ma.S = S;
-    ma.aux = nullptr;
-    ma.baux = nullptr;
-    ma.b_seg_off = ma.b_koff = ma.b_voff = nullptr;
-    ma.b_kheap = nullptr;
     return ma;
 }
-
-static int flush_delta(st_tree *t);
 
 // The batch merged into the base CSR (a whole new CSR).
 static int ingest_direct(st_tree *t, IngestIn &in) {
@@ -1334,13 +1331,13 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     uint8_t *reject = nullptr, *dirty = nullptr;
     uint32_t *mpos = nullptr;
     if (in.verify_rehash) {
-        CHK(verify_batch_paths(t, bp, sc, &reject, nullptr));
+        CHK(verify_batch_paths(t, bp, sc, &reject));
         if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
                                   (const uint8_t *)reject, in.clevel_out);
     }
 
     // merge (k_merge_pos / k_merge_old / k_merge_new): count, scan, write
-    MergeArgs ma = merge_args(t->seg_off, t->koff, t->kheap, t->voff, t->vheap, in, bp, reject, S);
+    MergeArgs ma = merge_args(view(t), in, bp, reject, S);
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *ss = nullptr, *sx = nullptr;
     CHK(sc.alloc(&ss, S + 1));
@@ -1364,7 +1361,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     HIPCHK(hipMemsetAsync(out.o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
     MergeOut mo;
     mo.seg_off = out.o.seg_off; mo.seg_voff = out.o.seg_voff; mo.koff = out.o.koff; mo.voff = out.o.voff;
-    mo.kheap = out.o.kheap; mo.vheap = out.o.vheap; mo.aux = nullptr;
+    mo.kheap = out.o.kheap; mo.vheap = out.o.vheap;
     LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
            (const BatchSums *)bx, (const SegSums *)sx, mo);
     LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, (const uint32_t *)mpos,
@@ -1382,199 +1379,174 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
         // dirty-path rehash: segments whose content changed and their ancestors
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
-        CHK(rehash_all(t, t->mark, nullptr));
+        CHK(rehash_all(t, t->mark));
     }
     t->fresh = false;
     return ST_OK;
 }
 
-// ------------------------------------------------------------------ the delta CSR (delta.h)
-// A streaming batch (insert semantics, a batch small next to the tree)
-// merges into the delta instead of the base CSR; the delta is folded into the
-// base when it exceeds its limit, and before any call but a streaming insert.
+// ------------------------------------------------------------------ the paged layout (pages.h)
+// Streaming insert batches (insert semantics, a batch small next to the
+// tree) go to the paged layout: the first one copies the CSR into pages with
+// slack; each batch then rewrites only the tails of the segments it touches
+// (or moves a segment that outgrew its page to the append region); a batch
+// whose moves do not fit the append region first rebuilds the pages (fresh
+// slack, an empty append region).  Every other call folds the pages back into
+// the canonical CSR first (flush_all).
 
-static DeltaView delta_view(const st_tree *t) {
-    DeltaView v;
-    v.seg_off = t->dl.seg_off;
-    v.voff = t->dl.voff;
-    v.vheap = t->dl.vheap;
-    v.aux = t->dl.aux;
-    return v;
-}
-
-// An empty delta CSR (every run empty) as the first streaming batch's "old" delta.
-static int ensure_delta(st_tree *t) {
-    if (t->dl.seg_off) return ST_OK;
-    CsrSet &c = t->dl;
-    CHK(dalloc_t(t, &c.seg_off, t->S + 1));
-    CHK(dalloc_t(t, &c.seg_voff, t->S + 1));
-    CHK(dalloc_t(t, &c.koff, 1));
-    CHK(dalloc_t(t, &c.voff, 1));
-    CHK(dalloc_t(t, &c.aux, 1));
-    CHK(dalloc(t, (void **)&c.kheap, HEAP_SLACK));
-    CHK(dalloc(t, (void **)&c.vheap, HEAP_SLACK));
-    c.cap_n = 1; c.cap_k = HEAP_SLACK; c.cap_v = HEAP_SLACK; c.cap_aux = 1;
-    HIPCHK(hipMemsetAsync(c.seg_off, 0, (t->S + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(c.seg_voff, 0, (t->S + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(c.koff, 0, 8, t->stream));
-    HIPCHK(hipMemsetAsync(c.voff, 0, 8, t->stream));
-    HIPCHK(hipMemsetAsync(c.kheap, 0, HEAP_SLACK, t->stream));
-    HIPCHK(hipMemsetAsync(c.vheap, 0, HEAP_SLACK, t->stream));
-    t->dl_n = 0;
-    t->dl_new = 0;
-    return ST_OK;
-}
-
-// Output buffers of a delta merge: the delta's spare set, grown as needed.
-static int delta_take(st_tree *t, uint64_t n1, uint64_t kb, uint64_t vb, CsrSet &o) {
-    CsrSet &sp = t->dl_spare;
-    if (!sp.seg_off) CHK(dalloc_t(t, &sp.seg_off, t->S + 1));
-    if (!sp.seg_voff) CHK(dalloc_t(t, &sp.seg_voff, t->S + 1));
-    auto grow = [&](auto *&p, uint64_t &cap, uint64_t want, uint64_t unit) -> int {
-        if (cap >= want && p) return ST_OK;
+static void pages_free(st_tree *t, Pages &g) {
+    for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.ecap, (void *)g.m.kcap,
+                    (void *)g.m.vcap, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
-        p = nullptr;
-        cap = 0;
-        const uint64_t w = want + want / 4 + 64;
-        CHK(dalloc(t, (void **)&p, w * unit));
-        cap = w;
+    const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e;
+    g = Pages();
+    g.batches = b; g.builds = bu; g.folds = f; g.reloc_e = r;
+}
+
+// Copy the tree's segments (CSR or pages) into a new layout: pages with
+// slack_pct percent of slack and an append region of at least `reserve`
+// (entries, key bytes, value bytes), or (slack_pct < 0) the canonical CSR.
+static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
+    const uint64_t S = t->S;
+    const DevTree src = view(t);
+    Scratch sc(t);
+    PageSums *sz = nullptr, *base = nullptr;
+    CHK(sc.alloc(&sz, S + 1));
+    CHK(sc.alloc(&base, S + 1));
+    HIPCHK(hipMemsetAsync(sz + S, 0, sizeof(PageSums), t->stream));
+    LAUNCH(t, "page_build", k_page_sizes, grid_for(S), 256, 0, src, slack_pct, sz);
+    CHK(exclusive_scan<PageSums>(t, sz, base, S + 1));
+    PageSums tot(0);
+    CHK(d2h(t, &tot, base + S, sizeof(PageSums)));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((S + 3) / 4, 65536);
+    if (slack_pct < 0) {   // back to the canonical CSR
+        CsrTaken out(t);
+        CHK(csr_take(t, tot.v[0] + 1, tot.v[1] + HEAP_SLACK, tot.v[2] + HEAP_SLACK, out.o));
+        HIPCHK(hipMemsetAsync(out.o.kheap + tot.v[1], 0, HEAP_SLACK, t->stream));
+        HIPCHK(hipMemsetAsync(out.o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
+        PageDst d{};
+        d.koff = out.o.koff; d.voff = out.o.voff; d.kheap = out.o.kheap; d.vheap = out.o.vheap;
+        d.cseg_off = out.o.seg_off; d.cseg_voff = out.o.seg_voff;
+        LAUNCH(t, "page_fold", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d);
+        out.install();
+        t->n = tot.v[0]; t->kbytes = tot.v[1]; t->vbytes = tot.v[2];
+        CHK(tsync(t));   // the pages' buffers are free once the copy has read them
+        pages_free(t, t->pg);
+        t->pg.folds++;
+        t->perm_valid = false;
         return ST_OK;
-    };
-    CHK(grow(sp.koff, sp.cap_n, n1, 8));
-    if (!sp.voff || sp.cap_aux < n1) {   // voff and aux share the entry capacity of koff
-        dfree(t, sp.voff); dfree(t, sp.aux);
-        sp.voff = nullptr; sp.aux = nullptr; sp.cap_aux = 0;
-        CHK(dalloc_t(t, &sp.voff, sp.cap_n));
-        CHK(dalloc_t(t, &sp.aux, sp.cap_n));
-        sp.cap_aux = sp.cap_n;
     }
-    CHK(grow(sp.kheap, sp.cap_k, kb, 1));
-    CHK(grow(sp.vheap, sp.cap_v, vb, 1));
-    o = sp;
-    sp = CsrSet();
+    Pages g;
+    g.cap_e = tot.v[0] + std::max<uint64_t>(reserve.v[0], tot.v[0] / 4) + 1;
+    g.cap_k = tot.v[1] + std::max<uint64_t>(reserve.v[1], tot.v[1] / 4);
+    g.cap_v = tot.v[2] + std::max<uint64_t>(reserve.v[2], tot.v[2] / 4);
+    struct Undo {   // a failed build frees what it allocated
+        st_tree *t; Pages &g; bool done = false;
+        ~Undo() { if (!done) pages_free(t, g); }
+    } undo{t, g};
+    for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
+    CHK(dalloc_t(t, &g.koff, g.cap_e));
+    CHK(dalloc_t(t, &g.voff, g.cap_e));
+    CHK(dalloc(t, (void **)&g.kheap, g.cap_k + HEAP_SLACK));
+    CHK(dalloc(t, (void **)&g.vheap, g.cap_v + HEAP_SLACK));
+    HIPCHK(hipMemsetAsync(g.kheap + g.cap_k, 0, HEAP_SLACK, t->stream));
+    HIPCHK(hipMemsetAsync(g.vheap + g.cap_v, 0, HEAP_SLACK, t->stream));
+    PageDst d{};
+    d.koff = g.koff; d.voff = g.voff; d.kheap = g.kheap; d.vheap = g.vheap; d.m = g.m;
+    LAUNCH(t, "page_build", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d);
+    g.use_e = tot.v[0]; g.use_k = tot.v[1]; g.use_v = tot.v[2];
+    g.on = true;
+    g.batches = t->pg.batches; g.builds = t->pg.builds + 1; g.folds = t->pg.folds; g.reloc_e = t->pg.reloc_e;
+    CHK(tsync(t));   // the old pages (if any) were read
+    pages_free(t, t->pg);
+    t->pg = g;
+    undo.done = true;
+    t->perm_valid = false;
     return ST_OK;
 }
 
-static void delta_install(st_tree *t, const CsrSet &o) {
-    csr_free(t, t->dl_spare);
-    t->dl_spare = t->dl;
-    t->dl = o;
+static int pages_fold(st_tree *t) {
+    if (!t->pg.on) return ST_OK;
+    return pages_build(t, -1, PageSums(0));
 }
 
-// Streaming batch size that goes to the delta: small next to the (owned
-// part of the) tree.
-static bool delta_eligible(const st_tree *t, const IngestIn &in) {
-    if (!in.verify_rehash || in.seg_given || in.bop || in.seg_replace || in.presorted || t->fresh || t->n == 0) return false;
-    if (t->dl_limit == ~0ull) return false;   // disabled (st_debug_knob)
+// A streaming batch: insert semantics, small next to the (owned part of the) tree.
+static bool pages_eligible(const st_tree *t, const IngestIn &in) {
+    if (t->pg_slack < 0 || !in.verify_rehash || in.seg_given || in.bop || in.seg_replace || t->fresh || t->n == 0) return false;
     const double own = t->partitioned ? (double)(t->part_hi - t->part_lo) / (double)t->S : 1.0;
     return (double)in.n * own * 32.0 <= (double)t->n;
 }
 
-static uint64_t delta_limit(const st_tree *t) {
-    if (t->dl_limit) return t->dl_limit;
-    return std::max<uint64_t>(t->n / 4, 1u << 20);
-}
-
-static int ingest_delta(st_tree *t, IngestIn &in) {
+static int ingest_paged(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
-    CHK(ensure_delta(t));
-    CHK(ensure_perm(t));   // the base's block-count order: valid until the next compaction
+    if (!t->pg.on) CHK(pages_build(t, t->pg_slack, PageSums(0)));
     Scratch sc(t);
     BatchPrep bp;
     CHK(batch_prepare(t, in, sc, bp));
-    const DeltaView old = delta_view(t);
-    uint8_t *reject = nullptr, *dirty = nullptr;
-    CHK(verify_batch_paths(t, bp, sc, &reject, &old));
+    uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
+    CHK(verify_batch_paths(t, bp, sc, &reject));
     if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
                               (const uint8_t *)reject, in.clevel_out);
-    // merge the batch into the delta (the base is not touched); the count
-    // pass also places every record in its segment's base run (baux) and
-    // counts the records that are new keys of the tree (SegSums v[3])
-    uint2 *baux = nullptr;
-    CHK(sc.alloc(&baux, n));
-    DevTree d = view(t);
-    MergeArgs ma = merge_args(t->dl.seg_off, t->dl.koff, t->dl.kheap, t->dl.voff, t->dl.vheap, in, bp, reject, S);
-    ma.aux = t->dl.aux;
-    ma.baux = baux;
-    ma.b_seg_off = t->seg_off; ma.b_koff = t->koff; ma.b_voff = t->voff; ma.b_kheap = t->kheap;
+    // merge positions and the merged sizes of every touched segment
+    MergeArgs ma = merge_args(view(t), in, bp, reject, S);
     BatchSums *bs = nullptr, *bx = nullptr;
-    SegSums *ss = nullptr, *sx = nullptr;
+    SegSums *ss = nullptr;
+    PageSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
-    CHK(sc.alloc(&ss, S + 1));
-    CHK(sc.alloc(&sx, S + 1));
+    CHK(sc.alloc(&ss, S));
     CHK(sc.alloc(&dirty, S));
+    CHK(sc.alloc(&mode, S));
+    CHK(sc.alloc(&rsz, S + 1));
+    CHK(sc.alloc(&rbase, S + 1));
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n + 1));
-    HIPCHK(hipMemsetAsync(ss + S, 0, sizeof(SegSums), t->stream));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
+    HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PageSums), t->stream));
     LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty);
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
-    CHK(exclusive_scan<SegSums>(t, ss, sx, S + 1));
-    SegSums tot(0);
-    CHK(d2h(t, &tot, sx + S, sizeof(SegSums)));
-    const uint64_t n_new = tot.v[0];
-    CsrSet o;
-    CHK(delta_take(t, n_new + 1, tot.v[1] + HEAP_SLACK, tot.v[2] + HEAP_SLACK, o));
-    bool installed = false;
-    struct Back {   // a failed merge returns the taken set to the spare slot
-        st_tree *t; CsrSet &o; bool &done;
-        ~Back() { if (!done) { csr_free(t, t->dl_spare); t->dl_spare = o; } }
-    } back{t, o, installed};
-    HIPCHK(hipMemsetAsync(o.kheap + tot.v[1], 0, HEAP_SLACK, t->stream));
-    HIPCHK(hipMemsetAsync(o.vheap + tot.v[2], 0, HEAP_SLACK, t->stream));
-    MergeOut mo;
-    mo.seg_off = o.seg_off; mo.seg_voff = o.seg_voff; mo.koff = o.koff; mo.voff = o.voff;
-    mo.kheap = o.kheap; mo.vheap = o.vheap; mo.aux = o.aux;
-    LAUNCH(t, "merge_write", k_merge_old, (uint32_t)((S + 255) / 256), 256, 0, ma, (const uint32_t *)mpos,
-           (const BatchSums *)bx, (const SegSums *)sx, mo);
-    LAUNCH(t, "merge_write", k_merge_new, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, (const uint32_t *)mpos,
-           (const BatchSums *)bx, (const SegSums *)sx, mo);
-    delta_install(t, o);
-    installed = true;
-    t->dl_n = n_new;
-    t->dl_new += tot.v[3];   // keys of the tree = base entries + delta entries that replace none
+    // in place or to a new page; the moves' places in the append region
+    PageSums tot(0);
+    for (int pass = 0;; pass++) {
+        LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, view(t), t->pg.m, (const uint64_t *)bp.bseg_off,
+               (const uint8_t *)reject, (const uint32_t *)mpos, (const SegSums *)ss, (const uint8_t *)dirty, t->pg_slack, mode, rsz);
+        CHK(exclusive_scan<PageSums>(t, rsz, rbase, S + 1));
+        CHK(d2h(t, &tot, rbase + S, sizeof(PageSums)));
+        const Pages &g = t->pg;
+        if (g.use_e + tot.v[0] + 1 <= g.cap_e && g.use_k + tot.v[1] <= g.cap_k && g.use_v + tot.v[2] <= g.cap_v) break;
+        if (pass) { g_err = "page build left no room for the batch's moves"; return ST_EDEVICE; }
+        // rebuild: every page gets fresh slack, the append region room for these moves
+        PageSums want(0);
+        for (int q = 0; q < 3; q++) want.v[q] = 2 * tot.v[q];
+        CHK(pages_build(t, t->pg_slack, want));
+        ma = merge_args(view(t), in, bp, reject, S);
+    }
+    PageMergeArgs pa;
+    pa.a = ma;
+    pa.m = t->pg.m;
+    pa.koff = t->pg.koff; pa.voff = t->pg.voff; pa.kheap = t->pg.kheap; pa.vheap = t->pg.vheap;
+    pa.pos = mpos; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
+    pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
+    LAUNCH(t, "page_merge", k_page_merge, (uint32_t)std::min<uint64_t>((S + 3) / 4, 65536), 256, 0, pa);
+    t->pg.use_e += tot.v[0]; t->pg.use_k += tot.v[1]; t->pg.use_v += tot.v[2];
+    t->pg.reloc_e += tot.v[0];
+    t->pg.batches++;
+    t->n += tot.v[3];
+    t->perm_valid = false;
     t->tiles_valid = false;
-    // dirty-path rehash over the merged views
+    // dirty-path rehash over the pages
     HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
-    LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, d, (const uint8_t *)dirty, t->mark);
-    const DeltaView nv = delta_view(t);
-    CHK(rehash_all(t, t->mark, &nv));
+    LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
+    CHK(rehash_all(t, t->mark));
     t->fresh = false;
-    if (t->dl_n > delta_limit(t)) CHK(flush_delta(t));
-    return ST_OK;
-}
-
-// Fold the delta into the base CSR (one full merge; hashes unchanged: the
-// merged views are the tree's content already).
-static int flush_delta(st_tree *t) {
-    if (!t->dl_n) return ST_OK;
-    const uint64_t n = t->dl_n;
-    Scratch sc(t);
-    uint32_t *seg = nullptr;
-    CHK(sc.alloc(&seg, n));
-    LAUNCH(t, "delta_fold", k_delta_entry_seg, grid_for(t->S), 256, 0, (const uint64_t *)t->dl.seg_off, t->S, seg);
-    IngestIn in{};
-    in.n = n; in.krec = t->dl.kheap; in.koff = t->dl.koff; in.vheap = t->dl.vheap; in.voff = t->dl.voff;
-    in.seg_given = seg; in.presorted = true; in.bseg_given = t->dl.seg_off;
-    in.verify_rehash = false;
-    CHK(ingest_direct(t, in));
-    // the delta is empty again (its buffers stay for the next streaming batch)
-    HIPCHK(hipMemsetAsync(t->dl.seg_off, 0, (t->S + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(t->dl.seg_voff, 0, (t->S + 1) * 8, t->stream));
-    HIPCHK(hipMemsetAsync(t->dl.koff, 0, 8, t->stream));
-    HIPCHK(hipMemsetAsync(t->dl.voff, 0, 8, t->stream));
-    t->dl_n = 0;
-    t->dl_new = 0;
-    t->dl_folds++;
     return ST_OK;
 }
 
 static int ingest(st_tree *t, IngestIn &in) {
     in.n_rejected = 0;
     if (in.n == 0) return ST_OK;
-    if (delta_eligible(t, in)) return ingest_delta(t, in);
-    CHK(flush_delta(t));
+    if (pages_eligible(t, in)) return ingest_paged(t, in);
+    CHK(pages_fold(t));
     return ingest_direct(t, in);
 }
 
@@ -1631,10 +1603,10 @@ static int flush_overlay(st_tree *t) {
 }
 
 // Every entry point that reads segments: the small inserts' overlay and the
-// streaming delta folded into the base CSR first.
+// streaming batches' pages folded into the canonical CSR first.
 static int flush_all(st_tree *t) {
     CHK(flush_overlay(t));
-    CHK(flush_delta(t));
+    CHK(pages_fold(t));
     return ST_OK;
 }
 #define FLUSH(t) CHK(flush_all(t))
@@ -1722,7 +1694,7 @@ static int small_prepare(st_tree *t, int op, uint64_t n, const HostRecords &hr, 
     // upper levels it wrote (st_rehash's error is reported by the next call
     // that waits, and that is this one)
     if (t->async_pending) CHK(tsync(t));
-    CHK(flush_delta(t));   // k_small reads the base CSR
+    CHK(pages_fold(t));   // k_small and its overlay flush work on the canonical CSR
     CHK(ensure_small(t));
     if (++t->small_seq == 0) t->small_seq = 1;
     const uint32_t seq = t->small_seq;
@@ -2075,7 +2047,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
             return ST_OK;
         }
     }
-    CHK(flush_overlay(t));   // the delta stays: a streaming batch may go to it (ingest)
+    CHK(flush_overlay(t));   // the pages stay: a streaming batch may go to them (ingest)
     uint8_t *krec = nullptr, *dv = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr;
     uint32_t *dcl = nullptr, *dseg = nullptr;
@@ -2110,7 +2082,7 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
 extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                                int on_device, uint64_t *n_corrupted) {
     ENTER(t);
-    CHK(flush_overlay(t));   // the delta stays: a streaming batch may go to it (ingest)
+    CHK(flush_overlay(t));   // the pages stay: a streaming batch may go to them (ingest)
     if (n_corrupted) *n_corrupted = 0;
     if (n == 0) return ST_OK;
     const int64_t *dkeys = keys;
@@ -2336,7 +2308,7 @@ extern "C" int st_rehash(st_tree *t, int upper) {
         return ST_EINVAL;
     }
     if (upper) CHK(rehash_levels(t, t->H, nullptr));
-    else CHK(rehash_all(t, nullptr, nullptr));
+    else CHK(rehash_all(t, nullptr));
     CHK(erec_after_rehash(t));
     t->fresh = false;
     t->async_pending = true;

@@ -404,10 +404,11 @@ class DeviceTree:
     def set_stream(self, stream_handle):
         _lib.check(self.L.st_set_stream(self.h, ctypes.c_void_p(stream_handle)), 'st_set_stream')
 
-    def delta_stats(self):
-        """(entries in the streaming delta, of them new keys, folds so far)."""
-        v = (ctypes.c_uint64 * 3)()
-        _lib.check(self.L.st_delta_stats(self.h, v), 'st_delta_stats')
+    def page_stats(self):
+        """(pages in use, batches through the pages, page builds, folds,
+        entry slots of segments moved to new pages) -- st_page_stats."""
+        v = np.zeros(5, np.uint64)
+        _lib.check(self.L.st_page_stats(self.h, _ptr(v)), 'st_page_stats')
         return tuple(int(x) for x in v)
 
     def debug_knob(self, knob, value):

@@ -1,7 +1,7 @@
 """Config-5 batch breakdown: a 100M-key tree (one partition = the whole
 range), then per-kernel times (HIP events on the library's stream,
 st_kernel_stats) over 5 timed 1M-key batches (50 % overwrites, 50 % new).
-Usage: python tools/part_breakdown.py [tree_keys] [batches] [delta]"""
+Usage: python tools/part_breakdown.py [tree_keys] [batches] [csr]   (csr: pages off)"""
 import os
 import sys
 import time
@@ -18,9 +18,9 @@ K = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 B = 1_000_000
 dev = torch.device('cuda', 0)
 t = synctree_hip.DeviceTree()
-if len(sys.argv) > 3 and sys.argv[3] == 'delta':   # the streaming delta on
+if len(sys.argv) > 3 and sys.argv[3] == 'csr':   # pages off: every batch merged into the CSR
     from riak_ensemble_amd import _lib  # noqa: E402
-    t.debug_knob(_lib.ST_DBG_DELTA_LIMIT, 0)
+    t.debug_knob(_lib.ST_DBG_PAGES, -1)
 seed = 0x5EED0005
 for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
@@ -41,7 +41,7 @@ t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
 names = ['key_segment', 'iota', 'radix_sort', 'run_bounds', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
-         'segment_hash', 'level_rehash', 'pack_int64', 'delta_aux', 'delta_count', 'delta_fold']
+         'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_merge', 'page_fold']
 t.set_timing(True)
 t.kernel_stats('*reset*')
 t0 = time.perf_counter()
@@ -63,5 +63,5 @@ for j in range(1, K + 1):
     k, v = batches[j]
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
-print('wall %.3f ms/batch (timing off), entries %d, delta (entries, new keys, folds) %s' % ((time.perf_counter() - t0) / K * 1e3, t.num_entries(), t.delta_stats()))
+print('wall %.3f ms/batch (timing off), entries %d, pages (on, batches, builds, folds, moved slots) %s' % ((time.perf_counter() - t0) / K * 1e3, t.num_entries(), t.page_stats()))
 t.close()
