@@ -210,30 +210,18 @@ __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64
     }
 }
 
-__global__ void k_iota(uint32_t *v, uint64_t n) {
-    for (uint64_t i = gtid(); i < n; i += gstride()) v[i] = (uint32_t)i;
+// Bucketing of a batch by segment (a counting sort: histogram, scan = the
+// run bounds, scatter).  The order inside a run is whatever the atomics
+// give; k_run_sort then orders every run by (key, batch index).
+__global__ void k_seg_hist(const uint32_t *seg, uint64_t n, unsigned long long *cnt) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) atomicAdd(&cnt[seg[i]], 1ull);
 }
-
-// bseg_off[s] = first position of segment s in the sorted batch (S+1 entries)
-__global__ void k_run_bounds(const uint32_t *sseg, uint64_t n, uint64_t S, uint64_t *bseg_off) {
-    for (uint64_t i = gtid(); i <= n; i += gstride()) {
-        const uint64_t cur = i < n ? sseg[i] : S;
-        const int64_t prev = i > 0 ? (int64_t)sseg[i - 1] : -1;
-        for (int64_t s = prev + 1; s <= (int64_t)cur; s++) bseg_off[s] = i;
-    }
-}
-
-// Same result for batches much smaller than S (a single-key insert/3): one
-// lane per segment, lower_bound of s in the sorted segment ids (the loop
-// form above would walk all S + 1 bounds in one lane).
-__global__ void k_run_bounds_search(const uint32_t *sseg, uint64_t n, uint64_t S, uint64_t *bseg_off) {
-    for (uint64_t s = gtid(); s <= S; s += gstride()) {
-        uint64_t lo = 0, hi = n;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (sseg[mid] < s) lo = mid + 1; else hi = mid;
-        }
-        bseg_off[s] = lo;
+__global__ void k_seg_scatter(const uint32_t *seg, uint64_t n, unsigned long long *cur, uint32_t *sseg, uint32_t *perm) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint32_t s = seg[i];
+        const unsigned long long p = atomicAdd(&cur[s], 1ull);
+        sseg[p] = s;
+        perm[p] = (uint32_t)i;
     }
 }
 

@@ -10,7 +10,6 @@
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
-#include <rocprim/rocprim.hpp>
 #include <chrono>
 #include <atomic>
 #include <map>
@@ -1245,10 +1244,8 @@ struct BatchPrep {
 static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
     const uint64_t n = in.n, S = t->S;
     CHK(sc.alloc(&bp.keep, n));
-    uint32_t *idx = nullptr;
     CHK(sc.alloc(&bp.seg, n));
     CHK(sc.alloc(&bp.sseg, n));
-    CHK(sc.alloc(&idx, n));
     CHK(sc.alloc(&bp.perm, n));
     CHK(sc.alloc(&bp.bseg_off, S + 1));
     if (in.seg_given) {
@@ -1257,24 +1254,14 @@ static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
         LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, bp.seg);
     }
     if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
-    LAUNCH(t, "iota", k_iota, grid_for(n), 256, 0, idx, n);
-    if (S > 1) {
-        unsigned end_bit = 0;
-        while ((1ull << end_bit) < S) end_bit++;
-        size_t bytes = 0;
-        HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, bp.seg, bp.sseg, idx, bp.perm, (size_t)n, 0u, end_bit, t->stream));
-        uint8_t *tmp = nullptr;
-        CHK(sc.bytes(&tmp, bytes));
-        TimedLaunch tl(t, "radix_sort");
-        HIPCHK(rocprim::radix_sort_pairs(tmp, bytes, bp.seg, bp.sseg, idx, bp.perm, (size_t)n, 0u, end_bit, t->stream));
-    } else {
-        HIPCHK(hipMemcpyAsync(bp.sseg, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
-        HIPCHK(hipMemcpyAsync(bp.perm, idx, n * 4, hipMemcpyDeviceToDevice, t->stream));
-    }
-    if (n < S)
-        LAUNCH(t, "run_bounds", k_run_bounds_search, grid_for(S + 1), 256, 0, (const uint32_t *)bp.sseg, n, S, bp.bseg_off);
-    else
-        LAUNCH(t, "run_bounds", k_run_bounds, grid_for(n + 1), 256, 0, (const uint32_t *)bp.sseg, n, S, bp.bseg_off);
+    // bucket by segment: histogram, scan (= the runs' bounds), scatter
+    unsigned long long *cur = nullptr;
+    CHK(sc.alloc(&cur, S + 1));
+    HIPCHK(hipMemsetAsync(cur, 0, (S + 1) * 8, t->stream));
+    LAUNCH(t, "bucket", k_seg_hist, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cur);
+    CHK(exclusive_scan<uint64_t>(t, reinterpret_cast<const uint64_t *>(cur), bp.bseg_off, S + 1));
+    HIPCHK(hipMemcpyAsync(cur, bp.bseg_off, S * 8, hipMemcpyDeviceToDevice, t->stream));
+    LAUNCH(t, "bucket", k_seg_scatter, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cur, bp.sseg, bp.perm);
     if (t->partitioned)
         LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bp.bseg_off, S, t->part_lo, t->part_hi);
     BatchView bv{in.krec, in.koff};

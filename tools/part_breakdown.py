@@ -39,7 +39,7 @@ for j in range(K + 1):
 k, v = batches[0]
 t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
-names = ['key_segment', 'iota', 'radix_sort', 'run_bounds', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
+names = ['key_segment', 'bucket', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
          'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_merge', 'page_fold']
 t.set_timing(True)
