@@ -393,6 +393,10 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * `value` percent of slack per page (0 = the default, 25 %); -1 = off (every
  * batch merges into the canonical CSR; the pages are folded first). */
 #define ST_DBG_PAGES 2
+/* ST_DBG_PAGE_CHECK: value != 0 runs every paged batch through a checked
+ * merge (a store outside its page is reported as ST_EDEVICE, not performed)
+ * and a consistency check of every page. */
+#define ST_DBG_PAGE_CHECK 3
 int st_debug_knob(st_tree *t, int knob, int64_t value);
 
 /* The paged segment layout of streaming insert batches (no reference

@@ -587,7 +587,15 @@ enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 // bytes -- in one coalesced pass and k_merge_new places the batch records:
 // the whole CSR is rewritten once, with no per-entry source list, length
 // arrays or entry-sized scans.
-__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty) {
+// Per sorted batch record, for the paged merge (pages.h): the old key and
+// value offsets of the entry at its position, relative to its segment's
+// first ones (a page rebuild moves segments, not their content), and its own
+// batch offsets.
+struct RecAt {
+    uint64_t ku, vu, bk, bv;
+};
+
+__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty, RecAt *rat) {
     for (uint64_t s = gtid(); s < a.S; s += gstride()) {
         const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
         uint64_t nold = a.seg_off ? a.seg_end[s] - i0 : 0;
@@ -615,6 +623,7 @@ __global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *
             const uint64_t e = i0 + lo;
             const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
             pos[j] = (uint32_t)lo;
+            if (rat) rat[j] = RecAt{a.koff[e] - a.koff[i0], a.voff[e] - a.voff[i0], a.bv.koff[bi], a.bvoff[bi]};
             const bool kept = a.keep[j] != 0;
             const bool ne = kept && !(a.bop && a.bop[bi]);
             if (kept && eq) {

@@ -110,6 +110,7 @@ struct st_tree {
     // any other call folds it back into the CSR first
     Pages pg;
     int pg_slack = 25;
+    bool pg_check = false;   // st_debug_knob ST_DBG_PAGE_CHECK: the checked page merge + a layout check per batch
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -821,6 +822,10 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
         t->pg_slack = value < 0 ? -1 : value == 0 ? 25 : (int)std::min<int64_t>(value, 400);
         return ST_OK;
     }
+    if (knob == ST_DBG_PAGE_CHECK) {
+        t->pg_check = value != 0;
+        return ST_OK;
+    }
     g_err = "unknown debug knob";
     return ST_EINVAL;
 }
@@ -1336,7 +1341,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     HIPCHK(hipMemsetAsync(ss + S, 0, sizeof(SegSums), t->stream));
     // records outside every run (a partition's clamped runs) keep sums 0
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty);
+    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty, (RecAt *)nullptr);
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     CHK(exclusive_scan<SegSums>(t, ss, sx, S + 1));
     SegSums tot(0);
@@ -1423,10 +1428,11 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
         t->perm_valid = false;
         return ST_OK;
     }
+    // the append region: slack_pct percent of the pages, or the room asked for
     Pages g;
-    g.cap_e = tot.v[0] + std::max<uint64_t>(reserve.v[0], tot.v[0] / 4) + 1;
-    g.cap_k = tot.v[1] + std::max<uint64_t>(reserve.v[1], tot.v[1] / 4);
-    g.cap_v = tot.v[2] + std::max<uint64_t>(reserve.v[2], tot.v[2] / 4);
+    g.cap_e = tot.v[0] + std::max<uint64_t>(reserve.v[0], tot.v[0] * slack_pct / 100) + 1;
+    g.cap_k = tot.v[1] + std::max<uint64_t>(reserve.v[1], tot.v[1] * slack_pct / 100);
+    g.cap_v = tot.v[2] + std::max<uint64_t>(reserve.v[2], tot.v[2] * slack_pct / 100);
     struct Undo {   // a failed build frees what it allocated
         st_tree *t; Pages &g; bool done = false;
         ~Undo() { if (!done) pages_free(t, g); }
@@ -1480,6 +1486,10 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     SegSums *ss = nullptr;
     PageSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
+    RecAt *rat = nullptr;
+    uint2 *kv0 = nullptr;
+    CHK(sc.alloc(&rat, n));
+    CHK(sc.alloc(&kv0, 2 * S));
     CHK(sc.alloc(&ss, S));
     CHK(sc.alloc(&dirty, S));
     CHK(sc.alloc(&mode, S));
@@ -1490,13 +1500,15 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&bx, n + 1));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PageSums), t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty);
+    LAUNCH(t, "merge_count", k_merge_pos8, (uint32_t)std::min<uint64_t>((S + 31) / 32, 8192), 256, 0, ma, mpos, bs, ss, dirty,
+           rat);
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     // in place or to a new page; the moves' places in the append region
     PageSums tot(0);
     for (int pass = 0;; pass++) {
-        LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, view(t), t->pg.m, (const uint64_t *)bp.bseg_off,
-               (const uint8_t *)reject, (const uint32_t *)mpos, (const SegSums *)ss, (const uint8_t *)dirty, t->pg_slack, mode, rsz);
+        LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
+               (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss,
+               (const uint8_t *)dirty, S, t->pg_slack, mode, rsz, kv0);
         CHK(exclusive_scan<PageSums>(t, rsz, rbase, S + 1));
         CHK(d2h(t, &tot, rbase + S, sizeof(PageSums)));
         const Pages &g = t->pg;
@@ -1512,9 +1524,39 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     pa.a = ma;
     pa.m = t->pg.m;
     pa.koff = t->pg.koff; pa.voff = t->pg.voff; pa.kheap = t->pg.kheap; pa.vheap = t->pg.vheap;
-    pa.pos = mpos; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
+    pa.pos = mpos; pa.sseg = bp.sseg; pa.rat = rat; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
+    pa.kv0 = kv0;
     pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
-    LAUNCH(t, "page_merge", k_page_merge, (uint32_t)std::min<uint64_t>((S + 3) / 4, 65536), 256, 0, pa);
+    pa.chk = nullptr;
+    const uint64_t njobs = tot.v[4];
+    PageJob *jobs = nullptr;
+    CHK(sc.alloc(&jobs, njobs + 1));
+    const uint32_t tgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((njobs + 31) / 32, 4096));   // an octet per job
+    LAUNCH(t, "page_jobs", k_page_jobs, grid_for(S), 256, 0, pa, jobs);
+    if (!t->pg_check) {
+        LAUNCH(t, "page_tails", k_page_tails<false>, tgrid, 256, 0, pa, (const PageJob *)jobs, njobs);
+        LAUNCH(t, "page_wide", k_page_wide<false>, grid_for(S), 256, 0, pa);
+        LAUNCH(t, "page_records", k_page_records<false>, grid_for(n), 256, 0, pa, n);
+    } else {   // checked build (debug knob): stores outside their pages reported, not performed
+        CHK(sc.alloc(&pa.chk, 32));
+        HIPCHK(hipMemsetAsync(pa.chk, 0, 256, t->stream));
+        LAUNCH(t, "page_tails", k_page_tails<true>, tgrid, 256, 0, pa, (const PageJob *)jobs, njobs);
+        LAUNCH(t, "page_wide", k_page_wide<true>, grid_for(S), 256, 0, pa);
+        LAUNCH(t, "page_records", k_page_records<true>, grid_for(n), 256, 0, pa, n);
+        LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff,
+               (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, pa.chk);
+        unsigned long long h[32];
+        CHK(d2h(t, h, pa.chk, 256));
+        if (h[0]) {
+            g_err = "page check: " + std::to_string(h[0]) + " violations; first code " + std::to_string(h[1]) + " segment " +
+                    std::to_string(h[2]) + " at " + std::to_string(h[3]) + " bound " + std::to_string(h[4]) + "; batch " +
+                    std::to_string(t->pg.batches) + "; koff";
+            for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[5 + q]);
+            g_err += "; voff";
+            for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[17 + q]);
+            return ST_EDEVICE;
+        }
+    }
     t->pg.use_e += tot.v[0]; t->pg.use_k += tot.v[1]; t->pg.use_v += tot.v[2];
     t->pg.reloc_e += tot.v[0];
     t->pg.batches++;

@@ -407,8 +407,8 @@ class DeviceTree:
     def page_stats(self):
         """(pages in use, batches through the pages, page builds, folds,
         entry slots of segments moved to new pages) -- st_page_stats."""
-        v = np.zeros(5, np.uint64)
-        _lib.check(self.L.st_page_stats(self.h, _ptr(v)), 'st_page_stats')
+        v = (ctypes.c_uint64 * 5)()
+        _lib.check(self.L.st_page_stats(self.h, v), 'st_page_stats')
         return tuple(int(x) for x in v)
 
     def debug_knob(self, knob, value):

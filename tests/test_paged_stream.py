@@ -47,6 +47,7 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack):
     assert dev.insert_int64(keys[:n0], _obj(range(n0))) == 0
     ora.bulk_load_int64(keys[:n0], _obj(range(n0)))
     dev.debug_knob(_lib.ST_DBG_PAGES, slack)
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)   # every page store bounds-checked, every page validated
     nxt = n0
     for b in range(30):
         old = rng.integers(0, nxt, batch // 2)                 # overwrites (Seq + 1), some repeated in the batch
@@ -118,6 +119,7 @@ def test_variable_keys_and_values_through_pages(slack):
     assert all(x is None for x in st)
     ora.bulk_load(ks, [base[k] for k in ks])
     dev.debug_knob(_lib.ST_DBG_PAGES, slack)
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)   # every page store bounds-checked, every page validated
     for b in range(12):
         bk = [ks[i] for i in rng.integers(0, len(ks), 300)] + [_rand_bin(rng, 1, 24) for _ in range(300)]
         bv = [_rand_bin(rng, 0, 40) for _ in bk]
@@ -150,6 +152,7 @@ def test_equal_numbers_through_pages():
         ref = R.insert(k, v, ref)
     assert all(x is None for x in dev.insert_batch(ks, vs))
     dev.debug_knob(_lib.ST_DBG_PAGES, 5)
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
     pairs = [(a, b) for a, b in _same_segment_pairs(S, 40) if isinstance(a, int) and a < 3000]
     assert len(pairs) >= 10
     for b in range(8):
@@ -182,6 +185,7 @@ def test_corrupted_segment_rejects_streamed_keys(pages):
     dev, ora = synctree_hip.DeviceTree(16, S), C.OTree(16, S)
     assert dev.insert_int64(keys[:n0], vals[:n0]) == 0
     ora.bulk_load_int64(keys[:n0], vals[:n0])
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
     if not pages:
         dev.debug_knob(_lib.ST_DBG_PAGES, -1)
     # a streamed batch, then corrupt a key's segment (corrupt/2 folds the pages)
