@@ -125,6 +125,19 @@ def _dec(b, i):
         if tail != []:
             raise BadTerm('improper list outside the restated domain')
         return xs, i
+    if tg == 99:   # FLOAT_EXT: "%.20e" in 31 bytes
+        need(31)
+        return float(b[i:i + 31].split(b'\0')[0].decode('ascii')), i + 31
+    if tg == 116:  # MAP_EXT
+        need(4)
+        n = struct.unpack('>I', b[i:i + 4])[0]
+        i += 4
+        pairs = []
+        for _ in range(n):
+            k, i = _dec(b, i)
+            v, i = _dec(b, i)
+            pairs.append((k, v))
+        return ST.ErlMap(pairs), i
     raise BadTerm('tag %d outside the restated domain' % tg)
 
 

@@ -26,10 +26,14 @@ Every function cites the reference line it restates
 
 Erlang terms are modelled as: integers -> ``int``, floats -> ``float``,
 binaries -> ``bytes``, atoms -> ``str``, tuples -> ``tuple``, proper lists ->
-``list``.  Erlang term order (ERTS): number < atom < tuple < nil < list <
-bitstring; numbers by value (an integer and a float compare as numbers),
-atoms by their text, tuples by size then elements, lists element-wise with a
-prefix first, binaries bytewise with a prefix first.  Keys outside
+``list``, maps -> any ``collections.abc.Mapping`` (its ``items()``).  Erlang
+term order (ERTS): number < atom < tuple < map < nil < list < bitstring;
+numbers by value (an integer and a float compare as numbers), atoms by their
+text, tuples by size then elements, maps by size, then their keys in map-key
+order, then their values in that order (map keys compare exactly: every
+integer before every float, 1 =/= 1.0 -- the ERTS "Term Comparisons" rules),
+lists element-wise with a prefix first, binaries bytewise with a prefix
+first.  Keys outside
 integer/atom/binary are hashed through term_to_binary (synctree.erl:267-268),
 restated below from the ERTS external term format (ETF_ATOMS selects the OTP
 era of atom encoding: 'latin1' = before OTP 26, 'utf8' = OTP 26+).
@@ -41,6 +45,7 @@ see tests/test_oracle_ref.py.
 
 import hashlib
 import math
+from collections.abc import Mapping
 
 WIDTH = 16                     # synctree.erl:88
 SEGMENTS = 1024 * 1024         # synctree.erl:89
@@ -53,6 +58,7 @@ CORRUPTED = 'corrupted'
 _TYPE_RANK_NUMBER = 0
 _TYPE_RANK_ATOM = 1
 _TYPE_RANK_TUPLE = 6
+_TYPE_RANK_MAP = 7
 _TYPE_RANK_NIL = 8
 _TYPE_RANK_LIST = 9
 _TYPE_RANK_BITSTRING = 10
@@ -83,7 +89,69 @@ def term_key(t):
         return (_TYPE_RANK_LIST, [term_key(e) for e in t])
     if isinstance(t, (bytes, bytearray)):
         return (_TYPE_RANK_BITSTRING, bytes(t))
+    if isinstance(t, Mapping):
+        items = _map_items(t)
+        return (_TYPE_RANK_MAP, len(items), tuple(exact_term_key(k) for k, _ in items),
+                tuple(term_key(v) for _, v in items))
     raise ErlangCrash('term outside the restated domain: %r' % (t,))
+
+
+def exact_term_key(t):
+    """Sort key of the exact order map keys compare in (=:=): numbers split
+    by type, integers first; everything under the key compares exactly."""
+    if isinstance(t, bool):
+        raise ErlangCrash('booleans are atoms in Erlang; pass "true"/"false"')
+    if isinstance(t, int):
+        return (_TYPE_RANK_NUMBER, 0, t)
+    if isinstance(t, float):
+        return (_TYPE_RANK_NUMBER, 1, t)
+    if isinstance(t, tuple):
+        return (_TYPE_RANK_TUPLE, len(t), tuple(exact_term_key(e) for e in t))
+    if isinstance(t, list) and t:
+        return (_TYPE_RANK_LIST, [exact_term_key(e) for e in t])
+    if isinstance(t, Mapping):
+        items = _map_items(t)
+        return (_TYPE_RANK_MAP, len(items), tuple(exact_term_key(k) for k, _ in items),
+                tuple(exact_term_key(v) for _, v in items))
+    return term_key(t)
+
+
+class ErlMap(Mapping):
+    """An Erlang map as the restatement models it: pairs with exactly
+    distinct keys (1 and 1.0 are two keys)."""
+
+    def __init__(self, pairs=()):
+        d = {}
+        for k, v in (pairs.items() if isinstance(pairs, Mapping) else pairs):
+            d[repr(exact_term_key(k))] = (k, v)
+        self._pairs = list(d.values())
+
+    def __getitem__(self, key):
+        ek = exact_term_key(key)
+        for k, v in self._pairs:
+            if exact_term_key(k) == ek:
+                return v
+        raise KeyError(key)
+
+    def __iter__(self):
+        return (k for k, _ in self._pairs)
+
+    def __len__(self):
+        return len(self._pairs)
+
+    def items(self):
+        return list(self._pairs)
+
+    def __eq__(self, other):
+        return isinstance(other, Mapping) and term_key(self) == term_key(other)
+
+    def __hash__(self):
+        return hash(repr(term_key(self)))
+
+
+def _map_items(m):
+    """A map's pairs in map-key order (the order of an ERTS flatmap)."""
+    return sorted(m.items(), key=lambda kv: exact_term_key(kv[0]))
 
 
 def _atom_ext(a):
@@ -129,6 +197,9 @@ def _ext(t):
         if len(t) < 65536 and all(type(e) is int and 0 <= e < 256 for e in t):
             return b'k' + len(t).to_bytes(2, 'big') + bytes(t)            # STRING_EXT
         return b'l' + len(t).to_bytes(4, 'big') + b''.join(_ext(e) for e in t) + b'j'
+    if isinstance(t, Mapping):   # MAP_EXT; a flatmap (<= 32 keys) writes its pairs in map-key order
+        items = _map_items(t)
+        return b't' + len(items).to_bytes(4, 'big') + b''.join(_ext(k) + _ext(v) for k, v in items)
     raise ErlangCrash('term outside the restated domain: %r' % (t,))
 
 

@@ -284,15 +284,17 @@ __global__ void k_snap_entries(DevTree t, uint64_t n, uint64_t sb, const uint64_
 
 // ---------------------------------------------------------------------------
 // Restore: binary_to_term of the records on the device.
-#define DK_DEPTH 48   // open tuples / lists of one restored key (deeper keys: ST_EINVAL)
+#define DK_DEPTH 48   // open tuples / lists of one key the device decodes (deeper keys: the host's)
 //
 // bad = malformed bytes (the reference's binary_to_term raises and fetch/3
 // answers Default: the node is absent); dom = a well-formed term the device
-// tree cannot hold (the whole restore fails with ST_EINVAL).
+// tree cannot hold (the whole restore fails with ST_EINVAL); host = a key
+// this decoder leaves to the host's (term_key.h segment_from_etf): maps,
+// FLOAT_EXT, keys nested deeper than DK_DEPTH.
 struct DEtf {
     const uint8_t *p, *e;
-    bool bad, dom;
-    __device__ DEtf(const uint8_t *a, const uint8_t *b) : p(a), e(b), bad(false), dom(false) {}
+    bool bad, dom, host;
+    __device__ DEtf(const uint8_t *a, const uint8_t *b) : p(a), e(b), bad(false), dom(false), host(false) {}
     __device__ bool need(uint64_t n) {
         if (bad || (uint64_t)(e - p) < n) bad = true;
         return !bad;
@@ -312,7 +314,7 @@ struct DEtf {
     }
     // a standard ETF tag outside the node domain, or garbage
     __device__ void other(uint32_t tg) {
-        if (tg == 70 || tg == 77 || tg == 80 || tg == 88 || tg == 90 || (tg >= 97 && tg <= 119)) dom = true;
+        if (tg == 70 || tg == 77 || tg == 80 || tg == 88 || tg == 90 || (tg >= 97 && tg <= 120)) dom = true;
         else bad = true;
     }
     __device__ bool integer(int64_t &v) {
@@ -556,7 +558,7 @@ struct DEtf {
                 sk_put(dst, o, KEYTAG_TUPLE);
                 for (int i = 3; i >= 0; i--) sk_put(dst, o, (n >> (8 * i)) & 0xFF);
                 if (n) {
-                    if (sp == DK_DEPTH) { dom = true; return false; }
+                    if (sp == DK_DEPTH) { host = true; return false; }
                     kind[sp] = 0; rem[sp] = n; sp++;
                     opened = true;
                 }
@@ -576,14 +578,15 @@ struct DEtf {
                 const uint32_t n = u32();
                 if (bad) return false;
                 if (n == 0) { dom = true; return false; }   // never written by term_to_binary
-                if (sp == DK_DEPTH) { dom = true; return false; }
+                if (sp == DK_DEPTH) { host = true; return false; }
                 sk_put(dst, o, KEYTAG_LIST);
                 kind[sp] = 1; rem[sp] = n; sp++;
                 opened = true;
                 break;
             }
+            case 99: case 116: host = true; return false;   // FLOAT_EXT, maps: the host's decoder
             default:
-                other(tg);   // pids, ports, refs, funs, maps, bitstrings, FLOAT_EXT: outside the key domain
+                other(tg);   // pids, ports, refs, funs, bitstrings: outside the key domain
                 return false;
             }
             if (dom) return false;
@@ -649,6 +652,7 @@ struct DEtf {
 #define RST_SKIPPED 1
 #define RST_DOM 2
 #define RST_DOMSLOT 3
+#define RST_HOST 4      // segments handed to the host decoder (segok 2)
 
 __device__ inline void rst_dom(unsigned long long *ctr, uint64_t r) {
     atomicOr(&ctr[RST_DOM], 1ull);
@@ -754,10 +758,11 @@ __global__ void k_rest_nodes(DevTree t, uint64_t R, const unsigned long long *re
             uint32_t kl = 0, len = 0;
             const uint8_t *v;
             good = in.tuple2() && in.key(nullptr, kl) && in.binary(v, len);
-            if (in.dom) break;
+            if (in.dom || in.host) break;
             kb += kl;
             vb += len;
         }
+        if (in.host) { segok[r - sb] = 2; atomicAdd(&ctr[RST_HOST], 1ull); continue; }
         if (good && !in.dom && cnt) good = in.nil();
         good = good && !in.dom && in.end();
         if (in.dom) { rst_dom(ctr, r); continue; }
@@ -778,7 +783,7 @@ __global__ void k_rest_segments(DevTree t, const unsigned long long *recof, cons
                                 unsigned long long *ctr) {
     const uint64_t sb = t.base[t.H + 1];
     for (uint64_t s = gtid(); s < t.S; s += gstride()) {
-        if (!segok[s]) continue;
+        if (segok[s] != 1) continue;
         const uint64_t i = recof[sb + s] - 1;
         DEtf in(vh + vo[i], vh + vo[i + 1]);
         uint32_t cnt = 0;
@@ -801,5 +806,34 @@ __global__ void k_rest_segments(DevTree t, const unsigned long long *recof, cons
             kp += kl;
             vp += len;
         }
+    }
+}
+
+// The segments the host decoded (hs[i], entries [he[i], he[i+1]) of the
+// host's key records hk / values hv with end offsets hko / hvo, one leading
+// 0): sizes before the scans, entries after them.
+__global__ void k_rest_host_sizes(uint64_t n, const uint64_t *hs, const uint64_t *he, const uint64_t *hko,
+                                  const uint64_t *hvo, uint64_t *ec, uint64_t *kc, uint64_t *vc) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t s = hs[i], a = he[i], b = he[i + 1];
+        ec[s] = b - a;
+        kc[s] = hko[b] - hko[a];
+        vc[s] = hvo[b] - hvo[a];
+    }
+}
+
+__global__ void k_rest_host_write(uint64_t n, const uint64_t *hs, const uint64_t *he, const uint64_t *hko,
+                                  const uint64_t *hvo, const uint8_t *hk, const uint8_t *hv, const uint64_t *seg_off,
+                                  const uint64_t *kbase, const uint64_t *vbase, uint64_t *koff, uint8_t *kheap,
+                                  uint64_t *voff, uint8_t *vheap) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t s = hs[i], a = he[i], b = he[i + 1];
+        const uint64_t e = seg_off[s], kp = kbase[s], vp = vbase[s], k0 = hko[a], v0 = hvo[a];
+        for (uint64_t j = a; j < b; j++) {
+            koff[e + j - a] = kp + hko[j] - k0;
+            voff[e + j - a] = vp + hvo[j] - v0;
+        }
+        for (uint64_t q = k0; q < hko[b]; q++) kheap[kp + q - k0] = hk[q];
+        for (uint64_t q = v0; q < hvo[b]; q++) vheap[vp + q - v0] = hv[q];
     }
 }

@@ -1487,9 +1487,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     PageSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
-    uint2 *kv0 = nullptr;
     CHK(sc.alloc(&rat, n));
-    CHK(sc.alloc(&kv0, 2 * S));
     CHK(sc.alloc(&ss, S));
     CHK(sc.alloc(&dirty, S));
     CHK(sc.alloc(&mode, S));
@@ -1500,15 +1498,14 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&bx, n + 1));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PageSums), t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos8, (uint32_t)std::min<uint64_t>((S + 31) / 32, 8192), 256, 0, ma, mpos, bs, ss, dirty,
-           rat);
+    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty, rat);
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     // in place or to a new page; the moves' places in the append region
     PageSums tot(0);
     for (int pass = 0;; pass++) {
         LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
                (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss,
-               (const uint8_t *)dirty, S, t->pg_slack, mode, rsz, kv0);
+               (const uint8_t *)dirty, S, t->pg_slack, mode, rsz);
         CHK(exclusive_scan<PageSums>(t, rsz, rbase, S + 1));
         CHK(d2h(t, &tot, rbase + S, sizeof(PageSums)));
         const Pages &g = t->pg;
@@ -1524,25 +1521,15 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     pa.a = ma;
     pa.m = t->pg.m;
     pa.koff = t->pg.koff; pa.voff = t->pg.voff; pa.kheap = t->pg.kheap; pa.vheap = t->pg.vheap;
-    pa.pos = mpos; pa.sseg = bp.sseg; pa.rat = rat; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
-    pa.kv0 = kv0;
+    pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
     pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
     pa.chk = nullptr;
-    const uint64_t njobs = tot.v[4];
-    PageJob *jobs = nullptr;
-    CHK(sc.alloc(&jobs, njobs + 1));
-    const uint32_t tgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((njobs + 31) / 32, 4096));   // an octet per job
-    LAUNCH(t, "page_jobs", k_page_jobs, grid_for(S), 256, 0, pa, jobs);
     if (!t->pg_check) {
-        LAUNCH(t, "page_tails", k_page_tails<false>, tgrid, 256, 0, pa, (const PageJob *)jobs, njobs);
-        LAUNCH(t, "page_wide", k_page_wide<false>, grid_for(S), 256, 0, pa);
-        LAUNCH(t, "page_records", k_page_records<false>, grid_for(n), 256, 0, pa, n);
-    } else {   // checked build (debug knob): stores outside their pages reported, not performed
+        LAUNCH(t, "page_merge", k_page_merge<false>, grid_for(S), 256, 0, pa);
+    } else {   // checked build (debug knob): merges that would leave their pages reported, not performed
         CHK(sc.alloc(&pa.chk, 32));
         HIPCHK(hipMemsetAsync(pa.chk, 0, 256, t->stream));
-        LAUNCH(t, "page_tails", k_page_tails<true>, tgrid, 256, 0, pa, (const PageJob *)jobs, njobs);
-        LAUNCH(t, "page_wide", k_page_wide<true>, grid_for(S), 256, 0, pa);
-        LAUNCH(t, "page_records", k_page_records<true>, grid_for(n), 256, 0, pa, n);
+        LAUNCH(t, "page_merge", k_page_merge<true>, grid_for(S), 256, 0, pa);
         LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff,
                (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, pa.chk);
         unsigned long long h[32];
@@ -2782,7 +2769,7 @@ __global__ void k_target_counts(DevTree t, const uint64_t *targets, uint64_t n, 
     for (uint64_t i = gtid(); i <= n; i += gstride()) {
         if (i == n) { cnt[i] = 0; break; }
         const uint64_t s = targets[i];
-        cnt[i] = status[i] ? 0 : t.seg_off[s + 1] - t.seg_off[s];
+        cnt[i] = status[i] ? 0 : t.seg_end[s] - t.seg_off[s];
     }
 }
 
@@ -3433,8 +3420,11 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     unsigned long long *recof = nullptr, *ctr = nullptr;
     uint16_t *stag = nullptr;
     uint4 *smd = nullptr;
+    uint64_t *dhs = nullptr, *dhe = nullptr, *dhko = nullptr, *dhvo = nullptr;
+    uint8_t *dhk = nullptr, *dhv = nullptr;
     auto done = [&](bool keep_new) {
-        void *ps[] = {dkh, dvh, did, segok, serec, dko, dvo, ec, kc, vc, kbase, vbase, recof, ctr, stag, smd};
+        void *ps[] = {dkh, dvh, did, segok, serec, dko, dvo, ec, kc, vc, kbase, vbase, recof, ctr, stag, smd,
+                      dhs, dhe, dhko, dhvo, dhk, dhv};
         for (void *p : ps) dfree(t, p);
         if (!keep_new) { dfree(t, nso); dfree(t, nsvo); dfree(t, nko); dfree(t, nvo); dfree(t, nkh); dfree(t, nvh); }
     };
@@ -3451,13 +3441,14 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     RCHK(h2d(t, dkh, kheap + (n ? koff[0] : 0), kin)); RCHK(h2d(t, dvh, vheap + (n ? voff[0] : 0), vin));
     RCHK(h2d(t, dko, ko0.data(), (n + 1) * 8)); RCHK(h2d(t, dvo, vo0.data(), (n + 1) * 8));
     RCHK(h2d(t, did, tree_id, id_len));
-    RCHK(dalloc_t(t, &recof, R)); RCHK(dalloc_t(t, &ctr, 4)); RCHK(dalloc_t(t, &stag, R)); RCHK(dalloc_t(t, &smd, R));
+    RCHK(dalloc_t(t, &recof, R)); RCHK(dalloc_t(t, &ctr, 5)); RCHK(dalloc_t(t, &stag, R)); RCHK(dalloc_t(t, &smd, R));
     RCHK(dalloc_t(t, &ec, S + 1)); RCHK(dalloc_t(t, &kc, S + 1)); RCHK(dalloc_t(t, &vc, S + 1)); RCHK(dalloc_t(t, &segok, S));
     RCHK(dalloc_t(t, &serec, R));
     HIPCHK(hipMemsetAsync(serec, 0, R, t->stream));
     HIPCHK(hipMemsetAsync(recof, 0, R * 8, t->stream));
     HIPCHK(hipMemsetAsync(ctr, 0, 3 * 8, t->stream));
     HIPCHK(hipMemsetAsync(ctr + RST_DOMSLOT, 0xFF, 8, t->stream));
+    HIPCHK(hipMemsetAsync(ctr + RST_HOST, 0, 8, t->stream));
     HIPCHK(hipMemsetAsync(stag, 0, R * 2, t->stream));
     HIPCHK(hipMemsetAsync(smd, 0, R * 16, t->stream));
     HIPCHK(hipMemsetAsync(ec + S, 0, 8, t->stream));
@@ -3467,7 +3458,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
                   (const uint8_t *)dkh, (const uint64_t *)dko, recof);
     LAUNCH(t, "rest_nodes", k_rest_nodes, grid_for(R), 256, 0, d, R, (const unsigned long long *)recof,
            (const uint8_t *)dvh, (const uint64_t *)dvo, stag, smd, ec, kc, vc, segok, serec, ctr);
-    unsigned long long hc[4] = {0, 0, 0, 0};
+    unsigned long long hc[5] = {0, 0, 0, 0, 0};
     auto domain_error = [&]() {
         const uint64_t r = hc[RST_DOMSLOT];
         uint32_t L = 0;
@@ -3480,6 +3471,52 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     };
     RCHK(d2h(t, hc, ctr, sizeof(hc)));
     if (hc[RST_DOM]) return domain_error();
+    // segments whose keys the device decoder leaves to the host (maps,
+    // FLOAT_EXT, deep nesting): decoded here (term_key.h), sized into the
+    // scans, written after them
+    std::vector<uint64_t> hs, he{0}, hko{0}, hvo{0};
+    std::vector<uint8_t> hk, hv;
+    if (hc[RST_HOST]) {
+        const uint64_t sb = t->base[t->H + 1];
+        std::vector<uint8_t> ok(S);
+        std::vector<unsigned long long> rof(S);
+        RCHK(d2h(t, ok.data(), segok, S));
+        RCHK(d2h(t, rof.data(), recof + sb, S * 8));
+        auto rcmp = [&](uint64_t j) {   // record j-1 vs record j, Erlang term order (rec_cmp)
+            const uint8_t *a = hk.data() + hko[j - 1], *b = hk.data() + hko[j];
+            const uint64_t la = krec_order_len(a, hko[j] - hko[j - 1]), lb = krec_order_len(b, hko[j + 1] - hko[j]);
+            const int c = memcmp(a, b, std::min(la, lb));
+            return c ? c : (la < lb ? -1 : la > lb ? 1 : 0);
+        };
+        for (uint64_t sg = 0; sg < S; sg++) {
+            if (ok[sg] != 2) continue;
+            const uint64_t i = rof[sg] - 1;
+            const size_t kz = hk.size(), vz = hv.size(), ez = hko.size();
+            int st = termkey::segment_from_etf(vheap + voff[i], voff[i + 1] - voff[i], hk, hko, hv, hvo);
+            for (uint64_t j = ez; st == termkey::SEG_OK && j + 1 < hko.size(); j++)
+                if (rcmp(j) >= 0) st = termkey::SEG_DOM;   // an orddict: strictly ascending
+            if (st == termkey::SEG_DOM) { hc[RST_DOMSLOT] = sb + sg; return domain_error(); }
+            if (st == termkey::SEG_BAD) {   // binary_to_term raises: the node is absent
+                hk.resize(kz); hv.resize(vz); hko.resize(ez); hvo.resize(ez);
+                hc[RST_SKIPPED]++;
+                continue;
+            }
+            hs.push_back(sg);
+            he.push_back(hko.size() - 1);
+            hc[RST_LOADED]++;
+        }
+    }
+    const uint64_t nh = hs.size();
+    if (nh) {
+        RCHK(dalloc_t(t, &dhs, nh)); RCHK(dalloc_t(t, &dhe, nh + 1));
+        RCHK(dalloc_t(t, &dhko, hko.size())); RCHK(dalloc_t(t, &dhvo, hvo.size()));
+        RCHK(dalloc(t, (void **)&dhk, hk.size() + 1)); RCHK(dalloc(t, (void **)&dhv, hv.size() + 1));
+        RCHK(h2d(t, dhs, hs.data(), nh * 8)); RCHK(h2d(t, dhe, he.data(), (nh + 1) * 8));
+        RCHK(h2d(t, dhko, hko.data(), hko.size() * 8)); RCHK(h2d(t, dhvo, hvo.data(), hvo.size() * 8));
+        RCHK(h2d(t, dhk, hk.data(), hk.size())); RCHK(h2d(t, dhv, hv.data(), hv.size()));
+        LAUNCH(t, "rest_host_sizes", k_rest_host_sizes, grid_for(nh), 256, 0, nh, (const uint64_t *)dhs,
+               (const uint64_t *)dhe, (const uint64_t *)dhko, (const uint64_t *)dhvo, ec, kc, vc);
+    }
     RCHK(dalloc_t(t, &nso, S + 1)); RCHK(dalloc_t(t, &kbase, S + 1)); RCHK(dalloc_t(t, &vbase, S + 1));
     RCHK(exclusive_scan<uint64_t>(t, ec, nso, S + 1));
     RCHK(exclusive_scan<uint64_t>(t, kc, kbase, S + 1));
@@ -3499,9 +3536,17 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     LAUNCH(t, "rest_segments", k_rest_segments, grid_for(S), 256, 0, d, (const unsigned long long *)recof,
            (const uint8_t *)dvh, (const uint64_t *)dvo, (const uint8_t *)segok, (const uint64_t *)nso,
            (const uint64_t *)kbase, (const uint64_t *)vbase, nko, nkh, nvo, nvh, ctr);
+    if (nh)
+        LAUNCH(t, "rest_host_write", k_rest_host_write, grid_for(nh), 256, 0, nh, (const uint64_t *)dhs,
+               (const uint64_t *)dhe, (const uint64_t *)dhko, (const uint64_t *)dhvo, (const uint8_t *)dhk,
+               (const uint8_t *)dhv, (const uint64_t *)nso, (const uint64_t *)kbase, (const uint64_t *)vbase, nko,
+               nkh, nvo, nvh);
     LAUNCH(t, "seg_voff", k_seg_voff, grid_for(S + 1), 256, 0, (const uint64_t *)nso, (const uint64_t *)nvo, S, nsvo);
-    RCHK(d2h(t, hc, ctr, sizeof(hc)));
-    if (hc[RST_DOM]) return domain_error();
+    {
+        unsigned long long hd[5];
+        RCHK(d2h(t, hd, ctr, sizeof(hd)));
+        if (hd[RST_DOM]) { hc[RST_DOMSLOT] = hd[RST_DOMSLOT]; return domain_error(); }
+    }
     // commit: node arrays and the new CSR
     HIPCHK(hipMemcpyAsync(t->tag, stag, R * 2, hipMemcpyDeviceToDevice, t->stream));
     HIPCHK(hipMemcpyAsync(t->md5, smd, R * 16, hipMemcpyDeviceToDevice, t->stream));

@@ -23,6 +23,8 @@
 //         (floats beyond int64 are integral: the SK of the equal integer)
 //   0x20  atom              [0x20][utf8, escaped][00 01]
 //   0x30  tuple             [0x30][arity u32 BE][SK(e1)]...[SK(en)]
+//   0x34  map               [0x34][size u32 BE][SKX(k1)]...[SKX(kn)][SK(v1)]...[SK(vn)]
+//                           with k1 < ... < kn in map-key order
 //   0x38  nil               [0x38]
 //   0x40  list              [0x40][SK(h1)]...[end]; end = [03] for a proper
 //                           list, [02][SK(T)] for a tail T < nil (number,
@@ -31,7 +33,13 @@
 //
 // Escaping (nested atoms / binaries only): 0x00 -> 00 FF, end -> 00 01.
 // ERTS type order: number < atom < (reference < fun < port < pid) < tuple <
-// (map) < nil < list < bitstring; the bracketed types are rejected.  Numbers
+// map < nil < list < bitstring; the bracketed types are rejected.  Maps order
+// by size, then their keys in map-key order, then their values in key order;
+// map keys compare EXACTLY (=:=, "integers are less than floats" in map-key
+// order: 1 and 1.0 are two keys, every integer sorts before every float).
+// SKX, the exact form used for map keys (and everything under them), is the
+// SK with numbers split by type: integers as above, floats as
+// [0x18][IEEE bits, order-preserving] (-0.0 as 0.0).  Numbers
 // compare by value, and an integer and a float of equal value (1 and 1.0,
 // also nested: {1} and {1.0}) have the SAME SK: they are equal keys (==), as
 // orddict:store/erase, lists:keyfind and orddict_delta treat them; the key
@@ -51,7 +59,9 @@
 #define KEYTAG_INT 0x10
 #define KEYTAG_NUMHI 0x11
 #define KEYTAG_ATOM 0x20
+#define KEYTAG_XFLOAT 0x18
 #define KEYTAG_TUPLE 0x30
+#define KEYTAG_MAP 0x34
 #define KEYTAG_NIL 0x38
 #define KEYTAG_LIST 0x40
 #define KEYTAG_BINARY 0x50
@@ -66,6 +76,7 @@ struct Etf {
     const uint8_t *p, *e;
     std::string err;
     int depth = 0;
+    bool dom = false;   // err is a well-formed term outside the key domain (not malformed bytes)
     bool need(size_t n) {
         if ((size_t)(e - p) < n) { if (err.empty()) err = "truncated term_to_binary"; return false; }
         return true;
@@ -74,6 +85,13 @@ struct Etf {
     uint32_t u16() { uint32_t v = ((uint32_t)p[0] << 8) | p[1]; p += 2; return v; }
     uint32_t u32() { uint32_t v = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; p += 4; return v; }
 };
+
+// the standard ETF tags: a term the decoder does not take is outside the
+// domain (pids, ports, refs, funs, bitstrings, compressed terms); any other
+// byte is garbage
+inline bool etf_known_tag(uint32_t tag) {
+    return tag == 70 || tag == 77 || tag == 80 || tag == 88 || tag == 90 || (tag >= 97 && tag <= 120);
+}
 
 // magnitude bytes (big-endian, no leading zeros) + sign -> SK
 inline void sk_integer(std::vector<uint8_t> &o, bool neg, const std::vector<uint8_t> &mag) {
@@ -150,10 +168,20 @@ inline void sk_float(std::vector<uint8_t> &o, double v) {
 }
 
 // term -> SK; returns the ERTS type class of the term (for list tails), or -1
-enum Cls { C_NUM = 0, C_ATOM = 1, C_TUPLE = 2, C_NIL = 3, C_LIST = 4, C_BIN = 5 };
+enum Cls { C_NUM = 0, C_ATOM = 1, C_TUPLE = 2, C_NIL = 3, C_LIST = 4, C_BIN = 5, C_MAP = 6 };
 
-inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, int64_t *ival, bool *is_big,
-                   std::vector<uint8_t> *bigmag, bool *bigneg);
+inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool exact, bool *is_int64, int64_t *ival,
+                   bool *is_big, std::vector<uint8_t> *bigmag, bool *bigneg);
+
+// a float in the exact (map-key) order: above every integer, by value
+inline void skx_float(std::vector<uint8_t> &o, double v) {
+    if (v == 0.0) v = 0.0;   // -0.0 =:= 0.0
+    uint64_t b;
+    std::memcpy(&b, &v, 8);
+    b = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    o.push_back(KEYTAG_XFLOAT);
+    for (int i = 7; i >= 0; i--) o.push_back((uint8_t)(b >> (8 * i)));
+}
 
 inline bool sk_bigint(Etf &in, uint32_t n, std::vector<uint8_t> &mag, bool &neg) {
     if (!in.need(1 + (size_t)n)) return false;
@@ -168,10 +196,10 @@ inline bool sk_bigint(Etf &in, uint32_t n, std::vector<uint8_t> &mag, bool &neg)
     return true;
 }
 
-inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o);
+inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o, bool exact);
 
-inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, int64_t *ival, bool *is_big,
-                   std::vector<uint8_t> *bigmag, bool *bigneg) {
+inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool exact, bool *is_int64, int64_t *ival,
+                   bool *is_big, std::vector<uint8_t> *bigmag, bool *bigneg) {
     if (++in.depth > 200) { in.err = "term nested too deeply"; return -1; }
     if (!in.need(1)) return -1;
     const uint32_t tag = in.u8();
@@ -222,7 +250,8 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
         double v;
         std::memcpy(&v, &b, 8);
         if (!std::isfinite(v)) { in.err = "non-finite float"; return -1; }
-        sk_float(o, v);
+        if (exact) skx_float(o, v);
+        else sk_float(o, v);
         cls = C_NUM;
         break;
     }
@@ -235,7 +264,8 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
         char *end = nullptr;
         const double v = std::strtod(buf, &end);
         if (end == buf || !std::isfinite(v)) { in.err = "bad FLOAT_EXT"; return -1; }
-        sk_float(o, v);
+        if (exact) skx_float(o, v);
+        else sk_float(o, v);
         cls = C_NUM;
         break;
     }
@@ -260,7 +290,7 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
         o.push_back(KEYTAG_TUPLE);
         for (int i = 3; i >= 0; i--) o.push_back((uint8_t)(n >> (8 * i)));
         for (uint32_t i = 0; i < n; i++)
-            if (sk_term(in, o, false, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
+            if (sk_term(in, o, false, exact, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
         cls = C_TUPLE;
         break;
     }
@@ -286,7 +316,7 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
     case 108: { // LIST_EXT
         in.p--;
         o.push_back(KEYTAG_LIST);
-        if (sk_list_rest(in, o) < 0) return -1;
+        if (sk_list_rest(in, o, exact) < 0) return -1;
         cls = C_LIST;
         break;
     }
@@ -300,8 +330,32 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
         cls = C_BIN;
         break;
     }
+    case 116: { // MAP_EXT: Arity, then Arity key/value pairs in any order
+        if (!in.need(4)) return -1;
+        const uint32_t n = in.u32();
+        if ((uint64_t)n * 2 > (uint64_t)(in.e - in.p)) { in.err = "truncated term_to_binary"; return -1; }
+        std::vector<std::vector<uint8_t>> ks(n), vs(n);
+        std::vector<uint32_t> ord(n);
+        for (uint32_t i = 0; i < n; i++) {
+            ord[i] = i;
+            if (sk_term(in, ks[i], false, true, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
+            if (sk_term(in, vs[i], false, exact, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
+        }
+        std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return ks[a] < ks[b]; });
+        for (uint32_t i = 1; i < n; i++)
+            if (ks[ord[i - 1]] == ks[ord[i]]) { in.err = "map with a repeated key"; return -1; }
+        o.push_back(KEYTAG_MAP);
+        for (int i = 3; i >= 0; i--) o.push_back((uint8_t)(n >> (8 * i)));
+        for (uint32_t i : ord) o.insert(o.end(), ks[i].begin(), ks[i].end());
+        for (uint32_t i : ord) o.insert(o.end(), vs[i].begin(), vs[i].end());
+        cls = C_MAP;
+        break;
+    }
     default:
-        in.err = "term type outside the key domain (pid/port/ref/fun/map/bitstring)";
+        // the standard tags of pids, ports, refs, funs, bitstrings, compressed
+        // terms: well-formed terms outside the domain; anything else is garbage
+        in.dom = etf_known_tag(tag);
+        in.err = in.dom ? "term type outside the key domain (pid/port/ref/fun/bitstring)" : "unknown term_to_binary tag";
         return -1;
     }
     in.depth--;
@@ -310,14 +364,14 @@ inline int sk_term(Etf &in, std::vector<uint8_t> &o, bool top, bool *is_int64, i
 
 // the elements and tail of a LIST_EXT at in.p (tag included); a tail that
 // is itself a list continues the same list
-inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o) {
+inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o, bool exact) {
     for (;;) {
         if (!in.need(5)) return -1;
         const uint32_t tag = in.u8();
         if (tag != 108) { in.err = "internal: expected LIST_EXT"; return -1; }
         const uint32_t n = in.u32();
         for (uint32_t i = 0; i < n; i++)
-            if (sk_term(in, o, false, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
+            if (sk_term(in, o, false, exact, nullptr, nullptr, nullptr, nullptr, nullptr) < 0) return -1;
         if (!in.need(1)) return -1;
         const uint32_t t = *in.p;
         if (t == 106) { in.p++; o.push_back(SK_LIST_END); return 0; }
@@ -338,7 +392,7 @@ inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o) {
         }
         // improper tail: compared with the other list's rest as a term
         std::vector<uint8_t> tail;
-        const int c = sk_term(in, tail, false, nullptr, nullptr, nullptr, nullptr, nullptr);
+        const int c = sk_term(in, tail, false, exact, nullptr, nullptr, nullptr, nullptr, nullptr);
         if (c < 0) return -1;
         o.push_back(c == C_BIN ? SK_TAIL_HIGH : SK_TAIL_LOW);
         o.insert(o.end(), tail.begin(), tail.end());
@@ -346,25 +400,24 @@ inline int sk_list_rest(Etf &in, std::vector<uint8_t> &o) {
     }
 }
 
-// term_to_binary(Key) bytes -> device key record (plain form for int64,
-// atom and binary keys).  Returns "" on success or the reason.
-inline std::string record_from_etf(const uint8_t *etf, size_t n, std::vector<uint8_t> &rec) {
-    if (n < 2 || etf[0] != 131) return "not a term_to_binary (version 131) encoding";
-    if (n > 0xFFFE) return "term_to_binary key longer than 65534 bytes";
-    Etf in{etf + 1, etf + n, std::string()};
+// One term at in.p (no version byte) -> its device key record (plain form
+// for int64, atom and binary keys); the ETF part of a term record is 131 ++
+// the term's bytes.  Returns "" on success or the reason (in.dom: a
+// well-formed term outside the key domain, else malformed bytes).
+inline std::string record_from_term(Etf &in, std::vector<uint8_t> &rec) {
+    const uint8_t *t0 = in.p;
     std::vector<uint8_t> sk;
     bool is64 = false, big = false, bneg = false;
     int64_t iv = 0;
     std::vector<uint8_t> bmag;
-    const int cls = sk_term(in, sk, true, &is64, &iv, &big, &bmag, &bneg);
+    const int cls = sk_term(in, sk, true, false, &is64, &iv, &big, &bmag, &bneg);
     if (cls < 0) return in.err;
-    if (in.p != in.e) return "trailing bytes after the term";
-    if (is64 || cls == C_ATOM || cls == C_BIN) {   // the plain domain
-        rec.insert(rec.end(), sk.begin(), sk.end());
-        return "";
-    }
     rec.insert(rec.end(), sk.begin(), sk.end());
-    rec.insert(rec.end(), etf, etf + n);
+    if (is64 || cls == C_ATOM || cls == C_BIN) return "";   // the plain domain
+    const size_t n = 1 + (size_t)(in.p - t0);
+    if (n > 0xFFFE) { in.dom = true; return "term_to_binary key longer than 65534 bytes"; }
+    rec.push_back(131);
+    rec.insert(rec.end(), t0, in.p);
     uint32_t seg_len = 0xFFFF;
     if (big) {   // ensure_binary(Integer) = <<Key:64>>: the low 64 bits, two's complement
         uint64_t lo = 0;
@@ -379,6 +432,62 @@ inline std::string record_from_etf(const uint8_t *etf, size_t n, std::vector<uin
     rec.push_back((uint8_t)(seg_len & 0xFF));
     rec.push_back((uint8_t)(seg_len >> 8));
     return "";
+}
+
+// term_to_binary(Key) bytes -> device key record.  "" or the reason.
+inline std::string record_from_etf(const uint8_t *etf, size_t n, std::vector<uint8_t> &rec) {
+    if (n < 2 || etf[0] != 131) return "not a term_to_binary (version 131) encoding";
+    if (n > 0xFFFE) return "term_to_binary key longer than 65534 bytes";
+    Etf in{etf + 1, etf + n, std::string()};
+    std::vector<uint8_t> r;
+    const std::string e = record_from_term(in, r);
+    if (!e.empty()) return e;
+    if (in.p != in.e) return "trailing bytes after the term";
+    rec.insert(rec.end(), r.begin(), r.end());
+    return "";
+}
+
+// A synctree_leveldb segment node, term_to_binary([{Key, Value}]) with
+// binary values (synctree_leveldb.erl:111-123, the host half of the
+// device restore for the segments its decoder hands over: map keys,
+// FLOAT_EXT, nesting deeper than its stack).  Appends the key records and
+// values; koff/voff get one end offset per entry.  Key order is the
+// caller's to check.
+enum SegStatus { SEG_OK = 0, SEG_BAD = 1, SEG_DOM = 2 };
+inline int segment_from_etf(const uint8_t *b, size_t n, std::vector<uint8_t> &krec, std::vector<uint64_t> &koff,
+                            std::vector<uint8_t> &val, std::vector<uint64_t> &voff) {
+    Etf in{b, b + n, std::string()};
+    auto other = [](uint32_t tg) { return etf_known_tag(tg) ? SEG_DOM : SEG_BAD; };
+    if (!in.need(1) || in.u8() != 131) return SEG_BAD;
+    if (in.p < in.e && *in.p == 80) return SEG_DOM;   // compressed
+    if (!in.need(1)) return SEG_BAD;
+    uint32_t tg = in.u8(), cnt = 0;
+    if (tg == 108) {
+        if (!in.need(4)) return SEG_BAD;
+        cnt = in.u32();
+    } else if (tg != 106) return other(tg);
+    for (uint32_t j = 0; j < cnt; j++) {
+        if (!in.need(1)) return SEG_BAD;
+        if ((tg = in.u8()) != 104) return other(tg);
+        if (!in.need(1)) return SEG_BAD;
+        if (in.u8() != 2) return SEG_DOM;
+        in.depth = 0;
+        if (!record_from_term(in, krec).empty()) return in.dom ? SEG_DOM : SEG_BAD;
+        koff.push_back(krec.size());
+        if (!in.need(1)) return SEG_BAD;
+        if ((tg = in.u8()) != 109) return other(tg);
+        if (!in.need(4)) return SEG_BAD;
+        const uint32_t len = in.u32();
+        if (!in.need(len)) return SEG_BAD;
+        val.insert(val.end(), in.p, in.p + len);
+        in.p += len;
+        voff.push_back(val.size());
+    }
+    if (cnt) {
+        if (!in.need(1)) return SEG_BAD;
+        if (in.u8() != 106) return SEG_DOM;   // an improper list
+    }
+    return in.p == in.e ? SEG_OK : SEG_BAD;
 }
 
 }  // namespace termkey

@@ -2,11 +2,12 @@
 
 Keys on the device path are (type, bytes) (src/synctree.erl:261-268):
 integers in int64 -> <<K:64/big>>, atoms -> atom_to_binary(K, utf8),
-binaries -> themselves, and every other key (tuples, lists, floats, integers
-outside int64) -> term_to_binary(K) (ST_KEY_TERM; the device derives the
-order-preserving record, riak_ensemble_amd/csrc/term_key.h).  In Python:
+binaries -> themselves, and every other key (tuples, lists, maps, floats,
+integers outside int64) -> term_to_binary(K) (ST_KEY_TERM; the device derives
+the order-preserving record, riak_ensemble_amd/csrc/term_key.h).  In Python:
 ``int`` is an Erlang integer, ``float`` a float, ``str`` an atom, ``bytes`` a
-binary, ``tuple`` a tuple and ``list`` a proper list.
+binary, ``tuple`` a tuple, ``list`` a proper list and :class:`Map` (or a
+``dict``) a map.  Pids, ports, refs and funs stay outside the key domain.
 
 term_to_binary here writes what ERTS writes with default options: atoms in
 the form of the configured OTP era (:data:`ETF_ATOMS`: ``'latin1'`` = before
@@ -19,6 +20,7 @@ Atoms returned by the API are plain strings: ``'notfound'``,
 """
 import ctypes
 import struct
+from collections.abc import Mapping
 
 import numpy as np
 
@@ -32,6 +34,74 @@ CORRUPTED = 'corrupted'
 _I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
 
 ETF_ATOMS = 'latin1'
+
+
+def exact_order(t):
+    """Sort key of Erlang's exact (map-key) term order: like term order, but
+    every integer sorts before every float and 1 =/= 1.0 (map keys compare
+    with =:=).  Under a map key everything compares exactly."""
+    if isinstance(t, bool):
+        raise TypeError('Python bools are not Erlang terms (use the atoms "true"/"false")')
+    if isinstance(t, int):
+        return (0, 0, t)
+    if isinstance(t, float):
+        return (0, 1, t)
+    if isinstance(t, str):
+        return (1, t.encode('utf-8'))
+    if isinstance(t, tuple):
+        return (6, len(t), tuple(exact_order(e) for e in t))
+    if isinstance(t, Mapping):
+        m = t if isinstance(t, Map) else Map(t)
+        return (7, len(m), tuple(exact_order(k) for k in m), tuple(exact_order(v) for v in m.values()))
+    if isinstance(t, list):
+        return (9, [exact_order(e) for e in t]) if t else (8,)
+    if isinstance(t, (bytes, bytearray, memoryview)):
+        return (10, bytes(t))
+    raise TypeError('%r is not a term of the key domain' % (t,))
+
+
+class Map(Mapping):
+    """An Erlang map: keys compare exactly (1 and 1.0 are two keys), and the
+    entries are kept in map-key order -- the order term_to_binary writes a
+    map of up to 32 keys in (ERTS flatmaps)."""
+    __slots__ = ('_items',)
+
+    def __init__(self, items=()):
+        if isinstance(items, Mapping):
+            items = items.items()
+        byk = {}
+        for k, v in items:
+            byk[repr(exact_order(k))] = (k, v)   # a later pair replaces an exactly equal key
+        self._items = tuple(sorted(byk.values(), key=lambda kv: exact_order(kv[0])))
+
+    def __getitem__(self, key):
+        ek = exact_order(key)
+        for k, v in self._items:
+            if exact_order(k) == ek:
+                return v
+        raise KeyError(key)
+
+    def __iter__(self):
+        return (k for k, _ in self._items)
+
+    def __len__(self):
+        return len(self._items)
+
+    def items(self):
+        return list(self._items)
+
+    def __eq__(self, other):
+        if not isinstance(other, Mapping):
+            return NotImplemented
+        o = other if isinstance(other, Map) else Map(other)
+        return len(o) == len(self) and all(exact_order(a) == exact_order(c) and b == d
+                                           for (a, b), (c, d) in zip(self._items, o._items))
+
+    def __hash__(self):
+        return hash(repr([exact_order(k) for k in self]))
+
+    def __repr__(self):
+        return 'Map(%r)' % (list(self._items),)
 
 
 def _etf(t, out, atoms):
@@ -78,8 +148,14 @@ def _etf(t, out, atoms):
             for e in t:
                 _etf(e, out, atoms)
             out += bytes([106])
+    elif isinstance(t, Mapping):
+        m = t if isinstance(t, Map) else Map(t)
+        out += bytes([116]) + struct.pack('>I', len(m))
+        for k, v in m.items():
+            _etf(k, out, atoms)
+            _etf(v, out, atoms)
     else:
-        raise TypeError('%r is not a term of the key domain (pids, ports, refs, funs, maps are not)' % (t,))
+        raise TypeError('%r is not a term of the key domain (pids, ports, refs, funs are not)' % (t,))
 
 
 def term_to_binary(t, atoms=None):
@@ -145,6 +221,14 @@ def _dec(b, i):
     if tag == 109:
         n = struct.unpack_from('>I', b, i)[0]
         return bytes(b[i + 4:i + 4 + n]), i + 4 + n
+    if tag == 116:
+        n, i = struct.unpack_from('>I', b, i)[0], i + 4
+        pairs = []
+        for _ in range(n):
+            k, i = _dec(b, i)
+            v, i = _dec(b, i)
+            pairs.append((k, v))
+        return Map(pairs), i
     raise ValueError('ETF tag %d outside the key domain' % tag)
 
 

@@ -216,6 +216,9 @@ def test_restore_undecodable_node_is_absent():
     assert t.modstate.verify() == R.verify(o2)
 
 
+_PID = bytes([88, 100, 0, 13]) + b'nonode@nohost' + bytes(12)   # NEW_PID_EXT
+
+
 @pytest.mark.gpu
 def test_restore_rejects_out_of_domain_nodes():
     from riak_ensemble_amd import synctree as S
@@ -224,8 +227,10 @@ def test_restore_rejects_out_of_domain_nodes():
         [(LR.db_key(b'', 0, 0), LR.term_to_binary(b'\x00' * 16))],             # 16-byte top hash
         [(LR.db_key(b'', 2, 0), LR.term_to_binary([(99, b'\x00' * 17)]))],    # child outside node {2,0}
         [(LR.db_key(b'', 6, 3), LR.term_to_binary([(2, b'a'), (1, b'b')]))],  # not an orddict
-        [(LR.db_key(b'', 6, 3), bytes([131, 108, 0, 0, 0, 1, 104, 2, 116, 0, 0, 0, 0,
-                                       109, 0, 0, 0, 1, 97, 106]))],               # a map key #{} (outside the key domain)
+        [(LR.db_key(b'', 6, 3), bytes([131, 108, 0, 0, 0, 1, 104, 2]) + _PID +
+          bytes([109, 0, 0, 0, 1, 97, 106]))],                                # a pid key (outside the key domain)
+        [(LR.db_key(b'', 6, 3), bytes([131, 108, 0, 0, 0, 1, 104, 2, 116, 0, 0, 0, 1, 100, 0, 1, 97]) + _PID +
+          bytes([109, 0, 0, 0, 1, 97, 106]))],                                # #{a => Pid}: the host decoder's
         [(LR.db_key(b'', 6, 3), LR.term_to_binary([(1, 5)]))],                # non-binary value
     ]
     for recs in bad:
@@ -335,13 +340,20 @@ def test_checkpoint_into_tracks_corrupt_and_rehash():
 def test_restore_term_keys_roundtrip():
     """Segments with term_to_binary keys -- tuples, lists, strings, floats,
     integers beyond int64, nested atoms and binaries -- decode on the device
+    (maps and keys nested deeper than its stack on the host, term_key.h)
     (synctree_leveldb:fetch/3 reopens any record it can decode,
     synctree_leveldb.erl:111-123): the restored tree equals the tree the
     oracle's synctree_leveldb DB was written from, record for record."""
     from test_term_keys import distinct_terms
     from riak_ensemble_amd import synctree as S
+    from riak_ensemble_amd.terms import Map
+    deep_t, deep_l = 'x', 'y'
+    for _ in range(60):   # nested deeper than the device decoder's stack: the host decodes the segment
+        deep_t, deep_l = (deep_t,), [deep_l]
     keys = distinct_terms(1500, 31) + [(1 << 64) + 5, -(1 << 70), 5.5, -2.0 ** 80, (1.5, 'a'), 'atom', b'bin', 7,
-                                       [104, 105], [], (), ((), [[]]), ('a\u0000b', b'\x00\xff')]
+                                       [104, 105], [], (), ((), [[]]), ('a\u0000b', b'\x00\xff'),
+                                       Map({'a': 1}), Map([(1, 'x'), (1.0, 'y')]), Map({}), (Map({2: [3]}),),
+                                       deep_t, deep_l]
     rng = random.Random(3)
     vals = [rng.randbytes(rng.choice([0, 8, 17])) for _ in keys]
     o, d = _pair(keys, vals)
@@ -358,3 +370,38 @@ def test_restore_term_keys_roundtrip():
     assert fresh.modstate.verify() is True
     fresh.modstate.rehash()
     assert fresh.modstate.top_hash() == d.modstate.top_hash()
+
+
+@pytest.mark.gpu
+def test_restore_float_ext_and_malformed_host_segments():
+    """A key written as FLOAT_EXT (the 31-byte "%.20e" form of OTP before 17)
+    decodes through the host half of the restore: the tree answers like the
+    oracle's (the node hashes cover values only), and the snapshot keeps the
+    key's bytes as stored.  A malformed map key makes its node absent (fetch/3
+    answers [] when binary_to_term raises, synctree_leveldb.erl:111-123)."""
+    import struct
+    from riak_ensemble_amd import synctree as S
+    from riak_ensemble_amd.terms import Map
+    keys = [1.5, 2.25, Map({'m': 1})] + list(range(100, 400))
+    vals = [struct.pack('>Q', i) for i in range(len(keys))]
+    o, d = _pair(keys, vals)
+    recs = dict(LR.tree_records(o.modstate.db, b'tree-7'))
+    new_f = b'F' + struct.pack('>d', 1.5)
+    old_f = b'c' + (b'%.20e' % 1.5).ljust(31, b'\0')
+    (fk,) = [k for k, v in recs.items() if new_f in v]
+    recs[fk] = recs[fk].replace(new_f, old_f)
+    mseg = LR.db_key(b'tree-7', R.height(o) + 1, R.get_segment(keys[2], o.segments))
+    assert mseg != fk and b't\x00\x00\x00\x01' in recs[mseg]
+    good = dict(recs)
+    recs[mseg] = recs[mseg].replace(b't\x00\x00\x00\x01', b't\x00\x00\x00\x05')   # pairs run past the end
+    t = S.new()
+    assert t.modstate.restore_leveldb(list(good.items()), b'tree-7') == (len(good), 0)
+    assert t.modstate.top_hash() == R.top_hash(o)
+    assert t.modstate.get_batch(keys) == [R.get(k, o) for k in keys]
+    assert t.modstate.verify() is True
+    assert t.modstate.compare(d.modstate) == ('ok', [])
+    assert dict(t.modstate.snapshot_leveldb(b'tree-7'))[fk] == good[fk]   # the FLOAT_EXT bytes kept
+    t2 = S.new()
+    assert t2.modstate.restore_leveldb(list(recs.items()), b'tree-7') == (len(recs) - 1, 1)
+    rest = [k for k in keys if k is not keys[2] and R.get_segment(k, o.segments) != R.get_segment(keys[2], o.segments)]
+    assert t2.modstate.get_batch(rest) == [R.get(k, o) for k in rest]

@@ -1,5 +1,5 @@
 """term_to_binary keys (synctree.erl:261-268): tuples,
-lists, floats and integers outside int64.  The host passes
+lists, maps, floats and integers outside int64.  The host passes
 term_to_binary(Key) (ST_KEY_TERM); the library derives an order-preserving
 record (riak_ensemble_amd/csrc/term_key.h) whose memcmp order is Erlang term
 order, and hashes term_to_binary(Key) -- or <<Key:64>> for an integer -- for
@@ -46,8 +46,13 @@ def rand_term(rng, depth=0):
         if k == 7:
             return []
         return rng.randint(0, 255)
-    if r < 0.8:
+    if r < 0.7:
         return tuple(rand_term(rng, depth + 1) for _ in range(rng.randint(0, 4)))
+    if r < 0.8:   # a map; keys compare exactly (1 and 1.0 are two keys)
+        pool = [1, 1.0, 2, 0.5, -3, 'a', (1,), (1.0,), b'k']
+        pairs = [(rng.choice(pool) if rng.random() < 0.5 else rand_term(rng, depth + 1), rand_term(rng, depth + 1))
+                 for _ in range(rng.randint(0, 4))]
+        return terms.Map(pairs)
     if rng.random() < 0.3:   # a "string"
         return [rng.randint(0, 255) for _ in range(rng.randint(1, 5))]
     return [rand_term(rng, depth + 1) for _ in range(rng.randint(1, 4))]
@@ -106,11 +111,54 @@ def test_key_record_order_is_erlang_term_order():
     assert terms.order_key(b'ab') == b'\x50ab'
 
 
+def test_map_keys_order_and_equality():
+    """Maps (synctree.erl:261-268 sends them through term_to_binary): ordered
+    by size, then keys in map-key order, then values (ERTS term comparison);
+    map keys compare exactly -- #{1 => a} and #{1.0 => a} are different keys,
+    and every integer key sorts before every float key -- while values compare
+    with ==, so #{a => 1} and #{a => 1.0} are one key."""
+    M = terms.Map
+    ms = [M({}), M({'a': 1}), M({'a': 1.0}), M({1: 'a'}), M([(1.0, 'a')]), M({2: 'a'}), M([(0.5, 'a')]),
+          M({'a': 1, 'b': 2}), M([(1, 'x'), (1.0, 'y')]), M({(1,): 0}), M([((1.0,), 0)]), M({'a': M({1: 2})}),
+          M({'a': M([(1.0, 2)])}), M({b'k': [1, 2]}), M({'z': (1, 2)}), M([(3, 'a'), (-3, 'a')]),
+          M({1 << 70: 'a'}), M([(2.0 ** 70, 'a')])]
+    near = [(9,), (9, 9, 9, 9), [], [1], 'atom', b'bin', 7, 7.5]
+    ts = ms + near
+    by_erlang = sorted(ts, key=R.term_key)
+    by_record = sorted(ts, key=terms.order_sk)   # (stable: the two == maps keep their order)
+    assert [repr(x) for x in by_erlang] == [repr(x) for x in by_record]
+    # the documented rules, spelled out
+    ok = terms.order_sk
+    assert ok(M({1: 'a'})) < ok(M([(1.0, 'a')]))              # integer key before float key
+    assert ok(M({2: 'a'})) < ok(M([(0.5, 'a')]))              # ... whatever their values
+    assert ok(M({1 << 70: 'a'})) < ok(M([(2.0 ** 70, 'a')]))
+    assert ok(M({'z': 0})) < ok(M({'a': 1, 'b': 2}))          # size first
+    assert ok(M({'a': 1})) == ok(M({'a': 1.0}))               # values compare with ==
+    assert ok(M({'a': M({1: 2})})) != ok(M({'a': M([(1.0, 2)])}))   # a map value's keys: exact
+    assert ok((9,)) < ok(M({})) < ok([])                      # tuple < map < nil
+    for a, b in [(M({'a': 1}), M({'a': 1.0})), (M({'a': (1, 2.0)}), M({'a': (1.0, 2)}))]:
+        assert R.term_key(a) == R.term_key(b)
+    assert R.term_key(M({1: 'a'})) != R.term_key(M([(1.0, 'a')]))
+    # term_to_binary writes a map's pairs in map-key order (a flatmap)
+    assert terms.term_to_binary(M([(1.0, 'a'), (2, 'b'), ('c', 1)])) == (
+        b'\x83t\x00\x00\x00\x03' + b'a\x02' + b'd\x00\x01b' + b'F' + __import__('struct').pack('>d', 1.0) +
+        b'd\x00\x01a' + b'd\x00\x01c' + b'a\x01')
+    assert terms.binary_to_term(terms.term_to_binary(M([(1, 'a'), (1.0, 'b')]))) == M([(1, 'a'), (1.0, 'b')])
+
+
 def test_term_key_rejects_outside_domain():
     with pytest.raises(TypeError):
         terms.key_parts(True)
     with pytest.raises(TypeError):
-        terms.key_parts({1: 2})
+        terms.key_parts({1, 2})   # a Python set: no Erlang term
+    with pytest.raises(TypeError):
+        terms.key_parts(object())
+    # pids, refs, ports and funs stay outside the device key domain (ST_EINVAL)
+    import ctypes
+    from riak_ensemble_amd import _lib as L
+    n = ctypes.c_uint64()
+    pid = b'\x83' + bytes([88, 100, 0, 13]) + b'nonode@nohost' + bytes(12)   # NEW_PID_EXT
+    assert L.load().st_key_record(3, pid, len(pid), None, 0, ctypes.byref(n)) == L.ST_EINVAL
     from riak_ensemble_amd import _lib
     # a malformed ETF is refused by the library (ST_EINVAL)
     with pytest.raises(ValueError):

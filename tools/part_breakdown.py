@@ -41,7 +41,7 @@ t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
 names = ['key_segment', 'bucket', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
-         'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_jobs', 'page_tails', 'page_wide', 'page_records', 'page_fold']
+         'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_merge', 'page_fold']
 t.set_timing(True)
 t.kernel_stats('*reset*')
 t0 = time.perf_counter()
