@@ -636,6 +636,7 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     for e in range(E):
         k = _dev_keys(workload.SEED ^ (rank * E + e + 1), 0, nk, dev, torch)
         t = synctree_hip.DeviceTree(device=local)
+        torch.cuda.synchronize()   # the library reads the keys on its own stream
         t.insert_int64_device(k.data_ptr(), vals.data_ptr(), nk, 17)
         trees.append(t)
         del k
@@ -807,6 +808,7 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         m = min(chunk, N - a)
         k = _dev_keys(seed, a, m, dev, torch)
         v = _dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
+        torch.cuda.synchronize()   # the library reads them on its own stream
         pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
         del k, v
     pt.combine()
@@ -819,6 +821,7 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         k = torch.cat([_dev_keys_at(seed, old, dev, torch), _dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
         seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
         batches.append((k.contiguous(), _dev_values(seq, dev, torch).contiguous()))
+    torch.cuda.synchronize()
     # one warm-up batch (it builds the pages), then K timed: each batch timed
     # on its own (a device synchronisation around it) so the batches that
     # rebuild the pages show; the reported rate is the amortised one (all K)

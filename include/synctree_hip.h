@@ -120,7 +120,9 @@ int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t 
 
 /* Same for integer keys (ST_KEY_INT) and fixed-width values.
  * keys[n] (int64), vals[n*vlen].  inputs_on_device != 0: both pointers are
- * device memory on this tree's device (no host staging).  *n_corrupted
+ * device memory on this tree's device (no host staging), read on the tree's
+ * stream: whatever produces them must be complete first (synchronised, or
+ * enqueued on that stream, st_set_stream).  *n_corrupted
  * (may be NULL) receives the number of rejected keys. */
 int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                     int inputs_on_device, uint64_t *n_corrupted);

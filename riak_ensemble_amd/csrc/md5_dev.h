@@ -276,6 +276,35 @@ __device__ __forceinline__ void md5_global_pf(const uint8_t *p, uint64_t len, ui
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }
 
+// md5_global_pf from block k0 on (st = the state after blocks [0, k0), the
+// message still `len` bytes from p); when cap_k is one of the blocks
+// visited, the state before it is copied to cap.  The streaming insert
+// saves the state before the first block a merge changes while it verifies
+// the old segment, and resumes from there to hash the merged one.
+template <bool TPUT>
+__device__ __forceinline__ void md5_global_span(const uint8_t *p, uint64_t len, uint64_t k0, uint32_t st[4],
+                                                uint64_t cap_k, uint32_t cap[4]) {
+    const uint64_t nblk = (len + 8) / 64 + 1;
+    uint32_t nx[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) nx[w] = 0u;
+    if (len > 64 * k0) load_block_global(p + 64 * k0, nx);
+    for (uint64_t k = k0; k < nblk; k++) {
+        if (k == cap_k) { cap[0] = st[0]; cap[1] = st[1]; cap[2] = st[2]; cap[3] = st[3]; }
+        uint32_t m[16];
+#pragma unroll
+        for (int w = 0; w < 16; w++) m[w] = nx[w];
+        const int64_t rem = (int64_t)len - (int64_t)(64 * k);
+        if (rem - 64 > 0) load_block_global(p + 64 * (k + 1), nx);
+        if (TPUT) {
+            if (rem < 64) pad_block(m, rem, k + 1 == nblk, len);
+            compress<true>(st, m);
+        } else {
+            compress_pad_lat(st, m, rem, k + 1 == nblk, len);
+        }
+    }
+}
+
 // MD5 of a message of `len` bytes staged in LDS at a 4-byte aligned address
 // (bytes beyond len are ignored; the region must be readable up to the next
 // 64-byte boundary past len).  Next block's words are read before the

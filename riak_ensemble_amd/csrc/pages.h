@@ -134,10 +134,11 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
 // page's sizes (mode 2), scanned for its place in the append region; v[3] =
 // the segment's new keys (for the tree's entry count).
 __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *voff, const uint64_t *bseg_off,
-                            const uint8_t *reject, const BatchSums *bs, const SegSums *ss, const uint8_t *dirty, uint64_t S,
+                            const uint8_t *reject, const BatchSums *bs, const SegSums *ss, uint8_t *dirty, uint64_t S,
                             int slack_pct, uint8_t *mode, PageSums *reloc) {
     for (uint64_t s = gtid(); s < S; s += gstride()) {
         const uint64_t j0 = bseg_off[s], je = bseg_off[s + 1];
+        if (reject && reject[s]) dirty[s] = 0;   // positions came before the verify (k_verify_pos)
         PageSums r(0);
         uint8_t md = 0;
         if (j0 != je && !(reject && reject[s]) && dirty[s]) {

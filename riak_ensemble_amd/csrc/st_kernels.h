@@ -595,56 +595,114 @@ struct RecAt {
     uint64_t ku, vu, bk, bv;
 };
 
-__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty, RecAt *rat) {
-    for (uint64_t s = gtid(); s < a.S; s += gstride()) {
-        const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
-        uint64_t nold = a.seg_off ? a.seg_end[s] - i0 : 0;
-        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-        const bool rej = a.seg_reject && a.seg_reject[s];
-        if (a.seg_replace && a.seg_replace[s]) nold = 0;
-        SegSums tot;
-        tot.v[0] = nold;
-        tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
-        tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
-        tot.v[3] = 0;
-        uint64_t lo = 0;
-        bool changed = false;
-        for (uint64_t j = j0; j < je; j++) {
-            BatchSums f(0);
-            if (rej) { pos[j] = 0; bs[j] = f; continue; }
-            const uint32_t bi = a.perm[j];
-            const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
-            const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
-            uint64_t hi = nold;
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
-                if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
-            }
-            const uint64_t e = i0 + lo;
-            const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
-            pos[j] = (uint32_t)lo;
-            if (rat) rat[j] = RecAt{a.koff[e] - a.koff[i0], a.voff[e] - a.voff[i0], a.bv.koff[bi], a.bvoff[bi]};
-            const bool kept = a.keep[j] != 0;
-            const bool ne = kept && !(a.bop && a.bop[bi]);
-            if (kept && eq) {
-                f.v[BS_EQ] = 1;
-                f.v[BS_KE] = a.koff[e + 1] - a.koff[e];
-                f.v[BS_VE] = a.voff[e + 1] - a.voff[e];
-            }
-            if (ne) {
-                f.v[BS_NE] = 1;
-                f.v[BS_KN] = kl;
-                f.v[BS_VN] = a.bvoff[bi + 1] - a.bvoff[bi];
-            }
-            bs[j] = f;
-            changed |= kept;
-            if (ne && !eq) tot.v[3] += 1;   // a new key of the tree
-            tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
-            tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
-            tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
+// Merge positions of one segment's batch run (a lane per segment): the run
+// is sorted, so each key's binary search starts at the previous one's
+// position.  Returns the value offset (relative to the segment's first
+// value) of the first entry the merge changes -- the first kept record's
+// position -- or ~0 when nothing changes.
+__device__ __forceinline__ uint64_t merge_pos_seg(const MergeArgs &a, uint64_t s, uint32_t *pos, BatchSums *bs,
+                                                  SegSums *ss, uint8_t *dirty, RecAt *rat) {
+    const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+    uint64_t nold = a.seg_off ? a.seg_end[s] - i0 : 0;
+    const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
+    const bool rej = a.seg_reject && a.seg_reject[s];
+    if (a.seg_replace && a.seg_replace[s]) nold = 0;
+    SegSums tot;
+    tot.v[0] = nold;
+    tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
+    tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
+    tot.v[3] = 0;
+    uint64_t lo = 0, first = ~0ull;
+    for (uint64_t j = j0; j < je; j++) {
+        BatchSums f(0);
+        if (rej) { pos[j] = 0; bs[j] = f; continue; }
+        const uint32_t bi = a.perm[j];
+        const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
+        const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
+        uint64_t hi = nold;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
+            if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
         }
-        ss[s] = tot;
-        if (dirty) dirty[s] = changed ? 1 : 0;
+        const uint64_t e = i0 + lo;
+        const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
+        pos[j] = (uint32_t)lo;
+        const uint64_t vu = a.voff[e] - a.voff[i0];
+        if (rat) rat[j] = RecAt{a.koff[e] - a.koff[i0], vu, a.bv.koff[bi], a.bvoff[bi]};
+        const bool kept = a.keep[j] != 0;
+        const bool ne = kept && !(a.bop && a.bop[bi]);
+        if (kept && eq) {
+            f.v[BS_EQ] = 1;
+            f.v[BS_KE] = a.koff[e + 1] - a.koff[e];
+            f.v[BS_VE] = a.voff[e + 1] - a.voff[e];
+        }
+        if (ne) {
+            f.v[BS_NE] = 1;
+            f.v[BS_KN] = kl;
+            f.v[BS_VN] = a.bvoff[bi + 1] - a.bvoff[bi];
+        }
+        bs[j] = f;
+        if (kept && first == ~0ull) first = vu;
+        if (ne && !eq) tot.v[3] += 1;   // a new key of the tree
+        tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
+        tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
+        tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
+    }
+    ss[s] = tot;
+    if (dirty) dirty[s] = first != ~0ull ? 1 : 0;
+    return first;
+}
+
+__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty, RecAt *rat) {
+    for (uint64_t s = gtid(); s < a.S; s += gstride()) merge_pos_seg(a, s, pos, bs, ss, dirty, rat);
+}
+
+// The MD5 state of a segment's values before the first block its merge
+// changes (k = that block; k == 0: none kept), saved by the verify of a
+// streaming batch for the hash after the merge.
+struct PrefixState {
+    uint4 st;
+    uint64_t k;
+};
+
+// A streaming batch's verify (insert/3's get_path check of each touched
+// segment, synctree.erl:189-209, 302-340) fused with its merge positions: a
+// lane per segment in seg_perm order computes the positions of its run (no
+// rejection yet: k_page_plan drops rejected runs), then, for a touched
+// segment, the MD5 of its old values, saving the state before the first
+// block the merge changes (ps) for the hash after the merge.
+__global__ void __launch_bounds__(256) k_verify_pos(DevTree t, MergeArgs a, const uint32_t *perm, const uint8_t *mask,
+                                                    uint8_t *ok, uint32_t *pos, BatchSums *bs, SegSums *ss,
+                                                    uint8_t *dirty, RecAt *rat, PrefixState *ps) {
+    const uint32_t L = t.H + 1;
+    for (uint64_t i = gtid(); i < t.S; i += gstride()) {
+        const uint64_t s = perm[i];
+        const uint64_t first = merge_pos_seg(a, s, pos, bs, ss, dirty, rat);
+        const uint64_t slot = t.base[L] + s;
+        if (!mask[slot]) continue;
+        const uint64_t eslot = (L == 1) ? 0 : slot;
+        const uint16_t et = t.tag[eslot];
+        PrefixState p;
+        p.k = 0;
+        p.st = make_uint4(0u, 0u, 0u, 0u);
+        bool good;
+        if (!(et & TAG_PRESENT)) {
+            good = t.seg_off[s] == t.seg_end[s];
+        } else {
+            uint32_t st[4], cap[4] = {0u, 0u, 0u, 0u};
+            stmd5::init(st);
+            const uint64_t ck = first == ~0ull ? ~0ull : first / 64;
+            const uint64_t v0 = t.seg_voff[s];
+            stmd5::md5_global_span<true>(t.vheap + v0, t.seg_vend[s] - v0, 0, st, ck, cap);
+            const uint4 e = t.md5[eslot];
+            good = (et == TAG_PRESENT) && e.x == st[0] && e.y == st[1] && e.z == st[2] && e.w == st[3];
+            if (ck != ~0ull && ck > 0) {
+                p.k = ck;
+                p.st = make_uint4(cap[0], cap[1], cap[2], cap[3]);
+            }
+        }
+        ok[slot] = good ? 1 : 0;
+        ps[s] = p;
     }
 }
 
@@ -1826,7 +1884,9 @@ __global__ void __launch_bounds__(256) k_seg_perm_scatter(DevTree t, uint32_t *g
 }
 
 // K1 segment_hash over the block-count order.
-__global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint32_t *perm, const uint8_t *mask) {
+// ps (optional): per segment, the MD5 state of its unchanged prefix (PrefixState, k_verify_pos)
+__global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint32_t *perm, const uint8_t *mask,
+                                                           const PrefixState *ps) {
     const uint32_t L1 = t.H + 1;
     for (uint64_t i = gtid(); i < t.S; i += gstride()) {
         const uint64_t s = perm[i];
@@ -1837,9 +1897,17 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
             if (L1 == 1) t.tag[0] = 0;
             continue;
         }
-        uint32_t dg[4];
+        uint32_t dg[4], cap[4];
         const uint64_t v0 = t.seg_voff[s];
-        stmd5::md5_global_pf<true>(t.vheap + v0, t.seg_vend[s] - v0, dg);
+        uint64_t k0 = 0;
+        if (ps && ps[s].k) {
+            const uint4 q = ps[s].st;
+            k0 = ps[s].k;
+            dg[0] = q.x; dg[1] = q.y; dg[2] = q.z; dg[3] = q.w;
+        } else {
+            stmd5::init(dg);
+        }
+        stmd5::md5_global_span<true>(t.vheap + v0, t.seg_vend[s] - v0, k0, dg, ~0ull, cap);
         const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;

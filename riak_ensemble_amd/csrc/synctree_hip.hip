@@ -114,6 +114,7 @@ struct st_tree {
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
+    bool perm_any = false;   // seg_perm holds a permutation (perhaps no longer by size)
     // hash-ready tiled messages in seg_perm order (K1; st_kernels.h)
     uint4 *tiles = nullptr;
     uint64_t tiles_cap = 0;         // uint4 units
@@ -955,7 +956,14 @@ static int ensure_perm(st_tree *t) {
     LAUNCH(t, "seg_perm", k_seg_perm_scan, 1, 256, 0, cnt);
     LAUNCH(t, "seg_perm", k_seg_perm_scatter, grid_for(t->S, 256, 1024), 256, 0, d, cnt, t->seg_perm);
     t->perm_valid = true;
+    t->perm_any = true;
     return ST_OK;
+}
+// Any permutation of the segments will do (the order only balances a wave's
+// lanes): the streaming batches reuse the last one instead of re-sorting.
+static int ensure_perm_any(st_tree *t) {
+    if (t->perm_any) return ST_OK;
+    return ensure_perm(t);
 }
 
 // Build the hash-ready tiled messages from the CSR (k_tile_order, scan,
@@ -1180,11 +1188,12 @@ static int rehash_tiled(st_tree *t) {
 // pages) in block-count order (k_segment_hash_perm), then the marked inner
 // nodes: W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the
 // per-level kernels above; other geometries: one k_level_hash launch per level.
-static int rehash_all(st_tree *t, const uint8_t *mask) {
+// ps: the prefix states of a streaming batch's verify (k_verify_pos) or NULL.
+static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr) {
     if (!mask) return rehash_tiled(t);
     DevTree d = view(t);
-    CHK(ensure_perm(t));
-    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask);
+    CHK(ps ? ensure_perm_any(t) : ensure_perm(t));
+    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask, ps);
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
@@ -1196,14 +1205,9 @@ static int rehash_all(st_tree *t, const uint8_t *mask) {
     return rehash_levels(t, t->H, mask);
 }
 
-// Verify every node marked in t->mark (levels 1..L); results in t->ok.
-static int verify_marked(st_tree *t, uint32_t L) {
+// Verify the inner nodes marked in t->mark (levels 1..min(L, H)); results in t->ok.
+static int verify_levels(st_tree *t, uint32_t L) {
     DevTree d = view(t);
-    if (L == t->H + 1) {   // segments in the length order of seg_perm: lanes of a wave hash alike-sized messages
-        CHK(ensure_perm(t));
-        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
-               (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
-    }
     const uint32_t lmax = L < t->H ? L : t->H;
     if (lmax >= 1) {
         const uint64_t nodes = t->base[lmax + 1] - t->base[1];
@@ -1212,6 +1216,17 @@ static int verify_marked(st_tree *t, uint32_t L) {
                (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
     }
     return ST_OK;
+}
+
+// Verify every node marked in t->mark (levels 1..L); results in t->ok.
+static int verify_marked(st_tree *t, uint32_t L) {
+    DevTree d = view(t);
+    if (L == t->H + 1) {   // segments in the length order of seg_perm: lanes of a wave hash alike-sized messages
+        CHK(ensure_perm(t));
+        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
+               (const uint32_t *)t->seg_perm, (const uint32_t *)nullptr, t->ok, (uint32_t *)nullptr);
+    }
+    return verify_levels(t, L);
 }
 
 // ------------------------------------------------------------------ ingest
@@ -1477,16 +1492,14 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     BatchPrep bp;
     CHK(batch_prepare(t, in, sc, bp));
     uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
-    CHK(verify_batch_paths(t, bp, sc, &reject));
-    if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
-                              (const uint8_t *)reject, in.clevel_out);
-    // merge positions and the merged sizes of every touched segment
-    MergeArgs ma = merge_args(view(t), in, bp, reject, S);
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *ss = nullptr;
     PageSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
+    PrefixState *ps = nullptr;
+    CHK(sc.alloc(&reject, S));
+    CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
     CHK(sc.alloc(&ss, S));
     CHK(sc.alloc(&dirty, S));
@@ -1498,14 +1511,31 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&bx, n + 1));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PageSums), t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty, rat);
+    // the touched segments' verify fused with the merge positions (every
+    // segment's merged sizes), then the inner nodes of their paths
+    MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
+    {
+        const DevTree d = view(t);
+        HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+        LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
+               (const uint64_t *)nullptr, S, t->mark);
+        CHK(ensure_perm_any(t));
+        LAUNCH(t, "verify_pos", k_verify_pos, grid_for(S), 256, 0, d, ma, (const uint32_t *)t->seg_perm,
+               (const uint8_t *)t->mark, t->ok, mpos, bs, ss, dirty, rat, ps);
+        CHK(verify_levels(t, t->H + 1));
+        LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
+               (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
+    }
+    if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
+                              (const uint8_t *)reject, in.clevel_out);
+    ma.seg_reject = reject;
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     // in place or to a new page; the moves' places in the append region
     PageSums tot(0);
     for (int pass = 0;; pass++) {
         LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
                (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss,
-               (const uint8_t *)dirty, S, t->pg_slack, mode, rsz);
+               dirty, S, t->pg_slack, mode, rsz);
         CHK(exclusive_scan<PageSums>(t, rsz, rbase, S + 1));
         CHK(d2h(t, &tot, rbase + S, sizeof(PageSums)));
         const Pages &g = t->pg;
@@ -1550,10 +1580,10 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     t->n += tot.v[3];
     t->perm_valid = false;
     t->tiles_valid = false;
-    // dirty-path rehash over the pages
+    // dirty-path rehash over the pages, each segment from its unchanged prefix's MD5 state
     HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
     LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
-    CHK(rehash_all(t, t->mark));
+    CHK(rehash_all(t, t->mark, ps));
     t->fresh = false;
     return ST_OK;
 }

@@ -95,7 +95,10 @@ class DeviceTree:
         return int(nc.value)
 
     def insert_int64_device(self, keys_ptr, vals_ptr, n, vlen):
-        """Same with device-resident inputs (int64 keys, n*vlen value bytes)."""
+        """Same with device-resident inputs (int64 keys, n*vlen value bytes).
+        The library reads them on its own stream: the work that produced them
+        must be complete (e.g. torch.cuda.synchronize()) or enqueued on the
+        tree's stream (set_stream)."""
         nc = ctypes.c_uint64(0)
         _lib.check(self.L.st_insert_int64(self.h, n, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(vals_ptr), vlen, 1,
                                           ctypes.byref(nc)), 'st_insert_int64')

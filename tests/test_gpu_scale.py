@@ -167,6 +167,7 @@ def test_config5_partitioned_streaming_100m():
     del ora
     kd = torch.from_numpy(keys).cuda()
     vd = torch.from_numpy(vals.reshape(-1)).cuda()
+    torch.cuda.synchronize()   # the library reads device inputs on its own stream
     for G in (1, 2, 4, 8):
         parts = [parallel.PartitionedTree(synctree_hip.DeviceTree(), _Local(r, G)) for r in range(G)]
         for p in parts:

@@ -901,7 +901,7 @@ int main() {
         if (check) for (uint64_t s = 0; s < S && ok; s++) if (blk(s) && memcmp(&got[s], &ref[s], 16)) ok = false;
         printf("%-12s %8.2f us  %s\n", name, best * 1000, check ? (ok ? "digests OK" : "DIGESTS DIFFER") : "");
     };
-    run("base", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, perm, (const uint8_t *)nullptr); });
+    run("base", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, perm, (const uint8_t *)nullptr, (const PrefixState *)nullptr); });
     (void)hipMemcpy(ref.data(), t.md5 + L6, S * 16, hipMemcpyDeviceToHost);
     run("loadonly", false, [&] { hipLaunchKernelGGL(k_loadonly, dim3(4096), dim3(256), 0, 0, t, perm); });
     run("compute", false, [&] { hipLaunchKernelGGL(k_compute, dim3(4096), dim3(256), 0, 0, t, perm); });
@@ -915,7 +915,7 @@ int main() {
         std::vector<uint32_t> id(S); for (uint64_t i = 0; i < S; i++) id[i] = (uint32_t)i;
         (void)hipMemcpy(idp, id.data(), S * 4, hipMemcpyHostToDevice);
         run("loadonly_nat", false, [&] { hipLaunchKernelGGL(k_loadonly, dim3(4096), dim3(256), 0, 0, t, idp); });
-        run("base_nat", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, idp, (const uint8_t *)nullptr); });
+        run("base_nat", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, idp, (const uint8_t *)nullptr, (const PrefixState *)nullptr); });
     }
     run("descpf", true, [&] { hipLaunchKernelGGL(k_descpf, dim3(S / 256), dim3(256), 0, 0, t, dd); });
     {
@@ -946,8 +946,8 @@ int main() {
         run("msg_load", false, [&] { hipLaunchKernelGGL(k_msgx<1>, dim3(4096), dim3(256), 0, 0, t, dmd, (const uint4 *)dm); });
         const size_t sb_lds = 256 * SB_NB + 256 * SB_TB + 16 * SB_NB + 16 * SB_TB + SB_NB + SB_TB + 4096 * 2 + 64;
         run("subtree", true, [&] { hipLaunchKernelGGL(k_subtree, dim3(S / 4096), dim3(1024), sb_lds, 0, t, dmo, (const uint4 *)dm); });
-        run("base+lv3", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, perm, (const uint8_t *)nullptr);
-                                     hipLaunchKernelGGL(k_levels3_16, dim3(256), dim3(256), levels3_16_lds_bytes(), 0, t, (const uint8_t *)nullptr); });
+        run("base+lv3", false, [&] { hipLaunchKernelGGL(k_segment_hash_perm, dim3(4096), dim3(256), 0, 0, t, perm, (const uint8_t *)nullptr, (const PrefixState *)nullptr);
+                                     hipLaunchKernelGGL(k_levels3_16, dim3(256), dim3(256), levels3_16_lds_bytes(), 0, t, (const uint8_t *)nullptr, (const PrefixState *)nullptr); });
         uint4 *m6 = t.md5 + L6; uint16_t *t6 = t.tag + L6;
         run("perm_lean", true, [&] { hipLaunchKernelGGL(k_perm_lean, dim3(4096), dim3(256), 0, 0, perm, dso, dsv, vh, m6, t6, (uint32_t)S); });
         run("msg_lean", true, [&] { hipLaunchKernelGGL(k_msg_lean, dim3(4096), dim3(256), 0, 0, dmd, (const uint4 *)dm, m6, t6, (uint32_t)S); });

@@ -26,6 +26,7 @@ for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
     k = bench._dev_keys(seed, a, m, dev, torch)
     v = bench._dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
+    torch.cuda.synchronize()   # the library reads them on its own stream
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
     del k, v
 torch.cuda.synchronize()
@@ -36,10 +37,11 @@ for j in range(K + 1):
     k = torch.cat([bench._dev_keys_at(seed, old, dev, torch), bench._dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
     seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
     batches.append((k.contiguous(), bench._dev_values(seq, dev, torch).contiguous()))
+torch.cuda.synchronize()
 k, v = batches[0]
 t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
-names = ['key_segment', 'bucket', 'run_sort', 'mark_paths', 'segment_verify', 'level_verify',
+names = ['key_segment', 'bucket', 'run_sort', 'mark_paths', 'segment_verify', 'verify_pos', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
          'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_merge', 'page_fold']
 t.set_timing(True)
