@@ -163,7 +163,12 @@ def main():
         el = float(t.item())
     assert tree.top_hash() == top0, 'rehash changed the top hash of a consistent tree'
 
-    # per-kernel HIP-event timing on the library stream (same steps, timing on)
+    # the kernel's GPU time without per-launch events: the span of the same
+    # steps back to back on the library stream, two events around the loop
+    # (the rehash is one launch: the span / steps is the launch's time plus
+    # the gaps between launches, never more than the step's wall time)
+    k1_span = _span_ms(tree, torch, dev, lambda: tree.rehash(), args.steps)
+    # per-launch HIP events (timing on), reported beside it
     tree.set_timing(True)
     tree.kernel_stats('*reset*')
     for _ in range(args.steps):
@@ -199,7 +204,8 @@ def main():
         inner_nodes = sum(16 ** l for l in range(5))
         meta_bytes = 17 * n + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner_nodes * 18 + 17 * 16 * 18
         seg_blocks += 349525   # inner-node MD5 blocks (full nodes: 5 each)
-        k1_avg_ms = max(k1_ms / max(k1_n, 1), 1e-9)
+        k1_avg_ms = max(k1_span, 1e-9)
+        k1_evt_ms = k1_ms / max(k1_n, 1)
         achieved_gbs = k1_bytes / (k1_avg_ms / 1e3) / 1e9
         t_hbm = k1_bytes / (HBM_PEAK_GBS * 1e9)
         t_valu = seg_blocks * MD5_SIMD_CYCLES_PER_BLOCK / (SIMDS * CLOCK_HZ)
@@ -210,7 +216,9 @@ def main():
                 'traffic': pmc['traffic_bytes'] if pmc and pmc.get('traffic_bytes') else None,
                 'kernel': K1_KERNEL + ' (K1 segment_hash + levels 5..1 + top, one launch)',
                 'kernel_avg_ms': round(k1_avg_ms, 4),
-                'kernel_time_source': 'HIP events on the library stream around every launch (%d launches)' % k1_n,
+                'kernel_time_source': 'GPU span of %d back-to-back rehash launches on the library stream / %d '
+                                      '(two events around the loop, none per launch)' % (args.steps, args.steps),
+                'kernel_avg_ms_events': round(k1_evt_ms, 4),
                 'bytes_per_launch': k1_bytes,
                 'bytes_formula': '17 B x %d keys (values) + 17 B x (%d non-empty segments + %d present inner nodes) '
                                  '(SURVEY §8(d))' % (n, nonempty, present_inner),
@@ -239,6 +247,7 @@ def main():
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, dev_index, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_d, vals_d, n, dev_index, torch)
             out['leveldb'] = _bench_leveldb(synctree_hip, tree, dev_index, torch)
+            out['rehash_after_mutation'] = _bench_rehash_after_mutation(tree, n, torch)
             out['repair'] = _bench_repair(tree, keys_h, torch)
     tree.close()
     del keys_d, vals_d
@@ -257,6 +266,23 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def _span_ms(tree, torch, dev, fn, k):
+    """GPU time per call of k back-to-back calls of fn on the tree's stream:
+    the tree is moved onto a torch stream for the loop and two events bracket
+    it (no per-launch events: nothing is added between the launches)."""
+    s = torch.cuda.Stream(device=dev)
+    tree.set_stream(s.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record(s)
+    for _ in range(k):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    tree.set_stream(0)
+    return e0.elapsed_time(e1) / k
 
 
 # ---------------------------------------------------------------- PMC traffic of K1
@@ -346,6 +372,59 @@ def _bench_cold_l3(tree, torch, dev, k1_bytes, hot_ms, reps=5):
     return {'kernel_avg_ms': round(avg, 4), 'achieved_GBps': round(gbs, 1), 'frac': round(gbs / HBM_PEAK_GBS, 4),
             'hot_kernel_avg_ms': round(hot_ms, 4), 'launches': n,
             'what': 'rehash kernel after a 1 GiB read per launch (Infinity Cache flushed): tiles read from HBM'}
+
+
+def _bench_rehash_after_mutation(tree, n0, torch, reps=10, batch=1000):
+    """rehash/1 right after an insert/3 batch: the rehash a
+    tree pays when its content changed since the last one (the repair path,
+    riak_ensemble_peer_tree.erl:264-277; any rehash after writes).  Each rep
+    inserts `batch` new keys (host path, a streaming batch into the pages),
+    then times rehash/1.  The first full rehash after a mutation hashes every
+    segment straight from the tree's segments (no tile build, rehash_all);
+    roofline over its kernels (HIP events): the same SURVEY §8(d) bytes as the
+    headline, 17 B per value + 17 B per present node written."""
+    rng = np.random.default_rng(11)
+    ts, tins = [], []
+    for r in range(reps + 1):
+        ks = [int(x) for x in rng.integers(1 << 62, (1 << 63) - 1, batch)]
+        vs = [bytes([0]) + (2).to_bytes(8, 'big') + (r * batch + i).to_bytes(8, 'big') for i in range(batch)]
+        tree.sync()
+        t0 = time.perf_counter()
+        tree.insert_batch(ks, vs)
+        tree.sync()
+        t1 = time.perf_counter()
+        if r == reps:   # the kernels of one more rep, on HIP events
+            tree.set_timing(True)
+            tree.kernel_stats('*reset*')
+        tree.rehash()
+        tree.sync()
+        t2 = time.perf_counter()
+        if r == reps:
+            ks_ms = {}
+            for nm in ('segment_hash', 'level_rehash', 'seg_perm', 'tile_build', 'rehash_fused', 'page_fold'):
+                c, ms = tree.kernel_stats(nm)
+                if c:
+                    ks_ms[nm] = round(ms, 4)
+            tree.set_timing(False)
+        elif r > 0:   # rep 0 builds the pages
+            tins.append(t1 - t0)
+            ts.append(t2 - t1)
+    ts.sort()
+    tins.sort()
+    n = tree.num_entries()
+    nonempty = int((tree.level_entries(tree.height + 1)[0] > 0).sum())
+    pres_inner = sum(int((tree.level_entries(l)[0] > 0).sum()) for l in range(1, tree.height + 1))
+    alg = 17 * n + 17 * (nonempty + pres_inner)
+    kern = ks_ms.get('segment_hash', 0.0) + ks_ms.get('level_rehash', 0.0)
+    gbs = alg / (kern / 1e3) / 1e9 if kern else None
+    return {'ms_per_rehash': round(ts[len(ts) // 2] * 1e3, 4), 'ms_per_insert_batch': round(tins[len(tins) // 2] * 1e3, 4),
+            'batch_keys': batch, 'reps': reps, 'entries': n, 'kernels_ms': ks_ms,
+            'roofline': {'bound': 'hbm', 'achieved': round(gbs, 1) if gbs else None, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4) if gbs else None, 'traffic': None,
+                         'bytes_per_rehash': alg, 'kernel_ms': round(kern, 4),
+                         'kernel': 'k_segment_hash_perm (every segment from the pages) + the level kernels'},
+            'what': 'insert/3 of %d new keys, then rehash/1 (wall, median of %d; the first full rehash after a '
+                    'mutation hashes from the segments, no tile build)' % (batch, reps)}
 
 
 def _bench_repair(tree, keys_h, torch, reps=10):
@@ -672,13 +751,17 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     stable = bool((allt.cpu().numpy() == before).all()) and int(before.reshape(-1, 18)[:, 0].sum()) == world * E
     # the group launch alone (HIP events on trees[0]'s stream) and its roofline:
     # per tree the same algorithmic bytes as the headline's launch
+    # the group launch's GPU time: the span of reps group rehashes on trees[0]'s
+    # stream (the launch's stream), no per-launch events; per-launch HIP
+    # events beside it
+    g_avg = _span_ms(trees[0], torch, dev, lambda: synctree_hip.rehash_group(trees), reps)
     trees[0].set_timing(True)
     trees[0].kernel_stats('*reset*')
     for _ in range(reps):
         synctree_hip.rehash_group(trees)
     g_n, g_ms = trees[0].kernel_stats('rehash_group')
     trees[0].set_timing(False)
-    g_avg = g_ms / max(g_n, 1)
+    g_evt = g_ms / max(g_n, 1)
     S = trees[0].segments
     H = trees[0].height
     # SURVEY §8(d) bytes per tree: 17 B per key (values) + a 17-B entry per
@@ -706,7 +789,7 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     return {'keys_per_s': round(world * E * nk * reps / el, 1), 'ms_per_batch': round(el * 1e3 / reps, 3),
             'ensembles_per_gpu': E, 'ensembles_total': world * E, 'keys_per_ensemble': nk, 'ranks': world,
             'tops_allgather_stable': stable, 'load_s': round(load_s, 2),
-            'kernel_ms_per_batch': round(g_avg, 4),
+            'kernel_ms_per_batch': round(g_avg, 4), 'kernel_ms_per_batch_events': round(g_evt, 4),
             'roofline': {'bound': 'hbm', 'achieved': round(g_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(g_gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': E * tree_bytes,
                          'bytes_per_tree': tree_bytes, 'bytes_per_tree_incl_metadata': meta_bytes,
@@ -715,7 +798,9 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
                          'kernel': K1_KERNEL + '<GROUP, 8 waves per window, 6 waves per SIMD>',
                          'note': 'SURVEY §8(d): per tree 17 B of value per key + a 17-B entry per present node '
                                  '(non-empty segments + present inner nodes, mean of %d sampled trees); kernel time '
-                                 'from HIP events on trees[0]\'s stream' % len(samp)},
+                                 '= GPU span of %d back-to-back group rehashes on trees[0]\'s stream / %d (host '
+                                 'preparation between them included: an upper bound of the launch)'
+                                 % (len(samp), reps, reps)},
             'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
             'per_key_multi': perkey,
             'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '

@@ -338,3 +338,12 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
             }
     }
 }
+
+// Empty segment s in place (a segment node deleted or stored as []): its
+// page keeps its capacity; *cnt = the entries it held.
+__global__ void k_page_clear(PageMeta m, uint64_t s, uint64_t *cnt) {
+    if (threadIdx.x | blockIdx.x) return;
+    *cnt = m.end[s] - m.beg[s];
+    m.end[s] = m.beg[s];
+    m.vend[s] = m.vbeg[s];
+}

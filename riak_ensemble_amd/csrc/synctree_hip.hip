@@ -125,6 +125,7 @@ struct st_tree {
     uint32_t *tmhmax = nullptr;     // the largest window's level-H message bytes (device word)
     uint32_t mh_bytes = 0;          // ... as read back at the last tile build
     bool tiles_valid = false;
+    bool tiles_wanted = false;      // a full rehash since the tiles went stale: the next one builds them
     uint32_t *lvl_cnt = nullptr;    // finished-children counters (k_rehash_fused climb)
     MailEntry *mail = nullptr;      // climb mailboxes (levels 1..H-2)
     uint32_t mail_epoch = 0;        // epoch of the last fused launch over this tree (MailEntry)
@@ -271,12 +272,18 @@ static void mem_forget_owner(const st_tree *t) {
 
 // Host synchronisation of a tree's stream; it also makes the blocks the tree
 // freed before it reusable.
+static int synced(st_tree *t);
 static int tsync(st_tree *t) {
     const hipError_t e = hipStreamSynchronize(t->stream);
     if (e != hipSuccess) {
         g_err = std::string("hipStreamSynchronize: ") + hipGetErrorString(e);
         return ST_EDEVICE;
     }
+    return synced(t);
+}
+// The tree's stream has drained (synchronised here, or idle while its work
+// ran and completed on a stream that was): bookkeeping and its device-error word.
+static int synced(st_tree *t) {
     t->sync_epoch.fetch_add(1, std::memory_order_release);
     t->reads_remote = false;
     t->async_pending = false;
@@ -1190,7 +1197,21 @@ static int rehash_tiled(st_tree *t) {
 // per-level kernels above; other geometries: one k_level_hash launch per level.
 // ps: the prefix states of a streaming batch's verify (k_verify_pos) or NULL.
 static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr) {
-    if (!mask) return rehash_tiled(t);
+    if (!mask) {
+        // The first full rehash after a mutation hashes straight from the
+        // CSR (a lane per segment, no tile build: the repair path's
+        // rehash/1, riak_ensemble_peer_tree.erl:264-277); the next one, the
+        // tree unchanged since, builds the tiles for the fused kernel.
+        if (t->tiles_valid || t->tiles_wanted || t->partitioned) return rehash_tiled(t);
+        t->tiles_wanted = true;
+        DevTree d = view(t);
+        CHK(ensure_perm_any(t));
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm,
+               (const uint8_t *)nullptr, (const PrefixState *)nullptr);
+        if (t->H == 0) return ST_OK;
+        if (t->W == 16) return levels16(t, t->H, nullptr);
+        return rehash_levels(t, t->H, nullptr);
+    }
     DevTree d = view(t);
     CHK(ps ? ensure_perm_any(t) : ensure_perm(t));
     LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask, ps);
@@ -1381,6 +1402,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     // the hash-ready tiles are stale now; the next full rehash rebuilds them
     // (streaming batches never pay for a tile rebuild they do not use)
     t->tiles_valid = false;
+    t->tiles_wanted = false;
 
     if (in.verify_rehash) {
         // dirty-path rehash: segments whose content changed and their ancestors
@@ -1472,6 +1494,9 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     t->perm_valid = false;
     return ST_OK;
 }
+
+// trees from this many entries delete segments in the pages (st_store_segment)
+#define PAGED_DELETE_MIN (1ull << 20)
 
 static int pages_fold(st_tree *t) {
     if (!t->pg.on) return ST_OK;
@@ -1580,6 +1605,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     t->n += tot.v[3];
     t->perm_valid = false;
     t->tiles_valid = false;
+    t->tiles_wanted = false;
     // dirty-path rehash over the pages, each segment from its unchanged prefix's MD5 state
     HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
     LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
@@ -1774,6 +1800,7 @@ static void small_served(st_tree *t, int op) {
         t->ov_pending = true;
         t->fresh = false;
         t->tiles_valid = false;
+        t->tiles_wanted = false;
         t->perm_valid = false;
     }
 }
@@ -2209,8 +2236,27 @@ extern "C" int st_corrupt(st_tree *t, uint8_t ktype, const uint8_t *kbytes, uint
 extern "C" int st_store_segment(st_tree *t, uint64_t segment, uint64_t n, const uint8_t *ktype, const uint8_t *kheap,
                                 const uint64_t *koff, const uint8_t *vheap, const uint64_t *voff) {
     ENTER(t);
-    FLUSH(t);
     if (segment >= t->S) { g_err = "segment out of range"; return ST_EINVAL; }
+    if (n == 0 && !t->partitioned && t->pg_slack >= 0 && (t->pg.on || t->n >= PAGED_DELETE_MIN)) {
+        // an emptied segment (delete_node, the repair path) in the pages: no
+        // CSR rewrite, the page just ends where it begins
+        CHK(flush_overlay(t));
+        if (!t->pg.on) CHK(pages_build(t, t->pg_slack, PageSums(0)));
+        Scratch sc(t);
+        uint64_t *dc = nullptr, c = 0;
+        CHK(sc.alloc(&dc, 1));
+        LAUNCH(t, "page_clear", k_page_clear, 1, 64, 0, t->pg.m, segment, dc);
+        CHK(d2h(t, &c, dc, 8));
+        t->n -= c;
+        t->perm_valid = false;
+        t->tiles_valid = false;
+        t->tiles_wanted = false;
+        t->fresh = false;
+        CHK(set_erec(t, t->base[t->H + 1] + segment, 1));
+        CHK(tsync(t));
+        return ST_OK;
+    }
+    FLUSH(t);
     HostRecords hr;
     CHK(pack_records(n, ktype, kheap, koff, hr));
     for (uint64_t i = 1; i < n; i++)
@@ -2347,7 +2393,11 @@ extern "C" int st_set_record_top(st_tree *t, const uint8_t *hash17) {
 extern "C" int st_rehash(st_tree *t, int upper) {
     ENTER_ANY(t);
     if (upper) CHK(alive(t));   // only a full rehash recomputes every level of a tree in error
-    FLUSH(t);
+    CHK(flush_overlay(t));
+    // the pages stay (no fold) unless this rehash builds the tiles (from the
+    // CSR): the upper levels, the rehash straight from the segments
+    // (rehash_all) and the fused kernel over valid tiles do not read the CSR
+    if (!upper && !t->tiles_valid && (t->tiles_wanted || t->partitioned)) CHK(pages_fold(t));
     if (upper && t->H == 0) { g_err = "rehash_upper at Height 0 does not terminate in the reference"; return ST_EINVAL; }
     if (t->partitioned && upper) {
         g_err = "a segment-range partition supports the full rehash (st_rehash upper = 0) only";
@@ -2386,11 +2436,16 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
         for (uint32_t j = 0; j < i; j++)
             if (trees[j] == u) { g_err = "a tree appears twice in the group"; return ST_EINVAL; }
     }
+    // each tree ready (tiles, counters) and its stream drained -- a tree with
+    // nothing enqueued since its last synchronisation is not waited for
+    // (hundreds of trees per group: the launch is not held up by idle syncs)
     for (uint32_t i = 0; i < n; i++) {
-        CHK(flush_all(trees[i]));
-        CHK(ensure_tiles(trees[i]));
-        CHK(ensure_lvl_cnt(trees[i]));
-        CHK(tsync(trees[i]));
+        st_tree *u = trees[i];
+        const bool idle = !u->async_pending && u->tiles_valid && u->lvl_cnt && !u->pg.on && !u->ov_pending;
+        CHK(flush_all(u));
+        CHK(ensure_tiles(u));
+        CHK(ensure_lvl_cnt(u));
+        if (!idle || u->stream == t->stream) CHK(tsync(u));
     }
     // every window of every tree in ONE launch of the fused kernel (K1 +
     // levels + top per tree): the trees' tails overlap each other's K1
@@ -2416,8 +2471,13 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     int first = ST_OK;
     if (hipStreamSynchronize(t->stream) != hipSuccess) CHK(tsync(t));   // a launch fault: report it
     for (uint32_t i = 0; i < n; i++) {
-        CHK(erec_after_rehash(trees[i]));
-        const int r = tsync(trees[i]);
+        // every tree's stream was drained before the launch, which completed:
+        // only the device-error words remain to be read
+        const int r = synced(trees[i]);
+        if (trees[i]->erec) {
+            CHK(erec_after_rehash(trees[i]));
+            trees[i]->async_pending = true;
+        }
         if (r == ST_OK) {
             trees[i]->fresh = false;
             trees[i]->poisoned = false;
@@ -3591,6 +3651,7 @@ extern "C" int st_restore_leveldb(st_tree *t, const uint8_t *tree_id, uint32_t i
     t->n = ne; t->kbytes = kb; t->vbytes = vb;
     t->perm_valid = false;
     t->tiles_valid = false;
+    t->tiles_wanted = false;
     t->fresh = false;
     done(true);
     CHK(tsync(t));   // the caller's buffers may go after return

@@ -82,9 +82,29 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack):
         assert dev.insert_int64(keys[idx], _obj(idx + 100, epoch=3)) == 0
         ora.insert_int64_seq(keys[idx], _obj(idx + 100, epoch=3))
     assert dev.page_stats()[0] == 1
-    dev.rehash()
+    dev.rehash()   # the first full rehash after the batches hashes the pages' segments: no fold
+    assert dev.page_stats()[0] == 1
     assert dev.top_hash() == ora.top_hash()
     _levels(dev, ora)
+    # the repair path (riak_ensemble_peer_tree.erl:264-277): delete segment
+    # nodes of a paged tree (the pages just empty them), then rehash/1 twice
+    # (from the segments, then the tiled fused kernel)
+    idx = rng.integers(0, nxt, batch)
+    assert dev.insert_int64(keys[idx], _obj(idx + 200, epoch=4)) == 0
+    ora.insert_int64_seq(keys[idx], _obj(idx + 200, epoch=4))
+    assert dev.page_stats()[0] == 1
+    H1 = dev.height + 1
+    for k in keys[idx[:3]]:
+        seg = ora.segment_of(int(k))
+        dev.delete_node(H1, seg)
+        ora.delete_node(H1, seg)
+    assert dev.page_stats()[0] == 1 and dev.num_entries() == ora.num_entries()
+    ora.rehash()
+    for _ in range(2):
+        dev.rehash()
+        assert dev.top_hash() == ora.top_hash()
+    _levels(dev, ora)
+    assert dev.get_batch([int(k) for k in keys[idx[:20]]]) == [ora.get(int(k)) for k in keys[idx[:20]]]
     dev.close()
 
 
