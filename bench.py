@@ -961,7 +961,20 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
     per.sort()
     entries = pt.tree.num_entries()
     pt.tree.close()
+    # roofline on the touched segments (the batch's floor): their values are
+    # read by the path verification, read by the dirty-path hash and written
+    # once by the merge -- 3 x their bytes (st_page_stats out[5], before each
+    # merge), over the wall time per batch (everything in it)
+    tv = (ps1[5] - ps0[5]) / max(K, 1)
+    alg = 3 * tv
+    gbs = alg / (el / K) / 1e9
+    roof = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None, 'bytes_per_batch': int(alg),
+            'touched_value_bytes_per_batch': int(tv),
+            'formula': '3 x the value bytes of the segments a batch touches (verify read + hash read + merge '
+                       'write), per batch, over the wall ms_per_batch (all kernels and host work of the batch)'}
     return {'batch_keys_per_s': round(K * B / el, 1), 'ms_per_batch': round(el * 1e3 / K, 4), 'batches': K,
+            'roofline': roof,
             'ms_per_batch_median': round(per[len(per) // 2] * 1e3, 4), 'ms_per_batch_max': round(per[-1] * 1e3, 4),
             'pages': {'batches': ps1[1] - ps0[1], 'page_builds': ps1[2] - ps0[2],
                       'moved_entry_slots': ps1[4] - ps0[4],

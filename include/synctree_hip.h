@@ -409,8 +409,9 @@ int st_debug_knob(st_tree *t, int knob, int64_t value);
  * into the canonical CSR first.  out[0] = pages in use, out[1] = batches
  * through the pages, out[2] = page builds (the first batch's, and rebuilds
  * when moved segments fill the append region), out[3] = folds, out[4] =
- * entry slots of the segments moved to new pages. */
-int st_page_stats(st_tree *t, uint64_t out[5]);
+ * entry slots of the segments moved to new pages, out[5] = value bytes of
+ * the segments the batches touched (before each merge). */
+int st_page_stats(st_tree *t, uint64_t out[6]);
 
 #ifdef __cplusplus
 }

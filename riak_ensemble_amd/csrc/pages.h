@@ -27,7 +27,9 @@ struct PageMeta {
     uint64_t *ecap, *kcap, *vcap;        // S each: page capacities (entry slot end, key / value byte ends)
 };
 
-typedef USum<4> PageSums;   // entries, key bytes, value bytes; k_page_plan: + new keys
+typedef USum<4> PageSums;   // entries, key bytes, value bytes (+ a spare)
+typedef USum<5> PlanSums;   // k_page_plan: a moved segment's new page (entries, key bytes, value bytes), new keys,
+                            // the touched segment's value bytes before the merge
 
 // Page capacity for a segment of c entries, kb key bytes and vb value bytes
 // (slack_pct: percent of slack; < 0: none, a gap-free CSR).  Byte caps are
@@ -135,11 +137,11 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
 // the segment's new keys (for the tree's entry count).
 __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *voff, const uint64_t *bseg_off,
                             const uint8_t *reject, const BatchSums *bs, const SegSums *ss, uint8_t *dirty, uint64_t S,
-                            int slack_pct, uint8_t *mode, PageSums *reloc) {
+                            int slack_pct, uint8_t *mode, PlanSums *reloc) {
     for (uint64_t s = gtid(); s < S; s += gstride()) {
         const uint64_t j0 = bseg_off[s], je = bseg_off[s + 1];
         if (reject && reject[s]) dirty[s] = 0;   // positions came before the verify (k_verify_pos)
-        PageSums r(0);
+        PlanSums r(0);
         uint8_t md = 0;
         if (j0 != je && !(reject && reject[s]) && dirty[s]) {
             const uint64_t b = m.beg[s];
@@ -154,8 +156,12 @@ __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *vo
                 grow = dk >= 0 && dv >= 0;
             }
             md = fits && grow ? 1 : 2;
-            if (md == 2) r = page_caps(x.v[0], x.v[1], x.v[2], slack_pct < 0 ? 0 : slack_pct);
+            if (md == 2) {
+                const PageSums c = page_caps(x.v[0], x.v[1], x.v[2], slack_pct < 0 ? 0 : slack_pct);
+                r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
+            }
             r.v[3] = x.v[3];
+            r.v[4] = voff[m.end[s]] - voff[b];
         }
         mode[s] = md;
         reloc[s] = r;
@@ -182,8 +188,8 @@ struct PageMergeArgs {
     const BatchSums *bx;          // exclusive scan over the sorted batch
     const SegSums *ss;            // per segment: merged count, key bytes, value bytes
     const uint8_t *mode;
-    const PageSums *rbase;        // exclusive scan of the relocation sizes
-    const PageSums *rsz;          // the relocation sizes
+    const PlanSums *rbase;        // exclusive scan of the relocation sizes
+    const PlanSums *rsz;          // the relocation sizes
     uint64_t e0, k0, v0;          // the append region's bases
     unsigned long long *chk;      // checked build (st_debug_knob ST_DBG_PAGE_CHECK): [0] violations, [1..4] the first
 };
@@ -257,7 +263,7 @@ __global__ void __launch_bounds__(256) k_page_merge(PageMergeArgs p) {
         const SegSums X = p.ss[s];
         uint64_t De = b, Dk = Kb, Dv = Vb, EC = p.m.ecap[s], KC = p.m.kcap[s], VC = p.m.vcap[s];
         if (md == 2) {
-            const PageSums R = p.rbase[s], Z = p.rsz[s];
+            const PlanSums R = p.rbase[s], Z = p.rsz[s];
             De = p.e0 + R.v[0]; Dk = p.k0 + R.v[1]; Dv = p.v0 + R.v[2];
             EC = De + Z.v[0]; KC = Dk + Z.v[1]; VC = Dv + Z.v[2];
         }

@@ -75,7 +75,7 @@ struct Pages {
     uint8_t *kheap = nullptr, *vheap = nullptr;
     uint64_t cap_e = 0, cap_k = 0, cap_v = 0;   // allocated entry slots / heap bytes
     uint64_t use_e = 0, use_k = 0, use_v = 0;   // the append region starts here
-    uint64_t batches = 0, builds = 0, folds = 0, reloc_e = 0;
+    uint64_t batches = 0, builds = 0, folds = 0, reloc_e = 0, touched_v = 0;
 };
 
 struct st_tree {
@@ -838,13 +838,14 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
     return ST_EINVAL;
 }
 
-extern "C" int st_page_stats(st_tree *t, uint64_t out[5]) {
+extern "C" int st_page_stats(st_tree *t, uint64_t out[6]) {
     ENTER_ANY(t);
     out[0] = t->pg.on ? 1 : 0;
     out[1] = t->pg.batches;
     out[2] = t->pg.builds;
     out[3] = t->pg.folds;
     out[4] = t->pg.reloc_e;
+    out[5] = t->pg.touched_v;
     return ST_OK;
 }
 
@@ -1427,9 +1428,9 @@ static void pages_free(st_tree *t, Pages &g) {
     for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.ecap, (void *)g.m.kcap,
                     (void *)g.m.vcap, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
-    const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e;
+    const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e, tv = g.touched_v;
     g = Pages();
-    g.batches = b; g.builds = bu; g.folds = f; g.reloc_e = r;
+    g.batches = b; g.builds = bu; g.folds = f; g.reloc_e = r; g.touched_v = tv;
 }
 
 // Copy the tree's segments (CSR or pages) into a new layout: pages with
@@ -1487,6 +1488,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     g.use_e = tot.v[0]; g.use_k = tot.v[1]; g.use_v = tot.v[2];
     g.on = true;
     g.batches = t->pg.batches; g.builds = t->pg.builds + 1; g.folds = t->pg.folds; g.reloc_e = t->pg.reloc_e;
+    g.touched_v = t->pg.touched_v;
     CHK(tsync(t));   // the old pages (if any) were read
     pages_free(t, t->pg);
     t->pg = g;
@@ -1519,7 +1521,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *ss = nullptr;
-    PageSums *rsz = nullptr, *rbase = nullptr;
+    PlanSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
     PrefixState *ps = nullptr;
@@ -1535,7 +1537,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n + 1));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
-    HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PageSums), t->stream));
+    HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PlanSums), t->stream));
     // the touched segments' verify fused with the merge positions (every
     // segment's merged sizes), then the inner nodes of their paths
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
@@ -1556,13 +1558,13 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     ma.seg_reject = reject;
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     // in place or to a new page; the moves' places in the append region
-    PageSums tot(0);
+    PlanSums tot(0);
     for (int pass = 0;; pass++) {
         LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
                (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss,
                dirty, S, t->pg_slack, mode, rsz);
-        CHK(exclusive_scan<PageSums>(t, rsz, rbase, S + 1));
-        CHK(d2h(t, &tot, rbase + S, sizeof(PageSums)));
+        CHK(exclusive_scan<PlanSums>(t, rsz, rbase, S + 1));
+        CHK(d2h(t, &tot, rbase + S, sizeof(PlanSums)));
         const Pages &g = t->pg;
         if (g.use_e + tot.v[0] + 1 <= g.cap_e && g.use_k + tot.v[1] <= g.cap_k && g.use_v + tot.v[2] <= g.cap_v) break;
         if (pass) { g_err = "page build left no room for the batch's moves"; return ST_EDEVICE; }
@@ -1601,6 +1603,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     }
     t->pg.use_e += tot.v[0]; t->pg.use_k += tot.v[1]; t->pg.use_v += tot.v[2];
     t->pg.reloc_e += tot.v[0];
+    t->pg.touched_v += tot.v[4];
     t->pg.batches++;
     t->n += tot.v[3];
     t->perm_valid = false;

@@ -409,8 +409,9 @@ class DeviceTree:
 
     def page_stats(self):
         """(pages in use, batches through the pages, page builds, folds,
-        entry slots of segments moved to new pages) -- st_page_stats."""
-        v = (ctypes.c_uint64 * 5)()
+        entry slots of segments moved to new pages, value bytes of the
+        segments the batches touched) -- st_page_stats."""
+        v = (ctypes.c_uint64 * 6)()
         _lib.check(self.L.st_page_stats(self.h, v), 'st_page_stats')
         return tuple(int(x) for x in v)
 

@@ -62,7 +62,8 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack):
         assert dev.num_entries() == ora.num_entries(), b
         if b % 6 == 5:
             _levels(dev, ora)
-    on, batches, builds, folds, moved = dev.page_stats()
+    on, batches, builds, folds, moved, touched = dev.page_stats()
+    assert touched > 0
     assert on == 1 and batches == 30 and folds == 0, dev.page_stats()
     assert moved > 0
     if slack <= 2:
