@@ -25,7 +25,16 @@
 struct PageMeta {
     uint64_t *beg, *end, *vbeg, *vend;   // S each: the DevTree view's seg_off / seg_end / seg_voff / seg_vend
     uint64_t *ecap, *kcap, *vcap;        // S each: page capacities (entry slot end, key / value byte ends)
+    uint16_t *klen;                      // S: the length every key record of the segment has (KLEN_MIXED: not
+                                         // one length, KLEN_NONE: no entries) -- fixed-stride merge positions
 };
+#define KLEN_MIXED KLEN_MIXED_   // st_kernels.h
+#define KLEN_NONE KLEN_NONE_
+// the uniform key length of a segment after adding records of length l
+__device__ __forceinline__ uint32_t klen_add(uint32_t cur, uint64_t l) {
+    if (l == 0 || l >= KLEN_NONE) return KLEN_MIXED;
+    return cur == KLEN_NONE ? (uint32_t)l : (cur == l ? cur : KLEN_MIXED);
+}
 
 typedef USum<4> PageSums;   // entries, key bytes, value bytes (+ a spare)
 typedef USum<5> PlanSums;   // k_page_plan: a moved segment's new page (entries, key bytes, value bytes), new keys,
@@ -100,15 +109,21 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
         const PageSums B = base[s];
         const uint64_t De = d.e0 + B.v[0], Dk = d.k0 + B.v[1], Dv = d.v0 + B.v[2];
         const uint64_t kb0 = t.koff[b], vb0 = t.voff[b];
+        const uint64_t l0 = c ? t.koff[b + 1] - kb0 : 0;
+        bool mixed = false;
         for (uint64_t i = lane; i <= c; i += 64) {   // offsets incl. the end slot
-            d.koff[De + i] = Dk + (t.koff[b + i] - kb0);
+            const uint64_t ko = t.koff[b + i];
+            d.koff[De + i] = Dk + (ko - kb0);
             d.voff[De + i] = Dv + (t.voff[b + i] - vb0);
+            if (i < c) mixed |= t.koff[b + i + 1] - ko != l0;
         }
+        const bool any_mixed = __ballot(mixed) != 0;
         wave_copy_gg(d.kheap + Dk, t.kheap + kb0, t.koff[e] - kb0);
         wave_copy_gg(d.vheap + Dv, t.vheap + vb0, t.voff[e] - vb0);
         if (lane == 0) {
             if (d.m.beg) {
                 const PageSums Z = sz[s];
+                d.m.klen[s] = (uint16_t)(c == 0 ? KLEN_NONE : any_mixed ? KLEN_MIXED : klen_add(KLEN_NONE, l0));
                 d.m.beg[s] = De;
                 d.m.end[s] = De + c;
                 d.m.vbeg[s] = Dv;
@@ -202,126 +217,177 @@ __device__ __forceinline__ bool pg_ok(unsigned long long *chk, bool ok, uint32_t
     return false;
 }
 
-// n bytes from src to dst, highest 16 bytes first (dst >= src, or the two
-// disjoint): every chunk is loaded before a lower chunk's store can reach
-// it, so four chunks go out together.  Unaligned 16-byte global loads /
-// stores (the heaps keep slack).
-__device__ __forceinline__ void lane_move_down(uint8_t *dst, const uint8_t *src, uint64_t n) {
-    uint64_t i = n;
-    while (i >= 64) {
-        uint4 v0, v1, v2, v3;
-        __builtin_memcpy(&v0, src + i - 16, 16);
-        __builtin_memcpy(&v1, src + i - 32, 16);
-        __builtin_memcpy(&v2, src + i - 48, 16);
-        __builtin_memcpy(&v3, src + i - 64, 16);
-        __builtin_memcpy(dst + i - 16, &v0, 16);
-        __builtin_memcpy(dst + i - 32, &v1, 16);
-        __builtin_memcpy(dst + i - 48, &v2, 16);
-        __builtin_memcpy(dst + i - 64, &v3, 16);
-        i -= 64;
-    }
-    while (i >= 16) {
+// A piece job: key bytes, value bytes, key offsets, value offsets
+struct PieceJob {
+    uint64_t kd, ks, nk, vd, vs, nv, ko, vo, a, e, de, dk, dv, fl;   // fl: bit 0 keys, 1 values, 2 key offs, 3 value offs
+};
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+// Wave-cooperative moves (every lane of the wave, a wave-uniform job): n
+// bytes from src to dst (dst >= src, or disjoint), top down in units of 64
+// lanes x 16 bytes, a unit's loads before its stores; the lowest chunk of a
+// piece clamps to its first 16 bytes (the bytes it shares with the chunk
+// above get the same values twice, both loaded in that unit); fewer than 16
+// bytes left below a stored unit are copied bytewise (a clamped chunk would
+// read bytes that unit already rewrote).  A wave's loads touch 8-9 lines,
+// where a lane per segment moving its own bytes touched 64: 1.43 against
+// 1.75 ms a config-5 batch.  (Four jobs' units loaded together before their
+// stores -- more loads in flight -- ran slower, 1.98 ms.)
+__device__ __forceinline__ void wave_move_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t lane) {
+    for (uint64_t top = n;;) {
+        if (top < 16) {
+            if (lane == 0)
+                for (uint64_t i = top; i-- > 0;) dst[i] = src[i];
+            break;
+        }
+        const int64_t hi = (int64_t)top - 16 * (int64_t)lane;
+        const bool act = hi > 0;
+        const uint64_t c0 = hi >= 16 ? (uint64_t)hi - 16 : 0;
         uint4 v;
-        __builtin_memcpy(&v, src + i - 16, 16);
-        __builtin_memcpy(dst + i - 16, &v, 16);
-        i -= 16;
+        if (act) __builtin_memcpy(&v, src + c0, 16);
+        __asm__ volatile("" ::: "memory");   // the unit's loads, all of them, before any store (no fused memcpy)
+        if (act) __builtin_memcpy(dst + c0, &v, 16);
+        if (top <= 1024) break;
+        top -= 1024;
     }
-    while (i) {
-        i--;
-        dst[i] = src[i];
+}
+// entries [a, e) of o moved by de and rebased by dk, top down, 64 per unit
+__device__ __forceinline__ void wave_move_offsets(uint64_t *o, uint64_t a, uint64_t e, uint64_t de, uint64_t dk,
+                                                  uint32_t lane) {
+    for (uint64_t top = e; top > a;) {
+        const bool act = top >= a + 1 + lane;
+        const uint64_t i = top - 1 - lane;
+        uint64_t x = 0;
+        if (act) x = o[i];
+        __asm__ volatile("" ::: "memory");
+        if (act) o[i + de] = x + dk;
+        top = top - a > 64 ? top - 64 : a;
+    }
+}
+// every lane's job (has = this lane has one), one after another by the whole wave
+__device__ __forceinline__ void wave_run_jobs(const PieceJob &J, bool has, uint32_t lane) {
+    uint64_t jm = __ballot(has);
+    while (jm) {
+        const uint32_t L = (uint32_t)__builtin_ctzll(jm);
+        jm &= jm - 1;
+        const uint64_t fl = rl64(J.fl, L);
+        if (fl & 1) wave_move_bytes((uint8_t *)rl64(J.kd, L), (const uint8_t *)rl64(J.ks, L), rl64(J.nk, L), lane);
+        if (fl & 2) wave_move_bytes((uint8_t *)rl64(J.vd, L), (const uint8_t *)rl64(J.vs, L), rl64(J.nv, L), lane);
+        const uint64_t a = rl64(J.a, L), e = rl64(J.e, L), de = rl64(J.de, L);
+        if (fl & 4) wave_move_offsets((uint64_t *)rl64(J.ko, L), a, e, de, rl64(J.dk, L), lane);
+        if (fl & 8) wave_move_offsets((uint64_t *)rl64(J.vo, L), a, e, de, rl64(J.dv, L), lane);
     }
 }
 
-// Offsets of old entries [a, e) of the page at o, moved by de entries and
-// rebased by dk (added), highest entry first, four at a time.
-__device__ __forceinline__ void lane_offsets_down(uint64_t *o, uint64_t a, uint64_t e, uint64_t de, uint64_t dk) {
-    uint64_t i = e;
-    while (i >= a + 4) {
-        const uint64_t x0 = o[i - 1], x1 = o[i - 2], x2 = o[i - 3], x3 = o[i - 4];
-        o[i - 1 + de] = x0 + dk;
-        o[i - 2 + de] = x1 + dk;
-        o[i - 3 + de] = x2 + dk;
-        o[i - 4 + de] = x3 + dk;
-        i -= 4;
-    }
-    while (i > a) {
-        i--;
-        o[i + de] = o[i] + dk;
-    }
-}
-
+// The merge, a lane per segment for its control (groups, records) and the
+// whole wave for every piece move: the wave's lanes step through their groups
+// together, top down; each round moves every lane's piece (wave_run_jobs),
+// then each lane writes its group's records into the gap above it.
 template <bool CHECK>
 __global__ void __launch_bounds__(256) k_page_merge(PageMergeArgs p) {
     const MergeArgs &a = p.a;
     unsigned long long *chk = CHECK ? p.chk : nullptr;
-    for (uint64_t s = gtid(); s < a.S; s += gstride()) {
-        const uint8_t md = p.mode[s];
-        if (!md) continue;
-        const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-        const uint64_t b = p.m.beg[s], c = p.m.end[s] - b;
-        const uint64_t Kb = p.koff[b], Vb = p.voff[b];
-        const SegSums X = p.ss[s];
-        uint64_t De = b, Dk = Kb, Dv = Vb, EC = p.m.ecap[s], KC = p.m.kcap[s], VC = p.m.vcap[s];
-        if (md == 2) {
-            const PlanSums R = p.rbase[s], Z = p.rsz[s];
-            De = p.e0 + R.v[0]; Dk = p.k0 + R.v[1]; Dv = p.v0 + R.v[2];
-            EC = De + Z.v[0]; KC = Dk + Z.v[1]; VC = Dv + Z.v[2];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t sb = w0 * 64; sb < a.S; sb += nw * 64) {
+        const uint64_t s = sb + lane;
+        const uint8_t md = s < a.S ? p.mode[s] : 0;
+        uint64_t j0 = 0, je = 0, b = 0, c = 0, Kb = 0, Vb = 0, De = 0, Dk = 0, Dv = 0, EC = 0, KC = 0, VC = 0;
+        SegSums X(0);
+        BatchSums B0(0);
+        bool live = md != 0;
+        if (live) {
+            j0 = a.bseg_off[s]; je = a.bseg_off[s + 1];
+            b = p.m.beg[s]; c = p.m.end[s] - b;
+            Kb = p.koff[b]; Vb = p.voff[b];
+            X = p.ss[s];
+            De = b; Dk = Kb; Dv = Vb; EC = p.m.ecap[s]; KC = p.m.kcap[s]; VC = p.m.vcap[s];
+            if (md == 2) {
+                const PlanSums R = p.rbase[s], Z = p.rsz[s];
+                De = p.e0 + R.v[0]; Dk = p.k0 + R.v[1]; Dv = p.v0 + R.v[2];
+                EC = De + Z.v[0]; KC = Dk + Z.v[1]; VC = Dv + Z.v[2];
+            }
+            // the merged segment fits its (new) page: every move below stays inside it
+            live = pg_ok(chk, De + X.v[0] < EC && Dk + X.v[1] <= KC && Dv + X.v[2] <= VC, 14, s, De + X.v[0], EC);
+            if (live) B0 = p.bx[j0];
         }
-        // the merged segment fits its (new) page: every move below stays inside it
-        if (!pg_ok(chk, De + X.v[0] < EC && Dk + X.v[1] <= KC && Dv + X.v[2] <= VC, 14, s, De + X.v[0], EC)) continue;
-        const BatchSums B0 = p.bx[j0];
-        uint64_t hi = c, khi = p.koff[b + c], vhi = p.voff[b + c];   // the current piece's end and its old offsets
+        uint32_t kl = (live && X.v[0]) ? p.m.klen[s] : KLEN_NONE;   // the merged segment's uniform key length
+        uint64_t hi = c, khi = live ? p.koff[b + c] : 0, vhi = live ? p.voff[b + c] : 0;   // the current piece's end
         uint64_t j = je;
-        while (j > j0) {
-            const uint64_t u = p.pos[j - 1];
-            uint64_t g0 = j - 1;
-            while (g0 > j0 && p.pos[g0 - 1] == u) g0--;
-            const BatchSums Bj = p.bx[j];
-            const bool eq = Bj.v[BS_EQ] != p.bx[j - 1].v[BS_EQ];   // the group's last record replaces entry u
-            const uint64_t lo = u + (eq ? 1 : 0);
-            const uint64_t de = (Bj.v[BS_NE] - B0.v[BS_NE]) - (Bj.v[BS_EQ] - B0.v[BS_EQ]);
-            const uint64_t dk = (Bj.v[BS_KN] - B0.v[BS_KN]) - (Bj.v[BS_KE] - B0.v[BS_KE]);
-            const uint64_t dv = (Bj.v[BS_VN] - B0.v[BS_VN]) - (Bj.v[BS_VE] - B0.v[BS_VE]);
-            const RecAt R = p.rat[j - 1];   // entry u's old offsets, page-relative (read before any rewrite)
-            const uint64_t ku = Kb + R.ku, vu = Vb + R.vu;
-            if (lo < hi) {
-                const uint64_t k0 = p.koff[b + lo], v0 = p.voff[b + lo];
-                if (md == 2 || dk) lane_move_down(p.kheap + Dk + (k0 - Kb) + dk, p.kheap + k0, khi - k0);
-                if (md == 2 || dv) lane_move_down(p.vheap + Dv + (v0 - Vb) + dv, p.vheap + v0, vhi - v0);
-                if (md == 2 || de || dk) lane_offsets_down(p.koff + b, lo, hi, (De - b) + de, (Dk - Kb) + dk);
-                if (md == 2 || de || dv) lane_offsets_down(p.voff + b, lo, hi, (De - b) + de, (Dv - Vb) + dv);
+        while (__ballot(live && j > j0)) {
+            const bool mine = live && j > j0;
+            PieceJob J{};
+            bool has = false;
+            uint64_t u = 0, g0 = 0, ku = 0, vu = 0;
+            if (mine) {
+                u = p.pos[j - 1];
+                g0 = j - 1;
+                while (g0 > j0 && p.pos[g0 - 1] == u) g0--;
+                const BatchSums Bj = p.bx[j];
+                const bool eq = Bj.v[BS_EQ] != p.bx[j - 1].v[BS_EQ];   // the group's last record replaces entry u
+                const uint64_t lo = u + (eq ? 1 : 0);
+                const uint64_t de = (Bj.v[BS_NE] - B0.v[BS_NE]) - (Bj.v[BS_EQ] - B0.v[BS_EQ]);
+                const uint64_t dk = (Bj.v[BS_KN] - B0.v[BS_KN]) - (Bj.v[BS_KE] - B0.v[BS_KE]);
+                const uint64_t dv = (Bj.v[BS_VN] - B0.v[BS_VN]) - (Bj.v[BS_VE] - B0.v[BS_VE]);
+                const RecAt R = p.rat[j - 1];   // entry u's old offsets, page-relative (read before any rewrite)
+                ku = Kb + R.ku;
+                vu = Vb + R.vu;
+                if (lo < hi) {
+                    const uint64_t k0 = p.koff[b + lo], v0 = p.voff[b + lo];
+                    J.kd = (uint64_t)(p.kheap + Dk + (k0 - Kb) + dk); J.ks = (uint64_t)(p.kheap + k0); J.nk = khi - k0;
+                    J.vd = (uint64_t)(p.vheap + Dv + (v0 - Vb) + dv); J.vs = (uint64_t)(p.vheap + v0); J.nv = vhi - v0;
+                    J.ko = (uint64_t)(p.koff + b); J.vo = (uint64_t)(p.voff + b);
+                    J.a = lo; J.e = hi; J.de = (De - b) + de; J.dk = (Dk - Kb) + dk; J.dv = (Dv - Vb) + dv;
+                    J.fl = ((md == 2 || dk) ? 1u : 0u) | ((md == 2 || dv) ? 2u : 0u) | ((md == 2 || de || dk) ? 4u : 0u) |
+                           ((md == 2 || de || dv) ? 8u : 0u);
+                    has = J.fl != 0;
+                }
             }
-            for (uint64_t r = j; r > g0; r--) {   // the group's records that produce an entry, highest first
-                const BatchSums &Br = p.bx[r - 1], &Bn = p.bx[r];
-                if (Bn.v[BS_NE] == Br.v[BS_NE]) continue;
-                const uint64_t nwi = De + u + (Br.v[BS_NE] - B0.v[BS_NE]) - (Br.v[BS_EQ] - B0.v[BS_EQ]);
-                const uint64_t nk = Dk + (ku - Kb) + (Br.v[BS_KN] - B0.v[BS_KN]) - (Br.v[BS_KE] - B0.v[BS_KE]);
-                const uint64_t nv = Dv + (vu - Vb) + (Br.v[BS_VN] - B0.v[BS_VN]) - (Br.v[BS_VE] - B0.v[BS_VE]);
-                const RecAt Q = p.rat[r - 1];
-                p.koff[nwi] = nk;
-                p.voff[nwi] = nv;
-                copy_bytes(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN]);
-                copy_bytes(p.vheap + nv, a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
+            wave_run_jobs(J, has, lane);
+            if (mine) {
+                for (uint64_t r = j; r > g0; r--) {   // the group's records that produce an entry, highest first
+                    const BatchSums &Br = p.bx[r - 1], &Bn = p.bx[r];
+                    if (Bn.v[BS_NE] == Br.v[BS_NE]) continue;
+                    const uint64_t nwi = De + u + (Br.v[BS_NE] - B0.v[BS_NE]) - (Br.v[BS_EQ] - B0.v[BS_EQ]);
+                    const uint64_t nk = Dk + (ku - Kb) + (Br.v[BS_KN] - B0.v[BS_KN]) - (Br.v[BS_KE] - B0.v[BS_KE]);
+                    const uint64_t nv = Dv + (vu - Vb) + (Br.v[BS_VN] - B0.v[BS_VN]) - (Br.v[BS_VE] - B0.v[BS_VE]);
+                    const RecAt Q = p.rat[r - 1];
+                    if (X.v[0]) kl = klen_add(kl, Bn.v[BS_KN] - Br.v[BS_KN]);
+                    p.koff[nwi] = nk;
+                    p.voff[nwi] = nv;
+                    copy_bytes(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN]);
+                    copy_bytes(p.vheap + nv, a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
+                }
+                hi = u; khi = ku; vhi = vu;
+                j = g0;
             }
-            hi = u; khi = ku; vhi = vu;
-            j = g0;
         }
-        if (md == 2 && hi) {   // the entries before the first record, unshifted, into the new page
-            lane_move_down(p.kheap + Dk, p.kheap + Kb, khi - Kb);
-            lane_move_down(p.vheap + Dv, p.vheap + Vb, vhi - Vb);
-            lane_offsets_down(p.koff + b, 0, hi, De - b, Dk - Kb);
-            lane_offsets_down(p.voff + b, 0, hi, De - b, Dv - Vb);
+        {   // mode 2: the entries before the first record, unshifted, into the new page
+            PieceJob J{};
+            const bool has = live && md == 2 && hi;
+            if (has) {
+                J.kd = (uint64_t)(p.kheap + Dk); J.ks = (uint64_t)(p.kheap + Kb); J.nk = khi - Kb;
+                J.vd = (uint64_t)(p.vheap + Dv); J.vs = (uint64_t)(p.vheap + Vb); J.nv = vhi - Vb;
+                J.ko = (uint64_t)(p.koff + b); J.vo = (uint64_t)(p.voff + b);
+                J.a = 0; J.e = hi; J.de = De - b; J.dk = Dk - Kb; J.dv = Dv - Vb; J.fl = 15;
+            }
+            wave_run_jobs(J, has, lane);
         }
-        p.koff[De + X.v[0]] = Dk + X.v[1];   // the end slot
-        p.voff[De + X.v[0]] = Dv + X.v[2];
-        p.m.end[s] = De + X.v[0];
-        p.m.vend[s] = Dv + X.v[2];
-        if (md == 2) {
-            p.m.beg[s] = De;
-            p.m.vbeg[s] = Dv;
-            p.m.ecap[s] = EC;
-            p.m.kcap[s] = KC;
-            p.m.vcap[s] = VC;
+        if (live) {
+            if (kl != p.m.klen[s]) p.m.klen[s] = (uint16_t)kl;
+            p.koff[De + X.v[0]] = Dk + X.v[1];   // the end slot
+            p.voff[De + X.v[0]] = Dv + X.v[2];
+            p.m.end[s] = De + X.v[0];
+            p.m.vend[s] = Dv + X.v[2];
+            if (md == 2) {
+                p.m.beg[s] = De;
+                p.m.vbeg[s] = Dv;
+                p.m.ecap[s] = EC;
+                p.m.kcap[s] = KC;
+                p.m.vcap[s] = VC;
+            }
         }
     }
 }
@@ -336,6 +402,11 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
         if (!pg_ok(chk, koff[b] <= koff[e] && koff[e] <= m.kcap[s] && m.kcap[s] <= cap_k, 21, s, koff[e], m.kcap[s])) continue;
         if (!pg_ok(chk, voff[b] <= voff[e] && voff[e] <= m.vcap[s] && m.vcap[s] <= cap_v, 22, s, voff[e], m.vcap[s])) continue;
         if (!pg_ok(chk, m.vbeg[s] == voff[b] && m.vend[s] == voff[e], 23, s, m.vbeg[s], voff[b])) continue;
+        const uint32_t L = m.klen[s];   // the uniform key length, if any, holds
+        if (!pg_ok(chk, L != KLEN_NONE || b == e, 25, s, e - b, L)) continue;
+        bool kl_ok = true;
+        for (uint64_t i = b; i < e && L != KLEN_MIXED && L != KLEN_NONE; i++) kl_ok &= koff[i + 1] - koff[i] == L;
+        if (!pg_ok(chk, kl_ok, 26, s, L, b)) continue;
         for (uint64_t i = b; i < e; i++)
             if (!pg_ok(chk, koff[i] <= koff[i + 1] && voff[i] <= voff[i + 1], 24, s, i, b)) {
                 if (chk[2] == s && chk[3] == i)   // the first violation: the page's offsets for the report
@@ -352,4 +423,5 @@ __global__ void k_page_clear(PageMeta m, uint64_t s, uint64_t *cnt) {
     *cnt = m.end[s] - m.beg[s];
     m.end[s] = m.beg[s];
     m.vend[s] = m.vbeg[s];
+    m.klen[s] = KLEN_NONE;
 }

@@ -238,21 +238,6 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
             fetch(Bf);
         }
     }
-    // The first wave out of K1 hashes one node-sized message of junk (M0 is
-    // unused until level H-1) while the others finish their streams: the
-    // level chain's node-hash code (md5_lds_node, not K1's) is then in the
-    // CU's instruction cache when level H starts, instead of being fetched
-    // on the chain's critical path.
-    {
-        uint32_t first = 0;
-        if (lane == 0) first = __hip_atomic_fetch_add(&MISC[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u;
-        if (__builtin_amdgcn_readfirstlane(first)) {
-            uint4 e;
-            uint32_t tg;
-            rw_node(M0, RW_MSG, e, tg);
-            if (e.x == 0x9e3779b9u && e.y == 0x7f4a7c15u && lane == 0) MISC[3] = 0u;   // (keeps the call)
-        }
-    }
     lds_barrier();
     RF_STAMP(1);
 

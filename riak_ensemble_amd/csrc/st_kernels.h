@@ -544,6 +544,7 @@ struct MergeArgs {
     BatchView bv;
     const uint64_t *bvoff;
     const uint8_t *bvheap;
+    const uint16_t *klen;       // NULL or per segment (pages.h PageMeta::klen): every key record this long
     uint64_t S;
 };
 
@@ -591,49 +592,60 @@ enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 // value offsets of the entry at its position, relative to its segment's
 // first ones (a page rebuild moves segments, not their content), and its own
 // batch offsets.
+#define KLEN_MIXED_ 0        // = pages.h KLEN_MIXED (no uniform key length)
+#define KLEN_NONE_ 0xFFFFu   // = pages.h KLEN_NONE (an empty segment)
 struct RecAt {
     uint64_t ku, vu, bk, bv;
 };
 
-// Merge positions of one segment's batch run (a lane per segment): the run
-// is sorted, so each key's binary search starts at the previous one's
-// position.  Returns the value offset (relative to the segment's first
-// value) of the first entry the merge changes -- the first kept record's
-// position -- or ~0 when nothing changes.
-__device__ __forceinline__ uint64_t merge_pos_seg(const MergeArgs &a, uint64_t s, uint32_t *pos, BatchSums *bs,
-                                                  SegSums *ss, uint8_t *dirty, RecAt *rat) {
-    const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
-    uint64_t nold = a.seg_off ? a.seg_end[s] - i0 : 0;
-    const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
-    const bool rej = a.seg_reject && a.seg_reject[s];
-    if (a.seg_replace && a.seg_replace[s]) nold = 0;
-    SegSums tot;
-    tot.v[0] = nold;
-    tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
-    tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
-    tot.v[3] = 0;
-    uint64_t lo = 0, first = ~0ull;
-    for (uint64_t j = j0; j < je; j++) {
+// Merge positions, a lane per sorted batch record: binary search of its key
+// among its segment's old keys.  (A lane per segment searched its run's keys
+// one after another: the longest run of a wave set its time, and the lanes of
+// untouched segments idled.)  Records outside every run (a partition's
+// clamped runs) are skipped and keep sums 0; a rejected segment's records get
+// position 0 and sums 0.
+__global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint32_t *pos, BatchSums *bs, RecAt *rat) {
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        const uint64_t s = sseg[j];
+        if (j < a.bseg_off[s] || j >= a.bseg_off[s + 1]) continue;
         BatchSums f(0);
-        if (rej) { pos[j] = 0; bs[j] = f; continue; }
+        if (a.seg_reject && a.seg_reject[s]) { pos[j] = 0; bs[j] = f; continue; }
+        const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+        const uint64_t nold = (!a.seg_off || (a.seg_replace && a.seg_replace[s])) ? 0 : a.seg_end[s] - i0;
         const uint32_t bi = a.perm[j];
         const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
         const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
-        uint64_t hi = nold;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
-            if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
+        uint32_t L = (a.klen && nold) ? a.klen[s] : KLEN_MIXED_;
+        if (L == KLEN_NONE_) L = KLEN_MIXED_;
+        uint64_t lo = 0, hi = nold, ke = 0;
+        bool eq;
+        if (L != KLEN_MIXED_) {   // every old key L bytes: entry i's key at k0 + L i, no offset loads
+            const uint8_t *k0 = a.kheap + a.koff[i0];
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (rec_cmp(k0 + L * mid, L, kb, kl) < 0) lo = mid + 1; else hi = mid;
+            }
+            eq = lo < nold && rec_cmp(k0 + L * lo, L, kb, kl) == 0;
+            ke = L;
+        } else {
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1, e = i0 + mid;
+                if (rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) < 0) lo = mid + 1; else hi = mid;
+            }
+            const uint64_t e = i0 + lo;
+            eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
+            if (eq) ke = a.koff[e + 1] - a.koff[e];
         }
         const uint64_t e = i0 + lo;
-        const bool eq = lo < nold && rec_cmp(a.kheap + a.koff[e], a.koff[e + 1] - a.koff[e], kb, kl) == 0;
         pos[j] = (uint32_t)lo;
-        const uint64_t vu = a.voff[e] - a.voff[i0];
-        if (rat) rat[j] = RecAt{a.koff[e] - a.koff[i0], vu, a.bv.koff[bi], a.bvoff[bi]};
+        if (rat)
+            rat[j] = RecAt{L != KLEN_MIXED_ ? L * lo : a.koff[e] - a.koff[i0], a.voff[e] - a.voff[i0], a.bv.koff[bi],
+                           a.bvoff[bi]};
         const bool kept = a.keep[j] != 0;
         const bool ne = kept && !(a.bop && a.bop[bi]);
         if (kept && eq) {
             f.v[BS_EQ] = 1;
-            f.v[BS_KE] = a.koff[e + 1] - a.koff[e];
+            f.v[BS_KE] = ke;
             f.v[BS_VE] = a.voff[e + 1] - a.voff[e];
         }
         if (ne) {
@@ -642,19 +654,40 @@ __device__ __forceinline__ uint64_t merge_pos_seg(const MergeArgs &a, uint64_t s
             f.v[BS_VN] = a.bvoff[bi + 1] - a.bvoff[bi];
         }
         bs[j] = f;
-        if (kept && first == ~0ull) first = vu;
-        if (ne && !eq) tot.v[3] += 1;   // a new key of the tree
-        tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
-        tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
-        tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
     }
+}
+
+// A segment's merged sizes (SegSums: entries, key bytes, value bytes, new
+// keys) from its old sizes and its run's BatchSums; dirty = a kept record.
+// Returns the value offset (relative to the segment's first value) of the
+// first entry the merge changes -- the first kept record's position -- or ~0.
+__device__ __forceinline__ uint64_t merge_sums_seg(const MergeArgs &a, uint64_t s, const BatchSums *bs, const RecAt *rat,
+                                                   const uint32_t *pos, SegSums *ss, uint8_t *dirty) {
+    const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+    const uint64_t nold = (!a.seg_off || (a.seg_replace && a.seg_replace[s])) ? 0 : a.seg_end[s] - i0;
+    const uint64_t j0 = a.bseg_off[s], je = a.bseg_off[s + 1];
+    SegSums tot;
+    tot.v[0] = nold;
+    tot.v[1] = nold ? a.koff[i0 + nold] - a.koff[i0] : 0;
+    tot.v[2] = nold ? a.voff[i0 + nold] - a.voff[i0] : 0;
+    tot.v[3] = 0;
+    uint64_t first = ~0ull;
+    if (!(a.seg_reject && a.seg_reject[s]))
+        for (uint64_t j = j0; j < je; j++) {
+            const BatchSums f = bs[j];
+            if (first == ~0ull && a.keep[j]) first = rat ? rat[j].vu : (pos[j] ? a.voff[i0 + pos[j]] - a.voff[i0] : 0);
+            if (f.v[BS_NE] && !f.v[BS_EQ]) tot.v[3] += 1;   // a new key of the tree
+            tot.v[0] += f.v[BS_NE] - f.v[BS_EQ];
+            tot.v[1] += f.v[BS_KN] - f.v[BS_KE];
+            tot.v[2] += f.v[BS_VN] - f.v[BS_VE];
+        }
     ss[s] = tot;
     if (dirty) dirty[s] = first != ~0ull ? 1 : 0;
     return first;
 }
 
-__global__ void k_merge_pos(MergeArgs a, uint32_t *pos, BatchSums *bs, SegSums *ss, uint8_t *dirty, RecAt *rat) {
-    for (uint64_t s = gtid(); s < a.S; s += gstride()) merge_pos_seg(a, s, pos, bs, ss, dirty, rat);
+__global__ void k_merge_sums(MergeArgs a, const BatchSums *bs, const uint32_t *pos, SegSums *ss, uint8_t *dirty) {
+    for (uint64_t s = gtid(); s < a.S; s += gstride()) merge_sums_seg(a, s, bs, nullptr, pos, ss, dirty);
 }
 
 // The MD5 state of a segment's values before the first block its merge
@@ -666,18 +699,18 @@ struct PrefixState {
 };
 
 // A streaming batch's verify (insert/3's get_path check of each touched
-// segment, synctree.erl:189-209, 302-340) fused with its merge positions: a
-// lane per segment in seg_perm order computes the positions of its run (no
+// segment, synctree.erl:189-209, 302-340) fused with its merged sizes: a lane
+// per segment in seg_perm order sums its run (k_merge_keys' positions, no
 // rejection yet: k_page_plan drops rejected runs), then, for a touched
 // segment, the MD5 of its old values, saving the state before the first
 // block the merge changes (ps) for the hash after the merge.
 __global__ void __launch_bounds__(256) k_verify_pos(DevTree t, MergeArgs a, const uint32_t *perm, const uint8_t *mask,
-                                                    uint8_t *ok, uint32_t *pos, BatchSums *bs, SegSums *ss,
-                                                    uint8_t *dirty, RecAt *rat, PrefixState *ps) {
+                                                    uint8_t *ok, const uint32_t *pos, const BatchSums *bs, SegSums *ss,
+                                                    uint8_t *dirty, const RecAt *rat, PrefixState *ps) {
     const uint32_t L = t.H + 1;
     for (uint64_t i = gtid(); i < t.S; i += gstride()) {
         const uint64_t s = perm[i];
-        const uint64_t first = merge_pos_seg(a, s, pos, bs, ss, dirty, rat);
+        const uint64_t first = merge_sums_seg(a, s, bs, rat, pos, ss, dirty);
         const uint64_t slot = t.base[L] + s;
         if (!mask[slot]) continue;
         const uint64_t eslot = (L == 1) ? 0 : slot;

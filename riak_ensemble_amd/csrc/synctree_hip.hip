@@ -1347,6 +1347,7 @@ static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPre
     ma.bv = BatchView{in.krec, in.koff};
     ma.bvoff = in.voff;
     ma.bvheap = in.vheap;
+    ma.klen = nullptr;
     ma.S = S;
     return ma;
 }
@@ -1378,7 +1379,8 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     HIPCHK(hipMemsetAsync(ss + S, 0, sizeof(SegSums), t->stream));
     // records outside every run (a partition's clamped runs) keep sums 0
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
-    LAUNCH(t, "merge_count", k_merge_pos, grid_for(S), 256, 0, ma, mpos, bs, ss, dirty, (RecAt *)nullptr);
+    LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, (RecAt *)nullptr);
+    LAUNCH(t, "merge_count", k_merge_sums, grid_for(S), 256, 0, ma, (const BatchSums *)bs, (const uint32_t *)mpos, ss, dirty);
     CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     CHK(exclusive_scan<SegSums>(t, ss, sx, S + 1));
     SegSums tot(0);
@@ -1426,7 +1428,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
 
 static void pages_free(st_tree *t, Pages &g) {
     for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.ecap, (void *)g.m.kcap,
-                    (void *)g.m.vcap, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
+                    (void *)g.m.vcap, (void *)g.m.klen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
     const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e, tv = g.touched_v;
     g = Pages();
@@ -1476,6 +1478,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
         ~Undo() { if (!done) pages_free(t, g); }
     } undo{t, g};
     for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
+    CHK(dalloc_t(t, &g.m.klen, S));
     CHK(dalloc_t(t, &g.koff, g.cap_e));
     CHK(dalloc_t(t, &g.voff, g.cap_e));
     CHK(dalloc(t, (void **)&g.kheap, g.cap_k + HEAP_SLACK));
@@ -1541,14 +1544,17 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // the touched segments' verify fused with the merge positions (every
     // segment's merged sizes), then the inner nodes of their paths
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
+    ma.klen = t->pg.m.klen;
     {
         const DevTree d = view(t);
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
+        LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat);
         LAUNCH(t, "verify_pos", k_verify_pos, grid_for(S), 256, 0, d, ma, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)t->mark, t->ok, mpos, bs, ss, dirty, rat, ps);
+               (const uint8_t *)t->mark, t->ok, (const uint32_t *)mpos, (const BatchSums *)bs, ss, dirty,
+               (const RecAt *)rat, ps);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
@@ -1573,6 +1579,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         for (int q = 0; q < 3; q++) want.v[q] = 2 * tot.v[q];
         CHK(pages_build(t, t->pg_slack, want));
         ma = merge_args(view(t), in, bp, reject, S);
+        ma.klen = t->pg.m.klen;
     }
     PageMergeArgs pa;
     pa.a = ma;

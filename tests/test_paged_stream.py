@@ -38,6 +38,7 @@ def _obj(seqs, epoch=1):
     (1 << 16, 300_000, 4_000, 1),      # H = 4, minimal slack: moves every batch, rebuilds
     (1 << 16, 300_000, 4_000, 25),     # the default slack
     (1 << 20, 1_000_000, 20_000, 2),   # H = 5, the config-5 geometry at 1/100 scale
+    (4096, 500_000, 6_000, 25),        # H = 3, ~120 entries a segment: pieces of kilobytes
 ])
 def test_int_keys_stream_through_pages(segments, n0, batch, slack):
     rng = np.random.default_rng(segments ^ n0 ^ slack)

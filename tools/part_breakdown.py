@@ -1,6 +1,7 @@
 """Config-5 batch breakdown: a 100M-key tree (one partition = the whole
 range), then per-kernel times (HIP events on the library's stream,
-st_kernel_stats) over 5 timed 1M-key batches (50 % overwrites, 50 % new).
+st_kernel_stats) over K timed 1M-key batches (50 % overwrites, 50 % new), then the wall
+time of K more such batches with no per-kernel events.
 Usage: python tools/part_breakdown.py [tree_keys] [batches] [csr]   (csr: pages off)"""
 import os
 import sys
@@ -32,7 +33,7 @@ for a in range(0, N, 10_000_000):
 torch.cuda.synchronize()
 rng = np.random.default_rng(5)
 batches = []
-for j in range(K + 1):
+for j in range(2 * K + 1):   # batch 0 warms up, 1..K timed with events, K+1..2K timed without
     old = torch.from_numpy(rng.integers(0, N, B // 2)).to(dev)
     k = torch.cat([bench._dev_keys_at(seed, old, dev, torch), bench._dev_keys(seed, N + j * B, B - B // 2, dev, torch)])
     seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
@@ -61,7 +62,7 @@ for nm in names:
 print('named kernels %.3f ms/batch, wall %.3f ms/batch (timing on)' % (tot / K, el))
 t.set_timing(False)
 t0 = time.perf_counter()
-for j in range(1, K + 1):
+for j in range(K + 1, 2 * K + 1):   # fresh batches (half new keys), as the timed ones
     k, v = batches[j]
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
