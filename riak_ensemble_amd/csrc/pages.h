@@ -150,17 +150,25 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
 // the highest address down); otherwise the segment moves.  reloc = the new
 // page's sizes (mode 2), scanned for its place in the append region; v[3] =
 // the segment's new keys (for the tree's entry count).
+// sd: the segments' merged-size deltas (k_merge_keys); sm: the merged sizes
+// of the touched segments (written here, read by k_page_merge).
 __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *voff, const uint64_t *bseg_off,
-                            const uint8_t *reject, const BatchSums *bs, const SegSums *ss, uint8_t *dirty, uint64_t S,
-                            int slack_pct, uint8_t *mode, PlanSums *reloc) {
+                            const uint8_t *reject, const BatchSums *bs, const SegSums *sd, SegSums *sm, uint8_t *dirty,
+                            uint64_t S, int slack_pct, uint8_t *mode, PlanSums *reloc) {
     for (uint64_t s = gtid(); s < S; s += gstride()) {
         const uint64_t j0 = bseg_off[s], je = bseg_off[s + 1];
-        if (reject && reject[s]) dirty[s] = 0;   // positions came before the verify (k_verify_pos)
+        if (reject && reject[s]) dirty[s] = 0;   // positions came before the verify (k_merge_keys)
         PlanSums r(0);
         uint8_t md = 0;
         if (j0 != je && !(reject && reject[s]) && dirty[s]) {
-            const uint64_t b = m.beg[s];
-            const SegSums x = ss[s];
+            const uint64_t b = m.beg[s], e = m.end[s];
+            const SegSums dd = sd[s];
+            SegSums x;
+            x.v[0] = (e - b) + dd.v[0];
+            x.v[1] = (koff[e] - koff[b]) + dd.v[1];
+            x.v[2] = (voff[e] - voff[b]) + dd.v[2];
+            x.v[3] = dd.v[3];
+            sm[s] = x;
             const bool fits = b + x.v[0] < m.ecap[s] && koff[b] + x.v[1] <= m.kcap[s] && voff[b] + x.v[2] <= m.vcap[s];
             bool grow = true;
             int64_t dk = 0, dv = 0;
@@ -176,7 +184,7 @@ __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *vo
                 r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
             }
             r.v[3] = x.v[3];
-            r.v[4] = voff[m.end[s]] - voff[b];
+            r.v[4] = voff[e] - voff[b];
         }
         mode[s] = md;
         reloc[s] = r;

@@ -604,7 +604,13 @@ struct RecAt {
 // untouched segments idled.)  Records outside every run (a partition's
 // clamped runs) are skipped and keep sums 0; a rejected segment's records get
 // position 0 and sums 0.
-__global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint32_t *pos, BatchSums *bs, RecAt *rat) {
+// sd (optional, zeroed; the streaming batch): every segment's merged-size
+// DELTAS (entries, key bytes, value bytes -- mod 2^64 -- and new keys) by
+// atomics, dirty (zeroed) set by a kept record, fpos (all ones) = the
+// smallest value offset a kept record changes (atomicMin): the per-segment
+// sums without a pass over every segment.
+__global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint32_t *pos, BatchSums *bs, RecAt *rat,
+                             SegSums *sd = nullptr, uint8_t *dirty = nullptr, unsigned long long *fpos = nullptr) {
     for (uint64_t j = gtid(); j < n; j += gstride()) {
         const uint64_t s = sseg[j];
         if (j < a.bseg_off[s] || j >= a.bseg_off[s + 1]) continue;
@@ -654,6 +660,15 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             f.v[BS_VN] = a.bvoff[bi + 1] - a.bvoff[bi];
         }
         bs[j] = f;
+        if (sd && kept) {
+            unsigned long long *d = reinterpret_cast<unsigned long long *>(&sd[s]);
+            if (f.v[BS_NE] != f.v[BS_EQ]) atomicAdd(&d[0], (unsigned long long)(f.v[BS_NE] - f.v[BS_EQ]));
+            if (f.v[BS_KN] != f.v[BS_KE]) atomicAdd(&d[1], (unsigned long long)(f.v[BS_KN] - f.v[BS_KE]));
+            if (f.v[BS_VN] != f.v[BS_VE]) atomicAdd(&d[2], (unsigned long long)(f.v[BS_VN] - f.v[BS_VE]));
+            if (ne && !eq) atomicAdd(&d[3], 1ull);   // a new key of the tree
+            dirty[s] = 1;
+            atomicMin(&fpos[s], (unsigned long long)(a.voff[e] - a.voff[i0]));
+        }
     }
 }
 
@@ -699,18 +714,15 @@ struct PrefixState {
 };
 
 // A streaming batch's verify (insert/3's get_path check of each touched
-// segment, synctree.erl:189-209, 302-340) fused with its merged sizes: a lane
-// per segment in seg_perm order sums its run (k_merge_keys' positions, no
-// rejection yet: k_page_plan drops rejected runs), then, for a touched
-// segment, the MD5 of its old values, saving the state before the first
-// block the merge changes (ps) for the hash after the merge.
-__global__ void __launch_bounds__(256) k_verify_pos(DevTree t, MergeArgs a, const uint32_t *perm, const uint8_t *mask,
-                                                    uint8_t *ok, const uint32_t *pos, const BatchSums *bs, SegSums *ss,
-                                                    uint8_t *dirty, const RecAt *rat, PrefixState *ps) {
+// segment, synctree.erl:189-209, 302-340): a lane per segment in seg_perm
+// order hashes a touched segment's old values, saving the state before the
+// first block its merge changes (fpos, k_merge_keys) in ps for the hash after
+// the merge.
+__global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *perm, const uint8_t *mask, uint8_t *ok,
+                                                    const unsigned long long *fpos, PrefixState *ps) {
     const uint32_t L = t.H + 1;
     for (uint64_t i = gtid(); i < t.S; i += gstride()) {
         const uint64_t s = perm[i];
-        const uint64_t first = merge_sums_seg(a, s, bs, rat, pos, ss, dirty);
         const uint64_t slot = t.base[L] + s;
         if (!mask[slot]) continue;
         const uint64_t eslot = (L == 1) ? 0 : slot;
@@ -724,6 +736,7 @@ __global__ void __launch_bounds__(256) k_verify_pos(DevTree t, MergeArgs a, cons
         } else {
             uint32_t st[4], cap[4] = {0u, 0u, 0u, 0u};
             stmd5::init(st);
+            const uint64_t first = fpos[s];
             const uint64_t ck = first == ~0ull ? ~0ull : first / 64;
             const uint64_t v0 = t.seg_voff[s];
             stmd5::md5_global_span<true>(t.vheap + v0, t.seg_vend[s] - v0, 0, st, ck, cap);
@@ -738,6 +751,7 @@ __global__ void __launch_bounds__(256) k_verify_pos(DevTree t, MergeArgs a, cons
         ps[s] = p;
     }
 }
+
 
 __device__ __forceinline__ uint64_t bound_pos(const uint32_t *pos, uint64_t lo, uint64_t hi, uint64_t li, bool upper) {
     while (lo < hi) {

@@ -1523,7 +1523,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(batch_prepare(t, in, sc, bp));
     uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
     BatchSums *bs = nullptr, *bx = nullptr;
-    SegSums *ss = nullptr;
+    SegSums *ss = nullptr, *sm = nullptr;
+    unsigned long long *fpos = nullptr;
     PlanSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
@@ -1532,6 +1533,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
     CHK(sc.alloc(&ss, S));
+    CHK(sc.alloc(&sm, S));
+    CHK(sc.alloc(&fpos, S));
     CHK(sc.alloc(&dirty, S));
     CHK(sc.alloc(&mode, S));
     CHK(sc.alloc(&rsz, S + 1));
@@ -1541,8 +1544,12 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&bx, n + 1));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PlanSums), t->stream));
-    // the touched segments' verify fused with the merge positions (every
-    // segment's merged sizes), then the inner nodes of their paths
+    HIPCHK(hipMemsetAsync(ss, 0, S * sizeof(SegSums), t->stream));
+    HIPCHK(hipMemsetAsync(dirty, 0, S, t->stream));
+    HIPCHK(hipMemsetAsync(fpos, 0xFF, S * 8, t->stream));
+    // merge positions (a lane per record, the segments' size deltas by
+    // atomics), then the touched segments' verify (saving each one's
+    // unchanged-prefix MD5 state) and the inner nodes of their paths
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
     ma.klen = t->pg.m.klen;
     {
@@ -1551,10 +1558,10 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
-        LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat);
-        LAUNCH(t, "verify_pos", k_verify_pos, grid_for(S), 256, 0, d, ma, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)t->mark, t->ok, (const uint32_t *)mpos, (const BatchSums *)bs, ss, dirty,
-               (const RecAt *)rat, ps);
+        LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat, ss,
+               dirty, fpos);
+        LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
+               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
@@ -1567,7 +1574,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     PlanSums tot(0);
     for (int pass = 0;; pass++) {
         LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
-               (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss,
+               (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss, sm,
                dirty, S, t->pg_slack, mode, rsz);
         CHK(exclusive_scan<PlanSums>(t, rsz, rbase, S + 1));
         CHK(d2h(t, &tot, rbase + S, sizeof(PlanSums)));
@@ -1585,7 +1592,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     pa.a = ma;
     pa.m = t->pg.m;
     pa.koff = t->pg.koff; pa.voff = t->pg.voff; pa.kheap = t->pg.kheap; pa.vheap = t->pg.vheap;
-    pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = ss; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
+    pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = sm; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
     pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
     pa.chk = nullptr;
     if (!t->pg_check) {

@@ -10,5 +10,5 @@ timeout -k 10 200 python -u tools/perkey_lat.py 2000 > gpurun_out/${TAG}_perkey_
 tail -4 gpurun_out/${TAG}_perkey_latency.txt
 ST_CMP_STAMPS=1 timeout -k 10 200 python -u tools/cmp_stamps.py > gpurun_out/${TAG}_cmp_stamps.txt 2>&1 || exit 1
 tail -12 gpurun_out/${TAG}_cmp_stamps.txt
-timeout -k 10 300 python -u bench.py --no-cpu --no-pmc --part-batches 6 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+timeout -k 10 300 python -u bench.py --no-cpu --no-pmc --part-batches 10 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
 head -c 400 gpurun_out/${TAG}_bench.json; echo
