@@ -392,8 +392,10 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * ST_EDEVICE instead of hashing a stale entry into the top hash. */
 #define ST_DBG_SKIP_MAIL 1
 /* ST_DBG_PAGES: streaming insert batches in the paged segment layout with
- * `value` percent of slack per page (0 = the default, 25 %); -1 = off (every
- * batch merges into the canonical CSR; the pages are folded first). */
+ * `value` percent of slack per page (0 = the default, 25 %), from the next
+ * streaming batch on (by default the first batch after any other call merges
+ * into the CSR and the second builds the pages); -1 = off (every batch merges
+ * into the canonical CSR; the pages are folded first). */
 #define ST_DBG_PAGES 2
 /* ST_DBG_PAGE_CHECK: value != 0 runs every paged batch through a checked
  * merge (a store outside its page is reported as ST_EDEVICE, not performed)

@@ -110,6 +110,7 @@ struct st_tree {
     // any other call folds it back into the CSR first
     Pages pg;
     int pg_slack = 25;
+    uint32_t pg_streak = 0;   // streaming batches since the last other call (pages are built at the second)
     bool pg_check = false;   // st_debug_knob ST_DBG_PAGE_CHECK: the checked page merge + a layout check per batch
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
@@ -828,6 +829,7 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
     if (knob == ST_DBG_PAGES) {
         if (value < 0) CHK(pages_fold(t));   // pages off: streaming batches merge into the CSR
         t->pg_slack = value < 0 ? -1 : value == 0 ? 25 : (int)std::min<int64_t>(value, 400);
+        if (value >= 0) t->pg_streak = std::max<uint32_t>(t->pg_streak, 1);   // pages from the next streaming batch
         return ST_OK;
     }
     if (knob == ST_DBG_PAGE_CHECK) {
@@ -1631,10 +1633,14 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     return ST_OK;
 }
 
+// A streaming batch goes to the pages -- except a lone one: the first after
+// any other call merges into the CSR (building the pages copies the whole
+// tree, which only a run of batches pays back).
 static int ingest(st_tree *t, IngestIn &in) {
     in.n_rejected = 0;
     if (in.n == 0) return ST_OK;
-    if (pages_eligible(t, in)) return ingest_paged(t, in);
+    if (pages_eligible(t, in) && (t->pg.on || t->pg_streak++ > 0)) return ingest_paged(t, in);
+    if (!pages_eligible(t, in)) t->pg_streak = 0;
     CHK(pages_fold(t));
     return ingest_direct(t, in);
 }
@@ -1696,6 +1702,7 @@ static int flush_overlay(st_tree *t) {
 static int flush_all(st_tree *t) {
     CHK(flush_overlay(t));
     CHK(pages_fold(t));
+    t->pg_streak = 0;
     return ST_OK;
 }
 #define FLUSH(t) CHK(flush_all(t))

@@ -92,6 +92,7 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack):
     # nodes of a paged tree (the pages just empty them), then rehash/1 twice
     # (from the segments, then the tiled fused kernel)
     idx = rng.integers(0, nxt, batch)
+    dev.debug_knob(_lib.ST_DBG_PAGES, slack)   # pages from this batch on (not only from the second of a run)
     assert dev.insert_int64(keys[idx], _obj(idx + 200, epoch=4)) == 0
     ora.insert_int64_seq(keys[idx], _obj(idx + 200, epoch=4))
     assert dev.page_stats()[0] == 1
@@ -208,8 +209,7 @@ def test_corrupted_segment_rejects_streamed_keys(pages):
     assert dev.insert_int64(keys[:n0], vals[:n0]) == 0
     ora.bulk_load_int64(keys[:n0], vals[:n0])
     dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
-    if not pages:
-        dev.debug_knob(_lib.ST_DBG_PAGES, -1)
+    dev.debug_knob(_lib.ST_DBG_PAGES, 0 if pages else -1)   # pages (from the first streamed batch) or none
     # a streamed batch, then corrupt a key's segment (corrupt/2 folds the pages)
     assert dev.insert_int64(keys[n0:n0 + 2000], vals[n0:n0 + 2000]) == 0
     ora.insert_int64_seq(keys[n0:n0 + 2000], vals[n0:n0 + 2000])
@@ -227,6 +227,8 @@ def test_corrupted_segment_rejects_streamed_keys(pages):
         r = ora.insert(k, v)
         exp.append(None if r is ora else r)
     assert any(e is not None for e in exp)
+    if pages:
+        dev.debug_knob(_lib.ST_DBG_PAGES, 0)   # corrupt/2 folded the pages: back on from this batch
     assert dev.insert_batch(bk, bv) == exp
     assert dev.page_stats()[0] == (1 if pages else 0)
     assert dev.top_hash() == ora.top_hash()
