@@ -274,18 +274,48 @@ __device__ __forceinline__ void wave_move_offsets(uint64_t *o, uint64_t a, uint6
         top = top - a > 64 ? top - 64 : a;
     }
 }
-// every lane's job (has = this lane has one), one after another by the whole wave
+// every lane's job (has = this lane has one), one after another by the whole
+// wave; a job's four arrays advance together, unit by unit: each unit's four
+// loads (key chunk, value chunk, key offset, value offset) go out before its
+// four stores -- one round trip a unit instead of one per array.
+__device__ __forceinline__ uint64_t bunits(uint64_t n) { return n >= 16 ? (n - 16) / 1024 + 1 : 0; }
 __device__ __forceinline__ void wave_run_jobs(const PieceJob &J, bool has, uint32_t lane) {
     uint64_t jm = __ballot(has);
     while (jm) {
         const uint32_t L = (uint32_t)__builtin_ctzll(jm);
         jm &= jm - 1;
         const uint64_t fl = rl64(J.fl, L);
-        if (fl & 1) wave_move_bytes((uint8_t *)rl64(J.kd, L), (const uint8_t *)rl64(J.ks, L), rl64(J.nk, L), lane);
-        if (fl & 2) wave_move_bytes((uint8_t *)rl64(J.vd, L), (const uint8_t *)rl64(J.vs, L), rl64(J.nv, L), lane);
-        const uint64_t a = rl64(J.a, L), e = rl64(J.e, L), de = rl64(J.de, L);
-        if (fl & 4) wave_move_offsets((uint64_t *)rl64(J.ko, L), a, e, de, rl64(J.dk, L), lane);
-        if (fl & 8) wave_move_offsets((uint64_t *)rl64(J.vo, L), a, e, de, rl64(J.dv, L), lane);
+        uint8_t *kd = (uint8_t *)rl64(J.kd, L), *vd = (uint8_t *)rl64(J.vd, L);
+        const uint8_t *ks = (const uint8_t *)rl64(J.ks, L), *vs = (const uint8_t *)rl64(J.vs, L);
+        const uint64_t nk = (fl & 1) ? rl64(J.nk, L) : 0, nv = (fl & 2) ? rl64(J.nv, L) : 0;
+        uint64_t *ko = (uint64_t *)rl64(J.ko, L), *vo = (uint64_t *)rl64(J.vo, L);
+        const uint64_t a = rl64(J.a, L), e = (fl & 12) ? rl64(J.e, L) : a;
+        const uint64_t de = rl64(J.de, L), dk = rl64(J.dk, L), dv = rl64(J.dv, L);
+        const uint64_t units = std::max(std::max(bunits(nk), bunits(nv)), (e - a + 63) / 64);
+        for (uint64_t u = 0; u < units; u++) {
+            const int64_t tk = (int64_t)nk - 1024 * (int64_t)u, tv = (int64_t)nv - 1024 * (int64_t)u;
+            const int64_t hk = tk - 16 * (int64_t)lane, hv = tv - 16 * (int64_t)lane;
+            const bool kA = tk >= 16 && hk > 0, vA = tv >= 16 && hv > 0;
+            const uint64_t kc = hk >= 16 ? (uint64_t)hk - 16 : 0, vc = hv >= 16 ? (uint64_t)hv - 16 : 0;
+            const uint64_t top = e - std::min(e - a, 64 * u);
+            const bool oA = top > a + lane;
+            const uint64_t oi = top - 1 - lane;
+            uint4 kx, vx;
+            uint64_t ox = 0, px = 0;
+            if (kA) __builtin_memcpy(&kx, ks + kc, 16);
+            if (vA) __builtin_memcpy(&vx, vs + vc, 16);
+            if (oA && (fl & 4)) ox = ko[oi];
+            if (oA && (fl & 8)) px = vo[oi];
+            __asm__ volatile("" ::: "memory");   // the unit's loads before its stores
+            if (kA) __builtin_memcpy(kd + kc, &kx, 16);
+            if (vA) __builtin_memcpy(vd + vc, &vx, 16);
+            if (oA && (fl & 4)) ko[oi + de] = ox + dk;
+            if (oA && (fl & 8)) vo[oi + de] = px + dv;
+        }
+        if (lane == 0) {   // bytes below the units (fewer than 16), highest first
+            for (uint64_t i = nk - std::min(nk, 1024 * bunits(nk)); i-- > 0;) kd[i] = ks[i];
+            for (uint64_t i = nv - std::min(nv, 1024 * bunits(nv)); i-- > 0;) vd[i] = vs[i];
+        }
     }
 }
 
