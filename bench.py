@@ -732,7 +732,8 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
         else:
             allt.copy_(mine)
 
-    step()
+    for _ in range(3):   # warm-up (the first builds every tree's tiles)
+        step()
     before = allt.cpu().numpy().copy()
     torch.cuda.synchronize()
     if dist:

@@ -3404,7 +3404,8 @@ extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
     std::vector<TreeTiles> h(n);
     for (uint32_t i = 0; i < n; i++) {
         if (trees[i]->device != t->device) { g_err = "trees on different devices"; return ST_EINVAL; }
-        if (trees[i]->stream != t->stream) CHK(tsync(trees[i]));
+        // a tree with nothing enqueued since its last synchronisation is not waited for
+        if (trees[i]->stream != t->stream && trees[i]->async_pending) CHK(tsync(trees[i]));
         h[i] = tree_tiles(trees[i]);
     }
     Scratch sc(t);
