@@ -8,6 +8,6 @@ R=$(pwd)
 OUT=$R/gpurun_out/trace_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu --no-extras --no-cold > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu --no-extras --no-cold --no-pmc > $OUT/bench.json 2> $OUT/bench.err
 echo "trace done"
 cat $OUT/bench.json
