@@ -1210,14 +1210,28 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
         DevTree d = view(t);
         CHK(ensure_perm_any(t));
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)nullptr, (const PrefixState *)nullptr);
+               (const uint8_t *)nullptr, (const PrefixState *)nullptr, (const uint32_t *)nullptr);
         if (t->H == 0) return ST_OK;
         if (t->W == 16) return levels16(t, t->H, nullptr);
         return rehash_levels(t, t->H, nullptr);
     }
     DevTree d = view(t);
-    CHK(ps ? ensure_perm_any(t) : ensure_perm(t));
-    LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask, ps);
+    if (ps) {   // a streaming batch: its changed segments, by the blocks left after their prefixes
+        Scratch sc(t);
+        uint32_t *cnt = nullptr, *list = nullptr;
+        CHK(sc.alloc(&cnt, PERM_BINS + 1));
+        CHK(sc.alloc(&list, t->S));
+        HIPCHK(hipMemsetAsync(cnt, 0, (PERM_BINS + 1) * 4, t->stream));
+        LAUNCH(t, "segment_hash", k_hash_list_count, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt);
+        LAUNCH(t, "segment_hash", k_hash_list_scan, 1, 256, 0, cnt);
+        LAUNCH(t, "segment_hash", k_hash_list_scatter, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt, list);
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)list, mask, ps,
+               (const uint32_t *)(cnt + PERM_BINS));
+    } else {
+        CHK(ensure_perm(t));
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask,
+               ps, (const uint32_t *)nullptr);
+    }
     if (t->H == 0) return ST_OK;
     if (t->W == 16 && t->H >= 3) {
         LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
