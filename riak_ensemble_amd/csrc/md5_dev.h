@@ -132,12 +132,14 @@ __device__ __forceinline__ void compress(uint32_t st[4], const uint32_t m[16]) {
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
 }
 
-// The latency form as ONE out-of-line copy per kernel (STMD5_NOINLINE, the
-// default): the per-key and compare kernels run their MD5 chains once per
-// launch on a cold instruction cache, and every inlined compression is ~2.5 KB
-// of code (k_small carried 11 copies, k_cmp_walk 8).  Twenty scalar arguments
-// and a four-word result stay in registers (the AMDGPU calling convention
-// passes up to 32 VGPR arguments); the call costs ~30 instructions a block.
+// The latency form as ONE out-of-line copy per kernel (STMD5_NOINLINE=1): the
+// per-key and compare kernels run their MD5 chains once per launch on a cold
+// instruction cache, and every inlined compression is ~2.5 KB of code
+// (k_small carried 11 copies, k_cmp_walk 8).  Twenty scalar arguments and a
+// four-word result stay in registers (the AMDGPU calling convention passes up
+// to 32 VGPR arguments); the call costs ~30 instructions a block.  Measured
+// again in round 5 the smaller code did not pay: the inline form is the
+// default.
 struct St4 { uint32_t a, b, c, d; };
 __device__ __noinline__ St4 compress_ool(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t m0, uint32_t m1,
                                          uint32_t m2, uint32_t m3, uint32_t m4, uint32_t m5, uint32_t m6, uint32_t m7,
@@ -149,7 +151,7 @@ __device__ __noinline__ St4 compress_ool(uint32_t a, uint32_t b, uint32_t c, uin
     return St4{st[0], st[1], st[2], st[3]};
 }
 #ifndef STMD5_NOINLINE
-#define STMD5_NOINLINE 1
+#define STMD5_NOINLINE 0   // round 5 A/B (tools/ab_latency.sh): inline is no slower -- insert1 kernel 34.3 vs 34.8 us, k_cmp_walk 43.6 vs 45.3 us
 #endif
 __device__ __forceinline__ void compress_lat(uint32_t st[4], const uint32_t m[16]) {
 #if STMD5_NOINLINE

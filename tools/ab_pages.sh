@@ -8,6 +8,6 @@ tail -1 gpurun_out/${tag}_tests.log
 for i in 1 2; do
   timeout -k 10 300 python3 tools/part_breakdown.py 100000000 20 > gpurun_out/${tag}_A$i.txt 2>&1 || { tail -5 gpurun_out/${tag}_A$i.txt; exit 1; }
   grep -E "page_merge|wall" gpurun_out/${tag}_A$i.txt
-  ST_LIB=abx/libB.so timeout -k 10 300 python3 tools/part_breakdown.py 100000000 20 > gpurun_out/${tag}_B$i.txt 2>&1 || { tail -5 gpurun_out/${tag}_B$i.txt; exit 1; }
+  ST_LIB=${LIBB:-abx/libB.so} timeout -k 10 300 python3 tools/part_breakdown.py 100000000 20 > gpurun_out/${tag}_B$i.txt 2>&1 || { tail -5 gpurun_out/${tag}_B$i.txt; exit 1; }
   grep -E "page_merge|wall" gpurun_out/${tag}_B$i.txt
 done
