@@ -4,7 +4,7 @@ timeout -k 10 400 python -u -m pytest tests/test_paged_stream.py tests/test_smal
 tail -1 gpurun_out/abc_tests.log
 timeout -k 10 300 python3 tools/part_breakdown.py 100000000 20 > gpurun_out/abc_A.txt 2>&1 || exit 1
 echo "== default"; grep -E "page_merge|timing off" gpurun_out/abc_A.txt
-for v in PM6 PM8; do
+for v in MK8 VC8; do
   ST_LIB=abx/lib$v.so timeout -k 10 300 python3 tools/part_breakdown.py 100000000 20 > gpurun_out/abc_$v.txt 2>&1 || exit 1
   echo "== $v"; grep -E "page_merge|timing off" gpurun_out/abc_$v.txt
 done
