@@ -229,94 +229,186 @@ __device__ __forceinline__ bool pg_ok(unsigned long long *chk, bool ok, uint32_t
 struct PieceJob {
     uint64_t kd, ks, nk, vd, vs, nv, ko, vo, a, e, de, dk, dv, fl;   // fl: bit 0 keys, 1 values, 2 key offs, 3 value offs
 };
+// The jobs' memory accesses.  A job's addresses are rebuilt from readlanes,
+// so the compiler cannot tell their address space: as generic pointers every
+// access was a FLAT one, and the waits FLAT needs serialised a unit's loads
+// one behind the other and each behind the previous stores.  Buffer
+// accesses through a job's (wave-uniform) bases, every lane issuing every
+// access: a lane with nothing to move gets an offset past the buffer's range
+// (loads return 0, stores are dropped), so a unit is four loads, one wait and
+// four stores, with no branch (and no wait) between them.
+typedef uint32_t pm_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t pm_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+#define PM_OOB 0x80000000u   // past every job buffer's range (0x7fffffff bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pm_rsrc(uint64_t base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7fffffff, 0x00020000);
+}
+
+// Wave-cooperative piece moves (every lane of the wave, a wave-uniform job):
+// every lane's job (has = this lane has one), one after another by the whole
+// wave.  A job's four arrays (key bytes, value bytes, key offsets, value
+// offsets) advance together, unit by unit -- 64 lanes x 16 bytes of each heap
+// and 64 entries of each offset array -- top down (dst >= src, or disjoint).
+// The lowest chunk of a piece clamps to its first 16 bytes (the bytes it
+// shares with the chunk above get the same values twice, both loaded in that
+// unit); fewer than 16 bytes left below the last full unit form a byte unit
+// of their own (a lane a byte: a clamped chunk would read bytes the unit
+// above already rewrote).  The units run as one sequence across the wave's
+// jobs (a unit's four loads and two byte loads, then its stores; PM_PIPE
+// issues the next unit's loads before them -- no unit reads what the unit
+// before it writes: moves go up, a piece's units top down, and different
+// jobs are different segments).  A wave's loads touch 8-9 lines, where a
+// lane per segment moving its own bytes touched 64: 1.43 against 1.75 ms a
+// config-5 batch.
 __device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
-// Wave-cooperative moves (every lane of the wave, a wave-uniform job): n
-// bytes from src to dst (dst >= src, or disjoint), top down in units of 64
-// lanes x 16 bytes, a unit's loads before its stores; the lowest chunk of a
-// piece clamps to its first 16 bytes (the bytes it shares with the chunk
-// above get the same values twice, both loaded in that unit); fewer than 16
-// bytes left below a stored unit are copied bytewise (a clamped chunk would
-// read bytes that unit already rewrote).  A wave's loads touch 8-9 lines,
-// where a lane per segment moving its own bytes touched 64: 1.43 against
-// 1.75 ms a config-5 batch.  (Four jobs' units loaded together before their
-// stores -- more loads in flight -- ran slower, 1.98 ms.)
-__device__ __forceinline__ void wave_move_bytes(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t lane) {
-    for (uint64_t top = n;;) {
-        if (top < 16) {
-            if (lane == 0)
-                for (uint64_t i = top; i-- > 0;) dst[i] = src[i];
-            break;
-        }
-        const int64_t hi = (int64_t)top - 16 * (int64_t)lane;
-        const bool act = hi > 0;
-        const uint64_t c0 = hi >= 16 ? (uint64_t)hi - 16 : 0;
-        uint4 v;
-        if (act) __builtin_memcpy(&v, src + c0, 16);
-        __asm__ volatile("" ::: "memory");   // the unit's loads, all of them, before any store (no fused memcpy)
-        if (act) __builtin_memcpy(dst + c0, &v, 16);
-        if (top <= 1024) break;
-        top -= 1024;
-    }
-}
-// entries [a, e) of o moved by de and rebased by dk, top down, 64 per unit
-__device__ __forceinline__ void wave_move_offsets(uint64_t *o, uint64_t a, uint64_t e, uint64_t de, uint64_t dk,
-                                                  uint32_t lane) {
-    for (uint64_t top = e; top > a;) {
-        const bool act = top >= a + 1 + lane;
-        const uint64_t i = top - 1 - lane;
-        uint64_t x = 0;
-        if (act) x = o[i];
-        __asm__ volatile("" ::: "memory");
-        if (act) o[i + de] = x + dk;
-        top = top - a > 64 ? top - 64 : a;
-    }
-}
-// every lane's job (has = this lane has one), one after another by the whole
-// wave; a job's four arrays advance together, unit by unit: each unit's four
-// loads (key chunk, value chunk, key offset, value offset) go out before its
-// four stores -- one round trip a unit instead of one per array.
 __device__ __forceinline__ uint64_t bunits(uint64_t n) { return n >= 16 ? (n - 16) / 1024 + 1 : 0; }
+struct PmJob {   // a job's wave-uniform registers
+    __amdgpu_buffer_rsrc_t KS, KD, VS, VD, KO, VO, KOD, VOD;
+    uint64_t nk, nv, a, e, dk, dv, units, fl;
+};
+struct PmUnit {   // one unit's offsets (PM_OOB: nothing) and loaded data
+    uint32_t kc, vc, kt, vt, ok, ov;
+    pm_u32x4 kx, vx;
+    pm_u32x2 ox, px;
+    uint32_t kb, vb;
+};
+__device__ __forceinline__ bool pm_next_job(uint64_t &jm, const PieceJob &J, PmJob &q) {
+    if (!jm) return false;
+    const uint32_t L = (uint32_t)__builtin_ctzll(jm);
+    jm &= jm - 1;
+    q.fl = rl64(J.fl, L);
+    q.nk = (q.fl & 1) ? rl64(J.nk, L) : 0;
+    q.nv = (q.fl & 2) ? rl64(J.nv, L) : 0;
+    q.a = rl64(J.a, L);
+    q.e = (q.fl & 12) ? rl64(J.e, L) : q.a;
+    q.dk = rl64(J.dk, L);
+    q.dv = rl64(J.dv, L);
+    const uint64_t de = rl64(J.de, L), ko = rl64(J.ko, L), vo = rl64(J.vo, L);
+    q.KS = pm_rsrc(rl64(J.ks, L)); q.KD = pm_rsrc(rl64(J.kd, L));
+    q.VS = pm_rsrc(rl64(J.vs, L)); q.VD = pm_rsrc(rl64(J.vd, L));
+    q.KO = pm_rsrc(ko); q.VO = pm_rsrc(vo); q.KOD = pm_rsrc(ko + 8 * de); q.VOD = pm_rsrc(vo + 8 * de);
+    const uint64_t uk = bunits(q.nk) + (q.nk > 1024 * bunits(q.nk) ? 1 : 0);   // + the byte unit
+    const uint64_t uv = bunits(q.nv) + (q.nv > 1024 * bunits(q.nv) ? 1 : 0);
+    q.units = std::max(std::max(uk, uv), (q.e - q.a + 63) / 64);
+    return true;
+}
+// unit u's offsets for one heap of n bytes: a 16-byte chunk (c) or a byte (t)
+__device__ __forceinline__ void pm_heap_offs(uint64_t n, uint64_t u, uint32_t lane, uint32_t &c, uint32_t &t) {
+    const uint64_t U = bunits(n);
+    c = t = PM_OOB;
+    if (u < U) {
+        const int64_t h = (int64_t)n - 1024 * (int64_t)u - 16 * (int64_t)lane;
+        if (h > 0) c = h >= 16 ? (uint32_t)(h - 16) : 0u;
+    } else if (u == U && n > 1024 * U && lane < n - 1024 * U) {   // the byte unit (fewer than 16 bytes left)
+        t = lane;
+    }
+}
+__device__ __forceinline__ void pm_load(const PmJob &q, uint64_t u, uint32_t lane, PmUnit &d) {
+    pm_heap_offs(q.nk, u, lane, d.kc, d.kt);
+    pm_heap_offs(q.nv, u, lane, d.vc, d.vt);
+    const uint64_t top = q.e - std::min(q.e - q.a, 64 * u);
+    const uint32_t oo = top > q.a + lane ? (uint32_t)(8 * (top - 1 - lane)) : PM_OOB;
+    d.ok = (q.fl & 4) ? oo : PM_OOB;
+    d.ov = (q.fl & 8) ? oo : PM_OOB;
+    d.kx = __builtin_amdgcn_raw_buffer_load_b128(q.KS, d.kc, 0, 0);
+    d.vx = __builtin_amdgcn_raw_buffer_load_b128(q.VS, d.vc, 0, 0);
+    d.ox = __builtin_amdgcn_raw_buffer_load_b64(q.KO, d.ok, 0, 0);
+    d.px = __builtin_amdgcn_raw_buffer_load_b64(q.VO, d.ov, 0, 0);
+    d.kb = __builtin_amdgcn_raw_buffer_load_b8(q.KS, d.kt, 0, 0);
+    d.vb = __builtin_amdgcn_raw_buffer_load_b8(q.VS, d.vt, 0, 0);
+}
+__device__ __forceinline__ void pm_store(const PmJob &q, const PmUnit &d) {
+    const uint64_t o1 = (((uint64_t)d.ox.y << 32) | d.ox.x) + q.dk, p1 = (((uint64_t)d.px.y << 32) | d.px.x) + q.dv;
+    __builtin_amdgcn_raw_buffer_store_b128(d.kx, q.KD, d.kc, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(d.vx, q.VD, d.vc, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(pm_u32x2{(uint32_t)o1, (uint32_t)(o1 >> 32)}, q.KOD, d.ok, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(pm_u32x2{(uint32_t)p1, (uint32_t)(p1 >> 32)}, q.VOD, d.ov, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)d.kb, q.KD, d.kt, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)d.vb, q.VD, d.vt, 0, 0);
+}
+// PM_PIPE 1: the next unit's loads before the current unit's stores (two
+// units in flight).  Slower: 1.11 against 1.02 ms a config-5 batch (the
+// second unit's registers spill more at 5 waves per SIMD).
+#ifndef PM_PIPE
+#define PM_PIPE 0
+#endif
 __device__ __forceinline__ void wave_run_jobs(const PieceJob &J, bool has, uint32_t lane) {
     uint64_t jm = __ballot(has);
-    while (jm) {
-        const uint32_t L = (uint32_t)__builtin_ctzll(jm);
-        jm &= jm - 1;
-        const uint64_t fl = rl64(J.fl, L);
-        uint8_t *kd = (uint8_t *)rl64(J.kd, L), *vd = (uint8_t *)rl64(J.vd, L);
-        const uint8_t *ks = (const uint8_t *)rl64(J.ks, L), *vs = (const uint8_t *)rl64(J.vs, L);
-        const uint64_t nk = (fl & 1) ? rl64(J.nk, L) : 0, nv = (fl & 2) ? rl64(J.nv, L) : 0;
-        uint64_t *ko = (uint64_t *)rl64(J.ko, L), *vo = (uint64_t *)rl64(J.vo, L);
-        const uint64_t a = rl64(J.a, L), e = (fl & 12) ? rl64(J.e, L) : a;
-        const uint64_t de = rl64(J.de, L), dk = rl64(J.dk, L), dv = rl64(J.dv, L);
-        const uint64_t units = std::max(std::max(bunits(nk), bunits(nv)), (e - a + 63) / 64);
-        for (uint64_t u = 0; u < units; u++) {
-            const int64_t tk = (int64_t)nk - 1024 * (int64_t)u, tv = (int64_t)nv - 1024 * (int64_t)u;
-            const int64_t hk = tk - 16 * (int64_t)lane, hv = tv - 16 * (int64_t)lane;
-            const bool kA = tk >= 16 && hk > 0, vA = tv >= 16 && hv > 0;
-            const uint64_t kc = hk >= 16 ? (uint64_t)hk - 16 : 0, vc = hv >= 16 ? (uint64_t)hv - 16 : 0;
-            const uint64_t top = e - std::min(e - a, 64 * u);
-            const bool oA = top > a + lane;
-            const uint64_t oi = top - 1 - lane;
-            uint4 kx, vx;
-            uint64_t ox = 0, px = 0;
-            if (kA) __builtin_memcpy(&kx, ks + kc, 16);
-            if (vA) __builtin_memcpy(&vx, vs + vc, 16);
-            if (oA && (fl & 4)) ox = ko[oi];
-            if (oA && (fl & 8)) px = vo[oi];
-            __asm__ volatile("" ::: "memory");   // the unit's loads before its stores
-            if (kA) __builtin_memcpy(kd + kc, &kx, 16);
-            if (vA) __builtin_memcpy(vd + vc, &vx, 16);
-            if (oA && (fl & 4)) ko[oi + de] = ox + dk;
-            if (oA && (fl & 8)) vo[oi + de] = px + dv;
+    PmJob A, B;
+    PmUnit DA, DB;
+    uint64_t uA = 0, uB = 0;
+    bool hA = pm_next_job(jm, J, A);
+    if (hA) pm_load(A, 0, lane, DA);
+    while (hA) {
+        bool hB = true;
+        if (uA + 1 < A.units) {
+            B = A;
+            uB = uA + 1;
+        } else {
+            hB = pm_next_job(jm, J, B);
+            uB = 0;
+            if (!hB) { B = A; uB = A.units; }   // past every array: loads of nothing (no branch, no join wait)
         }
-        if (lane == 0) {   // bytes below the units (fewer than 16), highest first
-            for (uint64_t i = nk - std::min(nk, 1024 * bunits(nk)); i-- > 0;) kd[i] = ks[i];
-            for (uint64_t i = nv - std::min(nv, 1024 * bunits(nv)); i-- > 0;) vd[i] = vs[i];
+        if (PM_PIPE) {
+            pm_load(B, uB, lane, DB);
+            pm_store(A, DA);
+        } else {
+            pm_store(A, DA);
+            pm_load(B, uB, lane, DB);
         }
+        A = B; DA = DB; uA = uB; hA = hB;
     }
+}
+
+// A record's key and value bytes into the page (sources in the batch, never
+// overlapping their destinations): up to 32 bytes each in at most two
+// (overlapping) loads, all four loads before any store -- one round trip
+// where copy_bytes' load/store pairs took one each.  Longer: copy_bytes.
+__device__ __forceinline__ void small_load(const uint8_t *s, uint64_t n, uint4 &a, uint4 &b) {
+    if (n >= 16) {
+        __builtin_memcpy(&a, s, 16);
+        __builtin_memcpy(&b, s + n - 16, 16);
+    } else if (n >= 8) {
+        __builtin_memcpy(&a, s, 8);
+        __builtin_memcpy(&b, s + n - 8, 8);
+    } else if (n >= 4) {
+        __builtin_memcpy(&a, s, 4);
+        __builtin_memcpy(&b, s + n - 4, 4);
+    } else if (n) {
+        a.x = s[0]; a.y = s[n >> 1]; b.x = s[n - 1];
+    }
+}
+__device__ __forceinline__ void small_store(uint8_t *d, uint64_t n, const uint4 &a, const uint4 &b) {
+    if (n >= 16) {
+        __builtin_memcpy(d, &a, 16);
+        __builtin_memcpy(d + n - 16, &b, 16);
+    } else if (n >= 8) {
+        __builtin_memcpy(d, &a, 8);
+        __builtin_memcpy(d + n - 8, &b, 8);
+    } else if (n >= 4) {
+        __builtin_memcpy(d, &a, 4);
+        __builtin_memcpy(d + n - 4, &b, 4);
+    } else if (n) {
+        d[0] = (uint8_t)a.x; d[n >> 1] = (uint8_t)a.y; d[n - 1] = (uint8_t)b.x;
+    }
+}
+__device__ __forceinline__ void copy2_disjoint(uint8_t *d1, const uint8_t *s1, uint64_t n1, uint8_t *d2,
+                                               const uint8_t *s2, uint64_t n2) {
+    if (n1 > 32 || n2 > 32) {
+        copy_bytes(d1, s1, n1);
+        copy_bytes(d2, s2, n2);
+        return;
+    }
+    uint4 a1 = make_uint4(0u, 0u, 0u, 0u), b1 = a1, a2 = a1, b2 = a1;
+    small_load(s1, n1, a1, b1);
+    small_load(s2, n2, a2, b2);
+    __asm__ volatile("" ::: "memory");   // every load before any store
+    small_store(d1, n1, a1, b1);
+    small_store(d2, n2, a2, b2);
 }
 
 // The merge, a lane per segment for its control (groups, records) and the
@@ -400,8 +492,8 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                     if (X.v[0]) kl = klen_add(kl, Bn.v[BS_KN] - Br.v[BS_KN]);
                     p.koff[nwi] = nk;
                     p.voff[nwi] = nv;
-                    copy_bytes(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN]);
-                    copy_bytes(p.vheap + nv, a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
+                    copy2_disjoint(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN], p.vheap + nv,
+                                   a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
                 }
                 hi = u; khi = ku; vhi = vu;
                 j = g0;
