@@ -108,6 +108,17 @@ __device__ __forceinline__ void rw_node(const uint8_t *msg, uint32_t len, uint4 
 // ensembles one GPU hosts, riak_ensemble_peer.erl:1845-1846): workgroup g
 // takes window g % nwin of tree group[g / nwin], each tree with its own slot
 // arrays, tiles, counters and mailboxes.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *rw_global(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
+#else   // the host pass of device code (address-space-qualified class objects do not copy there)
+template <class T>
+__device__ __forceinline__ T *rw_global(T *p) {
+    return p;
+}
+#endif
 template <bool STAMP, bool GROUP, int NW>
 __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
                                                           uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps,
@@ -119,6 +130,10 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
     const uint32_t gi = GROUP ? blockIdx.x / nwin : 0;
     const uint64_t root = GROUP ? (uint64_t)(blockIdx.x - gi * nwin) : root0 + blockIdx.x;
 #define RFT(f) (GROUP ? group[gi].f : tt0.f)
+    // the group's pointers come from memory, so the compiler cannot tell their
+    // address space: as global ones the fetches are global loads, not FLAT
+    // (whose waits cover the LDS traffic too)
+#define RFG(f) (rw_global(RFT(f)))
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const RwLayout LY(mhb);
     uint8_t *MH = lds;
@@ -134,9 +149,9 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
     // ---- the window's tile descriptors and presence bitmap into LDS
     TileInfo *TI = reinterpret_cast<TileInfo *>(lds + LY.m1);   // M1 is free until level H
     if (tid < 64) {
-        TI[tid] = RFT(tinfo)[root * 64 + tid];
-        PRES[tid] = RFT(pres)[root * 64 + tid];
-        reinterpret_cast<uint64_t *>(NOFF)[tid] = reinterpret_cast<const uint64_t *>(RFT(noff) + root * 256)[tid];
+        TI[tid] = RFG(tinfo)[root * 64 + tid];
+        PRES[tid] = RFG(pres)[root * 64 + tid];
+        reinterpret_cast<uint64_t *>(NOFF)[tid] = ((const __attribute__((address_space(1))) uint64_t *)(RFG(noff) + root * 256))[tid];
     }
     if (tid < 4) MISC[tid] = 0;
     lds_barrier();
@@ -183,13 +198,13 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
     if (fq < NT) fload(fq);
     auto fetch = [&](Buf &b) {
         const uint32_t r = 4 * fk, last = fL;
-        const uint4 *p = RFT(tiles) + fbase;
+        const auto p = RFG(tiles) + fbase;
         b.x0 = (p + (uint64_t)(r < last ? r : last) * 64)[lane];
         b.x1 = (p + (uint64_t)(r + 1 < last ? r + 1 : last) * 64)[lane];
         b.x2 = (p + (uint64_t)(r + 2 < last ? r + 2 : last) * 64)[lane];
         b.x3 = (p + (uint64_t)(r + 3 < last ? r + 3 : last) * 64)[lane];
-        b.ln = RFT(tln)[w0 + ft * 64 + lane];
-        b.li = (uint32_t)(RFT(tseg)[w0 + ft * 64 + lane] - seg0);
+        b.ln = RFG(tln)[w0 + ft * 64 + lane];
+        b.li = (uint32_t)(RFG(tseg)[w0 + ft * 64 + lane] - seg0);
         b.k = fk;
         b.B = fq < NT ? fB : 0u;
         b.R = fR;
@@ -251,7 +266,7 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
         const uint64_t nbytes = (t.base[H + 1] + t.S) * 16;
         const __amdgpu_buffer_rsrc_t md5r = __builtin_amdgcn_make_buffer_rsrc(
             GROUP ? group[gi].md5 : t.md5, (short)0, (int)(nbytes < 0xffffffffull ? nbytes : 0xffffffffull), 0x00020000);
-        uint16_t *tagp = GROUP ? group[gi].tag : t.tag;
+        const auto tagp = rw_global(GROUP ? group[gi].tag : t.tag);
         for (uint32_t i = tid - 256; i < 4096; i += NW * 64 - 256) {
             const uint32_t n = i >> 4, j = i & 15, p16 = rw_pres16(PRES, n);
             uint4 e = make_uint4(0, 0, 0, 0);
@@ -294,9 +309,9 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
             rw_node(msg, len, e, tg);
             RF_STAMP(ph == 0 ? 2 : ph == 1 ? 4 : ph == 2 ? 6 : ph == 3 ? 10 : 14);
             const uint64_t slot = t.base[l] + b;
-            if (tg) (GROUP ? group[gi].md5 : t.md5)[slot] = e;
-            (GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
-            if (l == 1) { (GROUP ? group[gi].md5 : t.md5)[0] = e; (GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
+            if (tg) rw_global(GROUP ? group[gi].md5 : t.md5)[slot] = e;
+            rw_global(GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
+            if (l == 1) { rw_global(GROUP ? group[gi].md5 : t.md5)[0] = e; rw_global(GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
         }
         if (l <= lmin) break;
         if (ph == 0) {          // level-H entries into the H-1 messages

@@ -1089,6 +1089,12 @@ __device__ __forceinline__ uint32_t wave_prefix_count(bool f, uint32_t lane) {
 // per dword (byte stores only for a run's last partial dword).  Every load of
 // an iteration is in flight together, so runs up to 1 KB cost one memory
 // round trip.  One out-of-line copy per kernel (instruction-cache footprint).
+// The sources are read as global memory and the destinations written as LDS
+// (address-space casts): as generic pointers every access was a FLAT one,
+// whose waits cover both memory and LDS traffic.
+typedef __attribute__((address_space(1))) const uint32_t wc_gu32;
+typedef __attribute__((address_space(3))) uint32_t wc_lu32;
+typedef __attribute__((address_space(3))) uint8_t wc_lu8;
 __device__ __noinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t *d0, const uint8_t *s1, uint32_t n1,
                                            uint8_t *d1, const uint8_t *s2, uint32_t n2, uint8_t *d2, const uint8_t *s3,
                                            uint32_t n3, uint8_t *d3) {
@@ -1105,7 +1111,7 @@ __device__ __noinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t 
         for (int r = 0; r < 4; r++) {
             const uintptr_t a = reinterpret_cast<uintptr_t>(src[r]);
             const uint32_t mis = (uint32_t)(a & 3);
-            const uint32_t *w = reinterpret_cast<const uint32_t *>(a - mis);
+            wc_gu32 *w = (wc_gu32 *)(a - mis);
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t q = q0 / 4 + u * 64 + lane;
@@ -1116,7 +1122,8 @@ __device__ __noinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t 
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(src[r]) & 3);
-            uint32_t *dw = reinterpret_cast<uint32_t *>(dst[r]);
+            wc_lu32 *dw = (wc_lu32 *)dst[r];
+            wc_lu8 *db = (wc_lu8 *)dst[r];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t q = q0 / 4 + u * 64 + lane;
@@ -1125,9 +1132,9 @@ __device__ __noinline__ void wave_copy4(const uint8_t *s0, uint32_t n0, uint8_t 
                     dw[q] = v;
                 } else if (4 * q < len[r]) {
                     const uint32_t nb = len[r] - 4 * q;   // 1..3
-                    dst[r][4 * q] = (uint8_t)v;
-                    if (nb > 1) dst[r][4 * q + 1] = (uint8_t)(v >> 8);
-                    if (nb > 2) dst[r][4 * q + 2] = (uint8_t)(v >> 16);
+                    db[4 * q] = (uint8_t)v;
+                    if (nb > 1) db[4 * q + 1] = (uint8_t)(v >> 8);
+                    if (nb > 2) db[4 * q + 2] = (uint8_t)(v >> 16);
                 }
             }
         }
