@@ -94,10 +94,10 @@ __device__ __forceinline__ void hdr_rec(SmallOut *out, uint32_t seq, uint32_t re
     put_rec(&out->hdr, seq, retry | (new_entries << 1), 0u);
 }
 
-struct Overlay {
-    uint64_t *idx;              // [S], ~0 = segment not in the overlay
-    uint8_t *heap;
-    unsigned long long *used;   // bump pointer (device)
+struct Overlay {   // device pointers: global memory (ST_GAS, st_kernels.h)
+    uint64_t ST_GAS *idx;              // [S], ~0 = segment not in the overlay
+    uint8_t ST_GAS *heap;
+    unsigned long long ST_GAS *used;   // bump pointer (device)
     uint64_t cap;
 };
 
@@ -487,8 +487,8 @@ __device__ __forceinline__ void small_body(const SmallReq *req, SmallOut *out) {
     // the request (host memory) into LDS: one round trip, dword per thread
     __shared__ __attribute__((aligned(16))) SmallReq rq;
     static_assert(sizeof(SmallReq) % 4 == 0, "request is copied in dwords");
-    for (uint32_t i = threadIdx.x; i < sizeof(SmallReq) / 4; i += blockDim.x)
-        reinterpret_cast<uint32_t *>(&rq)[i] = reinterpret_cast<const uint32_t *>(req)[i];
+    const uint32_t ST_GAS *rqw = (const uint32_t ST_GAS *)req;   // global loads (k_small_multi reads req from memory)
+    for (uint32_t i = threadIdx.x; i < sizeof(SmallReq) / 4; i += blockDim.x) reinterpret_cast<uint32_t *>(&rq)[i] = rqw[i];
     __syncthreads();
     const DevTree &t = rq.t;
     const Overlay &ov = rq.ov;

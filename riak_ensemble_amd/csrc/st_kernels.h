@@ -30,26 +30,42 @@
 
 #define ST_FLAG_ATOM_UTF8 1u   // DevTree.flags: ETF atoms as OTP >= 26 writes them (utf8 forms only)
 
+// Device code sees the tree's pointers as global memory (address space 1):
+// a DevTree read from LDS or from memory -- the per-key kernel's request, a
+// group's descriptors -- would otherwise hand every access to FLAT, whose
+// waits cover LDS and memory alike.  The host pass sees plain pointers (the
+// layout is the same).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ST_GAS __attribute__((address_space(1)))
+#else
+#define ST_GAS
+#endif
+// a host pointer stored into a DevTree (the device pass of host code sees the
+// address-space-qualified fields)
+template <class T>
+__host__ __device__ __forceinline__ T ST_GAS *gp(T *p) {
+    return (T ST_GAS *)p;
+}
 struct DevTree {
     uint32_t W, shift, H, flags;
     uint64_t S;
     uint64_t base[ST_MAXLEV + 2];
-    uint4 *md5;
-    uint16_t *tag;
+    uint4 ST_GAS *md5;
+    uint16_t ST_GAS *tag;
     // segment s: entries [seg_off[s], seg_end[s]) of koff/voff (each entry's
     // key and value end at the next entry's offsets; entry seg_end[s] holds
     // the ends of the last one), values [seg_voff[s], seg_vend[s]).  The
     // canonical CSR is gap-free (seg_end = seg_off + 1, seg_vend = seg_voff +
     // 1); the paged layout of streaming batches (pages.h) leaves slack after
     // every segment's page.
-    const uint64_t *seg_off;
-    const uint64_t *seg_end;
-    const uint64_t *seg_voff;
-    const uint64_t *seg_vend;
-    const uint64_t *koff;
-    const uint8_t *kheap;
-    const uint64_t *voff;
-    const uint8_t *vheap;
+    const uint64_t ST_GAS *seg_off;
+    const uint64_t ST_GAS *seg_end;
+    const uint64_t ST_GAS *seg_voff;
+    const uint64_t ST_GAS *seg_vend;
+    const uint64_t ST_GAS *koff;
+    const uint8_t ST_GAS *kheap;
+    const uint64_t ST_GAS *voff;
+    const uint8_t ST_GAS *vheap;
 };
 
 // Key records (term_key.h): the plain int64 / atom / binary form, or a term

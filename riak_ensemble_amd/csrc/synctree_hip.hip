@@ -469,27 +469,27 @@ static DevTree view(const st_tree *t) {
     d.flags = t->flags;
     d.S = t->S;
     for (int i = 0; i < ST_MAXLEV + 2; i++) d.base[i] = t->base[i];
-    d.md5 = t->md5;
-    d.tag = t->tag;
+    d.md5 = gp(t->md5);
+    d.tag = gp(t->tag);
     if (t->pg.on) {
-        d.seg_off = t->pg.m.beg;
-        d.seg_end = t->pg.m.end;
-        d.seg_voff = t->pg.m.vbeg;
-        d.seg_vend = t->pg.m.vend;
-        d.koff = t->pg.koff;
-        d.kheap = t->pg.kheap;
-        d.voff = t->pg.voff;
-        d.vheap = t->pg.vheap;
+        d.seg_off = gp(t->pg.m.beg);
+        d.seg_end = gp(t->pg.m.end);
+        d.seg_voff = gp(t->pg.m.vbeg);
+        d.seg_vend = gp(t->pg.m.vend);
+        d.koff = gp(t->pg.koff);
+        d.kheap = gp(t->pg.kheap);
+        d.voff = gp(t->pg.voff);
+        d.vheap = gp(t->pg.vheap);
         return d;
     }
-    d.seg_off = t->seg_off;
-    d.seg_end = t->seg_off + 1;
-    d.seg_voff = t->seg_voff;
-    d.seg_vend = t->seg_voff + 1;
-    d.koff = t->koff;
-    d.kheap = t->kheap;
-    d.voff = t->voff;
-    d.vheap = t->vheap;
+    d.seg_off = gp(t->seg_off);
+    d.seg_end = gp(t->seg_off + 1);
+    d.seg_voff = gp(t->seg_voff);
+    d.seg_vend = gp(t->seg_voff + 1);
+    d.koff = gp(t->koff);
+    d.kheap = gp(t->kheap);
+    d.voff = gp(t->voff);
+    d.vheap = gp(t->vheap);
     return d;
 }
 
