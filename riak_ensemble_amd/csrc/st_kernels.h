@@ -688,6 +688,36 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
     }
 }
 
+// The streaming batch's per-segment sums without atomics (k_merge_keys run
+// with sd == nullptr): the lane of each run's first record sums its run's
+// BatchSums -- the merged-size DELTAS (entries, key bytes, value bytes, new
+// keys), dirty = a kept record (insert semantics: kept == NE), fpos = the
+// smallest value offset a kept record changes (its rat.vu).
+__global__ void k_run_sums(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
+                           const RecAt *rat, SegSums *sd, uint8_t *dirty, unsigned long long *fpos) {
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        const uint64_t s = sseg[j];
+        if (j != bseg_off[s]) continue;
+        const uint64_t je = bseg_off[s + 1];
+        SegSums d(0);
+        uint64_t fp = ~0ull;
+        for (uint64_t r = j; r < je; r++) {
+            const BatchSums f = bs[r];
+            if (!f.v[BS_NE] && !f.v[BS_EQ]) continue;
+            d.v[0] += f.v[BS_NE] - f.v[BS_EQ];
+            d.v[1] += f.v[BS_KN] - f.v[BS_KE];
+            d.v[2] += f.v[BS_VN] - f.v[BS_VE];
+            d.v[3] += (f.v[BS_NE] && !f.v[BS_EQ]) ? 1 : 0;
+            fp = std::min<uint64_t>(fp, rat[r].vu);
+        }
+        if (fp != ~0ull) {
+            sd[s] = d;
+            dirty[s] = 1;
+            fpos[s] = fp;
+        }
+    }
+}
+
 // A segment's merged sizes (SegSums: entries, key bytes, value bytes, new
 // keys) from its old sizes and its run's BatchSums; dirty = a kept record.
 // Returns the value offset (relative to the segment's first value) of the

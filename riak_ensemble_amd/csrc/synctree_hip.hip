@@ -1574,8 +1574,18 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
-        LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat, ss,
-               dirty, fpos);
+#ifndef ST_RUN_SUMS
+#define ST_RUN_SUMS 1
+#endif
+        if (ST_RUN_SUMS) {   // the per-segment sums by the runs' first lanes (no atomics)
+            LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
+                   (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
+            LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
+                   n, (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos);
+        } else {
+            LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat, ss,
+                   dirty, fpos);
+        }
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
                (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
         CHK(verify_levels(t, t->H + 1));
