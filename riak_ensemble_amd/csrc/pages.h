@@ -208,7 +208,7 @@ struct PageMergeArgs {
     uint8_t *kheap, *vheap;
     const uint32_t *pos;
     const RecAt *rat;             // per record: old offsets at its position (page-relative), its batch offsets
-    const BatchSums *bx;          // exclusive scan over the sorted batch
+    const BatchSums *bx;          // per run: inclusive prefix sums of its records' BatchSums (k_run_sums)
     const SegSums *ss;            // per segment: merged count, key bytes, value bytes
     const uint8_t *mode;
     const PlanSums *rbase;        // exclusive scan of the relocation sizes
@@ -411,6 +411,11 @@ __device__ __forceinline__ void copy2_disjoint(uint8_t *d1, const uint8_t *s1, u
     small_store(d2, n2, a2, b2);
 }
 
+// The growth of a run's records [j0, x): their BatchSums summed (0 at j0).
+__device__ __forceinline__ BatchSums pm_bx(const PageMergeArgs &p, uint64_t j0, uint64_t x) {
+    return x == j0 ? BatchSums(0) : p.bx[x - 1];
+}
+
 // The merge, a lane per segment for its control (groups, records) and the
 // whole wave for every piece move: the wave's lanes step through their groups
 // together, top down; each round moves every lane's piece (wave_run_jobs),
@@ -431,7 +436,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
         const uint8_t md = s < a.S ? p.mode[s] : 0;
         uint64_t j0 = 0, je = 0, b = 0, c = 0, Kb = 0, Vb = 0, De = 0, Dk = 0, Dv = 0, EC = 0, KC = 0, VC = 0;
         SegSums X(0);
-        BatchSums B0(0);
+        const BatchSums B0(0);   // the growth before the run's first record (pm_bx: run-local sums)
         bool live = md != 0;
         if (live) {
             j0 = a.bseg_off[s]; je = a.bseg_off[s + 1];
@@ -446,7 +451,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
             }
             // the merged segment fits its (new) page: every move below stays inside it
             live = pg_ok(chk, De + X.v[0] < EC && Dk + X.v[1] <= KC && Dv + X.v[2] <= VC, 14, s, De + X.v[0], EC);
-            if (live) B0 = p.bx[j0];
+
         }
         uint32_t kl = (live && X.v[0]) ? p.m.klen[s] : KLEN_NONE;   // the merged segment's uniform key length
         uint64_t hi = c, khi = live ? p.koff[b + c] : 0, vhi = live ? p.voff[b + c] : 0;   // the current piece's end
@@ -460,8 +465,8 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                 u = p.pos[j - 1];
                 g0 = j - 1;
                 while (g0 > j0 && p.pos[g0 - 1] == u) g0--;
-                const BatchSums Bj = p.bx[j];
-                const bool eq = Bj.v[BS_EQ] != p.bx[j - 1].v[BS_EQ];   // the group's last record replaces entry u
+                const BatchSums Bj = pm_bx(p, j0, j);
+                const bool eq = Bj.v[BS_EQ] != pm_bx(p, j0, j - 1).v[BS_EQ];   // the group's last record replaces entry u
                 const uint64_t lo = u + (eq ? 1 : 0);
                 const uint64_t de = (Bj.v[BS_NE] - B0.v[BS_NE]) - (Bj.v[BS_EQ] - B0.v[BS_EQ]);
                 const uint64_t dk = (Bj.v[BS_KN] - B0.v[BS_KN]) - (Bj.v[BS_KE] - B0.v[BS_KE]);
@@ -483,7 +488,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
             wave_run_jobs(J, has, lane);
             if (mine) {
                 for (uint64_t r = j; r > g0; r--) {   // the group's records that produce an entry, highest first
-                    const BatchSums &Br = p.bx[r - 1], &Bn = p.bx[r];
+                    const BatchSums Br = pm_bx(p, j0, r - 1), Bn = pm_bx(p, j0, r);
                     if (Bn.v[BS_NE] == Br.v[BS_NE]) continue;
                     const uint64_t nwi = De + u + (Br.v[BS_NE] - B0.v[BS_NE]) - (Br.v[BS_EQ] - B0.v[BS_EQ]);
                     const uint64_t nk = Dk + (ku - Kb) + (Br.v[BS_KN] - B0.v[BS_KN]) - (Br.v[BS_KE] - B0.v[BS_KE]);

@@ -692,17 +692,22 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
 // with sd == nullptr): the lane of each run's first record sums its run's
 // BatchSums -- the merged-size DELTAS (entries, key bytes, value bytes, new
 // keys), dirty = a kept record (insert semantics: kept == NE), fpos = the
-// smallest value offset a kept record changes (its rat.vu).
+// smallest value offset a kept record changes (its rat.vu) -- and writes the
+// run's INCLUSIVE prefix sums into bxl (k_page_merge's growth before and
+// through each group: no scan over the whole batch).
 __global__ void k_run_sums(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
-                           const RecAt *rat, SegSums *sd, uint8_t *dirty, unsigned long long *fpos) {
+                           const RecAt *rat, SegSums *sd, uint8_t *dirty, unsigned long long *fpos, BatchSums *bxl) {
     for (uint64_t j = gtid(); j < n; j += gstride()) {
         const uint64_t s = sseg[j];
         if (j != bseg_off[s]) continue;
         const uint64_t je = bseg_off[s + 1];
         SegSums d(0);
+        BatchSums acc(0);
         uint64_t fp = ~0ull;
         for (uint64_t r = j; r < je; r++) {
             const BatchSums f = bs[r];
+            acc = acc + f;
+            bxl[r] = acc;
             if (!f.v[BS_NE] && !f.v[BS_EQ]) continue;
             d.v[0] += f.v[BS_NE] - f.v[BS_EQ];
             d.v[1] += f.v[BS_KN] - f.v[BS_KE];

@@ -1557,7 +1557,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&rbase, S + 1));
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
-    CHK(sc.alloc(&bx, n + 1));
+    CHK(sc.alloc(&bx, n));
     HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PlanSums), t->stream));
     HIPCHK(hipMemsetAsync(ss, 0, S * sizeof(SegSums), t->stream));
@@ -1574,18 +1574,11 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
-#ifndef ST_RUN_SUMS
-#define ST_RUN_SUMS 1
-#endif
-        if (ST_RUN_SUMS) {   // the per-segment sums by the runs' first lanes (no atomics)
-            LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
-                   (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
-            LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
-                   n, (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos);
-        } else {
-            LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat, ss,
-                   dirty, fpos);
-        }
+        // then the per-segment sums and the runs' prefix sums by each run's first lane (no atomics, no scan)
+        LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
+               (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
+        LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
+               (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos, bx);
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
                (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
         CHK(verify_levels(t, t->H + 1));
@@ -1595,7 +1588,6 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
                               (const uint8_t *)reject, in.clevel_out);
     ma.seg_reject = reject;
-    CHK(exclusive_scan<BatchSums>(t, bs, bx, n + 1));
     // in place or to a new page; the moves' places in the append region
     PlanSums tot(0);
     for (int pass = 0;; pass++) {
