@@ -246,6 +246,13 @@ def main():
         if not args.no_extras:
             out['build'] = _bench_build(synctree_hip, keys_d, vals_d, n, dev_index, torch)
             out['compare'] = _bench_compare(synctree_hip, tree, keys_d, vals_d, n, dev_index, torch)
+            out['verify'] = _bench_verify(tree, n)
+            # one exchange with one remote peer as riak_ensemble_exchange runs it:
+            # verify_upper precheck (:58-65) + compare + valid_obj_hash apply (:71-97)
+            out['exchange_total_ms'] = round(out['verify']['verify_upper']['ms'] +
+                                             out['compare']['exchange_apply_ms'], 4)
+            out['exchange_total_what'] = ('verify_upper ms + exchange_apply ms (st_exchange_apply = compare + '
+                                          'select + one batched insert of the newer remote values)')
             out['leveldb'] = _bench_leveldb(synctree_hip, tree, dev_index, torch)
             out['rehash_after_mutation'] = _bench_rehash_after_mutation(tree, n, torch)
             out['repair'] = _bench_repair(tree, keys_h, torch)
@@ -603,6 +610,52 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
                     'round trip per compare'}
 
 
+def _bench_verify(tree, n, reps=20):
+    """verify_upper/1 and verify/1 (synctree.erl:549-571) of the 10M-key tree.
+    verify_upper is the exchange's own precheck (riak_ensemble_exchange.erl:
+    58-65): every exchange runs it before its compare.  §8(d) bytes: the 17-B
+    entries every verified node's message holds (a node's hash input is its
+    children's entries; verify/1 adds every segment's values, 17 B per key)
+    plus the 17-B parent entry each node is checked against.  Wall time per
+    C-ABI call (the call returns the boolean: one host round trip), kernel
+    times from HIP events in a second pass."""
+    H = tree.height
+    pres = [None] + [tree.level_entries(l)[0] for l in range(1, H + 2)]
+    inner_nodes = sum(int(pres[l].sum()) for l in range(1, H + 1))     # present nodes of levels 1..H
+    child_entries = sum(int(pres[l].sum()) for l in range(2, H + 2))   # their message entries
+    out = {}
+    for name, upper in (('verify_upper', True), ('verify', False)):
+        assert tree.verify(upper=upper) is True
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            tree.verify(upper=upper)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        tree.set_timing(True)
+        tree.kernel_stats('*reset*')
+        for _ in range(reps):
+            tree.verify(upper=upper)
+        kms = {}
+        for k in ('verify_upper', 'mark_reachable', 'segment_verify', 'level_verify'):
+            c, ms = tree.kernel_stats(k)
+            if c:
+                kms[k] = round(ms / c, 4)
+        tree.set_timing(False)
+        ms = ts[len(ts) // 2] * 1e3
+        alg = 17 * (child_entries + inner_nodes) + (0 if upper else 17 * (n + int(pres[H + 1].sum())))
+        gbs = alg / (ms / 1e3) / 1e9
+        out[name] = {'ms': round(ms, 4), 'kernel_ms': kms,
+                     'roofline': {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                  'frac': round(gbs / HBM_PEAK_GBS, 4), 'bytes_per_call': alg,
+                                  'formula': '17 B x (child entries of the %d verified inner nodes + their parent '
+                                             'entries)%s, over the wall ms of one call'
+                                             % (inner_nodes, '' if upper else ' + 17 B x (keys + segments)')}}
+    out['what'] = ('median of %d C-ABI calls on the config-2 tree (10M keys); verify_upper/1 = the exchange '
+                   'precheck (riak_ensemble_exchange.erl:58-65)' % reps)
+    return out
+
+
 def _bench_leveldb(synctree_hip, tree, local, torch, reps=5):
     """synctree_leveldb format of the 10M-key tree:
     device encode of every node record, the host-inclusive snapshot (D2H of
@@ -715,7 +768,6 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     for e in range(E):
         k = _dev_keys(workload.SEED ^ (rank * E + e + 1), 0, nk, dev, torch)
         t = synctree_hip.DeviceTree(device=local)
-        torch.cuda.synchronize()   # the library reads the keys on its own stream
         t.insert_int64_device(k.data_ptr(), vals.data_ptr(), nk, 17)
         trees.append(t)
         del k
@@ -894,7 +946,6 @@ def _bench_partition(synctree_hip, dist, coll_dev, args, local, torch):
         m = min(chunk, N - a)
         k = _dev_keys(seed, a, m, dev, torch)
         v = _dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
-        torch.cuda.synchronize()   # the library reads them on its own stream
         pt.tree.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
         del k, v
     pt.combine()

@@ -35,14 +35,15 @@
  *      ST_KEY_ATOM   bytes = atom_to_binary(Key, utf8)
  *      ST_KEY_BINARY bytes = the binary
  *      ST_KEY_TERM   bytes = term_to_binary(Key) (any other key: tuples,
- *                    lists, floats, integers outside int64; the reference
- *                    hashes term_to_binary(Key), or <<Key:64>> for an
- *                    integer; riak_ensemble_amd/csrc/term_key.h)
- *    Keys are kept in Erlang term order (number < atom < tuple < nil < list <
- *    binary; numbers by value, atoms and binaries bytewise with a proper
- *    prefix first).  Pids, ports, refs, funs, maps and bitstrings are
- *    rejected with ST_EINVAL; an int64 / atom / binary passed as ST_KEY_TERM
- *    is the same key as its plain form.
+ *                    lists, maps, floats, integers outside int64; the
+ *                    reference hashes term_to_binary(Key), or <<Key:64>> for
+ *                    an integer; riak_ensemble_amd/csrc/term_key.h)
+ *    Keys are kept in Erlang term order (number < atom < tuple < map < nil <
+ *    list < binary; numbers by value, atoms and binaries bytewise with a
+ *    proper prefix first, maps by size, then keys, then values).  Pids,
+ *    ports, refs, funs and bitstrings that are not binaries are rejected
+ *    with ST_EINVAL; an int64 / atom / binary passed as ST_KEY_TERM is the
+ *    same key as its plain form.
  *  - Packed variable-length arrays: element i of a heap is
  *    heap[off[i] .. off[i+1]) with off[] of n+1 entries.
  *  - Hashes are 17 bytes: <<?H_MD5 = 0, md5/binary>> (src/synctree.erl:255-259).
@@ -120,12 +121,19 @@ int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, const uint8_t 
 
 /* Same for integer keys (ST_KEY_INT) and fixed-width values.
  * keys[n] (int64), vals[n*vlen].  inputs_on_device != 0: both pointers are
- * device memory on this tree's device (no host staging), read on the tree's
- * stream: whatever produces them must be complete first (synchronised, or
- * enqueued on that stream, st_set_stream).  *n_corrupted
- * (may be NULL) receives the number of rejected keys. */
+ * device memory on this tree's device (no host staging), written by work on
+ * the device's NULL stream (torch's default stream): the library orders its
+ * reads after that stream's work enqueued before the call (an event, no host
+ * wait) -- st_insert_int64_dev names another producer stream.  The call
+ * returns after its last read of the inputs.  *n_corrupted (may be NULL)
+ * receives the number of rejected keys. */
 int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                     int inputs_on_device, uint64_t *n_corrupted);
+/* st_insert_int64 with device inputs produced on `producer_stream` (a
+ * hipStream_t; NULL = the null stream): the tree's reads wait for the work
+ * enqueued on it before the call.  No caller-side synchronisation needed. */
+int st_insert_int64_dev(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                        void *producer_stream, uint64_t *n_corrupted);
 
 /* corrupt/2 (synctree.erl:241-247): erase Key from its segment without
  * updating the path (test aid). */
@@ -226,8 +234,12 @@ int st_combine_upper(st_tree *t, const uint8_t *present16, const uint8_t *hashes
 /* Ensemble sharding (riak_ensemble_peer.erl:1845-1846: one tree per peer):
  * the top-hash records of n trees on one device written to DEVICE memory
  * `out` (18 bytes per tree: present byte, then the 17-byte hash), the payload
- * of the cross-GPU all-gather of top hashes. */
+ * of the cross-GPU all-gather of top hashes.  The write into `out` waits for
+ * the work enqueued on the null stream before the call (a previous collective
+ * may still read `out`); the call returns after it.  st_tops_to_device_on
+ * names the caller's stream instead (NULL = the null stream). */
 int st_tops_to_device(st_tree **trees, uint32_t n, void *out);
+int st_tops_to_device_on(st_tree **trees, uint32_t n, void *out, void *stream);
 
 /* ---- reads ---------------------------------------------------------- */
 

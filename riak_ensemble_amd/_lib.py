@@ -55,6 +55,8 @@ _SIGS = {
                                        ctypes.c_void_p, ctypes.c_void_p]),
     'st_insert_int64': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint32, ctypes.c_int, u64p]),
+    'st_insert_int64_dev': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p, u64p]),
     'st_corrupt': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32]),
     'st_store_inner': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                       ctypes.c_void_p, ctypes.c_void_p]),
@@ -97,6 +99,7 @@ _SIGS = {
                                           u64p]),
     'st_compare_stats': (ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32, u64p]),
     'st_tops_to_device': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    'st_tops_to_device_on': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     'st_set_etf_atoms': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     'st_get1': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),

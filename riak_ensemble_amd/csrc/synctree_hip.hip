@@ -83,6 +83,7 @@ struct st_tree {
     int ncu = 256;   // compute units of the device (fixed-grid kernels)
     uint32_t flags = 0;   // DevTree.flags (ST_FLAG_ATOM_UTF8)
     hipStream_t own_stream = nullptr, stream = nullptr;
+    hipEvent_t ev_order = nullptr;   // cross-stream ordering of caller device buffers (order_after)
     uint64_t W = 16, S = 1 << 20;
     uint32_t shift = 4, H = 5;
     uint64_t base[ST_MAXLEV + 2] = {0};
@@ -672,9 +673,26 @@ static int rpin_reserve(st_tree *t, uint64_t bytes) {
 }
 static int h2d(st_tree *t, void *dst, const void *src, uint64_t bytes) {
     if (!bytes) return ST_OK;
+    t->async_pending = true;
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, t->stream));
     return ST_OK;
 }
+
+// Device buffers a caller hands in (or wants written) are produced / consumed
+// by work on the caller's own stream: the tree's next work is ordered after
+// everything enqueued on `producer` so far (an event, no host wait).  NULL is
+// the device's null stream -- torch's default stream -- which the library's
+// non-blocking streams are otherwise NOT ordered against.
+static int order_after(st_tree *t, hipStream_t producer) {
+    if (producer == t->stream) return ST_OK;
+    if (!t->ev_order) HIPCHK(hipEventCreateWithFlags(&t->ev_order, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(t->ev_order, producer));
+    HIPCHK(hipStreamWaitEvent(t->stream, t->ev_order, 0));
+    t->async_pending = true;
+    return ST_OK;
+}
+// (The consumer side needs no event: every call that writes caller memory
+// returns after a host synchronisation of its stream.)
 
 static uint32_t inner_block(const st_tree *t) { return 64; }
 static size_t inner_shmem(const st_tree *t) { return (size_t)inner_block(t) * lane_region_bytes((uint32_t)t->W); }
@@ -792,6 +810,7 @@ extern "C" void st_destroy(st_tree *t) {
     if (t->sout) (void)hipHostFree(t->sout);
     if (t->sreq) (void)hipHostFree(t->sreq);
     if (t->cw.res) (void)hipHostFree(t->cw.res);
+    if (t->ev_order) (void)hipEventDestroy(t->ev_order);
     for (auto &p : t->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     mem_forget_owner(t);   // the stream was idle: the blocks freed above have no pending use
     if (t->own_stream) (void)hipStreamDestroy(t->own_stream);
@@ -2192,12 +2211,26 @@ extern "C" int st_insert_batch(st_tree *t, uint64_t n, const uint8_t *ktype, con
     return r;
 }
 
+static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                        int on_device, hipStream_t producer, uint64_t *n_corrupted);
 extern "C" int st_insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
                                int on_device, uint64_t *n_corrupted) {
     ENTER(t);
+    return insert_int64(t, n, keys, vals, vlen, on_device, nullptr, n_corrupted);
+}
+extern "C" int st_insert_int64_dev(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                                   void *producer_stream, uint64_t *n_corrupted) {
+    ENTER(t);
+    return insert_int64(t, n, keys, vals, vlen, 1, (hipStream_t)producer_stream, n_corrupted);
+}
+static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8_t *vals, uint32_t vlen,
+                        int on_device, hipStream_t producer, uint64_t *n_corrupted) {
     CHK(flush_overlay(t));   // the pages stay: a streaming batch may go to them (ingest)
     if (n_corrupted) *n_corrupted = 0;
     if (n == 0) return ST_OK;
+    // device inputs: read only after the producer's writes (the call returns
+    // after its last read of them, so the caller may reuse them at once)
+    if (on_device) CHK(order_after(t, producer));
     const int64_t *dkeys = keys;
     const uint8_t *dvals = vals;
     int64_t *tk = nullptr;
@@ -3410,6 +3443,9 @@ extern "C" int st_key_record(uint8_t ktype, const uint8_t *bytes, uint64_t len, 
 // Top-hash records of n trees (one device) into device memory `out`
 // (18 bytes per tree: present, hash17), for an RCCL all-gather.
 extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
+    return st_tops_to_device_on(trees, n, out, nullptr);
+}
+extern "C" int st_tops_to_device_on(st_tree **trees, uint32_t n, void *out, void *stream) {
     if (n == 0) return ST_OK;
     for (uint32_t i = 0; i < n; i++)
         if (!trees[i]) { g_err = "NULL tree"; return ST_EINVAL; }
@@ -3428,6 +3464,9 @@ extern "C" int st_tops_to_device(st_tree **trees, uint32_t n, void *out) {
     TreeTiles *dtt = nullptr;
     CHK(sc.alloc(&dtt, n));
     HIPCHK(hipMemcpyAsync(dtt, h.data(), n * sizeof(TreeTiles), hipMemcpyHostToDevice, t->stream));
+    // `out` may still be read by the caller's stream (e.g. the previous
+    // all-gather): written only after that stream's work so far
+    CHK(order_after(t, (hipStream_t)stream));
     LAUNCH(t, "tops_out", k_tops_out, grid_for((uint64_t)n * 18), 256, 0, (const TreeTiles *)dtt, n, (uint8_t *)out);
     CHK(tsync(t));
     return ST_OK;

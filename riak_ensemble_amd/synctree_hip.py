@@ -94,14 +94,17 @@ class DeviceTree:
                                           ctypes.byref(nc)), 'st_insert_int64')
         return int(nc.value)
 
-    def insert_int64_device(self, keys_ptr, vals_ptr, n, vlen):
-        """Same with device-resident inputs (int64 keys, n*vlen value bytes).
-        The library reads them on its own stream: the work that produced them
-        must be complete (e.g. torch.cuda.synchronize()) or enqueued on the
-        tree's stream (set_stream)."""
+    def insert_int64_device(self, keys_ptr, vals_ptr, n, vlen, stream=None):
+        """Same with device-resident inputs (int64 keys, n*vlen value bytes)
+        written by work on `stream` (a hipStream_t handle, e.g. torch's
+        ``current_stream().cuda_stream``; None / 0 = the null stream, torch's
+        default): the library orders its reads after that stream's work
+        (st_insert_int64_dev, an event, no host wait) and returns after its
+        last read of them."""
         nc = ctypes.c_uint64(0)
-        _lib.check(self.L.st_insert_int64(self.h, n, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(vals_ptr), vlen, 1,
-                                          ctypes.byref(nc)), 'st_insert_int64')
+        _lib.check(self.L.st_insert_int64_dev(self.h, n, ctypes.c_void_p(keys_ptr), ctypes.c_void_p(vals_ptr), vlen,
+                                              ctypes.c_void_p(stream or None), ctypes.byref(nc)),
+                   'st_insert_int64_dev')
         return int(nc.value)
 
     def corrupt(self, key):
@@ -522,12 +525,14 @@ def get1_multi(trees, keys, vcap=1 << 20):
     return out
 
 
-def tops_to_device(trees, dev_ptr):
+def tops_to_device(trees, dev_ptr, stream=None):
     """Top-hash records (18 B each: present, hash17) of `trees` into device
-    memory at dev_ptr (st_tops_to_device), e.g. a torch uint8 tensor to
-    all-gather across ranks."""
+    memory at dev_ptr (st_tops_to_device_on), e.g. a torch uint8 tensor to
+    all-gather across ranks; the write waits for the work enqueued on
+    `stream` (None = the null stream, torch's default) before the call."""
     if not trees:
         return
     L = trees[0].L
     arr = (ctypes.c_void_p * len(trees))(*[t.h.value for t in trees])
-    _lib.check(L.st_tops_to_device(arr, len(trees), ctypes.c_void_p(dev_ptr)), 'st_tops_to_device')
+    _lib.check(L.st_tops_to_device_on(arr, len(trees), ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream or None)),
+               'st_tops_to_device_on')

@@ -18,7 +18,6 @@ trees = []
 for e in range(E):
     k = bench._dev_keys(workload.SEED ^ (e + 1), 0, N, dev, torch)
     t = synctree_hip.DeviceTree()
-    torch.cuda.synchronize()
     t.insert_int64_device(k.data_ptr(), vals.data_ptr(), N, 17)
     trees.append(t)
 torch.cuda.synchronize()

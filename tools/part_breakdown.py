@@ -27,7 +27,6 @@ for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
     k = bench._dev_keys(seed, a, m, dev, torch)
     v = bench._dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
-    torch.cuda.synchronize()   # the library reads them on its own stream
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
     del k, v
 torch.cuda.synchronize()

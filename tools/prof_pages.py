@@ -21,7 +21,6 @@ for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
     k = bench._dev_keys(seed, a, m, dev, torch)
     v = bench._dev_values(torch.arange(a, a + m, dtype=torch.int64, device=dev), dev, torch)
-    torch.cuda.synchronize()
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), m, 17)
     del k, v
 rng = np.random.default_rng(5)
@@ -30,7 +29,6 @@ for j in range(K + 1):
     k = torch.cat([bench._dev_keys_at(seed, old, dev, torch), bench._dev_keys(seed, N + j * B, B - B // 2, dev, torch)]).contiguous()
     seq = torch.cat([old + 1, torch.arange(N + j * B, N + j * B + (B - B // 2), device=dev)])
     v = bench._dev_values(seq, dev, torch).contiguous()
-    torch.cuda.synchronize()
     t.insert_int64_device(k.data_ptr(), v.data_ptr(), B, 17)
 torch.cuda.synchronize()
 print('pages', t.page_stats(), 'entries', t.num_entries())
