@@ -542,7 +542,7 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
     tree_a.kernel_stats('*reset*')
     for _ in range(reps):
         tree_a.compare_device(tb)
-    kern = {k: round(tree_a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_walk', 'cmp_gather')}
+    kern = {k: round(tree_a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_walk',)}
     tree_a.set_timing(False)
     vis, algo = _compare_roofline(tree_a, dt * 1e3)
     t0 = time.perf_counter()
@@ -605,9 +605,9 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
             'exchange_apply_ms': round(dt_apply * 1e3, 4),
             'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
                               'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),
-            'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 (frontier, verify + '
-                    'merge-join, device scan, reorder) with the ordered diff records left on the device; one host '
-                    'round trip per compare'}
+            'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 in one launch (frontier, '
+                    'verify + merge-join, each wave\'s records placed after the higher waves\' by their published '
+                    'counts) with the ordered diff records left on the device; one host round trip per compare'}
 
 
 def _bench_verify(tree, n, reps=20):

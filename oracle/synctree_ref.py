@@ -198,6 +198,12 @@ def _ext(t):
             return b'k' + len(t).to_bytes(2, 'big') + bytes(t)            # STRING_EXT
         return b'l' + len(t).to_bytes(4, 'big') + b''.join(_ext(e) for e in t) + b'j'
     if isinstance(t, Mapping):   # MAP_EXT; a flatmap (<= 32 keys) writes its pairs in map-key order
+        # a hashmap (> 32 keys) is written in ERTS hash order and OTP 26+
+        # orders a flatmap's atom keys by atom index: not restated
+        if len(t) > 32:
+            raise ErlangCrash('map of more than 32 pairs: ETF order not restated (ERTS hash order)')
+        if ETF_ATOMS == 'utf8' and sum(1 for k in t if isinstance(k, str)) > 1:
+            raise ErlangCrash('OTP 26+ map with several atom keys: ETF order not restated (atom index)')
         items = _map_items(t)
         return b't' + len(items).to_bytes(4, 'big') + b''.join(_ext(k) + _ext(v) for k, v in items)
     raise ErlangCrash('term outside the restated domain: %r' % (t,))

@@ -330,20 +330,6 @@ __global__ void k_mark_from_segments(DevTree t, const uint8_t *segflag, uint8_t 
     }
 }
 
-// Reachability for verify/5 (synctree.erl:560-571): node (l,b) is visited iff
-// every entry on its path from level 2 down is present; (1,0) always is.
-__global__ void k_mark_reachable(DevTree t, uint32_t maxd, uint8_t *mark) {
-    const uint64_t lo = t.base[1], hi = t.base[maxd + 1];
-    for (uint64_t slot = lo + gtid(); slot < hi; slot += gstride()) {
-        uint32_t l = 1;
-        while (t.base[l + 1] <= slot) l++;
-        const uint64_t b = slot - t.base[l];
-        bool r = true;
-        for (uint32_t q = 2; q <= l && r; q++) r = (t.tag[t.base[q] + (b >> (t.shift * (l - q)))] & TAG_PRESENT) != 0;
-        mark[slot] = r ? 1 : 0;
-    }
-}
-
 // First failing level on each target's root->target path (0 = verified).
 __global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, const uint64_t *targets,
                               uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus) {
@@ -993,8 +979,8 @@ __global__ void k_lookup(DevTree t, BatchView bv, const uint32_t *seg, uint64_t 
 // its entries differ.  k_cmp_walk evaluates it per node, verifies every
 // visited node on both sides against its parent's entry (exchange_get's
 // verified_hashes, synctree.erl:288-298) and merge-joins every visited
-// segment pair (exchange_final); k_cmp_gather concatenates the per-wave
-// record regions.  Only the entries under visited nodes beyond level H are
+// segment pair (exchange_final); each wave then writes its records after those
+// of the waves above it.  Only the entries under visited nodes beyond level H are
 // read.  err: min over (level, bucket, side) of a failed verification -- the
 // reference's first crash in visiting order (local before remote).
 
@@ -1023,6 +1009,45 @@ __device__ __forceinline__ bool verify_segment(const DevTree &t, uint64_t s) {
     stmd5::md5_global_pf(t.vheap + v0, t.seg_vend[s] - v0, d);
     const uint4 e = t.md5[eslot];
     return (et == TAG_PRESENT) && e.x == d[0] && e.y == d[1] && e.z == d[2] && e.w == d[3];
+}
+
+// verify/1 and verify_upper/1 (synctree.erl:549-571) in one launch: the
+// top-down walk checks node (l, b) iff every entry on its path below the top
+// (levels 2..l, its own included) is present -- a node whose parent entry
+// is absent is never fetched -- and the answer is false iff a checked
+// node's hash differs from its parent's entry.  A lane per slot of levels
+// 1..lmax, then (segs) a lane per segment; reachability from the ancestors'
+// tags inline (no mark pass, no memsets); a failure sets *fail, a word of
+// host-mapped memory the host zeroed (system-scope OR, no copy back).
+__device__ __forceinline__ bool path_present(const DevTree &t, uint32_t l, uint64_t b) {
+    uint32_t all = TAG_PRESENT;   // the ancestors' tags eight at a time (one round trip, not one per level)
+    for (uint32_t q0 = 2; q0 <= l; q0 += 8) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++)
+            if (q0 + k <= l) all &= t.tag[t.base[q0 + k] + (b >> (t.shift * (l - q0 - k)))];
+    }
+    return (all & TAG_PRESENT) != 0;
+}
+__global__ void k_verify_tree(DevTree t, uint32_t lmax, int segs, uint32_t *fail) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(t.W);
+    const uint64_t lo = t.base[1], nin = t.base[lmax + 1] - lo;
+    const uint64_t n = nin + (segs ? t.S : 0);
+    bool bad = false;
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        if (i < nin) {
+            const uint64_t slot = lo + i;
+            uint32_t l = 1;
+            while (t.base[l + 1] <= slot) l++;
+            const uint64_t b = slot - t.base[l];
+            if (path_present(t, l, b)) bad |= !verify_inner_node(t, l, b, reg);
+        } else {
+            const uint64_t s = i - nin;
+            if (path_present(t, t.H + 1, s)) bad |= !verify_segment(t, s);
+        }
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == __ffsll((long long)__ballot(bad)) - 1)
+        __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint64_t err_code(uint32_t level, uint64_t bucket, uint32_t side) {
@@ -1386,6 +1411,158 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
     return __shfl(c, 0, 64);
 }
 
+// The merge-joins of several listed segment pairs at once (lanes 0..G-1 hold
+// pair g's segment and bounds): the key and value offsets of every pair in
+// ONE memory round trip, their key and value bytes in one more, then each
+// pair's merge-join from LDS in list order (lds_merge_pair).  One pair at a
+// time (seg_merge_wave) a wave holding two pairs paid four round trips, and
+// those waves set the compare's end.  Returns false (nothing written) when
+// the batch's key bytes do not fit the LDS area: the caller merges its pairs
+// one at a time.
+#define CMP_BATCH 8
+__device__ __forceinline__ uint32_t batch_find(uint32_t e, uint32_t x, uint32_t G) {   // largest g < G with e_g <= x
+    uint32_t g = 0;
+    for (uint32_t h = 1; h < G; h++) g += __shfl(e, (int)h, 64) <= x ? 1u : 0u;
+    return g;
+}
+__device__ bool cmp_merge_batch(const DevTree &A, const DevTree &B, uint32_t G, uint64_t s, const SegPair &q,
+                                int filter, uint8_t *lds, DiffRec *out, uint64_t &pos, uint64_t base, uint64_t lim,
+                                uint64_t &bytes) {
+    const uint32_t lane = threadIdx.x & 63;
+    const bool in = lane < G;
+    const uint32_t nA = in ? (uint32_t)(q.a1 - q.a0) : 0, nB = in ? (uint32_t)(q.b1 - q.b0) : 0;
+    const uint32_t vA = in ? (uint32_t)(q.va1 - q.va0) : 0, vB = in ? (uint32_t)(q.vb1 - q.vb0) : 0;
+    const uint32_t eA = wave_excl_scan(in ? nA + 1 : 0), eB = wave_excl_scan(in ? nB + 1 : 0);
+    const uint32_t TA = __shfl(eA + (in ? nA + 1 : 0), 63, 64), TB = __shfl(eB + (in ? nB + 1 : 0), 63, 64);
+    const uint32_t vAo = wave_excl_scan((vA + 3) & ~3u), vBo = wave_excl_scan((vB + 3) & ~3u);
+    const bool vl = __shfl(vAo + ((vA + 3) & ~3u), 63, 64) <= CMP_VB && __shfl(vBo + ((vB + 3) & ~3u), 63, 64) <= CMP_VB;
+    uint32_t *ao = reinterpret_cast<uint32_t *>(lds);
+    uint32_t *bo = ao + CMP_CAP + 1;
+    uint32_t *avo = bo + CMP_CAP + 1;
+    uint32_t *bvo = avo + CMP_CAP + 1;
+    uint32_t *ur = bvo + CMP_CAP + 1;
+    uint8_t *ak = reinterpret_cast<uint8_t *>(ur + 2 * CMP_CAP);
+    uint8_t *bk = ak + CMP_KB;
+    uint8_t *av = bk + CMP_KB;
+    uint8_t *bv = av + CMP_VB;
+    uint4 *pa = reinterpret_cast<uint4 *>(bv + CMP_VB);
+    uint4 *pb = pa + CMP_CAP;
+    uint64_t *kbase = reinterpret_cast<uint64_t *>(ur);   // each pair's first key offset, 64-bit (ur is free until the merges)
+    // round trip 1: every pair's key and value offsets (both sides), all loads before the stores
+    const uint32_t T = TA > TB ? TA : TB;
+    for (uint32_t x0 = 0; x0 < T; x0 += 4 * 64) {
+        uint64_t ka[4], va[4], kb[4], vb[4];
+        uint32_t fa[4], fb[4];   // pair index + 1 when x is its first entry
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t x = x0 + 64 * u + lane;
+            ka[u] = va[u] = kb[u] = vb[u] = 0;
+            fa[u] = fb[u] = 0;
+            if (x < TA) {
+                const uint32_t g = batch_find(eA, x, G), e0 = __shfl(eA, (int)g, 64);
+                const uint64_t e = __shfl(q.a0, (int)g, 64) + (x - e0);
+                ka[u] = A.koff[e];
+                va[u] = A.voff[e] - __shfl(q.va0, (int)g, 64);
+                fa[u] = x == e0 ? g + 1 : 0;
+            }
+            if (x < TB) {
+                const uint32_t g = batch_find(eB, x, G), e0 = __shfl(eB, (int)g, 64);
+                const uint64_t e = __shfl(q.b0, (int)g, 64) + (x - e0);
+                kb[u] = B.koff[e];
+                vb[u] = B.voff[e] - __shfl(q.vb0, (int)g, 64);
+                fb[u] = x == e0 ? g + 1 : 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t x = x0 + 64 * u + lane;
+            if (x < TA) { ao[x] = (uint32_t)ka[u]; avo[x] = (uint32_t)va[u]; }
+            if (x < TB) { bo[x] = (uint32_t)kb[u]; bvo[x] = (uint32_t)vb[u]; }
+            if (fa[u]) kbase[fa[u] - 1] = ka[u];
+            if (fb[u]) kbase[CMP_BATCH + fb[u] - 1] = kb[u];
+        }
+    }
+    wave_sync_lds();
+    // per pair: key base and bytes; the keys' places in LDS
+    const uint64_t kA0 = in ? kbase[lane] : 0, kB0 = in ? kbase[CMP_BATCH + lane] : 0;
+    const uint32_t kbA = in ? ao[eA + nA] - (uint32_t)kA0 : 0, kbB = in ? bo[eB + nB] - (uint32_t)kB0 : 0;
+    const uint32_t kAo = wave_excl_scan((kbA + 3) & ~3u), kBo = wave_excl_scan((kbB + 3) & ~3u);
+    if (__shfl(kAo + ((kbA + 3) & ~3u), 63, 64) > CMP_KB || __shfl(kBo + ((kbB + 3) & ~3u), 63, 64) > CMP_KB) {
+        wave_sync_lds();
+        return false;
+    }
+    for (uint32_t x = lane; x < T; x += 64) {   // key offsets relative to the pair's first key
+        if (x < TA) ao[x] -= (uint32_t)__shfl(kA0, (int)batch_find(eA, x, G), 64);
+        if (x < TB) bo[x] -= (uint32_t)__shfl(kB0, (int)batch_find(eB, x, G), 64);
+    }
+    // round trip 2: the key bytes and value bytes of every pair: run r = 4g + kind
+    // (keys A, keys B, values A, values B), a lane per destination dword over
+    // the runs' concatenation, every load of a chunk before its stores
+    const uint32_t NR = 4 * G;
+    const bool rin = lane < NR;
+    const uint32_t rg = rin ? lane >> 2 : 0, rk = lane & 3;
+    uint64_t rsrc = 0;
+    uint32_t rlen = 0, rdst = 0;
+    {
+        const uint64_t ka0 = __shfl(kA0, (int)rg, 64), kb0 = __shfl(kB0, (int)rg, 64);
+        const uint64_t va0 = __shfl(q.va0, (int)rg, 64), vb0 = __shfl(q.vb0, (int)rg, 64);
+        const uint32_t lka = __shfl(kbA, (int)rg, 64), lkb = __shfl(kbB, (int)rg, 64);
+        const uint32_t lva = __shfl(vA, (int)rg, 64), lvb = __shfl(vB, (int)rg, 64);
+        const uint32_t oka = __shfl(kAo, (int)rg, 64), okb = __shfl(kBo, (int)rg, 64);
+        const uint32_t ova = __shfl(vAo, (int)rg, 64), ovb = __shfl(vBo, (int)rg, 64);
+        if (rin) {
+            if (rk == 0) { rsrc = reinterpret_cast<uint64_t>(A.kheap + ka0); rlen = lka; rdst = (uint32_t)(ak - lds) + oka; }
+            if (rk == 1) { rsrc = reinterpret_cast<uint64_t>(B.kheap + kb0); rlen = lkb; rdst = (uint32_t)(bk - lds) + okb; }
+            if (rk == 2) { rsrc = reinterpret_cast<uint64_t>(A.vheap + va0); rlen = vl ? lva : 0; rdst = (uint32_t)(av - lds) + ova; }
+            if (rk == 3) { rsrc = reinterpret_cast<uint64_t>(B.vheap + vb0); rlen = vl ? lvb : 0; rdst = (uint32_t)(bv - lds) + ovb; }
+        }
+    }
+    const uint32_t rnd = (rlen + 3) >> 2;
+    const uint32_t rdp = wave_excl_scan(rnd);
+    const uint32_t D = __shfl(rdp + rnd, 63, 64);
+    for (uint32_t x0 = 0; x0 < D; x0 += 8 * 64) {
+        uint32_t v[8], d[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t x = x0 + 64 * u + lane;
+            v[u] = 0;
+            d[u] = ~0u;
+            if (x < D) {
+                uint32_t lo = 0, hi = NR;   // the run holding dword x: largest r with rdp_r <= x
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((uint32_t)__shfl(rdp, (int)mid, 64) <= x) lo = mid; else hi = mid;
+                }
+                const uint64_t src = __shfl(rsrc, (int)lo, 64);
+                const uint32_t len = __shfl(rlen, (int)lo, 64), qd = x - __shfl(rdp, (int)lo, 64);
+                const uint32_t mis = (uint32_t)(src & 3);
+                wc_gu32 *w = (wc_gu32 *)(src - mis);
+                const uint32_t a = w[qd];
+                const uint32_t b = (mis && 4 * (qd + 1) < len + mis) ? w[qd + 1] : 0u;
+                v[u] = __builtin_amdgcn_alignbyte(b, a, mis);
+                d[u] = __shfl(rdst, (int)lo, 64) + 4 * qd;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (d[u] != ~0u) *(wc_lu32 *)(lds + d[u]) = v[u];
+    }
+    wave_sync_lds();
+    for (uint32_t g = 0; g < G; g++) {
+        const uint64_t sg = __shfl(s, (int)g, 64);
+        const uint32_t na = __shfl(nA, (int)g, 64), nb = __shfl(nB, (int)g, 64);
+        const uint32_t ea = __shfl(eA, (int)g, 64), eb = __shfl(eB, (int)g, 64);
+        const uint32_t oka = __shfl(kAo, (int)g, 64), okb = __shfl(kBo, (int)g, 64);
+        const uint32_t ova = __shfl(vAo, (int)g, 64), ovb = __shfl(vBo, (int)g, 64);
+        const uint64_t a0 = __shfl(q.a0, (int)g, 64), b0 = __shfl(q.b0, (int)g, 64);
+        pos += lds_merge_pair(A, B, sg, filter, a0, b0, na, nb, ao + ea, bo + eb, avo + ea, bvo + eb, ak + oka, bk + okb,
+                              av + ova, bv + ovb, vl, ur, pa, pb, out, base + pos, lim);
+        bytes += 2 * (16 + 16 + 18) + 16 * ((uint64_t)na + nb + 2) + __shfl(vA, (int)g, 64) + __shfl(vB, (int)g, 64) +
+                 __shfl(kbA, (int)g, 64) + __shfl(kbB, (int)g, 64);
+    }
+    return true;
+}
+
 // LDS of a compare-walk wave: the shared area (lane regions for inner-node
 // staging / the merge-join), then the work list, then per-level counters
 #define CMP_LIST 256
@@ -1555,13 +1732,41 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         } else if (sg) {
             p = seg_pair(A, B, sj);
         }
-        for (uint64_t m = __ballot(sg); m; m &= m - 1) {
+        for (uint64_t m = __ballot(sg); m;) {
+            // the next pairs in list order whose entries fit the LDS area together
+            uint32_t G = 0, TA = 0, TB = 0;
+            int my = 0;
+            uint64_t mm = m;
+            while (mm && G < CMP_BATCH) {
+                const int j = __ffsll((long long)mm) - 1;
+                const uint32_t na = (uint32_t)__shfl(p.a1 - p.a0, j, 64), nb = (uint32_t)__shfl(p.b1 - p.b0, j, 64);
+                if (TA + na + 1 > CMP_CAP + 1 || TB + nb + 1 > CMP_CAP + 1) break;
+                if (lane == G) my = j;
+                TA += na + 1;
+                TB += nb + 1;
+                G++;
+                mm &= mm - 1;
+            }
+            bool done = false;
+            if (G > 1) {
+                uint64_t by = 0;
+                done = cmp_merge_batch(A, B, G, __shfl(sj, my, 64), shfl_pair(p, my), c.filter, c.shared, c.scratch, c.pos,
+                                       c.rb, c.lim, by);
+                c.bytes += by;
+                wave_sync_lds();
+            }
+            if (done) {
+                m = mm;
+                continue;
+            }
+            // one pair (alone, oversized, or a batch whose key bytes do not fit)
             const int j = __ffsll((long long)m) - 1;
             uint64_t by;
             c.pos += seg_merge_wave(A, B, __shfl(sj, j, 64), shfl_pair(p, j), c.filter, c.shared, c.scratch, c.rb + c.pos,
                                     c.lim, &by);
             c.bytes += by;
             wave_sync_lds();
+            m &= m - 1;
         }
     }
     CW_STAMP(c, 4);
@@ -1576,13 +1781,16 @@ __device__ __forceinline__ void cmp_append(uint64_t *list, uint32_t &n, bool f, 
     n += (uint32_t)__popcll(m);
 }
 
+#define ST_DERR_CMP 2u   // TreeTiles::err / tree error bit: a compare wave's count never arrived
 __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filter, uint64_t lo2, uint64_t hi2, uint32_t nw,
-                                                 uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *wcnt,
-                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *werr, uint64_t *stamps) {
+                                                 uint32_t slice, DiffRec *scratch, uint64_t R, uint64_t *look,
+                                                 uint32_t *wst, uint64_t *wbytes, uint64_t *rare, uint32_t ep, DiffRec *out,
+                                                 uint64_t cap, uint64_t *res, uint32_t *derr, uint64_t *stamps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + wave;
-    if (w >= nw) return;
+    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (gw >= nw) return;
+    const uint32_t w = nw - 1 - gw;   // the top of the grid first: a wave waits only for waves dispatched before it
     uint8_t *wl = lds + (uint64_t)wave * slice;
     const uint32_t H = A.H, L1 = H + 1, sh = A.shift, W = A.W;
     CmpWalk c;
@@ -1713,88 +1921,71 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
         const uint64_t y = __shfl_xor(em, o, 64);
         em = y < em ? y : em;
     }
-    if (lane == 0) {
-        wcnt[w] = c.pos;
-        wbytes[w] = c.bytes;
-        werr[w] = em;
-    }
+    if (lane == 0) wbytes[w] = c.bytes;
     for (uint32_t l = lane; l < ST_STATW; l += 64) wst[(uint64_t)w * ST_STATW + l] = (l >= 1 && l <= L1) ? c.cnt[l] : 0;
+
+    // The wave's records go after those of every higher wave (AccFun = Keys
+    // ++ Acc, highest segments first): each wave publishes its record count
+    // in an epoch-stamped word (one atomic store: no ordering argument between
+    // words) and sums the counts of the waves above it.  Waves are numbered
+    // from the top of the grid down (w = nw-1 is dispatched first), so a wave
+    // only waits for waves dispatched before it.  The rare cases -- records
+    // past a wave's scratch region, a failed verification -- go to two words
+    // by atomic max / min before the count is published (epoch in the high
+    // bits, so a stale word never wins).  Wave 0 holds the total and reports
+    // it to the host-mapped result block.
+    const uint64_t cnt = c.pos;
+    const uint64_t EP = (uint64_t)ep << 48;
+    if (lane == 0) {
+        if (cnt > R) (void)__hip_atomic_fetch_max(&rare[1], EP | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (em != ~0ull) {   // (level << 40) | (bucket << 1) | side: the same order as err_code
+            const uint64_t pk = ((em >> 56) << 40) | (em & ((1ull << 40) - 1));
+            (void)__hip_atomic_fetch_min(&rare[0], ((uint64_t)(0xFFFFu - ep) << 48) | pk, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_store(&look[w], EP | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t above = 0;
+    bool lost = false;
+    {
+        const uint32_t K = (nw - 1 - w + 63) / 64;   // <= 64 words per lane (nw <= 4096)
+        for (uint32_t k0 = 0; k0 < K; k0 += 16) {
+            uint32_t pend = 0;
+            for (uint32_t k = 0; k < 16 && k0 + k < K; k++)
+                if (w + 1 + (k0 + k) * 64 + lane < nw) pend |= 1u << k;
+            for (uint32_t it = 0; __ballot(pend != 0) && it < (1u << 18); it++) {
+                for (uint32_t m = pend; m; m &= m - 1) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(m);
+                    const uint64_t x = __hip_atomic_load(&look[w + 1 + (k0 + k) * 64 + lane], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    if ((x >> 48) == ep) { above += x & ((1ull << 48) - 1); pend &= ~(1u << k); }
+                }
+                if (__ballot(pend != 0)) __builtin_amdgcn_s_sleep(1);
+            }
+            lost |= pend != 0;
+        }
+        for (int o = 32; o; o >>= 1) above += __shfl_xor(above, o, 64);
+        lost = __ballot(lost) != 0;
+    }
+    if (lost) {   // a count never arrived (bounded wait): an error, not a result
+        if (derr) __hip_atomic_store(derr, ST_DERR_CMP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    // this wave's records (those its scratch region holds) to their place
+    const uint64_t own = cnt < R ? cnt : R;
+    for (uint64_t i = lane; i < own; i += 64)
+        if (above + i < cap) out[above + i] = scratch[c.rb + i];
+    if (w == 0 && lane == 0) {
+        const uint64_t nd = __hip_atomic_load(&rare[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t er = __hip_atomic_load(&rare[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        res[0] = above + cnt;
+        res[1] = (nd >> 48) == ep ? nd & ((1ull << 48) - 1) : 0;
+        res[2] = (er >> 48) == 0xFFFFu - ep ? (((er >> 40) & 0xFFu) << 56) | (er & ((1ull << 40) - 1)) : ~0ull;
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(&res[3]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
-// The waves' regions -> the record buffer (wave w after every higher wave).
-// Wave 0 also reduces the per-wave results into res (host-mapped): the
-// total, the largest per-wave count (the scratch a rerun needs when it
-// exceeds R) and the first failed verification.  A wave per region.
-__global__ void __launch_bounds__(256) k_cmp_gather(uint32_t nw, const uint64_t *wcnt, const uint64_t *werr,
-                                                   const DiffRec *scratch, uint64_t R, DiffRec *out, uint64_t cap,
-                                                   uint64_t *res) {
-    // Every workgroup scans all nw wave counts in LDS (one round trip of
-    // L2-resident loads, nw <= 256 x CMP_GK): wave w's region goes after the
-    // regions of every higher wave, at total - (inclusive prefix through w).
-    constexpr uint32_t CMP_GK = 16;
-    __shared__ uint64_t part[256];
-    __shared__ uint64_t incl[256 * CMP_GK];
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t K = (nw + 255) / 256;   // counts per thread (<= CMP_GK: nw <= 4096, checked by the host)
-    uint64_t loc[CMP_GK], sum = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < CMP_GK; i++) {
-        const uint32_t v = tid * K + i;
-        loc[i] = (i < K && v < nw) ? wcnt[v] : 0;
-        sum += loc[i];
-    }
-    part[tid] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < 256; off <<= 1) {   // inclusive scan of the per-thread sums
-        const uint64_t x = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += x;
-        __syncthreads();
-    }
-    uint64_t run = part[tid] - sum;
-#pragma unroll
-    for (uint32_t i = 0; i < CMP_GK; i++) {
-        if (i < K) { run += loc[i]; incl[tid * K + i] = run; }
-    }
-    __syncthreads();
-    const uint64_t total = part[255];
-    if (blockIdx.x == 0) {   // the largest per-wave count and the first failed verification
-        uint64_t mx = 0, em = ~0ull;
-        for (uint32_t v = tid; v < nw; v += 256) {
-            const uint64_t x = wcnt[v], y = werr[v];
-            mx = x > mx ? x : mx;
-            em = y < em ? y : em;
-        }
-        for (int o = 32; o; o >>= 1) {
-            const uint64_t x = __shfl_xor(mx, o, 64), y = __shfl_xor(em, o, 64);
-            mx = x > mx ? x : mx;
-            em = y < em ? y : em;
-        }
-        __syncthreads();
-        if (lane == 0) { part[tid >> 6] = mx; incl[tid >> 6] = em; }
-        __syncthreads();
-        if (tid == 0) {
-            for (int q = 1; q < 4; q++) {
-                mx = part[q] > mx ? part[q] : mx;
-                em = incl[q] < em ? incl[q] : em;
-            }
-            res[0] = total;
-            res[1] = mx;
-            res[2] = em;
-            __threadfence_system();
-            res[3] = 1;   // the host spins on this word
-        }
-        __syncthreads();   // (no reader of part / incl below in workgroup 0 before this)
-        return;            // workgroup 0 copies nothing: its waves' regions are copied by the last workgroup
-    }
-    // workgroups 1..: wave q copies the region of wave w = (blockIdx.x - 1) * 4 + q
-    const uint32_t w = (blockIdx.x - 1) * 4 + (tid >> 6);
-    if (w >= nw) return;
-    const uint64_t n = wcnt[w], above = total - incl[w];
-    if (n > R || above + n > cap) return;   // the host grows the buffers and runs again
-    const DiffRec *src = scratch + (uint64_t)w * R;
-    for (uint64_t k = lane; k < n; k += 64) out[above + k] = src[k];
-}
 
 // Diff records -> byte lengths of key / local value / remote value
 __global__ void k_diff_lengths(DevTree A, DevTree B, const DiffRec *r, uint64_t n, uint64_t *kl, uint64_t *al,

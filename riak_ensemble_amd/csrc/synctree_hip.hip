@@ -52,6 +52,9 @@ struct CmpWork {
     uint64_t *res = nullptr, *res_dev = nullptr;   // host-mapped: total, max per-wave count, first error
     DiffRec *rec = nullptr, *scratch = nullptr;
     uint64_t cap = 0;
+    // wcnt: the waves' epoch-stamped record counts; werr[0..1]: the epoch-
+    // stamped first error (atomic min) and largest overflowing count (max)
+    uint32_t epoch = 0;
 };
 
 struct Pending {
@@ -296,6 +299,7 @@ static int synced(st_tree *t) {
         g_err = std::string("device error 0x") + std::to_string(w) +
                 ((w & ST_DERR_MAIL) ? ": fused rehash: a window root's mailbox entry never arrived (bounded wait "
                                       "timed out); the tree's upper levels are invalid until a clean full rehash"
+                : (w & ST_DERR_CMP) ? ": compare walk: a wave's record count never arrived (bounded wait timed out)"
                                     : "");
         return ST_EDEVICE;
     }
@@ -2566,23 +2570,19 @@ extern "C" int st_verify(st_tree *t, int upper, int *ok) {
     FLUSH(t);
     const uint32_t maxd = upper ? t->H : t->H + 1;
     if (maxd == 0) { g_err = "verify_upper at Height 0 crashes in the reference"; return ST_EINVAL; }
-    DevTree d = view(t);
-    HIPCHK(hipMemsetAsync(t->flag, 0, 4, t->stream));
-    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
-    LAUNCH(t, "mark_reachable", k_mark_reachable, grid_for(t->base[maxd + 1] - 1), 256, 0, d, maxd, t->mark);
-    if (maxd == t->H + 1)
-        LAUNCH(t, "segment_verify", (k_segment_hash<MODE_VERIFY>), grid_for(t->S), 256, 0, d, (const uint8_t *)t->mark,
-               (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint8_t *)nullptr, t->flag);
+    // one launch (k_verify_tree); the answer comes back through a word of the
+    // tree's host-mapped block (zeroed here, ORed by a failing wave)
     const uint32_t lmax = maxd < t->H ? maxd : t->H;
-    if (lmax >= 1) {
-        const uint64_t nodes = t->base[lmax + 1] - t->base[1];
-        LAUNCH(t, "level_verify", (k_level_hash<MODE_VERIFY>), grid_for(nodes, inner_block(t)), inner_block(t),
-               inner_shmem(t), d, 1u, lmax, (const uint8_t *)t->mark, (const uint32_t *)nullptr,
-               (const uint32_t *)nullptr, (uint8_t *)nullptr, t->flag);
-    }
-    uint32_t f = 0;
-    CHK(d2h(t, &f, t->flag, 4));
-    *ok = f == 0;
+    volatile uint32_t *fl = t->derr + 8;
+    *fl = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (lmax >= 1)   // the inner nodes: a 64-lane block, each lane's message staged in LDS
+        LAUNCH(t, "verify_upper", k_verify_tree, grid_for(t->base[lmax + 1] - t->base[1], inner_block(t)), inner_block(t),
+               inner_shmem(t), view(t), lmax, 0, t->derr_dev + 8);
+    if (maxd == t->H + 1)   // the segments (verify/1): no LDS, full occupancy
+        LAUNCH(t, "segment_verify", k_verify_tree, grid_for(t->S), 256, 0, view(t), 0u, 1, t->derr_dev + 8);
+    CHK(tsync(t));
+    *ok = __atomic_load_n(const_cast<uint32_t *>(fl), __ATOMIC_ACQUIRE) == 0;
     return ST_OK;
 }
 
@@ -3082,11 +3082,12 @@ static int ensure_cmp_work(st_tree *t) {
     CmpWork &w = t->cw;
     if (w.wcnt) return ST_OK;
     const uint32_t per_cu = std::max<uint32_t>(1, (160 * 1024) / (CMP_WPG * cmp_slice(t)));
-    w.nw = std::min<uint32_t>((uint32_t)std::max(1, t->ncu) * per_cu * CMP_WPG, 4096);   // k_cmp_gather scans <= 4096
+    w.nw = std::min<uint32_t>((uint32_t)std::max(1, t->ncu) * per_cu * CMP_WPG, 4096);   // <= 64 count words per lane
     CHK(dalloc_t(t, &w.wcnt, w.nw));
     CHK(dalloc_t(t, &w.wbytes, w.nw));
     CHK(dalloc_t(t, &w.wst, (uint64_t)w.nw * ST_STATW));
-    CHK(dalloc_t(t, &w.werr, w.nw));
+    CHK(dalloc_t(t, &w.werr, 2));
+    w.epoch = 0;   // the first compare resets the words (epoch wrap)
     if (hipHostMalloc((void **)&w.res, 4 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         w.res = nullptr;
         g_err = "hipHostMalloc failed";
@@ -3159,9 +3160,18 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             CHK(sc.alloc(&stamps, (uint64_t)w.nw * 16));
             HIPCHK(hipMemsetAsync(stamps, 0, (uint64_t)w.nw * 128, t->stream));
         }
-        A->reads_remote = true;   // until the gather's completion word is seen
+        if (++w.epoch > 0xFFFFu || w.epoch == 1) {   // the words' epochs wrap: start them afresh
+            w.epoch = 1;
+            HIPCHK(hipMemsetAsync(w.wcnt, 0, (uint64_t)w.nw * 8, t->stream));
+            HIPCHK(hipMemsetAsync(w.werr, 0xFF, 8, t->stream));
+            HIPCHK(hipMemsetAsync(w.werr + 1, 0, 8, t->stream));
+        }
+        w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        A->reads_remote = true;   // until the walk's completion word is seen
         LAUNCH(t, "cmp_walk", k_cmp_walk, (w.nw + CMP_WPG - 1) / CMP_WPG, 64 * CMP_WPG, (size_t)CMP_WPG * slice, da, db,
-               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, stamps);
+               filter, lo2, hi2, w.nw, slice, w.scratch, w.R, w.wcnt, w.wst, w.wbytes, w.werr, w.epoch, w.rec, w.cap,
+               w.res_dev, t->derr_dev, stamps);
         if (stamp) {
             std::vector<uint64_t> h((uint64_t)w.nw * 16);
             HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
@@ -3180,12 +3190,18 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
                 fprintf(stderr, "cmp stamp %-9s n=%4zu min %7.2f med %7.2f p90 %7.2f max %7.2f us\n", nm[k], v.size(), v[0],
                         v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
+            std::vector<uint32_t> ord(w.nw);   // the slowest waves: visited segments and phase ends
+            for (uint32_t x = 0; x < w.nw; x++) ord[x] = x;
+            std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return h[a * 16 + 4] > h[b * 16 + 4]; });
+            for (uint32_t r = 0; r < 6 && r < w.nw; r++) {
+                const uint32_t x = ord[r];
+                fprintf(stderr, "cmp slow wave %4u segs %3llu verify %7.2f merge %7.2f end %7.2f us\n", x,
+                        (unsigned long long)h[x * 16 + 6], (h[x * 16 + 3] - t0) / 100.0, (h[x * 16 + 4] - t0) / 100.0,
+                        (h[x * 16 + 5] - t0) / 100.0);
+            }
         }
-        w.res[0] = w.res[1] = w.res[2] = w.res[3] = 0;
-        LAUNCH(t, "cmp_gather", k_cmp_gather, (w.nw + 3) / 4 + 1, 256, 0, w.nw, (const uint64_t *)w.wcnt,
-               (const uint64_t *)w.werr, (const DiffRec *)w.scratch, w.R, w.rec, w.cap, w.res_dev);
         CHK(wait_mapped(t, reinterpret_cast<volatile uint32_t *>(&w.res[3])));
-        A->reads_remote = false;   // the gather wrote its word last: the walk over B has completed
+        A->reads_remote = false;   // wave 0 writes it after every wave's count: every read of B has completed
         const uint64_t ntot = w.res[0], need = w.res[1], e = w.res[2];
         if (e != ~0ull) {
             *status = ST_CORRUPTED;

@@ -104,6 +104,22 @@ class Map(Mapping):
         return 'Map(%r)' % (list(self._items),)
 
 
+def _map_etf_domain(m, atoms):
+    """term_to_binary writes a map's pairs in map-key order only for a
+    flatmap (at most 32 keys) whose order ERTS derives from the keys' term
+    order: a larger map is a hashmap, written in the runtime's hash order, and
+    OTP 26+ orders the atom keys of a flatmap by atom index.  Those byte
+    strings cannot be restated here (a key's segment is md5 of them,
+    synctree.erl:251-268): pass such keys as ERTS-produced ETF bytes
+    (ST_KEY_TERM, what the NIF does) instead."""
+    if len(m) > 32:
+        raise TypeError('a map key of more than 32 pairs is written in ERTS hash order: pass its '
+                        'term_to_binary bytes (ST_KEY_TERM) instead')
+    if atoms == 'utf8' and sum(1 for k in m if isinstance(k, str)) > 1:
+        raise TypeError('OTP 26+ writes the atom keys of a map in atom-index order: pass the map key\'s '
+                        'term_to_binary bytes (ST_KEY_TERM) instead')
+
+
 def _etf(t, out, atoms):
     if isinstance(t, bool):
         raise TypeError('Python bools are not Erlang terms (use the atoms "true"/"false")')
@@ -150,6 +166,7 @@ def _etf(t, out, atoms):
             out += bytes([106])
     elif isinstance(t, Mapping):
         m = t if isinstance(t, Map) else Map(t)
+        _map_etf_domain(m, atoms)
         out += bytes([116]) + struct.pack('>I', len(m))
         for k, v in m.items():
             _etf(k, out, atoms)

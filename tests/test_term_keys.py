@@ -315,3 +315,27 @@ def test_compare_long_common_key_prefixes():
         assert [(k, v) for _, k, v in res[1]] == R.local_compare(ra, rb)
     dev.close()
     dev2.close()
+
+
+def test_map_keys_outside_the_restated_etf_are_refused(monkeypatch):
+    """ERTS writes a hashmap (> 32 pairs) in its hash order and, from OTP 26,
+    a flatmap's atom keys in atom-index order: neither byte string can be
+    restated, so such a key (whose segment is md5 of those bytes,
+    synctree.erl:251-268) is refused rather than silently put in another
+    segment than the Erlang peer's.  The NIF passes ERTS's own bytes."""
+    big = terms.Map([(i, i) for i in range(33)])
+    with pytest.raises(TypeError):
+        terms.term_to_binary(big)
+    with pytest.raises(R.ErlangCrash):
+        R.term_to_binary(big)
+    ok = terms.Map([(i, i) for i in range(32)])
+    assert terms.term_to_binary(ok) == R.term_to_binary(ok)
+    two_atoms = terms.Map([('a', 1), ('b', 2)])
+    assert terms.term_to_binary(two_atoms, atoms='latin1') == R.term_to_binary(two_atoms)
+    monkeypatch.setattr(R, 'ETF_ATOMS', 'utf8')
+    with pytest.raises(TypeError):
+        terms.term_to_binary(two_atoms, atoms='utf8')
+    with pytest.raises(R.ErlangCrash):
+        R.term_to_binary(two_atoms)
+    one_atom = terms.Map([('a', 1), (2, 2)])
+    assert terms.term_to_binary(one_atom, atoms='utf8') == R.term_to_binary(one_atom)

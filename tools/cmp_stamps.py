@@ -37,5 +37,5 @@ for _ in range(reps):
     a.compare_device(b)
 torch.cuda.synchronize()
 print('ms/compare %.4f' % ((time.perf_counter() - t0) / reps * 1e3),
-      {k: round(a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_walk', 'cmp_gather')}, flush=True)
+      {k: round(a.kernel_stats(k)[1] / reps, 4) for k in ('cmp_walk',)}, flush=True)
 print('visited', a.compare_stats())
