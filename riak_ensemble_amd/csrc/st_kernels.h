@@ -1975,6 +1975,7 @@ __global__ void __launch_bounds__(256) k_cmp_walk(DevTree A, DevTree B, int filt
     const uint64_t own = cnt < R ? cnt : R;
     for (uint64_t i = lane; i < own; i += 64)
         if (above + i < cap) out[above + i] = scratch[c.rb + i];
+    CW_STAMP(c, 11);
     if (w == 0 && lane == 0) {
         const uint64_t nd = __hip_atomic_load(&rare[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t er = __hip_atomic_load(&rare[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
