@@ -2146,7 +2146,7 @@ __global__ void k_clamp_runs(uint64_t *bseg_off, uint64_t S, uint64_t lo, uint64
 __device__ __forceinline__ uint32_t hash_bin(const DevTree &t, const uint8_t *mask, const PrefixState *ps, uint64_t s) {
     if (!mask[t.base[t.H + 1] + s]) return PERM_BINS;   // not in the list
     if (t.seg_off[s] == t.seg_end[s]) return PERM_BINS - 1;
-    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - ps[s].k;
+    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - (ps ? ps[s].k : 0);
     return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
 }
 __global__ void __launch_bounds__(256) k_hash_list_count(DevTree t, const uint8_t *mask, const PrefixState *ps,
@@ -2267,6 +2267,138 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;
         if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
+    }
+}
+
+// The MD5 of a streaming batch's segments (pages.h: every page starts 16-byte
+// aligned), a lane per segment of a list ordered by the blocks each hashes
+// (its lanes run alike-long loops), every block staged through LDS by
+// coalesced loads: at step j, load instruction q, lane l fetches the 16-byte
+// chunk (l & 3) of block j of the wave's segment 16 q + (l >> 2) -- four
+// lanes on one 64-byte block, 16 blocks per instruction, where a lane
+// reading its own segment touched 64 lines per instruction -- and each lane
+// then reads its block from its LDS row.  Block j + 1's loads are in flight
+// while block j is compressed.
+// VERIFY: the touched segments' old values from block 0 (insert/3's get_path
+// check, synctree.erl:189-209, 302-340) into ok[slot], saving the state
+// before the first block the merge changes (fpos) in ps.  Otherwise: the
+// changed segments' new values from their saved prefix states, into the
+// segment entries (rehash of the dirty path).
+#define SPAN_ROW 80   // bytes per LDS row: 64 + 16 (rows at a 20-dword stride)
+template <bool VERIFY>
+__global__ void __launch_bounds__(256) k_span_md5(DevTree t, const uint32_t *list, const uint32_t *ntot,
+                                                  const unsigned long long *fpos, PrefixState *ps, uint8_t *ok) {
+    __shared__ __attribute__((aligned(16))) uint8_t rows[4 * 64 * SPAN_ROW];
+    const uint32_t lane = threadIdx.x & 63;
+    uint8_t *R = rows + (threadIdx.x >> 6) * 64 * SPAN_ROW;
+    const uint32_t L1 = t.H + 1;
+    const uint64_t n = *ntot;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwv = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i0 = w0 * 64; i0 < n; i0 += nwv * 64) {
+        const uint64_t i = i0 + lane;
+        const bool act = i < n;
+        const uint64_t s = act ? list[i] : 0;
+        const uint64_t slot = t.base[L1] + s, eslot = L1 == 1 ? 0 : slot;
+        uint64_t v0 = 0, len = 0;
+        bool empty = true;
+        if (act) {
+            v0 = t.seg_voff[s];
+            len = t.seg_vend[s] - v0;
+            empty = t.seg_off[s] == t.seg_end[s];
+        }
+        const uint64_t nblk = (len + 8) / 64 + 1;
+        uint32_t st[4], cap[4] = {0u, 0u, 0u, 0u};
+        stmd5::init(st);
+        uint64_t k0 = 0, ck = ~0ull;
+        uint16_t et = 0;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        bool hash;
+        if (VERIFY) {
+            if (act) { et = t.tag[eslot]; e = t.md5[eslot]; }
+            hash = act && (et & TAG_PRESENT);
+            const unsigned long long f = act ? fpos[s] : ~0ull;
+            ck = f == ~0ull ? ~0ull : (uint64_t)f / 64;
+        } else {
+            hash = act && !empty;
+            if (hash && ps[s].k) {
+                const uint4 q = ps[s].st;
+                k0 = ps[s].k;
+                st[0] = q.x; st[1] = q.y; st[2] = q.z; st[3] = q.w;
+            }
+            if (act && empty) {
+                t.tag[slot] = 0;
+                if (L1 == 1) t.tag[0] = 0;
+            }
+        }
+        const uint64_t nj = hash ? nblk - k0 : 0;   // the blocks this lane hashes
+        const uint64_t base = v0 + 64 * k0;
+        const int64_t lim = hash ? (int64_t)len - 64 * (int64_t)k0 : -1;   // message bytes from base
+        uint64_t sb[4];
+        int64_t sl[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {   // the segments whose chunks this lane fetches
+            const int src = 16 * q + (int)(lane >> 2);
+            sb[q] = __shfl(base, src, 64);
+            sl[q] = __shfl(lim, src, 64);
+        }
+        uint64_t jmax = nj;
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t y = __shfl_xor(jmax, o, 64);
+            jmax = y > jmax ? y : jmax;
+        }
+        const int64_t co = 16 * (int64_t)(lane & 3);
+        uint4 g[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            g[q] = co < sl[q] ? uint4(*(const uint4 ST_GAS *)(t.vheap + sb[q] + co)) : make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t j = 0; j < jmax; j++) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                *reinterpret_cast<uint4 *>(R + (16 * q + (lane >> 2)) * SPAN_ROW + co) = g[q];
+            wave_sync_lds();
+            uint32_t m[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(R + lane * SPAN_ROW + 16 * q);
+                m[4 * q] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
+            }
+            wave_sync_lds();   // every row read before the next step's stores
+            if (j + 1 < jmax) {
+                const int64_t off = 64 * (int64_t)(j + 1) + co;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    g[q] = off < sl[q] ? uint4(*(const uint4 ST_GAS *)(t.vheap + sb[q] + off)) : make_uint4(0u, 0u, 0u, 0u);
+            }
+            if (j < nj) {
+                const uint64_t k = k0 + j;
+                if (VERIFY && k == ck) { cap[0] = st[0]; cap[1] = st[1]; cap[2] = st[2]; cap[3] = st[3]; }
+                const int64_t rem = (int64_t)len - 64 * (int64_t)k;
+                if (rem < 64) stmd5::pad_block(m, rem, k + 1 == nblk, len);
+                stmd5::compress<true>(st, m);
+            }
+        }
+        if (VERIFY) {
+            if (act) {
+                bool good;
+                PrefixState p;
+                p.k = 0;
+                p.st = make_uint4(0u, 0u, 0u, 0u);
+                if (!(et & TAG_PRESENT)) {
+                    good = empty;
+                } else {
+                    good = et == TAG_PRESENT && e.x == st[0] && e.y == st[1] && e.z == st[2] && e.w == st[3];
+                    if (ck != ~0ull && ck > 0) { p.k = ck; p.st = make_uint4(cap[0], cap[1], cap[2], cap[3]); }
+                }
+                ok[slot] = good ? 1 : 0;
+                ps[s] = p;
+            }
+        } else if (hash) {
+            const uint4 h = make_uint4(st[0], st[1], st[2], st[3]);
+            t.md5[slot] = h;
+            t.tag[slot] = TAG_PRESENT;
+            if (L1 == 1) { t.md5[0] = h; t.tag[0] = TAG_PRESENT; }
+        }
     }
 }
 

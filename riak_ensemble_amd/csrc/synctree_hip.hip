@@ -1222,6 +1222,10 @@ static int rehash_tiled(st_tree *t) {
 // nodes: W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the
 // per-level kernels above; other geometries: one k_level_hash launch per level.
 // ps: the prefix states of a streaming batch's verify (k_verify_pos) or NULL.
+// k_span_md5's grid: up to 16 four-wave blocks per CU (it loops over its list)
+static uint32_t span_grid(const st_tree *t) {
+    return (uint32_t)std::min<uint64_t>((t->S + 255) / 256, (uint64_t)std::max(1, t->ncu) * 16);
+}
 static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr) {
     if (!mask) {
         // The first full rehash after a mutation hashes straight from the
@@ -1248,8 +1252,8 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
         LAUNCH(t, "segment_hash", k_hash_list_count, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt);
         LAUNCH(t, "segment_hash", k_hash_list_scan, 1, 256, 0, cnt);
         LAUNCH(t, "segment_hash", k_hash_list_scatter, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt, list);
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)list, mask, ps,
-               (const uint32_t *)(cnt + PERM_BINS));
+        LAUNCH(t, "segment_hash", k_span_md5<false>, span_grid(t), 256, 0, d, (const uint32_t *)list,
+               (const uint32_t *)(cnt + PERM_BINS), (const unsigned long long *)nullptr, (PrefixState *)ps, (uint8_t *)nullptr);
     } else {
         CHK(ensure_perm(t));
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask,
@@ -1602,8 +1606,18 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
         LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
                (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos, bx);
-        LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
+        // the touched segments, longest first (a lane per segment), through LDS-staged coalesced loads
+        uint32_t *vcnt = nullptr, *vlist = nullptr;
+        CHK(sc.alloc(&vcnt, PERM_BINS + 1));
+        CHK(sc.alloc(&vlist, S));
+        HIPCHK(hipMemsetAsync(vcnt, 0, (PERM_BINS + 1) * 4, t->stream));
+        LAUNCH(t, "segment_verify", k_hash_list_count, grid_for(S, 256, 1024), 256, 0, d, (const uint8_t *)t->mark,
+               (const PrefixState *)nullptr, vcnt);
+        LAUNCH(t, "segment_verify", k_hash_list_scan, 1, 256, 0, vcnt);
+        LAUNCH(t, "segment_verify", k_hash_list_scatter, grid_for(S, 256, 1024), 256, 0, d, (const uint8_t *)t->mark,
+               (const PrefixState *)nullptr, vcnt, vlist);
+        LAUNCH(t, "segment_verify", k_span_md5<true>, span_grid(t), 256, 0, d, (const uint32_t *)vlist,
+               (const uint32_t *)(vcnt + PERM_BINS), (const unsigned long long *)fpos, ps, t->ok);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
