@@ -1455,22 +1455,25 @@ __device__ bool cmp_merge_batch(const DevTree &A, const DevTree &B, uint32_t G, 
         uint32_t fa[4], fb[4];   // pair index + 1 when x is its first entry
 #pragma unroll
         for (int u = 0; u < 4; u++) {
+            // every lane runs the shuffles (a bpermute from a lane outside the
+            // branch reads no value): x clamped, the loads predicated
             const uint32_t x = x0 + 64 * u + lane;
+            const uint32_t xa = x < TA ? x : TA - 1, xb = x < TB ? x : TB - 1;
+            const uint32_t ga = batch_find(eA, xa, G), ea0 = __shfl(eA, (int)ga, 64);
+            const uint64_t ea = __shfl(q.a0, (int)ga, 64) + (xa - ea0), vaa = __shfl(q.va0, (int)ga, 64);
+            const uint32_t gb = batch_find(eB, xb, G), eb0 = __shfl(eB, (int)gb, 64);
+            const uint64_t eb = __shfl(q.b0, (int)gb, 64) + (xb - eb0), vbb = __shfl(q.vb0, (int)gb, 64);
             ka[u] = va[u] = kb[u] = vb[u] = 0;
             fa[u] = fb[u] = 0;
             if (x < TA) {
-                const uint32_t g = batch_find(eA, x, G), e0 = __shfl(eA, (int)g, 64);
-                const uint64_t e = __shfl(q.a0, (int)g, 64) + (x - e0);
-                ka[u] = A.koff[e];
-                va[u] = A.voff[e] - __shfl(q.va0, (int)g, 64);
-                fa[u] = x == e0 ? g + 1 : 0;
+                ka[u] = A.koff[ea];
+                va[u] = A.voff[ea] - vaa;
+                fa[u] = x == ea0 ? ga + 1 : 0;
             }
             if (x < TB) {
-                const uint32_t g = batch_find(eB, x, G), e0 = __shfl(eB, (int)g, 64);
-                const uint64_t e = __shfl(q.b0, (int)g, 64) + (x - e0);
-                kb[u] = B.koff[e];
-                vb[u] = B.voff[e] - __shfl(q.vb0, (int)g, 64);
-                fb[u] = x == e0 ? g + 1 : 0;
+                kb[u] = B.koff[eb];
+                vb[u] = B.voff[eb] - vbb;
+                fb[u] = x == eb0 ? gb + 1 : 0;
             }
         }
 #pragma unroll
@@ -1491,9 +1494,12 @@ __device__ bool cmp_merge_batch(const DevTree &A, const DevTree &B, uint32_t G, 
         wave_sync_lds();
         return false;
     }
-    for (uint32_t x = lane; x < T; x += 64) {   // key offsets relative to the pair's first key
-        if (x < TA) ao[x] -= (uint32_t)__shfl(kA0, (int)batch_find(eA, x, G), 64);
-        if (x < TB) bo[x] -= (uint32_t)__shfl(kB0, (int)batch_find(eB, x, G), 64);
+    for (uint32_t x0 = 0; x0 < T; x0 += 64) {   // key offsets relative to the pair's first key
+        const uint32_t x = x0 + lane;
+        const uint32_t ka0 = (uint32_t)__shfl(kA0, (int)batch_find(eA, x < TA ? x : TA - 1, G), 64);
+        const uint32_t kb0 = (uint32_t)__shfl(kB0, (int)batch_find(eB, x < TB ? x : TB - 1, G), 64);
+        if (x < TA) ao[x] -= ka0;
+        if (x < TB) bo[x] -= kb0;
     }
     // round trip 2: the key bytes and value bytes of every pair: run r = 4g + kind
     // (keys A, keys B, values A, values B), a lane per destination dword over
@@ -1525,22 +1531,25 @@ __device__ bool cmp_merge_batch(const DevTree &A, const DevTree &B, uint32_t G, 
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const uint32_t x = x0 + 64 * u + lane;
+            const uint32_t xc = x < D ? x : D - 1;   // shuffles on every lane, loads predicated
+            uint32_t lo = 0, hi = NR;   // the run holding dword xc: largest r with rdp_r <= xc
+            for (uint32_t it = 0; it < 6; it++) {   // NR <= 32: at most 5 halvings, a fixed trip count
+                const uint32_t mid = (lo + hi) >> 1;
+                const uint32_t pm = (uint32_t)__shfl(rdp, (int)mid, 64);
+                if (hi - lo > 1) { if (pm <= xc) lo = mid; else hi = mid; }
+            }
+            const uint64_t src = __shfl(rsrc, (int)lo, 64);
+            const uint32_t len = __shfl(rlen, (int)lo, 64), qd = xc - __shfl(rdp, (int)lo, 64);
+            const uint32_t dd = __shfl(rdst, (int)lo, 64) + 4 * qd;
             v[u] = 0;
             d[u] = ~0u;
             if (x < D) {
-                uint32_t lo = 0, hi = NR;   // the run holding dword x: largest r with rdp_r <= x
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((uint32_t)__shfl(rdp, (int)mid, 64) <= x) lo = mid; else hi = mid;
-                }
-                const uint64_t src = __shfl(rsrc, (int)lo, 64);
-                const uint32_t len = __shfl(rlen, (int)lo, 64), qd = x - __shfl(rdp, (int)lo, 64);
                 const uint32_t mis = (uint32_t)(src & 3);
                 wc_gu32 *w = (wc_gu32 *)(src - mis);
                 const uint32_t a = w[qd];
                 const uint32_t b = (mis && 4 * (qd + 1) < len + mis) ? w[qd + 1] : 0u;
                 v[u] = __builtin_amdgcn_alignbyte(b, a, mis);
-                d[u] = __shfl(rdst, (int)lo, 64) + 4 * qd;
+                d[u] = dd;
             }
         }
 #pragma unroll
@@ -2146,7 +2155,7 @@ __global__ void k_clamp_runs(uint64_t *bseg_off, uint64_t S, uint64_t lo, uint64
 __device__ __forceinline__ uint32_t hash_bin(const DevTree &t, const uint8_t *mask, const PrefixState *ps, uint64_t s) {
     if (!mask[t.base[t.H + 1] + s]) return PERM_BINS;   // not in the list
     if (t.seg_off[s] == t.seg_end[s]) return PERM_BINS - 1;
-    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - (ps ? ps[s].k : 0);
+    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - ps[s].k;
     return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
 }
 __global__ void __launch_bounds__(256) k_hash_list_count(DevTree t, const uint8_t *mask, const PrefixState *ps,
@@ -2267,138 +2276,6 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;
         if (L1 == 1) { t.md5[0] = e; t.tag[0] = TAG_PRESENT; }
-    }
-}
-
-// The MD5 of a streaming batch's segments (pages.h: every page starts 16-byte
-// aligned), a lane per segment of a list ordered by the blocks each hashes
-// (its lanes run alike-long loops), every block staged through LDS by
-// coalesced loads: at step j, load instruction q, lane l fetches the 16-byte
-// chunk (l & 3) of block j of the wave's segment 16 q + (l >> 2) -- four
-// lanes on one 64-byte block, 16 blocks per instruction, where a lane
-// reading its own segment touched 64 lines per instruction -- and each lane
-// then reads its block from its LDS row.  Block j + 1's loads are in flight
-// while block j is compressed.
-// VERIFY: the touched segments' old values from block 0 (insert/3's get_path
-// check, synctree.erl:189-209, 302-340) into ok[slot], saving the state
-// before the first block the merge changes (fpos) in ps.  Otherwise: the
-// changed segments' new values from their saved prefix states, into the
-// segment entries (rehash of the dirty path).
-#define SPAN_ROW 80   // bytes per LDS row: 64 + 16 (rows at a 20-dword stride)
-template <bool VERIFY>
-__global__ void __launch_bounds__(256) k_span_md5(DevTree t, const uint32_t *list, const uint32_t *ntot,
-                                                  const unsigned long long *fpos, PrefixState *ps, uint8_t *ok) {
-    __shared__ __attribute__((aligned(16))) uint8_t rows[4 * 64 * SPAN_ROW];
-    const uint32_t lane = threadIdx.x & 63;
-    uint8_t *R = rows + (threadIdx.x >> 6) * 64 * SPAN_ROW;
-    const uint32_t L1 = t.H + 1;
-    const uint64_t n = *ntot;
-    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwv = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t i0 = w0 * 64; i0 < n; i0 += nwv * 64) {
-        const uint64_t i = i0 + lane;
-        const bool act = i < n;
-        const uint64_t s = act ? list[i] : 0;
-        const uint64_t slot = t.base[L1] + s, eslot = L1 == 1 ? 0 : slot;
-        uint64_t v0 = 0, len = 0;
-        bool empty = true;
-        if (act) {
-            v0 = t.seg_voff[s];
-            len = t.seg_vend[s] - v0;
-            empty = t.seg_off[s] == t.seg_end[s];
-        }
-        const uint64_t nblk = (len + 8) / 64 + 1;
-        uint32_t st[4], cap[4] = {0u, 0u, 0u, 0u};
-        stmd5::init(st);
-        uint64_t k0 = 0, ck = ~0ull;
-        uint16_t et = 0;
-        uint4 e = make_uint4(0u, 0u, 0u, 0u);
-        bool hash;
-        if (VERIFY) {
-            if (act) { et = t.tag[eslot]; e = t.md5[eslot]; }
-            hash = act && (et & TAG_PRESENT);
-            const unsigned long long f = act ? fpos[s] : ~0ull;
-            ck = f == ~0ull ? ~0ull : (uint64_t)f / 64;
-        } else {
-            hash = act && !empty;
-            if (hash && ps[s].k) {
-                const uint4 q = ps[s].st;
-                k0 = ps[s].k;
-                st[0] = q.x; st[1] = q.y; st[2] = q.z; st[3] = q.w;
-            }
-            if (act && empty) {
-                t.tag[slot] = 0;
-                if (L1 == 1) t.tag[0] = 0;
-            }
-        }
-        const uint64_t nj = hash ? nblk - k0 : 0;   // the blocks this lane hashes
-        const uint64_t base = v0 + 64 * k0;
-        const int64_t lim = hash ? (int64_t)len - 64 * (int64_t)k0 : -1;   // message bytes from base
-        uint64_t sb[4];
-        int64_t sl[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {   // the segments whose chunks this lane fetches
-            const int src = 16 * q + (int)(lane >> 2);
-            sb[q] = __shfl(base, src, 64);
-            sl[q] = __shfl(lim, src, 64);
-        }
-        uint64_t jmax = nj;
-        for (int o = 32; o; o >>= 1) {
-            const uint64_t y = __shfl_xor(jmax, o, 64);
-            jmax = y > jmax ? y : jmax;
-        }
-        const int64_t co = 16 * (int64_t)(lane & 3);
-        uint4 g[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            g[q] = co < sl[q] ? uint4(*(const uint4 ST_GAS *)(t.vheap + sb[q] + co)) : make_uint4(0u, 0u, 0u, 0u);
-        for (uint64_t j = 0; j < jmax; j++) {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                *reinterpret_cast<uint4 *>(R + (16 * q + (lane >> 2)) * SPAN_ROW + co) = g[q];
-            wave_sync_lds();
-            uint32_t m[16];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(R + lane * SPAN_ROW + 16 * q);
-                m[4 * q] = v.x; m[4 * q + 1] = v.y; m[4 * q + 2] = v.z; m[4 * q + 3] = v.w;
-            }
-            wave_sync_lds();   // every row read before the next step's stores
-            if (j + 1 < jmax) {
-                const int64_t off = 64 * (int64_t)(j + 1) + co;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    g[q] = off < sl[q] ? uint4(*(const uint4 ST_GAS *)(t.vheap + sb[q] + off)) : make_uint4(0u, 0u, 0u, 0u);
-            }
-            if (j < nj) {
-                const uint64_t k = k0 + j;
-                if (VERIFY && k == ck) { cap[0] = st[0]; cap[1] = st[1]; cap[2] = st[2]; cap[3] = st[3]; }
-                const int64_t rem = (int64_t)len - 64 * (int64_t)k;
-                if (rem < 64) stmd5::pad_block(m, rem, k + 1 == nblk, len);
-                stmd5::compress<true>(st, m);
-            }
-        }
-        if (VERIFY) {
-            if (act) {
-                bool good;
-                PrefixState p;
-                p.k = 0;
-                p.st = make_uint4(0u, 0u, 0u, 0u);
-                if (!(et & TAG_PRESENT)) {
-                    good = empty;
-                } else {
-                    good = et == TAG_PRESENT && e.x == st[0] && e.y == st[1] && e.z == st[2] && e.w == st[3];
-                    if (ck != ~0ull && ck > 0) { p.k = ck; p.st = make_uint4(cap[0], cap[1], cap[2], cap[3]); }
-                }
-                ok[slot] = good ? 1 : 0;
-                ps[s] = p;
-            }
-        } else if (hash) {
-            const uint4 h = make_uint4(st[0], st[1], st[2], st[3]);
-            t.md5[slot] = h;
-            t.tag[slot] = TAG_PRESENT;
-            if (L1 == 1) { t.md5[0] = h; t.tag[0] = TAG_PRESENT; }
-        }
     }
 }
 

@@ -1222,10 +1222,6 @@ static int rehash_tiled(st_tree *t) {
 // nodes: W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the
 // per-level kernels above; other geometries: one k_level_hash launch per level.
 // ps: the prefix states of a streaming batch's verify (k_verify_pos) or NULL.
-// k_span_md5's grid: up to 16 four-wave blocks per CU (it loops over its list)
-static uint32_t span_grid(const st_tree *t) {
-    return (uint32_t)std::min<uint64_t>((t->S + 255) / 256, (uint64_t)std::max(1, t->ncu) * 16);
-}
 static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr) {
     if (!mask) {
         // The first full rehash after a mutation hashes straight from the
@@ -1252,8 +1248,8 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
         LAUNCH(t, "segment_hash", k_hash_list_count, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt);
         LAUNCH(t, "segment_hash", k_hash_list_scan, 1, 256, 0, cnt);
         LAUNCH(t, "segment_hash", k_hash_list_scatter, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt, list);
-        LAUNCH(t, "segment_hash", k_span_md5<false>, span_grid(t), 256, 0, d, (const uint32_t *)list,
-               (const uint32_t *)(cnt + PERM_BINS), (const unsigned long long *)nullptr, (PrefixState *)ps, (uint8_t *)nullptr);
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)list, mask, ps,
+               (const uint32_t *)(cnt + PERM_BINS));
     } else {
         CHK(ensure_perm(t));
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask,
@@ -1585,9 +1581,10 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n));
-    HIPCHK(hipMemsetAsync(bs, 0, (n + 1) * sizeof(BatchSums), t->stream));
+    // (no memsets of the per-record sums or the segments' deltas: every
+    // reader reads only what k_merge_keys / k_run_sums wrote -- records inside
+    // a run, deltas of a dirty segment)
     HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PlanSums), t->stream));
-    HIPCHK(hipMemsetAsync(ss, 0, S * sizeof(SegSums), t->stream));
     HIPCHK(hipMemsetAsync(dirty, 0, S, t->stream));
     HIPCHK(hipMemsetAsync(fpos, 0xFF, S * 8, t->stream));
     // merge positions (a lane per record, the segments' size deltas by
@@ -1606,18 +1603,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
         LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
                (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos, bx);
-        // the touched segments, longest first (a lane per segment), through LDS-staged coalesced loads
-        uint32_t *vcnt = nullptr, *vlist = nullptr;
-        CHK(sc.alloc(&vcnt, PERM_BINS + 1));
-        CHK(sc.alloc(&vlist, S));
-        HIPCHK(hipMemsetAsync(vcnt, 0, (PERM_BINS + 1) * 4, t->stream));
-        LAUNCH(t, "segment_verify", k_hash_list_count, grid_for(S, 256, 1024), 256, 0, d, (const uint8_t *)t->mark,
-               (const PrefixState *)nullptr, vcnt);
-        LAUNCH(t, "segment_verify", k_hash_list_scan, 1, 256, 0, vcnt);
-        LAUNCH(t, "segment_verify", k_hash_list_scatter, grid_for(S, 256, 1024), 256, 0, d, (const uint8_t *)t->mark,
-               (const PrefixState *)nullptr, vcnt, vlist);
-        LAUNCH(t, "segment_verify", k_span_md5<true>, span_grid(t), 256, 0, d, (const uint32_t *)vlist,
-               (const uint32_t *)(vcnt + PERM_BINS), (const unsigned long long *)fpos, ps, t->ok);
+        LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
+               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
