@@ -1239,13 +1239,14 @@ __device__ uint64_t lds_merge_pair(const DevTree &A, const DevTree &B, uint64_t 
                                    uint32_t nA, uint32_t nB, const uint32_t *ao, const uint32_t *bo, const uint32_t *avo,
                                    const uint32_t *bvo, const uint8_t *ak, const uint8_t *bk, const uint8_t *av,
                                    const uint8_t *bv, bool vl, uint32_t *ur, uint4 *pa, uint4 *pb, DiffRec *out,
-                                   uint64_t base, uint64_t lim) {
+                                   uint64_t base, uint64_t lim, uint64_t *stamp = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nu_max = (uint32_t)(nA + nB);
     for (uint32_t u = lane; u < nu_max; u += 64) ur[u] = 0xffffffffu;
     for (uint32_t i = lane; i < nA; i += 64) pa[i] = lds_key_prefix(ak + ao[i], ao[i + 1] - ao[i]);
     for (uint32_t j = lane; j < nB; j += 64) pb[j] = lds_key_prefix(bk + bo[j], bo[j + 1] - bo[j]);
     wave_sync_lds();
+    if (stamp && (threadIdx.x & 63) == 0) stamp[15] = __builtin_amdgcn_s_memrealtime();
     uint64_t cnt = 0;
     uint32_t mcarry = 0;
     for (uint32_t c = 0; c < nA; c += 64) {   // A side: matched-and-different or local-only
@@ -1330,8 +1331,10 @@ __device__ __forceinline__ SegPair shfl_pair(const SegPair &p, int j) {
     return q;
 }
 
+#define MS_STAMP(st, k) do { if ((st) && (threadIdx.x & 63) == 0) (st)[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t s, const SegPair &P, int filter,
-                                   uint8_t *lds, DiffRec *out, uint64_t base, uint64_t lim, uint64_t *algo_bytes) {
+                                   uint8_t *lds, DiffRec *out, uint64_t base, uint64_t lim, uint64_t *algo_bytes,
+                                   uint64_t *stamp = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t a0 = P.a0, a1 = P.a1, b0 = P.b0, b1 = P.b1;
     const uint64_t va0 = P.va0, va1 = P.va1, vb0 = P.vb0, vb1 = P.vb1;
@@ -1356,6 +1359,7 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
         for (uint64_t i = lane; i <= nA; i += 64) { ao[i] = (uint32_t)A.koff[a0 + i]; avo[i] = (uint32_t)(A.voff[a0 + i] - va0); }
         for (uint64_t i = lane; i <= nB; i += 64) { bo[i] = (uint32_t)B.koff[b0 + i]; bvo[i] = (uint32_t)(B.voff[b0 + i] - vb0); }
         wave_sync_lds();
+        MS_STAMP(stamp, 12);
         const uint32_t bytesA = ao[nA] - (uint32_t)ka0, bytesB = bo[nB] - (uint32_t)kb0;
         *algo_bytes += (uint64_t)bytesA + bytesB;
         const uint64_t vA = va1 - va0, vB = vb1 - vb0;
@@ -1366,8 +1370,10 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
             // one round trip: key bytes and value bytes of both sides
             wave_copy4(A.kheap + ka0, bytesA, ak, B.kheap + kb0, bytesB, bk, A.vheap + va0, vl ? (uint32_t)vA : 0u, av,
                        B.vheap + vb0, vl ? (uint32_t)vB : 0u, bv);
+            MS_STAMP(stamp, 13);
             const uint64_t cnt = lds_merge_pair(A, B, s, filter, a0, b0, (uint32_t)nA, (uint32_t)nB, ao, bo, avo, bvo, ak, bk,
-                                                av, bv, vl, ur, pa, pb, out, base, lim);
+                                                av, bv, vl, ur, pa, pb, out, base, lim, stamp);
+            MS_STAMP(stamp, 14);
             return cnt;
         }
         *algo_bytes -= (uint64_t)bytesA + bytesB;   // counted again below
@@ -1409,167 +1415,6 @@ __device__ uint64_t seg_merge_wave(const DevTree &A, const DevTree &B, uint64_t 
         }
     }
     return __shfl(c, 0, 64);
-}
-
-// The merge-joins of several listed segment pairs at once (lanes 0..G-1 hold
-// pair g's segment and bounds): the key and value offsets of every pair in
-// ONE memory round trip, their key and value bytes in one more, then each
-// pair's merge-join from LDS in list order (lds_merge_pair).  One pair at a
-// time (seg_merge_wave) a wave holding two pairs paid four round trips, and
-// those waves set the compare's end.  Returns false (nothing written) when
-// the batch's key bytes do not fit the LDS area: the caller merges its pairs
-// one at a time.
-#define CMP_BATCH 8
-__device__ __forceinline__ uint32_t batch_find(uint32_t e, uint32_t x, uint32_t G) {   // largest g < G with e_g <= x
-    uint32_t g = 0;
-    for (uint32_t h = 1; h < G; h++) g += __shfl(e, (int)h, 64) <= x ? 1u : 0u;
-    return g;
-}
-__device__ bool cmp_merge_batch(const DevTree &A, const DevTree &B, uint32_t G, uint64_t s, const SegPair &q,
-                                int filter, uint8_t *lds, DiffRec *out, uint64_t &pos, uint64_t base, uint64_t lim,
-                                uint64_t &bytes) {
-    const uint32_t lane = threadIdx.x & 63;
-    const bool in = lane < G;
-    const uint32_t nA = in ? (uint32_t)(q.a1 - q.a0) : 0, nB = in ? (uint32_t)(q.b1 - q.b0) : 0;
-    const uint32_t vA = in ? (uint32_t)(q.va1 - q.va0) : 0, vB = in ? (uint32_t)(q.vb1 - q.vb0) : 0;
-    const uint32_t eA = wave_excl_scan(in ? nA + 1 : 0), eB = wave_excl_scan(in ? nB + 1 : 0);
-    const uint32_t TA = __shfl(eA + (in ? nA + 1 : 0), 63, 64), TB = __shfl(eB + (in ? nB + 1 : 0), 63, 64);
-    const uint32_t vAo = wave_excl_scan((vA + 3) & ~3u), vBo = wave_excl_scan((vB + 3) & ~3u);
-    const bool vl = __shfl(vAo + ((vA + 3) & ~3u), 63, 64) <= CMP_VB && __shfl(vBo + ((vB + 3) & ~3u), 63, 64) <= CMP_VB;
-    uint32_t *ao = reinterpret_cast<uint32_t *>(lds);
-    uint32_t *bo = ao + CMP_CAP + 1;
-    uint32_t *avo = bo + CMP_CAP + 1;
-    uint32_t *bvo = avo + CMP_CAP + 1;
-    uint32_t *ur = bvo + CMP_CAP + 1;
-    uint8_t *ak = reinterpret_cast<uint8_t *>(ur + 2 * CMP_CAP);
-    uint8_t *bk = ak + CMP_KB;
-    uint8_t *av = bk + CMP_KB;
-    uint8_t *bv = av + CMP_VB;
-    uint4 *pa = reinterpret_cast<uint4 *>(bv + CMP_VB);
-    uint4 *pb = pa + CMP_CAP;
-    uint64_t *kbase = reinterpret_cast<uint64_t *>(ur);   // each pair's first key offset, 64-bit (ur is free until the merges)
-    // round trip 1: every pair's key and value offsets (both sides), all loads before the stores
-    const uint32_t T = TA > TB ? TA : TB;
-    for (uint32_t x0 = 0; x0 < T; x0 += 4 * 64) {
-        uint64_t ka[4], va[4], kb[4], vb[4];
-        uint32_t fa[4], fb[4];   // pair index + 1 when x is its first entry
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            // every lane runs the shuffles (a bpermute from a lane outside the
-            // branch reads no value): x clamped, the loads predicated
-            const uint32_t x = x0 + 64 * u + lane;
-            const uint32_t xa = x < TA ? x : TA - 1, xb = x < TB ? x : TB - 1;
-            const uint32_t ga = batch_find(eA, xa, G), ea0 = __shfl(eA, (int)ga, 64);
-            const uint64_t ea = __shfl(q.a0, (int)ga, 64) + (xa - ea0), vaa = __shfl(q.va0, (int)ga, 64);
-            const uint32_t gb = batch_find(eB, xb, G), eb0 = __shfl(eB, (int)gb, 64);
-            const uint64_t eb = __shfl(q.b0, (int)gb, 64) + (xb - eb0), vbb = __shfl(q.vb0, (int)gb, 64);
-            ka[u] = va[u] = kb[u] = vb[u] = 0;
-            fa[u] = fb[u] = 0;
-            if (x < TA) {
-                ka[u] = A.koff[ea];
-                va[u] = A.voff[ea] - vaa;
-                fa[u] = x == ea0 ? ga + 1 : 0;
-            }
-            if (x < TB) {
-                kb[u] = B.koff[eb];
-                vb[u] = B.voff[eb] - vbb;
-                fb[u] = x == eb0 ? gb + 1 : 0;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t x = x0 + 64 * u + lane;
-            if (x < TA) { ao[x] = (uint32_t)ka[u]; avo[x] = (uint32_t)va[u]; }
-            if (x < TB) { bo[x] = (uint32_t)kb[u]; bvo[x] = (uint32_t)vb[u]; }
-            if (fa[u]) kbase[fa[u] - 1] = ka[u];
-            if (fb[u]) kbase[CMP_BATCH + fb[u] - 1] = kb[u];
-        }
-    }
-    wave_sync_lds();
-    // per pair: key base and bytes; the keys' places in LDS
-    const uint64_t kA0 = in ? kbase[lane] : 0, kB0 = in ? kbase[CMP_BATCH + lane] : 0;
-    const uint32_t kbA = in ? ao[eA + nA] - (uint32_t)kA0 : 0, kbB = in ? bo[eB + nB] - (uint32_t)kB0 : 0;
-    const uint32_t kAo = wave_excl_scan((kbA + 3) & ~3u), kBo = wave_excl_scan((kbB + 3) & ~3u);
-    if (__shfl(kAo + ((kbA + 3) & ~3u), 63, 64) > CMP_KB || __shfl(kBo + ((kbB + 3) & ~3u), 63, 64) > CMP_KB) {
-        wave_sync_lds();
-        return false;
-    }
-    for (uint32_t x0 = 0; x0 < T; x0 += 64) {   // key offsets relative to the pair's first key
-        const uint32_t x = x0 + lane;
-        const uint32_t ka0 = (uint32_t)__shfl(kA0, (int)batch_find(eA, x < TA ? x : TA - 1, G), 64);
-        const uint32_t kb0 = (uint32_t)__shfl(kB0, (int)batch_find(eB, x < TB ? x : TB - 1, G), 64);
-        if (x < TA) ao[x] -= ka0;
-        if (x < TB) bo[x] -= kb0;
-    }
-    // round trip 2: the key bytes and value bytes of every pair: run r = 4g + kind
-    // (keys A, keys B, values A, values B), a lane per destination dword over
-    // the runs' concatenation, every load of a chunk before its stores
-    const uint32_t NR = 4 * G;
-    const bool rin = lane < NR;
-    const uint32_t rg = rin ? lane >> 2 : 0, rk = lane & 3;
-    uint64_t rsrc = 0;
-    uint32_t rlen = 0, rdst = 0;
-    {
-        const uint64_t ka0 = __shfl(kA0, (int)rg, 64), kb0 = __shfl(kB0, (int)rg, 64);
-        const uint64_t va0 = __shfl(q.va0, (int)rg, 64), vb0 = __shfl(q.vb0, (int)rg, 64);
-        const uint32_t lka = __shfl(kbA, (int)rg, 64), lkb = __shfl(kbB, (int)rg, 64);
-        const uint32_t lva = __shfl(vA, (int)rg, 64), lvb = __shfl(vB, (int)rg, 64);
-        const uint32_t oka = __shfl(kAo, (int)rg, 64), okb = __shfl(kBo, (int)rg, 64);
-        const uint32_t ova = __shfl(vAo, (int)rg, 64), ovb = __shfl(vBo, (int)rg, 64);
-        if (rin) {
-            if (rk == 0) { rsrc = reinterpret_cast<uint64_t>(A.kheap + ka0); rlen = lka; rdst = (uint32_t)(ak - lds) + oka; }
-            if (rk == 1) { rsrc = reinterpret_cast<uint64_t>(B.kheap + kb0); rlen = lkb; rdst = (uint32_t)(bk - lds) + okb; }
-            if (rk == 2) { rsrc = reinterpret_cast<uint64_t>(A.vheap + va0); rlen = vl ? lva : 0; rdst = (uint32_t)(av - lds) + ova; }
-            if (rk == 3) { rsrc = reinterpret_cast<uint64_t>(B.vheap + vb0); rlen = vl ? lvb : 0; rdst = (uint32_t)(bv - lds) + ovb; }
-        }
-    }
-    const uint32_t rnd = (rlen + 3) >> 2;
-    const uint32_t rdp = wave_excl_scan(rnd);
-    const uint32_t D = __shfl(rdp + rnd, 63, 64);
-    for (uint32_t x0 = 0; x0 < D; x0 += 8 * 64) {
-        uint32_t v[8], d[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint32_t x = x0 + 64 * u + lane;
-            const uint32_t xc = x < D ? x : D - 1;   // shuffles on every lane, loads predicated
-            uint32_t lo = 0, hi = NR;   // the run holding dword xc: largest r with rdp_r <= xc
-            for (uint32_t it = 0; it < 6; it++) {   // NR <= 32: at most 5 halvings, a fixed trip count
-                const uint32_t mid = (lo + hi) >> 1;
-                const uint32_t pm = (uint32_t)__shfl(rdp, (int)mid, 64);
-                if (hi - lo > 1) { if (pm <= xc) lo = mid; else hi = mid; }
-            }
-            const uint64_t src = __shfl(rsrc, (int)lo, 64);
-            const uint32_t len = __shfl(rlen, (int)lo, 64), qd = xc - __shfl(rdp, (int)lo, 64);
-            const uint32_t dd = __shfl(rdst, (int)lo, 64) + 4 * qd;
-            v[u] = 0;
-            d[u] = ~0u;
-            if (x < D) {
-                const uint32_t mis = (uint32_t)(src & 3);
-                wc_gu32 *w = (wc_gu32 *)(src - mis);
-                const uint32_t a = w[qd];
-                const uint32_t b = (mis && 4 * (qd + 1) < len + mis) ? w[qd + 1] : 0u;
-                v[u] = __builtin_amdgcn_alignbyte(b, a, mis);
-                d[u] = dd;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (d[u] != ~0u) *(wc_lu32 *)(lds + d[u]) = v[u];
-    }
-    wave_sync_lds();
-    for (uint32_t g = 0; g < G; g++) {
-        const uint64_t sg = __shfl(s, (int)g, 64);
-        const uint32_t na = __shfl(nA, (int)g, 64), nb = __shfl(nB, (int)g, 64);
-        const uint32_t ea = __shfl(eA, (int)g, 64), eb = __shfl(eB, (int)g, 64);
-        const uint32_t oka = __shfl(kAo, (int)g, 64), okb = __shfl(kBo, (int)g, 64);
-        const uint32_t ova = __shfl(vAo, (int)g, 64), ovb = __shfl(vBo, (int)g, 64);
-        const uint64_t a0 = __shfl(q.a0, (int)g, 64), b0 = __shfl(q.b0, (int)g, 64);
-        pos += lds_merge_pair(A, B, sg, filter, a0, b0, na, nb, ao + ea, bo + eb, avo + ea, bvo + eb, ak + oka, bk + okb,
-                              av + ova, bv + ovb, vl, ur, pa, pb, out, base + pos, lim);
-        bytes += 2 * (16 + 16 + 18) + 16 * ((uint64_t)na + nb + 2) + __shfl(vA, (int)g, 64) + __shfl(vB, (int)g, 64) +
-                 __shfl(kbA, (int)g, 64) + __shfl(kbB, (int)g, 64);
-    }
-    return true;
 }
 
 // LDS of a compare-walk wave: the shared area (lane regions for inner-node
@@ -1741,41 +1586,13 @@ __device__ __forceinline__ void cmp_flush(const DevTree &A, const DevTree &B, Cm
         } else if (sg) {
             p = seg_pair(A, B, sj);
         }
-        for (uint64_t m = __ballot(sg); m;) {
-            // the next pairs in list order whose entries fit the LDS area together
-            uint32_t G = 0, TA = 0, TB = 0;
-            int my = 0;
-            uint64_t mm = m;
-            while (mm && G < CMP_BATCH) {
-                const int j = __ffsll((long long)mm) - 1;
-                const uint32_t na = (uint32_t)__shfl(p.a1 - p.a0, j, 64), nb = (uint32_t)__shfl(p.b1 - p.b0, j, 64);
-                if (TA + na + 1 > CMP_CAP + 1 || TB + nb + 1 > CMP_CAP + 1) break;
-                if (lane == G) my = j;
-                TA += na + 1;
-                TB += nb + 1;
-                G++;
-                mm &= mm - 1;
-            }
-            bool done = false;
-            if (G > 1) {
-                uint64_t by = 0;
-                done = cmp_merge_batch(A, B, G, __shfl(sj, my, 64), shfl_pair(p, my), c.filter, c.shared, c.scratch, c.pos,
-                                       c.rb, c.lim, by);
-                c.bytes += by;
-                wave_sync_lds();
-            }
-            if (done) {
-                m = mm;
-                continue;
-            }
-            // one pair (alone, oversized, or a batch whose key bytes do not fit)
+        for (uint64_t m = __ballot(sg); m; m &= m - 1) {
             const int j = __ffsll((long long)m) - 1;
             uint64_t by;
             c.pos += seg_merge_wave(A, B, __shfl(sj, j, 64), shfl_pair(p, j), c.filter, c.shared, c.scratch, c.rb + c.pos,
-                                    c.lim, &by);
+                                    c.lim, &by, c.stamp);
             c.bytes += by;
             wave_sync_lds();
-            m &= m - 1;
         }
     }
     CW_STAMP(c, 4);

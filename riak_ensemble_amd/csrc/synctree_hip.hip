@@ -3179,9 +3179,9 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
             CHK(tsync(t));
             uint64_t t0 = ~0ull;
             for (uint32_t x = 0; x < w.nw; x++) t0 = std::min(t0, h[x * 16]);
-            static const char *nm[12] = {"start", "levels", "children", "verify", "merge", "end", "", "staged",
-                                         "flush", "inner", "values", "placed"};
-            for (int k = 0; k < 12; k++) {
+            static const char *nm[16] = {"start", "levels", "children", "verify", "merge", "end", "", "staged",
+                                         "flush", "inner", "values", "placed", "m.offs", "m.bytes", "m.merged", "m.pfx"};
+            for (int k = 0; k < 16; k++) {
                 if (k == 6) continue;
                 std::vector<double> v;
                 for (uint32_t x = 0; x < w.nw; x++)
