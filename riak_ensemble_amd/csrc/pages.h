@@ -20,6 +20,16 @@
 // ends of the last entry's key and value), entry capacity up to ecap[s]
 // (end[s] < ecap[s]), key bytes [koff[beg], koff[end]) below kcap[s], value
 // bytes [vbeg[s] = voff[beg], vend[s] = voff[end]) below vcap[s].
+//
+// UNIFORM pages: when every key record of a segment has one length L (klen)
+// and every value one length V (vlen) -- int64 keys and 17-byte ObjHash
+// values always do (riak_ensemble_peer.erl:1717-1724) -- entry i's offsets
+// are koff[beg] + L i and voff[beg] + V i, and a page keeps only its first
+// and end slots (page_uniform): a batch then moves key and value bytes, not
+// the two 8-byte offset arrays (16 of the 42 bytes an entry moves).  A batch
+// that puts a record of another length into a uniform page first writes
+// every offset of that page (k_page_materialize), and the page keeps them
+// from then on.
 #pragma once
 
 struct PageMeta {
@@ -27,6 +37,7 @@ struct PageMeta {
     uint64_t *ecap, *kcap, *vcap;        // S each: page capacities (entry slot end, key / value byte ends)
     uint16_t *klen;                      // S: the length every key record of the segment has (KLEN_MIXED: not
                                          // one length, KLEN_NONE: no entries) -- fixed-stride merge positions
+    uint16_t *vlen;                      // S: the same for its values
 };
 #define KLEN_MIXED KLEN_MIXED_   // st_kernels.h
 #define KLEN_NONE KLEN_NONE_
@@ -35,6 +46,9 @@ __device__ __forceinline__ uint32_t klen_add(uint32_t cur, uint64_t l) {
     if (l == 0 || l >= KLEN_NONE) return KLEN_MIXED;
     return cur == KLEN_NONE ? (uint32_t)l : (cur == l ? cur : KLEN_MIXED);
 }
+
+// A page whose entry offsets are implicit (only its first and end slots kept)
+__device__ __forceinline__ bool page_uniform(uint32_t kl, uint32_t vl) { return kl != KLEN_MIXED && vl != KLEN_MIXED; }
 
 typedef USum<4> PageSums;   // entries, key bytes, value bytes (+ a spare)
 typedef USum<5> PlanSums;   // k_page_plan: a moved segment's new page (entries, key bytes, value bytes), new keys,
@@ -101,7 +115,10 @@ struct PageDst {
     uint64_t *cseg_off, *cseg_voff;  // canonical destination
     uint64_t e0, k0, v0;             // bases added to the scanned offsets
 };
-__global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *base, const PageSums *sz, PageDst d) {
+// sm: the source's page metadata when the source is paged (its uniform pages
+// keep no per-entry offsets: generated here), else nullptr (a CSR).
+__global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *base, const PageSums *sz, PageDst d,
+                                                   const uint16_t *sklen, const uint16_t *svlen) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t s = w0; s < t.S; s += nw) {
@@ -109,21 +126,29 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
         const PageSums B = base[s];
         const uint64_t De = d.e0 + B.v[0], Dk = d.k0 + B.v[1], Dv = d.v0 + B.v[2];
         const uint64_t kb0 = t.koff[b], vb0 = t.voff[b];
-        const uint64_t l0 = c ? t.koff[b + 1] - kb0 : 0;
-        bool mixed = false;
+        const uint32_t SL = sklen ? sklen[s] : KLEN_MIXED, SV = svlen ? svlen[s] : KLEN_MIXED;
+        const bool gen = sklen && page_uniform(SL, SV) && c;   // a uniform source page: offsets by stride
+        const uint64_t l0 = c ? (gen ? SL : t.koff[b + 1] - kb0) : 0;
+        const uint64_t w0v = c ? (gen ? SV : t.voff[b + 1] - vb0) : 0;
+        bool mixed = false, mixedv = false;
         for (uint64_t i = lane; i <= c; i += 64) {   // offsets incl. the end slot
-            const uint64_t ko = t.koff[b + i];
+            const uint64_t ko = gen ? kb0 + SL * i : t.koff[b + i];
+            const uint64_t vo = gen ? vb0 + SV * i : t.voff[b + i];
             d.koff[De + i] = Dk + (ko - kb0);
-            d.voff[De + i] = Dv + (t.voff[b + i] - vb0);
-            if (i < c) mixed |= t.koff[b + i + 1] - ko != l0;
+            d.voff[De + i] = Dv + (vo - vb0);
+            if (i < c && !gen) {
+                mixed |= t.koff[b + i + 1] - ko != l0;
+                mixedv |= t.voff[b + i + 1] - vo != w0v;
+            }
         }
-        const bool any_mixed = __ballot(mixed) != 0;
+        const bool any_mixed = __ballot(mixed) != 0, any_mixedv = __ballot(mixedv) != 0;
         wave_copy_gg(d.kheap + Dk, t.kheap + kb0, t.koff[e] - kb0);
         wave_copy_gg(d.vheap + Dv, t.vheap + vb0, t.voff[e] - vb0);
         if (lane == 0) {
             if (d.m.beg) {
                 const PageSums Z = sz[s];
                 d.m.klen[s] = (uint16_t)(c == 0 ? KLEN_NONE : any_mixed ? KLEN_MIXED : klen_add(KLEN_NONE, l0));
+                d.m.vlen[s] = (uint16_t)(c == 0 ? KLEN_NONE : any_mixedv ? KLEN_MIXED : klen_add(KLEN_NONE, w0v));
                 d.m.beg[s] = De;
                 d.m.end[s] = De + c;
                 d.m.vbeg[s] = Dv;
@@ -172,14 +197,20 @@ __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *vo
             const bool fits = b + x.v[0] < m.ecap[s] && koff[b] + x.v[1] <= m.kcap[s] && voff[b] + x.v[2] <= m.vcap[s];
             bool grow = true;
             int64_t dk = 0, dv = 0;
-            for (uint64_t j = j0; j < je && grow; j++) {
+            const uint32_t kl0 = m.klen[s], vl0 = m.vlen[s];
+            uint32_t kl = kl0, vl = vl0;   // the merged segment's uniform lengths
+            for (uint64_t j = j0; j < je; j++) {
                 const BatchSums &f = bs[j];
                 dk += (int64_t)f.v[BS_KN] - (int64_t)f.v[BS_KE];
                 dv += (int64_t)f.v[BS_VN] - (int64_t)f.v[BS_VE];
-                grow = dk >= 0 && dv >= 0;
+                grow = grow && dk >= 0 && dv >= 0;
+                if (f.v[BS_NE]) { kl = klen_add(kl, f.v[BS_KN]); vl = klen_add(vl, f.v[BS_VN]); }
             }
             md = fits && grow ? 1 : 2;
-            if (md == 2) {
+            // offsets kept after the merge (4), and written for every entry first (8: a uniform page turning mixed)
+            const bool expl = !page_uniform(kl, vl);
+            md |= (expl ? 4 : 0) | (expl && page_uniform(kl0, vl0) && e > b ? 8 : 0);
+            if ((md & 3) == 2) {
                 const PageSums c = page_caps(x.v[0], x.v[1], x.v[2], slack_pct < 0 ? 0 : slack_pct);
                 r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
             }
@@ -188,6 +219,30 @@ __global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *vo
         }
         mode[s] = md;
         reloc[s] = r;
+    }
+}
+
+// A uniform page a batch turns mixed (k_page_plan mode bit 8): every entry's
+// offsets written from the stride before the merge moves them.  A wave per
+// such segment (rare: only a record of another length meets a uniform page).
+__global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *koff, uint64_t *voff, const uint8_t *mode,
+                                                          const uint8_t *reject, uint64_t S) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t s0 = w0 * 64; s0 < S; s0 += nw * 64) {
+        const uint64_t mine = s0 + lane;
+        uint64_t todo = __ballot(mine < S && (mode[mine] & 8) && !(reject && reject[mine]));
+        while (todo) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t s = s0 + j;
+            const uint64_t b = m.beg[s], c = m.end[s] - b;
+            const uint64_t L = m.klen[s], V = m.vlen[s], K0 = koff[b], V0 = voff[b];
+            for (uint64_t i = lane; i <= c; i += 64) {
+                koff[b + i] = K0 + L * i;
+                voff[b + i] = V0 + V * i;
+            }
+        }
     }
 }
 
@@ -433,7 +488,8 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t sb = w0 * 64; sb < a.S; sb += nw * 64) {
         const uint64_t s = sb + lane;
-        const uint8_t md = s < a.S ? p.mode[s] : 0;
+        const uint8_t mb = s < a.S ? p.mode[s] : 0, md = mb & 3;
+        const bool expl = (mb & 4) != 0;   // the merged page keeps per-entry offsets (pages.h: uniform pages do not)
         uint64_t j0 = 0, je = 0, b = 0, c = 0, Kb = 0, Vb = 0, De = 0, Dk = 0, Dv = 0, EC = 0, KC = 0, VC = 0;
         SegSums X(0);
         const BatchSums B0(0);   // the growth before the run's first record (pm_bx: run-local sums)
@@ -454,6 +510,10 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
 
         }
         uint32_t kl = (live && X.v[0]) ? p.m.klen[s] : KLEN_NONE;   // the merged segment's uniform key length
+        uint32_t vl = (live && X.v[0]) ? p.m.vlen[s] : KLEN_NONE;   // ... and value length
+        // the page as it is: uniform = entry i's offsets by stride (its slots between the first and the end are stale)
+        const uint32_t L0 = live ? p.m.klen[s] : KLEN_MIXED, V0 = live ? p.m.vlen[s] : KLEN_MIXED;
+        const bool stride = page_uniform(L0, V0);
         uint64_t hi = c, khi = live ? p.koff[b + c] : 0, vhi = live ? p.voff[b + c] : 0;   // the current piece's end
         uint64_t j = je;
         while (__ballot(live && j > j0)) {
@@ -475,13 +535,14 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                 ku = Kb + R.ku;
                 vu = Vb + R.vu;
                 if (lo < hi) {
-                    const uint64_t k0 = p.koff[b + lo], v0 = p.voff[b + lo];
+                    const uint64_t k0 = stride ? Kb + (uint64_t)L0 * lo : p.koff[b + lo];
+                    const uint64_t v0 = stride ? Vb + (uint64_t)V0 * lo : p.voff[b + lo];
                     J.kd = (uint64_t)(p.kheap + Dk + (k0 - Kb) + dk); J.ks = (uint64_t)(p.kheap + k0); J.nk = khi - k0;
                     J.vd = (uint64_t)(p.vheap + Dv + (v0 - Vb) + dv); J.vs = (uint64_t)(p.vheap + v0); J.nv = vhi - v0;
                     J.ko = (uint64_t)(p.koff + b); J.vo = (uint64_t)(p.voff + b);
                     J.a = lo; J.e = hi; J.de = (De - b) + de; J.dk = (Dk - Kb) + dk; J.dv = (Dv - Vb) + dv;
-                    J.fl = ((md == 2 || dk) ? 1u : 0u) | ((md == 2 || dv) ? 2u : 0u) | ((md == 2 || de || dk) ? 4u : 0u) |
-                           ((md == 2 || de || dv) ? 8u : 0u);
+                    J.fl = ((md == 2 || dk) ? 1u : 0u) | ((md == 2 || dv) ? 2u : 0u) |
+                           (expl && (md == 2 || de || dk) ? 4u : 0u) | (expl && (md == 2 || de || dv) ? 8u : 0u);
                     has = J.fl != 0;
                 }
             }
@@ -494,9 +555,14 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                     const uint64_t nk = Dk + (ku - Kb) + (Br.v[BS_KN] - B0.v[BS_KN]) - (Br.v[BS_KE] - B0.v[BS_KE]);
                     const uint64_t nv = Dv + (vu - Vb) + (Br.v[BS_VN] - B0.v[BS_VN]) - (Br.v[BS_VE] - B0.v[BS_VE]);
                     const RecAt Q = p.rat[r - 1];
-                    if (X.v[0]) kl = klen_add(kl, Bn.v[BS_KN] - Br.v[BS_KN]);
-                    p.koff[nwi] = nk;
-                    p.voff[nwi] = nv;
+                    if (X.v[0]) {
+                        kl = klen_add(kl, Bn.v[BS_KN] - Br.v[BS_KN]);
+                        vl = klen_add(vl, Bn.v[BS_VN] - Br.v[BS_VN]);
+                    }
+                    if (expl) {
+                        p.koff[nwi] = nk;
+                        p.voff[nwi] = nv;
+                    }
                     copy2_disjoint(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN], p.vheap + nv,
                                    a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
                 }
@@ -511,14 +577,19 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                 J.kd = (uint64_t)(p.kheap + Dk); J.ks = (uint64_t)(p.kheap + Kb); J.nk = khi - Kb;
                 J.vd = (uint64_t)(p.vheap + Dv); J.vs = (uint64_t)(p.vheap + Vb); J.nv = vhi - Vb;
                 J.ko = (uint64_t)(p.koff + b); J.vo = (uint64_t)(p.voff + b);
-                J.a = 0; J.e = hi; J.de = De - b; J.dk = Dk - Kb; J.dv = Dv - Vb; J.fl = 15;
+                J.a = 0; J.e = hi; J.de = De - b; J.dk = Dk - Kb; J.dv = Dv - Vb; J.fl = expl ? 15 : 3;
             }
             wave_run_jobs(J, has, lane);
         }
         if (live) {
             if (kl != p.m.klen[s]) p.m.klen[s] = (uint16_t)kl;
+            if (vl != p.m.vlen[s]) p.m.vlen[s] = (uint16_t)vl;
             p.koff[De + X.v[0]] = Dk + X.v[1];   // the end slot
             p.voff[De + X.v[0]] = Dv + X.v[2];
+            if (md == 2) {   // the first slot (a uniform page keeps no other)
+                p.koff[De] = Dk;
+                p.voff[De] = Dv;
+            }
             p.m.end[s] = De + X.v[0];
             p.m.vend[s] = Dv + X.v[2];
             if (md == 2) {
@@ -542,10 +613,16 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
         if (!pg_ok(chk, koff[b] <= koff[e] && koff[e] <= m.kcap[s] && m.kcap[s] <= cap_k, 21, s, koff[e], m.kcap[s])) continue;
         if (!pg_ok(chk, voff[b] <= voff[e] && voff[e] <= m.vcap[s] && m.vcap[s] <= cap_v, 22, s, voff[e], m.vcap[s])) continue;
         if (!pg_ok(chk, m.vbeg[s] == voff[b] && m.vend[s] == voff[e], 23, s, m.vbeg[s], voff[b])) continue;
-        const uint32_t L = m.klen[s];   // the uniform key length, if any, holds
-        if (!pg_ok(chk, L != KLEN_NONE || b == e, 25, s, e - b, L)) continue;
+        const uint32_t L = m.klen[s], V = m.vlen[s];   // the uniform lengths, if any, hold
+        if (!pg_ok(chk, (L != KLEN_NONE && V != KLEN_NONE) || b == e, 25, s, e - b, L)) continue;
+        if (page_uniform(L, V)) {   // offsets by stride: only the first and end slots are kept
+            const uint64_t n = e - b;
+            pg_ok(chk, b == e || (koff[e] - koff[b] == (uint64_t)L * n && voff[e] - voff[b] == (uint64_t)V * n), 26, s, L, b);
+            continue;
+        }
         bool kl_ok = true;
         for (uint64_t i = b; i < e && L != KLEN_MIXED && L != KLEN_NONE; i++) kl_ok &= koff[i + 1] - koff[i] == L;
+        for (uint64_t i = b; i < e && V != KLEN_MIXED && V != KLEN_NONE; i++) kl_ok &= voff[i + 1] - voff[i] == V;
         if (!pg_ok(chk, kl_ok, 26, s, L, b)) continue;
         for (uint64_t i = b; i < e; i++)
             if (!pg_ok(chk, koff[i] <= koff[i + 1] && voff[i] <= voff[i + 1], 24, s, i, b)) {
@@ -564,4 +641,5 @@ __global__ void k_page_clear(PageMeta m, uint64_t s, uint64_t *cnt) {
     m.end[s] = m.beg[s];
     m.vend[s] = m.vbeg[s];
     m.klen[s] = KLEN_NONE;
+    m.vlen[s] = KLEN_NONE;
 }

@@ -547,6 +547,8 @@ struct MergeArgs {
     const uint64_t *bvoff;
     const uint8_t *bvheap;
     const uint16_t *klen;       // NULL or per segment (pages.h PageMeta::klen): every key record this long
+    const uint16_t *vlen;       // NULL or per segment (PageMeta::vlen): every value this long (with klen: a uniform
+                                // page, whose per-entry offsets are by stride, pages.h)
     uint64_t S;
 };
 
@@ -625,6 +627,8 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
         const uint64_t kl = a.bv.koff[bi + 1] - a.bv.koff[bi];
         uint32_t L = (a.klen && nold) ? a.klen[s] : KLEN_MIXED_;
         if (L == KLEN_NONE_) L = KLEN_MIXED_;
+        uint32_t V = (a.vlen && nold) ? a.vlen[s] : KLEN_MIXED_;   // uniform values: offsets by stride
+        if (V == KLEN_NONE_ || L == KLEN_MIXED_) V = KLEN_MIXED_;
         uint64_t lo = 0, hi = nold, ke = 0;
         bool eq;
         if (L != KLEN_MIXED_) {   // every old key L bytes: entry i's key at k0 + L i, no offset loads
@@ -647,14 +651,14 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
         const uint64_t e = i0 + lo;
         pos[j] = (uint32_t)lo;
         if (rat)
-            rat[j] = RecAt{L != KLEN_MIXED_ ? L * lo : a.koff[e] - a.koff[i0], a.voff[e] - a.voff[i0], a.bv.koff[bi],
-                           a.bvoff[bi]};
+            rat[j] = RecAt{L != KLEN_MIXED_ ? L * lo : a.koff[e] - a.koff[i0],
+                           V != KLEN_MIXED_ ? V * lo : a.voff[e] - a.voff[i0], a.bv.koff[bi], a.bvoff[bi]};
         const bool kept = a.keep[j] != 0;
         const bool ne = kept && !(a.bop && a.bop[bi]);
         if (kept && eq) {
             f.v[BS_EQ] = 1;
             f.v[BS_KE] = ke;
-            f.v[BS_VE] = a.voff[e + 1] - a.voff[e];
+            f.v[BS_VE] = V != KLEN_MIXED_ ? V : a.voff[e + 1] - a.voff[e];
         }
         if (ne) {
             f.v[BS_NE] = 1;
@@ -669,7 +673,7 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             if (f.v[BS_VN] != f.v[BS_VE]) atomicAdd(&d[2], (unsigned long long)(f.v[BS_VN] - f.v[BS_VE]));
             if (ne && !eq) atomicAdd(&d[3], 1ull);   // a new key of the tree
             dirty[s] = 1;
-            atomicMin(&fpos[s], (unsigned long long)(a.voff[e] - a.voff[i0]));
+            atomicMin(&fpos[s], (unsigned long long)(V != KLEN_MIXED_ ? V * lo : a.voff[e] - a.voff[i0]));
         }
     }
 }

@@ -1387,6 +1387,7 @@ static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPre
     ma.bvoff = in.voff;
     ma.bvheap = in.vheap;
     ma.klen = nullptr;
+    ma.vlen = nullptr;
     ma.S = S;
     return ma;
 }
@@ -1467,7 +1468,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
 
 static void pages_free(st_tree *t, Pages &g) {
     for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.ecap, (void *)g.m.kcap,
-                    (void *)g.m.vcap, (void *)g.m.klen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
+                    (void *)g.m.vcap, (void *)g.m.klen, (void *)g.m.vlen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
     const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e, tv = g.touched_v;
     g = Pages();
@@ -1480,6 +1481,8 @@ static void pages_free(st_tree *t, Pages &g) {
 static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     const uint64_t S = t->S;
     const DevTree src = view(t);
+    // a paged source: its uniform pages keep no per-entry offsets (pages.h)
+    const uint16_t *sklen = t->pg.on ? t->pg.m.klen : nullptr, *svlen = t->pg.on ? t->pg.m.vlen : nullptr;
     Scratch sc(t);
     PageSums *sz = nullptr, *base = nullptr;
     CHK(sc.alloc(&sz, S + 1));
@@ -1498,7 +1501,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
         PageDst d{};
         d.koff = out.o.koff; d.voff = out.o.voff; d.kheap = out.o.kheap; d.vheap = out.o.vheap;
         d.cseg_off = out.o.seg_off; d.cseg_voff = out.o.seg_voff;
-        LAUNCH(t, "page_fold", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d);
+        LAUNCH(t, "page_fold", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d, sklen, svlen);
         out.install();
         t->n = tot.v[0]; t->kbytes = tot.v[1]; t->vbytes = tot.v[2];
         CHK(tsync(t));   // the pages' buffers are free once the copy has read them
@@ -1518,6 +1521,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     } undo{t, g};
     for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
     CHK(dalloc_t(t, &g.m.klen, S));
+    CHK(dalloc_t(t, &g.m.vlen, S));
     CHK(dalloc_t(t, &g.koff, g.cap_e));
     CHK(dalloc_t(t, &g.voff, g.cap_e));
     CHK(dalloc(t, (void **)&g.kheap, g.cap_k + HEAP_SLACK));
@@ -1526,7 +1530,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     HIPCHK(hipMemsetAsync(g.vheap + g.cap_v, 0, HEAP_SLACK, t->stream));
     PageDst d{};
     d.koff = g.koff; d.voff = g.voff; d.kheap = g.kheap; d.vheap = g.vheap; d.m = g.m;
-    LAUNCH(t, "page_build", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d);
+    LAUNCH(t, "page_build", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d, sklen, svlen);
     g.use_e = tot.v[0]; g.use_k = tot.v[1]; g.use_v = tot.v[2];
     g.on = true;
     g.batches = t->pg.batches; g.builds = t->pg.builds + 1; g.folds = t->pg.folds; g.reloc_e = t->pg.reloc_e;
@@ -1592,6 +1596,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // unchanged-prefix MD5 state) and the inner nodes of their paths
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
     ma.klen = t->pg.m.klen;
+    ma.vlen = t->pg.m.vlen;
     {
         const DevTree d = view(t);
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
@@ -1629,6 +1634,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         CHK(pages_build(t, t->pg_slack, want));
         ma = merge_args(view(t), in, bp, reject, S);
         ma.klen = t->pg.m.klen;
+        ma.vlen = t->pg.m.vlen;
     }
     PageMergeArgs pa;
     pa.a = ma;
@@ -1637,6 +1643,9 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = sm; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
     pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
     pa.chk = nullptr;
+    // uniform pages a record of another length turns mixed: their offsets first
+    LAUNCH(t, "page_merge", k_page_materialize, grid_for(S, 256, 4096), 256, 0, t->pg.m, t->pg.koff, t->pg.voff,
+           (const uint8_t *)mode, (const uint8_t *)reject, S);
     if (!t->pg_check) {
         LAUNCH(t, "page_merge", k_page_merge<false>, grid_for(S), 256, 0, pa);
     } else {   // checked build (debug knob): merges that would leave their pages reported, not performed

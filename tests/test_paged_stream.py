@@ -34,13 +34,14 @@ def _obj(seqs, epoch=1):
     return v
 
 
-@pytest.mark.parametrize('segments,n0,batch,slack', [
-    (1 << 16, 300_000, 4_000, 1),      # H = 4, minimal slack: moves every batch, rebuilds
-    (1 << 16, 300_000, 4_000, 25),     # the default slack
-    (1 << 20, 1_000_000, 20_000, 2),   # H = 5, the config-5 geometry at 1/100 scale
-    (4096, 500_000, 6_000, 25),        # H = 3, ~120 entries a segment: pieces of kilobytes
+@pytest.mark.parametrize('segments,n0,batch,slack,check', [
+    (1 << 16, 300_000, 4_000, 1, True),      # H = 4, minimal slack: moves every batch, rebuilds
+    (1 << 16, 300_000, 4_000, 25, True),     # the default slack
+    (1 << 20, 1_000_000, 20_000, 2, True),   # H = 5, the config-5 geometry at 1/100 scale
+    (4096, 500_000, 6_000, 25, True),        # H = 3, ~120 entries a segment: pieces of kilobytes
+    (1 << 16, 300_000, 4_000, 2, False),     # the production merge (no checked stores), rebuilds and deletes
 ])
-def test_int_keys_stream_through_pages(segments, n0, batch, slack):
+def test_int_keys_stream_through_pages(segments, n0, batch, slack, check):
     rng = np.random.default_rng(segments ^ n0 ^ slack)
     keys = workload.keys_int63(n0 + 40 * batch, workload.SEED ^ 0xDE17A)
     dev = synctree_hip.DeviceTree(16, segments)
@@ -48,7 +49,7 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack):
     assert dev.insert_int64(keys[:n0], _obj(range(n0))) == 0
     ora.bulk_load_int64(keys[:n0], _obj(range(n0)))
     dev.debug_knob(_lib.ST_DBG_PAGES, slack)
-    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)   # every page store bounds-checked, every page validated
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1 if check else 0)   # every page store bounds-checked, every page validated
     nxt = n0
     for b in range(30):
         old = rng.integers(0, nxt, batch // 2)                 # overwrites (Seq + 1), some repeated in the batch
@@ -157,6 +158,48 @@ def test_variable_keys_and_values_through_pages(slack):
     _levels(dev, ora)
     probe = ks[::97]
     assert dev.get_batch(probe) == [ora.get(k) for k in probe]
+    dev.close()
+
+
+def test_uniform_pages_turning_mixed():
+    """Int keys with 17-byte values: every page is UNIFORM (one key length,
+    one value length: only its first and end offset slots are kept, pages.h).
+    Batches that put a longer value, a shorter value or a binary key into
+    such pages turn them mixed (their offsets are written first), interleaved with
+    uniform batches; every batch against the C restatement of insert/3."""
+    rng = np.random.default_rng(2024)
+    S, n0 = 1 << 16, 300_000
+    keys = workload.keys_int63(n0 + 200_000, workload.SEED ^ 0x0FF5E7)
+    dev, ora = synctree_hip.DeviceTree(16, S), C.OTree(16, S)
+    assert dev.insert_int64(keys[:n0], _obj(range(n0))) == 0
+    ora.bulk_load_int64(keys[:n0], _obj(range(n0)))
+    dev.debug_knob(_lib.ST_DBG_PAGES, 3)
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
+    nxt = n0
+    for b in range(16):
+        if b % 4 == 3:   # a mixed batch: other value lengths, term keys, overwrites of uniform entries
+            old = [int(k) for k in keys[rng.integers(0, nxt, 200)]]
+            bk = old + [b'k-%d-%d' % (b, j) for j in range(100)] + [int(k) for k in keys[nxt:nxt + 100]]
+            nxt += 100
+            bv = [_rand_bin(rng, 0, 40) for _ in bk]
+            assert all(x is None for x in dev.insert_batch(bk, bv))
+            for k, v in zip(bk, bv):
+                ora.insert(k, v)
+        else:            # a uniform batch: int keys, 17-byte values
+            old = rng.integers(0, nxt, 2000)
+            new = np.arange(nxt, nxt + 2000)
+            nxt += 2000
+            idx = rng.permutation(np.concatenate([old, new]))
+            assert dev.insert_int64(keys[idx], _obj(idx + 7 + b, epoch=5)) == 0
+            assert ora.insert_int64_seq(keys[idx], _obj(idx + 7 + b, epoch=5)) == 0
+        assert dev.top_hash() == ora.top_hash(), 'top hash differs after batch %d' % b
+        assert dev.num_entries() == ora.num_entries(), b
+    assert dev.page_stats()[0] == 1 and dev.page_stats()[3] == 0
+    _levels(dev, ora)
+    probe = [int(k) for k in keys[rng.integers(0, nxt, 300)]]
+    assert dev.get_batch(probe) == [ora.get(k) for k in probe]   # folds the pages (offsets from the stride)
+    assert dev.verify()
+    _levels(dev, ora)
     dev.close()
 
 
