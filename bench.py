@@ -501,7 +501,7 @@ def _bench_build(synctree_hip, keys_d, vals_d, n, local, torch, reps=3):
         t.close()
     best = min(times[1:])
     return {'keys_per_s': round(n / best, 1), 'seconds': round(best, 4),
-            'what': 'st_insert_int64: key->segment MD5, radix sort, run sort, merge, gather, dirty rehash (all levels)'}
+            'what': 'st_insert_int64: key->segment MD5, counting sort by segment, run sort, merge, dirty rehash (all levels)'}
 
 
 def _compare_roofline(tree_a, ms):

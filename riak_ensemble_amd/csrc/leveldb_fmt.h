@@ -35,7 +35,8 @@
 //   k_snap_write        one lane per record: key, list header / NIL, inner
 //                       nodes' children, the {0,0} hash
 //   k_snap_entries      one lane per segment entry: {Key, Value} bytes
-// (three rocPRIM scans between them give the offsets).  Node content is read
+// (three exclusive scans between them give the offsets: the library's
+// three-launch scan, synctree_hip.hip exclusive_scan).  Node content is read
 // once and every output byte written once.
 #pragma once
 #include "st_kernels.h"

@@ -566,7 +566,7 @@ static int use_device(st_tree *t) {
 
 // Exclusive scan (reduce, scan the tile sums, scan the tiles): three plain
 // launches with no inter-workgroup communication inside a kernel (it replaced
-// rocprim's look-back scan while chasing the open issue in DESIGN.md §3.4;
+// a look-back scan while chasing the round-2 ingest defect, DESIGN.md §3.3;
 // the issue is upstream of the scan: its INPUT is seen differently).
 constexpr uint32_t SCAN_T = 256, SCAN_I = 16, SCAN_TILE = SCAN_T * SCAN_I;
 
