@@ -409,10 +409,15 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
  * into the CSR and the second builds the pages); -1 = off (every batch merges
  * into the canonical CSR; the pages are folded first). */
 #define ST_DBG_PAGES 2
-/* ST_DBG_PAGE_CHECK: value != 0 runs every paged batch through a checked
- * merge (a store outside its page is reported as ST_EDEVICE, not performed)
- * and a consistency check of every page. */
+/* ST_DBG_PAGE_CHECK: value != 0 validates every page before and after each
+ * paged batch, bounds-checks the pages the batch's positions and verify
+ * kernels read, and runs the merge checked (a store outside its page is not
+ * performed): any violation is ST_EDEVICE (the tree then refuses reads until
+ * a clean full rehash) instead of an access outside the page arrays. */
 #define ST_DBG_PAGE_CHECK 3
+/* ST_DBG_PAGE_POISON: fault injection for the checked mode: segment `value`'s
+ * page (pages on) claims entries past its capacity. */
+#define ST_DBG_PAGE_POISON 4
 int st_debug_knob(st_tree *t, int knob, int64_t value);
 
 /* The paged segment layout of streaming insert batches (no reference

@@ -633,6 +633,14 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
     }
 }
 
+// Fault injection (st_debug_knob ST_DBG_PAGE_POISON): segment s's page now
+// claims entries past its capacity -- what a merge that stored outside its
+// page would leave -- so the checked mode can be shown to refuse it.
+__global__ void k_page_poison(PageMeta m, uint64_t s) {
+    if (threadIdx.x | blockIdx.x) return;
+    m.end[s] = m.ecap[s] + 7;
+}
+
 // Empty segment s in place (a segment node deleted or stored as []): its
 // page keeps its capacity; *cnt = the entries it held.
 __global__ void k_page_clear(PageMeta m, uint64_t s, uint64_t *cnt) {

@@ -596,6 +596,19 @@ enum { BS_EQ = 0, BS_NE, BS_KE, BS_KN, BS_VE, BS_VN };
 // value offsets of the entry at its position, relative to its segment's
 // first ones (a page rebuild moves segments, not their content), and its own
 // batch offsets.
+// The checked mode of streaming batches (st_debug_knob ST_DBG_PAGE_CHECK):
+// the page arrays' capacities, and the violation record (pages.h pg_ok) the
+// kernels that read pages fill instead of indexing out of them.
+struct PageBounds {
+    uint64_t cap_e, cap_k, cap_v;
+    unsigned long long *chk;   // nullptr: unchecked
+};
+__device__ __forceinline__ bool page_bounds_ok(unsigned long long *chk, bool ok, uint32_t code, uint64_t s, uint64_t x,
+                                               uint64_t bound) {
+    if (ok || !chk) return true;
+    if (atomicAdd(&chk[0], 1ull) == 0) { chk[1] = code; chk[2] = s; chk[3] = x; chk[4] = bound; }
+    return false;
+}
 #define KLEN_MIXED_ 0        // = pages.h KLEN_MIXED (no uniform key length)
 #define KLEN_NONE_ 0xFFFFu   // = pages.h KLEN_NONE (an empty segment)
 struct RecAt {
@@ -613,14 +626,28 @@ struct RecAt {
 // atomics, dirty (zeroed) set by a kept record, fpos (all ones) = the
 // smallest value offset a kept record changes (atomicMin): the per-segment
 // sums without a pass over every segment.
+// pb.chk (checked mode): a segment whose entries or key / value bytes lie
+// outside the page arrays is reported (codes 30, 31) and not searched.
 __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint32_t *pos, BatchSums *bs, RecAt *rat,
-                             SegSums *sd = nullptr, uint8_t *dirty = nullptr, unsigned long long *fpos = nullptr) {
+                             SegSums *sd = nullptr, uint8_t *dirty = nullptr, unsigned long long *fpos = nullptr,
+                             PageBounds pb = PageBounds{0, 0, 0, nullptr}) {
     for (uint64_t j = gtid(); j < n; j += gstride()) {
         const uint64_t s = sseg[j];
         if (j < a.bseg_off[s] || j >= a.bseg_off[s + 1]) continue;
         BatchSums f(0);
         if (a.seg_reject && a.seg_reject[s]) { pos[j] = 0; bs[j] = f; continue; }
         const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;
+        if (pb.chk && a.seg_off) {
+            const uint64_t e1 = a.seg_end[s];
+            if (!page_bounds_ok(pb.chk, i0 <= e1 && e1 < pb.cap_e, 30, s, e1, pb.cap_e) ||
+                !page_bounds_ok(pb.chk, a.koff[i0] <= a.koff[e1] && a.koff[e1] <= pb.cap_k && a.voff[i0] <= a.voff[e1] &&
+                                            a.voff[e1] <= pb.cap_v, 31, s, a.koff[e1], pb.cap_k)) {
+                pos[j] = 0;
+                bs[j] = f;
+                if (rat) rat[j] = RecAt{0, 0, 0, 0};
+                continue;
+            }
+        }
         const uint64_t nold = (!a.seg_off || (a.seg_replace && a.seg_replace[s])) ? 0 : a.seg_end[s] - i0;
         const uint32_t bi = a.perm[j];
         const uint8_t *kb = a.bv.kheap + a.bv.koff[bi];
@@ -759,8 +786,11 @@ struct PrefixState {
 // order hashes a touched segment's old values, saving the state before the
 // first block its merge changes (fpos, k_merge_keys) in ps for the hash after
 // the merge.
+// pb.chk (checked mode): a segment whose value span lies outside the value
+// array is reported (code 32) and not hashed.
 __global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *perm, const uint8_t *mask, uint8_t *ok,
-                                                    const unsigned long long *fpos, PrefixState *ps) {
+                                                    const unsigned long long *fpos, PrefixState *ps,
+                                                    PageBounds pb = PageBounds{0, 0, 0, nullptr}) {
     const uint32_t L = t.H + 1;
     for (uint64_t i = gtid(); i < t.S; i += gstride()) {
         const uint64_t s = perm[i];
@@ -772,7 +802,10 @@ __global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *p
         p.k = 0;
         p.st = make_uint4(0u, 0u, 0u, 0u);
         bool good;
-        if (!(et & TAG_PRESENT)) {
+        if (!page_bounds_ok(pb.chk, t.seg_voff[s] <= t.seg_vend[s] && t.seg_vend[s] <= pb.cap_v, 32, s, t.seg_vend[s],
+                            pb.cap_v)) {
+            good = false;
+        } else if (!(et & TAG_PRESENT)) {
             good = t.seg_off[s] == t.seg_end[s];
         } else {
             uint32_t st[4], cap[4] = {0u, 0u, 0u, 0u};

@@ -859,6 +859,12 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
         t->pg_check = value != 0;
         return ST_OK;
     }
+    if (knob == ST_DBG_PAGE_POISON) {   // a page whose entries leave its capacity (the checked mode must refuse it)
+        if (!t->pg.on || value < 0 || (uint64_t)value >= t->S) { g_err = "no pages / segment out of range"; return ST_EINVAL; }
+        LAUNCH(t, "page_poison", k_page_poison, 1, 64, 0, t->pg.m, (uint64_t)value);
+        CHK(tsync(t));
+        return ST_OK;
+    }
     g_err = "unknown debug knob";
     return ST_EINVAL;
 }
@@ -1558,6 +1564,23 @@ static bool pages_eligible(const st_tree *t, const IngestIn &in) {
     return (double)in.n * own * 32.0 <= (double)t->n;
 }
 
+// The checked mode's verdict (ST_DBG_PAGE_CHECK): any violation the kernels
+// counted in chk is ST_EDEVICE, with the first one in the message, and the
+// tree refuses reads until a clean full rehash (its pages are not trusted).
+static int page_check_report(st_tree *t, const unsigned long long *chk, const char *when) {
+    unsigned long long h[32];
+    CHK(d2h(t, h, chk, 256));
+    if (!h[0]) return ST_OK;
+    g_err = std::string("page check ") + when + ": " + std::to_string(h[0]) + " violations; first code " +
+            std::to_string(h[1]) + " segment " + std::to_string(h[2]) + " at " + std::to_string(h[3]) + " bound " +
+            std::to_string(h[4]) + "; batch " + std::to_string(t->pg.batches) + "; koff";
+    for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[5 + q]);
+    g_err += "; voff";
+    for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[17 + q]);
+    t->poisoned = true;
+    return ST_EDEVICE;
+}
+
 static int ingest_paged(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
     if (!t->pg.on) CHK(pages_build(t, t->pg_slack, PageSums(0)));
@@ -1594,6 +1617,18 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // merge positions (a lane per record, the segments' size deltas by
     // atomics), then the touched segments' verify (saving each one's
     // unchanged-prefix MD5 state) and the inner nodes of their paths
+    // checked mode: every page is validated BEFORE the batch too (a page a
+    // defect left outside its capacity is refused here, ST_EDEVICE, instead of
+    // being indexed by the kernels below), and the positions and verify
+    // kernels bounds-check the pages they read
+    unsigned long long *chk = nullptr;
+    if (t->pg_check) {
+        CHK(sc.alloc(&chk, 32));
+        HIPCHK(hipMemsetAsync(chk, 0, 256, t->stream));
+        LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff,
+               (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk);
+        CHK(page_check_report(t, chk, "before the batch"));
+    }
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
     ma.klen = t->pg.m.klen;
     ma.vlen = t->pg.m.vlen;
@@ -1604,12 +1639,13 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
         // then the per-segment sums and the runs' prefix sums by each run's first lane (no atomics, no scan)
+        const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
         LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
-               (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr);
+               (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr, pb);
         LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
                (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos, bx);
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps);
+               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps, pb);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
                (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
@@ -1649,22 +1685,11 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     if (!t->pg_check) {
         LAUNCH(t, "page_merge", k_page_merge<false>, grid_for(S), 256, 0, pa);
     } else {   // checked build (debug knob): merges that would leave their pages reported, not performed
-        CHK(sc.alloc(&pa.chk, 32));
-        HIPCHK(hipMemsetAsync(pa.chk, 0, 256, t->stream));
+        pa.chk = chk;   // (the pre-batch check found nothing: zero)
         LAUNCH(t, "page_merge", k_page_merge<true>, grid_for(S), 256, 0, pa);
         LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff,
                (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, pa.chk);
-        unsigned long long h[32];
-        CHK(d2h(t, h, pa.chk, 256));
-        if (h[0]) {
-            g_err = "page check: " + std::to_string(h[0]) + " violations; first code " + std::to_string(h[1]) + " segment " +
-                    std::to_string(h[2]) + " at " + std::to_string(h[3]) + " bound " + std::to_string(h[4]) + "; batch " +
-                    std::to_string(t->pg.batches) + "; koff";
-            for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[5 + q]);
-            g_err += "; voff";
-            for (int q = 0; q < 12; q++) g_err += " " + std::to_string(h[17 + q]);
-            return ST_EDEVICE;
-        }
+        CHK(page_check_report(t, chk, "after the merge"));
     }
     t->pg.use_e += tot.v[0]; t->pg.use_k += tot.v[1]; t->pg.use_v += tot.v[2];
     t->pg.reloc_e += tot.v[0];

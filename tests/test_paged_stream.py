@@ -278,3 +278,26 @@ def test_corrupted_segment_rejects_streamed_keys(pages):
     _levels(dev, ora)
     assert dev.get_batch(bk[:50]) == [ora.get(k) for k in bk[:50]]
     dev.close()
+
+
+def test_checked_mode_refuses_a_page_outside_its_capacity():
+    """The checked mode (ST_DBG_PAGE_CHECK) against the defect class of round
+    5's paged-merge fault (a page left pointing past its capacity, then
+    indexed by the next batch's positions kernel): a poisoned page
+    (ST_DBG_PAGE_POISON) is refused before the batch reads it -- ST_EDEVICE,
+    the tree in error -- instead of an access outside the page arrays."""
+    S, n0 = 1 << 16, 200_000
+    keys = workload.keys_int63(n0 + 20_000, workload.SEED ^ 0x9015)
+    dev = synctree_hip.DeviceTree(16, S)
+    assert dev.insert_int64(keys[:n0], _obj(range(n0))) == 0
+    dev.debug_knob(_lib.ST_DBG_PAGES, 10)
+    dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
+    assert dev.insert_int64(keys[n0:n0 + 4000], _obj(range(4000))) == 0
+    assert dev.page_stats()[0] == 1
+    victim = dev.segments_of([int(keys[n0 + 5000])])[0]
+    dev.debug_knob(_lib.ST_DBG_PAGE_POISON, victim)
+    with pytest.raises(_lib.DeviceError, match='page check before the batch'):
+        dev.insert_int64(keys[n0 + 4000:n0 + 8000], _obj(range(4000)))
+    with pytest.raises(_lib.DeviceError):
+        dev.top_hash()   # the tree refuses reads after a device error
+    dev.close()
