@@ -92,6 +92,8 @@ def parse():
                     help='config-5 leg: timed write batches')
     ap.add_argument('--part-batch-keys', type=int, default=1_000_000, help='config-5 leg: keys per write batch')
     ap.add_argument('--pmc-probe', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--trace-probe', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--no-trace', action='store_true', help='skip the rocprofv3 kernel-trace pass (config-4 launch time)')
     return ap.parse_args()
 
 
@@ -104,13 +106,18 @@ def main():
         sys.exit(subprocess.call(cmd))
     if args.pmc_probe:
         return pmc_probe(args)
+    if args.trace_probe:
+        return trace_probe(args)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     pmc = None
+    trace = None
     if rank == 0 and world == 1 and not args.no_pmc:
         pmc = k1_pmc_traffic(args)          # child processes, before this one touches the GPU
+    if rank == 0 and world == 1 and not args.no_trace and not args.no_extras:
+        trace = group_kernel_trace(args)    # likewise
 
     import torch
     ndev = torch.cuda.device_count()
@@ -260,7 +267,7 @@ def main():
     del keys_d, vals_d
     if not args.no_extras:
         # configs 4 and 5 run on every rank
-        ens = _bench_ensembles(synctree_hip, dist, coll_dev, args, dev_index, torch)
+        ens = _bench_ensembles(synctree_hip, dist, coll_dev, args, dev_index, torch, trace)
         part = _bench_partition(synctree_hip, dist, coll_dev, args, dev_index, torch)
         if rank == 0:
             out['ensembles'] = ens
@@ -354,6 +361,62 @@ def k1_pmc_traffic(args):
     except (KeyError, TypeError):
         pass
     return res
+
+
+def trace_probe(args):
+    """Child of group_kernel_trace (run under rocprofv3 --kernel-trace): the
+    config-4 group (args.ensembles trees x args.ensemble_keys keys) rehashed
+    as one st_rehash_group launch, 2 warm-up + 8 traced launches."""
+    import torch
+    from riak_ensemble_amd import synctree_hip, workload
+    dev = torch.device('cuda', 0)
+    E, nk = args.ensembles, args.ensemble_keys
+    vals = _dev_values(torch.arange(nk, dtype=torch.int64, device=dev), dev, torch)
+    trees = []
+    for e in range(E):
+        k = _dev_keys(workload.SEED ^ (e + 1), 0, nk, dev, torch)
+        t = synctree_hip.DeviceTree(device=0)
+        t.insert_int64_device(k.data_ptr(), vals.data_ptr(), nk, 17)
+        trees.append(t)
+    for _ in range(10):
+        synctree_hip.rehash_group(trees)
+    for t in trees:
+        t.close()
+
+
+def group_kernel_trace(args):
+    """The config-4 group launch's duration as rocprofv3 --kernel-trace --stats
+    reports it (a child process under the profiler, before this process
+    touches the GPU): mean / min / max over the launches after the first two
+    (tile builds and warm-up).  The bench's roofline for config 4 is priced on
+    this mean, so a committed rocprof CSV reproduces it."""
+    prof = shutil.which('rocprofv3')
+    if not prof:
+        return {'error': 'rocprofv3 not found'}
+    env = dict(os.environ, TMPDIR=tempfile.gettempdir())
+    d = tempfile.mkdtemp(prefix='trace_')
+    cmd = ['timeout', '-s', 'KILL', '240', prof, '--kernel-trace', '--kernel-include-regex', 'k_rehash_fused', '-f', 'csv',
+           '-d', d, '-o', 'tr', '--', sys.executable, os.path.abspath(__file__), '--trace-probe', '--ensembles',
+           str(args.ensembles), '--ensemble-keys', str(args.ensemble_keys)]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
+    durs = []
+    import csv
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith('kernel_trace.csv'):
+                for row in csv.DictReader(open(os.path.join(root, f))):
+                    if 'k_rehash_fused' in row.get('Kernel_Name', ''):
+                        durs.append((int(row['Start_Timestamp']), int(row['End_Timestamp']) - int(row['Start_Timestamp'])))
+    shutil.rmtree(d, ignore_errors=True)
+    if r.returncode != 0 or len(durs) < 3:
+        return {'error': 'rc=%d, %d launches: %s' % (r.returncode, len(durs), r.stderr.decode()[-300:])}
+    durs.sort()
+    ms = [x[1] / 1e6 for x in durs[2:]]
+    return {'kernel_ms_mean': round(sum(ms) / len(ms), 4), 'kernel_ms_min': round(min(ms), 4),
+            'kernel_ms_max': round(max(ms), 4), 'launches': len(ms), 'pass_s': round(time.perf_counter() - t0, 1),
+            'what': 'rocprofv3 --kernel-trace of a child process: the group launch (k_rehash_fused<GROUP>) over the '
+                    'same %d x %d-key ensembles, launches 3..10' % (args.ensembles, args.ensemble_keys)}
 
 
 # ---------------------------------------------------------------- legs
@@ -751,7 +814,7 @@ def _dev_values(seq, dev, torch, epoch=1):
     return v
 
 
-def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
+def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, trace=None, reps=5):
     """Config 4 on every rank: E ensembles x nk keys per GPU (ensemble e of rank
     r seeded SEED ^ (r * E + e + 1)), rehashed as ONE st_rehash_group batch,
     then every ensemble's top hash all-gathered across the ranks (RCCL
@@ -827,7 +890,13 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
     tree_bytes = int(17 * nk + 17 * (sum(nonempty) + sum(pinner)) / len(samp))
     inner = sum(16 ** lv for lv in range(H))
     meta_bytes = 17 * nk + S * 8 + (S // 64) * 16 + S // 8 + S * 18 + inner * 18
-    g_gbs = E * tree_bytes / (g_avg / 1e3) / 1e9 if g_avg > 0 else 0.0
+    # the roofline's launch time: rocprof's mean of the group launch (a child
+    # process traced on this box) when available, else the span below
+    k_ms = trace['kernel_ms_mean'] if trace and 'kernel_ms_mean' in trace else g_avg
+    k_src = ('rocprofv3 --kernel-trace mean of the group launch (ensembles.kernel_trace)' if k_ms is not g_avg else
+             'GPU span of %d back-to-back group rehashes on trees[0]\'s stream / %d (host preparation between them '
+             'included: an upper bound of the launch)' % (reps, reps))
+    g_gbs = E * tree_bytes / (k_ms / 1e3) / 1e9 if k_ms > 0 else 0.0
     mem0 = trees[0].mem_stats()
     perkey = _bench_perkey_multi(trees, synctree_hip, torch)
     # per-tree rehash for comparison (rank-local, untimed for the headline)
@@ -845,15 +914,14 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, reps=5):
             'kernel_ms_per_batch': round(g_avg, 4), 'kernel_ms_per_batch_events': round(g_evt, 4),
             'roofline': {'bound': 'hbm', 'achieved': round(g_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(g_gbs / HBM_PEAK_GBS, 4), 'bytes_per_launch': E * tree_bytes,
+                         'kernel_ms': round(k_ms, 4), 'kernel_time_source': k_src,
                          'bytes_per_tree': tree_bytes, 'bytes_per_tree_incl_metadata': meta_bytes,
                          'tile_bytes_per_tree': mem0['tiles'],
                          'sample_nonempty_segments': nonempty, 'sample_present_inner': pinner,
                          'kernel': K1_KERNEL + '<GROUP, 8 waves per window, 6 waves per SIMD>',
                          'note': 'SURVEY §8(d): per tree 17 B of value per key + a 17-B entry per present node '
-                                 '(non-empty segments + present inner nodes, mean of %d sampled trees); kernel time '
-                                 '= GPU span of %d back-to-back group rehashes on trees[0]\'s stream / %d (host '
-                                 'preparation between them included: an upper bound of the launch)'
-                                 % (len(samp), reps, reps)},
+                                 '(non-empty segments + present inner nodes, mean of %d sampled trees)' % len(samp)},
+            'kernel_trace': trace,
             'per_tree_rehash_keys_per_s_rank0': round(nk / per_tree, 1),
             'per_key_multi': perkey,
             'what': 'config4: %d ensembles x %d keys on each of %d GPU(s) (%d total); per step: st_rehash_group of '

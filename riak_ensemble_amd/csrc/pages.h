@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t klen_add(uint32_t cur, uint64_t l) {
 __device__ __forceinline__ bool page_uniform(uint32_t kl, uint32_t vl) { return kl != KLEN_MIXED && vl != KLEN_MIXED; }
 
 typedef USum<4> PageSums;   // entries, key bytes, value bytes (+ a spare)
-typedef USum<5> PlanSums;   // k_page_plan: a moved segment's new page (entries, key bytes, value bytes), new keys,
+typedef USum<5> PlanSums;   // k_run_plan: a moved segment's new page (entries, key bytes, value bytes), new keys,
                             // the touched segment's value bytes before the merge
 
 // Page capacity for a segment of c entries, kb key bytes and vb value bytes
@@ -168,61 +168,7 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
     }
 }
 
-// Per touched segment: merge in place (1) or move to a new page (2), or
-// nothing (0: no run, a rejected run, no kept record).  In place needs room
-// in the page and every prefix of the run adding >= 0 key and value bytes
-// (no replacement that shrinks the bytes before a piece: the moves run from
-// the highest address down); otherwise the segment moves.  reloc = the new
-// page's sizes (mode 2), scanned for its place in the append region; v[3] =
-// the segment's new keys (for the tree's entry count).
-// sd: the segments' merged-size deltas (k_merge_keys); sm: the merged sizes
-// of the touched segments (written here, read by k_page_merge).
-__global__ void k_page_plan(PageMeta m, const uint64_t *koff, const uint64_t *voff, const uint64_t *bseg_off,
-                            const uint8_t *reject, const BatchSums *bs, const SegSums *sd, SegSums *sm, uint8_t *dirty,
-                            uint64_t S, int slack_pct, uint8_t *mode, PlanSums *reloc) {
-    for (uint64_t s = gtid(); s < S; s += gstride()) {
-        const uint64_t j0 = bseg_off[s], je = bseg_off[s + 1];
-        if (reject && reject[s]) dirty[s] = 0;   // positions came before the verify (k_merge_keys)
-        PlanSums r(0);
-        uint8_t md = 0;
-        if (j0 != je && !(reject && reject[s]) && dirty[s]) {
-            const uint64_t b = m.beg[s], e = m.end[s];
-            const SegSums dd = sd[s];
-            SegSums x;
-            x.v[0] = (e - b) + dd.v[0];
-            x.v[1] = (koff[e] - koff[b]) + dd.v[1];
-            x.v[2] = (voff[e] - voff[b]) + dd.v[2];
-            x.v[3] = dd.v[3];
-            sm[s] = x;
-            const bool fits = b + x.v[0] < m.ecap[s] && koff[b] + x.v[1] <= m.kcap[s] && voff[b] + x.v[2] <= m.vcap[s];
-            bool grow = true;
-            int64_t dk = 0, dv = 0;
-            const uint32_t kl0 = m.klen[s], vl0 = m.vlen[s];
-            uint32_t kl = kl0, vl = vl0;   // the merged segment's uniform lengths
-            for (uint64_t j = j0; j < je; j++) {
-                const BatchSums &f = bs[j];
-                dk += (int64_t)f.v[BS_KN] - (int64_t)f.v[BS_KE];
-                dv += (int64_t)f.v[BS_VN] - (int64_t)f.v[BS_VE];
-                grow = grow && dk >= 0 && dv >= 0;
-                if (f.v[BS_NE]) { kl = klen_add(kl, f.v[BS_KN]); vl = klen_add(vl, f.v[BS_VN]); }
-            }
-            md = fits && grow ? 1 : 2;
-            // offsets kept after the merge (4), and written for every entry first (8: a uniform page turning mixed)
-            const bool expl = !page_uniform(kl, vl);
-            md |= (expl ? 4 : 0) | (expl && page_uniform(kl0, vl0) && e > b ? 8 : 0);
-            if ((md & 3) == 2) {
-                const PageSums c = page_caps(x.v[0], x.v[1], x.v[2], slack_pct < 0 ? 0 : slack_pct);
-                r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
-            }
-            r.v[3] = x.v[3];
-            r.v[4] = voff[e] - voff[b];
-        }
-        mode[s] = md;
-        reloc[s] = r;
-    }
-}
-
-// A uniform page a batch turns mixed (k_page_plan mode bit 8): every entry's
+// A uniform page a batch turns mixed (k_run_plan mode bit 8): every entry's
 // offsets written from the stride before the merge moves them.  A wave per
 // such segment (rare: only a record of another length meets a uniform page).
 __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *koff, uint64_t *voff, const uint8_t *mode,
@@ -246,6 +192,76 @@ __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *
     }
 }
 
+// The runs' sums and the pages' plan in one pass: the lane of each run's
+// first record sums the run (its BatchSums' inclusive prefix sums into bxl
+// -- k_page_merge's growth before and through each group --, the segment's
+// size deltas, dirty, fpos = the smallest value offset a kept record
+// changes) and plans its page: merge in place (1) or move to a new page (2)
+// -- in place needs room in the page and every prefix of the run adding >=
+// 0 key and value bytes (the moves run from the highest address down) --,
+// reloc = the new page's sizes (mode 2, scanned for its place in the append
+// region), v[3] its new keys, v[4] its value bytes before the merge; mode
+// bit 4: the merged page keeps per-entry offsets (not uniform), bit 8: a
+// uniform page turning mixed (k_page_materialize first).  No pass over all S
+// segments.  Runs before
+// the verify: k_path_status drops a rejected segment's plan.  mode / reloc
+// must be zero for the segments without a run (the caller clears them).
+__global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
+                           const RecAt *rat, PageMeta m, const uint64_t *koff, const uint64_t *voff, int slack_pct,
+                           uint8_t *dirty, unsigned long long *fpos, BatchSums *bxl, SegSums *sm, uint8_t *mode,
+                           PlanSums *reloc) {
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        const uint64_t s = sseg[j];
+        if (j != bseg_off[s]) continue;
+        const uint64_t je = bseg_off[s + 1];
+        SegSums d(0);
+        BatchSums acc(0);
+        uint64_t fp = ~0ull;
+        bool grow = true;
+        int64_t dk = 0, dv = 0;
+        const uint32_t kl0 = m.klen[s], vl0 = m.vlen[s];
+        uint32_t kl = kl0, vl = vl0;
+        for (uint64_t r = j; r < je; r++) {
+            const BatchSums f = bs[r];
+            acc = acc + f;
+            bxl[r] = acc;
+            dk += (int64_t)f.v[BS_KN] - (int64_t)f.v[BS_KE];
+            dv += (int64_t)f.v[BS_VN] - (int64_t)f.v[BS_VE];
+            grow = grow && dk >= 0 && dv >= 0;
+            if (f.v[BS_NE]) { kl = klen_add(kl, f.v[BS_KN]); vl = klen_add(vl, f.v[BS_VN]); }
+            if (!f.v[BS_NE] && !f.v[BS_EQ]) continue;
+            d.v[0] += f.v[BS_NE] - f.v[BS_EQ];
+            d.v[1] += f.v[BS_KN] - f.v[BS_KE];
+            d.v[2] += f.v[BS_VN] - f.v[BS_VE];
+            d.v[3] += (f.v[BS_NE] && !f.v[BS_EQ]) ? 1 : 0;
+            fp = std::min<uint64_t>(fp, rat[r].vu);
+        }
+        if (fp == ~0ull) continue;   // no kept record: nothing to merge (mode and reloc stay 0)
+        dirty[s] = 1;
+        fpos[s] = fp;
+        const uint64_t b = m.beg[s], e = m.end[s];
+        SegSums x;
+        x.v[0] = (e - b) + d.v[0];
+        x.v[1] = (koff[e] - koff[b]) + d.v[1];
+        x.v[2] = (voff[e] - voff[b]) + d.v[2];
+        x.v[3] = d.v[3];
+        sm[s] = x;
+        const bool fits = b + x.v[0] < m.ecap[s] && koff[b] + x.v[1] <= m.kcap[s] && voff[b] + x.v[2] <= m.vcap[s];
+        uint8_t md = fits && grow ? 1 : 2;
+        const bool expl = !page_uniform(kl, vl);
+        md |= (expl ? 4 : 0) | (expl && page_uniform(kl0, vl0) && e > b ? 8 : 0);
+        PlanSums r(0);
+        if ((md & 3) == 2) {
+            const PageSums c = page_caps(x.v[0], x.v[1], x.v[2], slack_pct < 0 ? 0 : slack_pct);
+            r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
+        }
+        r.v[3] = x.v[3];
+        r.v[4] = voff[e] - voff[b];
+        mode[s] = md;
+        reloc[s] = r;
+    }
+}
+
 // The merge of one batch run into its segment's page (mode 1, in place) or
 // into a new page (mode 2): the closed form of k_merge_old / k_merge_new
 // (st_kernels.h) per segment, a lane per segment.  The run's records with
@@ -254,7 +270,7 @@ __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *
 // and shift by the running sums through the group (entries +NE-EQ, key bytes
 // +KN-KE, value bytes +VN-VE).  The groups are visited from the last to the
 // first; each piece moves highest address first (in place every shift is >=
-// 0, k_page_plan, so no source is overwritten before it is read), then the
+// 0, k_run_plan, so no source is overwritten before it is read), then the
 // group's records are written into the gap.
 struct PageMergeArgs {
     MergeArgs a;
@@ -263,7 +279,7 @@ struct PageMergeArgs {
     uint8_t *kheap, *vheap;
     const uint32_t *pos;
     const RecAt *rat;             // per record: old offsets at its position (page-relative), its batch offsets
-    const BatchSums *bx;          // per run: inclusive prefix sums of its records' BatchSums (k_run_sums)
+    const BatchSums *bx;          // per run: inclusive prefix sums of its records' BatchSums (k_run_plan)
     const SegSums *ss;            // per segment: merged count, key bytes, value bytes
     const uint8_t *mode;
     const PlanSums *rbase;        // exclusive scan of the relocation sizes

@@ -331,8 +331,13 @@ __global__ void k_mark_from_segments(DevTree t, const uint8_t *segflag, uint8_t 
 }
 
 // First failing level on each target's root->target path (0 = verified).
+// plan_mode / plan_sz / plan_dirty (a streaming batch, k_run_plan planned
+// before the verify): a rejected segment's plan is dropped -- no merge, no
+// relocation, no rehash, no new keys counted.
 __global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, const uint64_t *targets,
-                              uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus) {
+                              uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus,
+                              uint8_t *plan_mode = nullptr, void *plan_sz = nullptr, size_t plan_sz_bytes = 0,
+                              uint8_t *plan_dirty = nullptr) {
     for (uint64_t i = gtid(); i < ntargets; i += gstride()) {
         uint64_t tb;
         if (bseg_off) {
@@ -348,6 +353,12 @@ __global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, c
         }
         if (seg_reject) seg_reject[i] = (uint8_t)bad;
         if (tstatus) tstatus[i] = bad;
+        if (bad && plan_mode) {
+            plan_mode[i] = 0;
+            plan_dirty[i] = 0;
+            uint64_t *z = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(plan_sz) + i * plan_sz_bytes);
+            for (size_t q = 0; q < plan_sz_bytes / 8; q++) z[q] = 0;
+        }
     }
 }
 
@@ -701,41 +712,6 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             if (ne && !eq) atomicAdd(&d[3], 1ull);   // a new key of the tree
             dirty[s] = 1;
             atomicMin(&fpos[s], (unsigned long long)(V != KLEN_MIXED_ ? V * lo : a.voff[e] - a.voff[i0]));
-        }
-    }
-}
-
-// The streaming batch's per-segment sums without atomics (k_merge_keys run
-// with sd == nullptr): the lane of each run's first record sums its run's
-// BatchSums -- the merged-size DELTAS (entries, key bytes, value bytes, new
-// keys), dirty = a kept record (insert semantics: kept == NE), fpos = the
-// smallest value offset a kept record changes (its rat.vu) -- and writes the
-// run's INCLUSIVE prefix sums into bxl (k_page_merge's growth before and
-// through each group: no scan over the whole batch).
-__global__ void k_run_sums(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
-                           const RecAt *rat, SegSums *sd, uint8_t *dirty, unsigned long long *fpos, BatchSums *bxl) {
-    for (uint64_t j = gtid(); j < n; j += gstride()) {
-        const uint64_t s = sseg[j];
-        if (j != bseg_off[s]) continue;
-        const uint64_t je = bseg_off[s + 1];
-        SegSums d(0);
-        BatchSums acc(0);
-        uint64_t fp = ~0ull;
-        for (uint64_t r = j; r < je; r++) {
-            const BatchSums f = bs[r];
-            acc = acc + f;
-            bxl[r] = acc;
-            if (!f.v[BS_NE] && !f.v[BS_EQ]) continue;
-            d.v[0] += f.v[BS_NE] - f.v[BS_EQ];
-            d.v[1] += f.v[BS_KN] - f.v[BS_KE];
-            d.v[2] += f.v[BS_VN] - f.v[BS_VE];
-            d.v[3] += (f.v[BS_NE] && !f.v[BS_EQ]) ? 1 : 0;
-            fp = std::min<uint64_t>(fp, rat[r].vu);
-        }
-        if (fp != ~0ull) {
-            sd[s] = d;
-            dirty[s] = 1;
-            fpos[s] = fp;
         }
     }
 }

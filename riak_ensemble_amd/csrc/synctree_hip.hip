@@ -1589,7 +1589,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(batch_prepare(t, in, sc, bp));
     uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
     BatchSums *bs = nullptr, *bx = nullptr;
-    SegSums *ss = nullptr, *sm = nullptr;
+    SegSums *sm = nullptr;
     unsigned long long *fpos = nullptr;
     PlanSums *rsz = nullptr, *rbase = nullptr;
     uint32_t *mpos = nullptr;
@@ -1598,7 +1598,6 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&reject, S));
     CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
-    CHK(sc.alloc(&ss, S));
     CHK(sc.alloc(&sm, S));
     CHK(sc.alloc(&fpos, S));
     CHK(sc.alloc(&dirty, S));
@@ -1608,12 +1607,13 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n));
-    // (no memsets of the per-record sums or the segments' deltas: every
-    // reader reads only what k_merge_keys / k_run_sums wrote -- records inside
-    // a run, deltas of a dirty segment)
-    HIPCHK(hipMemsetAsync(rsz + S, 0, sizeof(PlanSums), t->stream));
+    // (no memsets of the per-record sums: every reader reads only what
+    // k_merge_keys / k_run_plan wrote for records inside a run; the plan's
+    // mode and sizes are zero for a segment without a kept record)
     HIPCHK(hipMemsetAsync(dirty, 0, S, t->stream));
     HIPCHK(hipMemsetAsync(fpos, 0xFF, S * 8, t->stream));
+    HIPCHK(hipMemsetAsync(mode, 0, S, t->stream));
+    HIPCHK(hipMemsetAsync(rsz, 0, (S + 1) * sizeof(PlanSums), t->stream));
     // merge positions (a lane per record, the segments' size deltas by
     // atomics), then the touched segments' verify (saving each one's
     // unchanged-prefix MD5 state) and the inner nodes of their paths
@@ -1642,13 +1642,17 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
         LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
                (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr, pb);
-        LAUNCH(t, "run_sums", k_run_sums, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
-               (const BatchSums *)bs, (const RecAt *)rat, ss, dirty, fpos, bx);
+        // each run summed and its page planned by the run's first lane (in place
+        // or moved; a rejected segment's plan is dropped by k_path_status below)
+        LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
+               (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
+               (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
                (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps, pb);
         CHK(verify_levels(t, t->H + 1));
         LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
-               (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr);
+               (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr, mode, (void *)rsz,
+               sizeof(PlanSums), dirty);
     }
     if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
                               (const uint8_t *)reject, in.clevel_out);
@@ -1656,9 +1660,16 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // in place or to a new page; the moves' places in the append region
     PlanSums tot(0);
     for (int pass = 0;; pass++) {
-        LAUNCH(t, "page_plan", k_page_plan, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff, (const uint64_t *)t->pg.voff,
-               (const uint64_t *)bp.bseg_off, (const uint8_t *)reject, (const BatchSums *)bs, (const SegSums *)ss, sm,
-               dirty, S, t->pg_slack, mode, rsz);
+        if (pass) {   // the pages were rebuilt: plan again against their new capacities
+            HIPCHK(hipMemsetAsync(mode, 0, S, t->stream));
+            HIPCHK(hipMemsetAsync(rsz, 0, (S + 1) * sizeof(PlanSums), t->stream));
+            LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
+                   n, (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
+                   (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
+            LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, view(t), t->H + 1, (const uint64_t *)bp.bseg_off,
+                   (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr, mode, (void *)rsz,
+                   sizeof(PlanSums), dirty);
+        }
         CHK(exclusive_scan<PlanSums>(t, rsz, rbase, S + 1));
         CHK(d2h(t, &tot, rbase + S, sizeof(PlanSums)));
         const Pages &g = t->pg;
