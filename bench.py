@@ -986,7 +986,29 @@ def _bench_perkey_multi(trees, synctree_hip, torch, rounds=40):
         assert t1.insert1(int(rng.integers(0, 1 << 62)), bytes(rounds_v[0][r % E])) is None
         one.append(time.perf_counter() - tb)
     one.sort()
+    # the crossover with a host-side path: one insert/3 into each of N trees
+    # per call, N = 1 .. E (ctypes included, median of 15 calls), beside the
+    # C port's insert on the host (config1.per_key_latency_us.cpu_insert_in_c)
+    curve = {}
+    for N in [x for x in (1, 2, 4, 8, 16, 32, 64, 128, 256) if x < E] + [E]:
+        sub = (ctypes.c_void_p * N)(*[t.h.value for t in trees[:N]])
+        ko_n = np.ascontiguousarray(ko[:N + 1])
+        vo_n = np.ascontiguousarray(vo[:N + 1])
+        lat_n = []
+        for r in range(15):
+            kk = np.ascontiguousarray(rng.integers(0, 1 << 62, N, dtype=np.int64).astype('>i8')).view(np.uint8)
+            vv = np.ascontiguousarray(rounds_v[r % rounds][:N])
+            tb = time.perf_counter()
+            _lib.check(L.st_insert1_multi(sub, N, p(kt), p(kk), p(ko_n), p(vv), p(vo_n), p(st), None, None),
+                       'st_insert1_multi')
+            lat_n.append(time.perf_counter() - tb)
+            assert not st[:N].any()
+        lat_n.sort()
+        curve[N] = round(lat_n[len(lat_n) // 2] * 1e6, 1)
     return {'inserts_per_s': round(E * (rounds - 1) / el, 1), 'trees_per_launch': E,
+            'us_per_call_by_trees': curve,
+            'us_per_call_by_trees_what': 'st_insert1_multi with one insert/3 into each of N trees per call (one '
+                                         'launch), median of 15 calls, ctypes included',
             'ms_per_launch_median': round(lat[len(lat) // 2] * 1e3, 4), 'ms_per_launch_max': round(lat[-1] * 1e3, 4),
             'get_ms_per_launch': round(get_s * 1e3, 4),
             'single_tree_insert1_us_median': round(one[len(one) // 2] * 1e6, 1),
