@@ -1139,27 +1139,6 @@ __device__ __forceinline__ int pfx_cmp(const uint4 &x, const uint4 &y) {
 // step that meets an equal key lands on it: keys of a segment are unique).
 __device__ __forceinline__ uint32_t lds_lower_bound(const uint4 *pk, const uint32_t *off, const uint8_t *kb, uint32_t n,
                                                     const uint4 &kp, const uint8_t *k, uint32_t kl, bool *eq) {
-    if (n <= 32) {   // a short segment: count the smaller keys, eight independent prefix reads per round trip
-        uint32_t lt = 0;
-        bool found = false, tie = false;
-        for (uint32_t m0 = 0; m0 < n; m0 += 8) {
-            uint4 q[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) q[u] = m0 + u < n ? pk[m0 + u] : make_uint4(~0u, ~0u, ~0u, ~0u);
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                if (m0 + u >= n) break;
-                const int c = pfx_cmp(q[u], kp);
-                lt += c < 0 ? 1u : 0u;
-                found |= c == 0;
-                tie |= c == 2;
-            }
-        }
-        if (!tie) {
-            *eq = found;
-            return lt;
-        }
-    }
     uint32_t lo = 0, hi = n;
     bool found = false;
     while (lo < hi) {
@@ -1177,13 +1156,6 @@ __device__ __forceinline__ uint32_t lds_lower_bound(const uint4 *pk, const uint3
 // per step (one LDS round trip), no early exit inside a step.
 __device__ __forceinline__ bool lds_bytes_eq(const uint8_t *a, uint32_t la, const uint8_t *b, uint32_t lb) {
     if (la != lb) return false;
-    if (la <= 24) {   // the common value (a 17-byte ObjHash): every byte read at once, one round trip
-        uint32_t d = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 24; k++)
-            if (k < la) d |= (uint32_t)(a[k] ^ b[k]);
-        return d == 0;
-    }
     for (uint32_t i = 0; i < la; i += 8) {
         uint32_t d = 0;
 #pragma unroll
