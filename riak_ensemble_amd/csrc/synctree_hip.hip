@@ -3186,7 +3186,9 @@ static int compare_core(st_tree *A, st_tree *B, int filter, CompareOut &co, uint
         return ST_EINVAL;
     }
     st_tree *t = A;   // work is enqueued on the local tree's stream
-    if (B->stream != A->stream) CHK(tsync(B));
+    // the remote's own pending work (an st_rehash it did not wait for) first;
+    // an idle remote stream is not synchronised (a host round trip per compare)
+    if (B->stream != A->stream && B->async_pending) CHK(tsync(B));
     CHK(ensure_cmp_work(t));
     CmpWork &w = t->cw;
     CHK(grow_records(t, 4096, 64));
