@@ -492,10 +492,12 @@ __device__ __forceinline__ BatchSums pm_bx(const PageMergeArgs &p, uint64_t j0, 
 // together, top down; each round moves every lane's piece (wave_run_jobs),
 // then each lane writes its group's records into the gap above it.
 template <bool CHECK>
-// at least 5 waves per SIMD (<= 102 VGPRs; 142 unbounded, 3 waves): the
-// kernel waits on memory, and the extra waves cut it 1.39 -> 1.22 ms
+// 4 waves per SIMD (<= 128 VGPRs: 127, no spill).  Round 5 took 5 (1.39 ->
+// 1.22 ms against 3); with the uniform pages' state the 5-wave build spills 46
+// VGPRs and the 4-wave one is faster: 0.624 against 0.689 ms a config-5 batch
+// (6 waves 0.762, two units in flight 0.79; profiles/r06i_merge_waves_ab.txt)
 #ifndef PM_WAVES
-#define PM_WAVES 5
+#define PM_WAVES 4
 #endif
 __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
     const MergeArgs &a = p.a;
