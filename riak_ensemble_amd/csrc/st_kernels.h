@@ -115,6 +115,14 @@ __host__ __device__ __forceinline__ uint64_t krec_order_len(const uint8_t *p, ui
     return len - 4 - el - (sl == 0xFFFF ? 0 : sl);
 }
 
+// The 8 big-endian bytes at p (any alignment) as an integer.
+__device__ __forceinline__ uint64_t krec_be64(const uint8_t *p) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+    return v;
+}
+
 // Plain byte order: memcmp over the common prefix, then length.
 __device__ __forceinline__ int bytes_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
     uint64_t m = la < lb ? la : lb;
@@ -669,7 +677,35 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
         if (V == KLEN_NONE_ || L == KLEN_MIXED_) V = KLEN_MIXED_;
         uint64_t lo = 0, hi = nold, ke = 0;
         bool eq;
-        if (L != KLEN_MIXED_) {   // every old key L bytes: entry i's key at k0 + L i, no offset loads
+        if (L == 9 && kl == 9 && kb[0] == KEYTAG_INT) {
+            // int64 keys among 9-byte records (a 9-byte record with the int
+            // tag is an int64, krec_is_term): each probe is (tag, 8-byte
+            // big-endian payload), all of it in ONE round trip (three dword
+            // loads of the aligned window -- a record's bytes and up to 3 of
+            // its neighbour's, heaps keep slack); a different tag decides
+            // by itself (its first order byte).
+            const uint8_t *k0 = a.kheap + a.koff[i0];
+            const uint64_t kv = krec_be64(kb + 1);
+            bool hit = false;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                const uintptr_t ad = reinterpret_cast<uintptr_t>(k0 + 9 * mid);
+                const uint32_t o = (uint32_t)(ad & 3);
+                const uint32_t ST_GAS *w = reinterpret_cast<const uint32_t ST_GAS *>(ad - o);
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, o), y = __builtin_amdgcn_alignbyte(w2, w1, o);
+                const uint32_t z = (uint32_t)(((uint64_t)w2 >> (8 * o)) & 0xffu);
+                const uint32_t tag = x & 0xffu;
+                // payload bytes 1..8 little-endian in (lo32, hi32), then big-endian order
+                const uint32_t p0 = (x >> 8) | (y << 24), p1 = (y >> 8) | (z << 24);
+                const uint64_t pv = ((uint64_t)__builtin_bswap32(p0) << 32) | __builtin_bswap32(p1);
+                const int c = tag != KEYTAG_INT ? (tag < KEYTAG_INT ? -1 : 1) : (pv < kv ? -1 : (pv > kv ? 1 : 0));
+                hit |= c == 0;
+                if (c < 0) lo = mid + 1; else hi = mid;
+            }
+            eq = hit;   // the keys of a segment are unique: an equal probe is where the search ends
+            ke = L;
+        } else if (L != KLEN_MIXED_) {   // every old key L bytes: entry i's key at k0 + L i, no offset loads
             const uint8_t *k0 = a.kheap + a.koff[i0];
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
