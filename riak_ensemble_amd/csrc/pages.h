@@ -174,6 +174,8 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
 __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *koff, uint64_t *voff, const uint8_t *mode,
                                                           const uint8_t *reject, uint64_t S) {
     const uint32_t lane = threadIdx.x & 63;
+    // (a batch without room in the append region is merged only after a page
+    // build; materialising first is harmless: a uniform page's offsets written out)
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t s0 = w0 * 64; s0 < S; s0 += nw * 64) {
         const uint64_t mine = s0 + lane;
@@ -200,12 +202,11 @@ __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *
 // -- in place needs room in the page and every prefix of the run adding >=
 // 0 key and value bytes (the moves run from the highest address down) --,
 // reloc = the new page's sizes (mode 2, scanned for its place in the append
-// region), v[3] its new keys, v[4] its value bytes before the merge; mode
-// bit 4: the merged page keeps per-entry offsets (not uniform), bit 8: a
-// uniform page turning mixed (k_page_materialize first).  No pass over all S
-// segments.  Runs before
-// the verify: k_path_status drops a rejected segment's plan.  mode / reloc
-// must be zero for the segments without a run (the caller clears them).
+// region, k_page_place), v[3] its new keys, v[4] its value bytes before the
+// merge; mode bit 4: the merged page keeps per-entry offsets (not uniform),
+// bit 8: a uniform page turning mixed (k_page_materialize first).  No pass
+// over all S segments.  Runs before the verify: k_page_place drops a rejected
+// segment's plan and writes mode / dirty 0 for the segments without a run.
 __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
                            const RecAt *rat, PageMeta m, const uint64_t *koff, const uint64_t *voff, int slack_pct,
                            uint8_t *dirty, unsigned long long *fpos, BatchSums *bxl, SegSums *sm, uint8_t *mode,
@@ -236,7 +237,12 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
             d.v[3] += (f.v[BS_NE] && !f.v[BS_EQ]) ? 1 : 0;
             fp = std::min<uint64_t>(fp, rat[r].vu);
         }
-        if (fp == ~0ull) continue;   // no kept record: nothing to merge (mode and reloc stay 0)
+        if (fp == ~0ull) {   // no kept record: nothing to merge (no memsets before: every run's segment is written)
+            dirty[s] = 0;
+            fpos[s] = ~0ull;
+            mode[s] = 0;
+            continue;
+        }
         dirty[s] = 1;
         fpos[s] = fp;
         const uint64_t b = m.beg[s], e = m.end[s];
@@ -262,6 +268,104 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
     }
 }
 
+// The plan settled after the verify, a lane per segment (S-wide): the path
+// status of every segment with a run (k_path_status: the first level whose
+// node failed; a rejected segment's plan is dropped -- no merge, no rehash,
+// no new keys counted), mode / dirty 0 for the segments without one, and
+// every moved page's place in the append region: a workgroup scan of the
+// moved pages' sizes and one atomic per workgroup and quantity (the order of
+// the places across workgroups is the atomics' order: the layout may differ
+// from run to run, the content does not).  acc (zeroed by the caller), at
+// q * PP_LINE for q = 0..4: the moves' entries / key bytes / value bytes, the
+// batch's new keys, the touched segments' value bytes before the merge.  No scan over S, and
+// the host reads the totals once, at the end of the batch: a batch whose moves
+// do not fit the append region is not merged (page_room below) and the host
+// rebuilds the pages and merges it again.
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, uint32_t lane) {
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+#define PP_ITER 4    // segments per thread: a workgroup owns 1024 consecutive segments, one atomic per quantity
+#define PP_LINE 16   // acc quantities a 128-byte line apart (no two atomics' addresses share a line)
+__global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *bseg_off, const uint8_t *ok,
+                                                    uint8_t *reject, uint8_t *mode, uint8_t *dirty, const PlanSums *rsz,
+                                                    PlanSums *rbase, unsigned long long *acc) {
+    __shared__ uint64_t wt[PP_ITER][4][3], wr[4][2], base[3];
+    const uint32_t L = t.H + 1, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t s0 = (uint64_t)blockIdx.x * 256 * PP_ITER;
+    uint64_t c[PP_ITER][3], x[PP_ITER][3], r3 = 0, r4 = 0;
+#pragma unroll
+    for (int it = 0; it < PP_ITER; it++) {
+        const uint64_t s = s0 + (uint64_t)it * 256 + tid;
+        c[it][0] = c[it][1] = c[it][2] = 0;
+        if (s < t.S) {
+            if (bseg_off[s] == bseg_off[s + 1]) {
+                reject[s] = 0; mode[s] = 0; dirty[s] = 0;
+            } else {
+                uint32_t bad = 0;
+                for (uint32_t l = 1; l <= L; l++)
+                    if (!ok[t.base[l] + (s >> (t.shift * (L - l)))]) { bad = l; break; }
+                reject[s] = (uint8_t)bad;
+                const uint8_t md = mode[s];
+                if (bad) {
+                    mode[s] = 0; dirty[s] = 0;
+                } else if (md) {
+                    const PlanSums z = rsz[s];
+                    if ((md & 3) == 2) { c[it][0] = z.v[0]; c[it][1] = z.v[1]; c[it][2] = z.v[2]; }
+                    r3 += z.v[3]; r4 += z.v[4];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            x[it][q] = wave_incl_scan(c[it][q], lane);
+            if (lane == 63) wt[it][w][q] = x[it][q];
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) { r3 += __shfl_xor(r3, o); r4 += __shfl_xor(r4, o); }
+    if (lane == 0) { wr[w][0] = r3; wr[w][1] = r4; }
+    __syncthreads();
+    if (tid < 5) {   // one atomic per quantity and workgroup, each on its own line
+        uint64_t tot = 0;
+        for (int v = 0; v < 4; v++) {
+            if (tid < 3)
+                for (int it = 0; it < PP_ITER; it++) tot += wt[it][v][tid];
+            else
+                tot += wr[v][tid - 3];
+        }
+        const uint64_t b0 = tot ? atomicAdd(&acc[tid * PP_LINE], (unsigned long long)tot) : 0;
+        if (tid < 3) base[tid] = b0;
+    }
+    __syncthreads();
+    uint64_t run[3] = {base[0], base[1], base[2]};
+#pragma unroll
+    for (int it = 0; it < PP_ITER; it++) {
+        const uint64_t s = s0 + (uint64_t)it * 256 + tid;
+        uint64_t before[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            before[q] = run[q] + x[it][q] - c[it][q];
+            for (uint32_t v = 0; v < 4; v++) {
+                if (v < w) before[q] += wt[it][v][q];
+                run[q] += wt[it][v][q];
+            }
+        }
+        if (s < t.S && (c[it][0] | c[it][1] | c[it][2])) {   // a moved page (its caps are never all zero)
+            PlanSums R(0);
+            R.v[0] = before[0]; R.v[1] = before[1]; R.v[2] = before[2];
+            rbase[s] = R;
+        }
+    }
+}
+// the batch's moves fit the append region (the host's check after the batch is the same)
+__device__ __forceinline__ bool page_room(const unsigned long long *acc, uint64_t e0, uint64_t k0, uint64_t v0,
+                                          uint64_t ce, uint64_t ck, uint64_t cv) {
+    return e0 + acc[0] + 1 <= ce && k0 + acc[PP_LINE] <= ck && v0 + acc[2 * PP_LINE] <= cv;
+}
+
 // The merge of one batch run into its segment's page (mode 1, in place) or
 // into a new page (mode 2): the closed form of k_merge_old / k_merge_new
 // (st_kernels.h) per segment, a lane per segment.  The run's records with
@@ -282,9 +386,11 @@ struct PageMergeArgs {
     const BatchSums *bx;          // per run: inclusive prefix sums of its records' BatchSums (k_run_plan)
     const SegSums *ss;            // per segment: merged count, key bytes, value bytes
     const uint8_t *mode;
-    const PlanSums *rbase;        // exclusive scan of the relocation sizes
+    const PlanSums *rbase;        // the moved pages' places (k_page_place)
     const PlanSums *rsz;          // the relocation sizes
     uint64_t e0, k0, v0;          // the append region's bases
+    uint64_t ce, ck, cv;          // ... and its ends
+    const unsigned long long *acc;   // the batch's totals (k_page_place): no room, no merge
     unsigned long long *chk;      // checked build (st_debug_knob ST_DBG_PAGE_CHECK): [0] violations, [1..4] the first
 };
 
@@ -504,6 +610,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
     unsigned long long *chk = CHECK ? p.chk : nullptr;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    if (!page_room(p.acc, p.e0, p.k0, p.v0, p.ce, p.ck, p.cv)) return;   // the host rebuilds the pages and merges again
     for (uint64_t sb = w0 * 64; sb < a.S; sb += nw * 64) {
         const uint64_t s = sb + lane;
         const uint8_t mb = s < a.S ? p.mode[s] : 0, md = mb & 3;

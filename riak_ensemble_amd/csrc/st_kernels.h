@@ -339,13 +339,9 @@ __global__ void k_mark_from_segments(DevTree t, const uint8_t *segflag, uint8_t 
 }
 
 // First failing level on each target's root->target path (0 = verified).
-// plan_mode / plan_sz / plan_dirty (a streaming batch, k_run_plan planned
-// before the verify): a rejected segment's plan is dropped -- no merge, no
-// relocation, no rehash, no new keys counted.
+// (A streaming batch's segments: k_page_place, pages.h.)
 __global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, const uint64_t *targets,
-                              uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus,
-                              uint8_t *plan_mode = nullptr, void *plan_sz = nullptr, size_t plan_sz_bytes = 0,
-                              uint8_t *plan_dirty = nullptr) {
+                              uint64_t ntargets, const uint8_t *ok, uint8_t *seg_reject, uint32_t *tstatus) {
     for (uint64_t i = gtid(); i < ntargets; i += gstride()) {
         uint64_t tb;
         if (bseg_off) {
@@ -361,12 +357,6 @@ __global__ void k_path_status(DevTree t, uint32_t L, const uint64_t *bseg_off, c
         }
         if (seg_reject) seg_reject[i] = (uint8_t)bad;
         if (tstatus) tstatus[i] = bad;
-        if (bad && plan_mode) {
-            plan_mode[i] = 0;
-            plan_dirty[i] = 0;
-            uint64_t *z = reinterpret_cast<uint64_t *>(reinterpret_cast<uint8_t *>(plan_sz) + i * plan_sz_bytes);
-            for (size_t q = 0; q < plan_sz_bytes / 8; q++) z[q] = 0;
-        }
     }
 }
 
@@ -800,11 +790,15 @@ struct PrefixState {
 // the merge.
 // pb.chk (checked mode): a segment whose value span lies outside the value
 // array is reported (code 32) and not hashed.
+// ntot (optional): perm is a list of *ntot segments (k_hash_list_* over the
+// touched ones, longest first: no lane idles on an untouched segment), not all S.
 __global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *perm, const uint8_t *mask, uint8_t *ok,
                                                     const unsigned long long *fpos, PrefixState *ps,
-                                                    PageBounds pb = PageBounds{0, 0, 0, nullptr}) {
+                                                    PageBounds pb = PageBounds{0, 0, 0, nullptr},
+                                                    const uint32_t *ntot = nullptr) {
     const uint32_t L = t.H + 1;
-    for (uint64_t i = gtid(); i < t.S; i += gstride()) {
+    const uint64_t n = ntot ? (uint64_t)*ntot : t.S;
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
         const uint64_t s = perm[i];
         const uint64_t slot = t.base[L] + s;
         if (!mask[slot]) continue;
@@ -2021,7 +2015,7 @@ __global__ void k_clamp_runs(uint64_t *bseg_off, uint64_t S, uint64_t lo, uint64
 __device__ __forceinline__ uint32_t hash_bin(const DevTree &t, const uint8_t *mask, const PrefixState *ps, uint64_t s) {
     if (!mask[t.base[t.H + 1] + s]) return PERM_BINS;   // not in the list
     if (t.seg_off[s] == t.seg_end[s]) return PERM_BINS - 1;
-    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - ps[s].k;
+    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - (ps ? ps[s].k : 0);
     return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
 }
 __global__ void __launch_bounds__(256) k_hash_list_count(DevTree t, const uint8_t *mask, const PrefixState *ps,

@@ -1317,6 +1317,8 @@ struct IngestIn {
     uint32_t *clevel_out;
     uint32_t *seg_out;
     uint64_t n_rejected;
+    bool count_rejected;     // the caller wants clevel_out's nonzero count ...
+    bool rejected_counted;   // ... and the paged path counted it with its totals (n_rejected)
 };
 
 // The batch in merge order: segment per record (seg), sorted segments
@@ -1595,6 +1597,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
     PrefixState *ps = nullptr;
+    unsigned long long *acc = nullptr;
     CHK(sc.alloc(&reject, S));
     CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
@@ -1602,18 +1605,17 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&fpos, S));
     CHK(sc.alloc(&dirty, S));
     CHK(sc.alloc(&mode, S));
-    CHK(sc.alloc(&rsz, S + 1));
-    CHK(sc.alloc(&rbase, S + 1));
+    CHK(sc.alloc(&rsz, S));
+    CHK(sc.alloc(&rbase, S));
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n));
-    // (no memsets of the per-record sums: every reader reads only what
-    // k_merge_keys / k_run_plan wrote for records inside a run; the plan's
-    // mode and sizes are zero for a segment without a kept record)
-    HIPCHK(hipMemsetAsync(dirty, 0, S, t->stream));
-    HIPCHK(hipMemsetAsync(fpos, 0xFF, S * 8, t->stream));
-    HIPCHK(hipMemsetAsync(mode, 0, S, t->stream));
-    HIPCHK(hipMemsetAsync(rsz, 0, (S + 1) * sizeof(PlanSums), t->stream));
+    CHK(sc.alloc(&acc, 6 * PP_LINE));
+    // No memsets of the per-segment plan: k_run_plan writes every segment
+    // with a run, k_page_place every other one; the per-record sums are read
+    // only inside runs.  acc: the batch's totals (k_page_place, a line
+    // apart), then the rejected records (insert_int64's count, read with them).
+    HIPCHK(hipMemsetAsync(acc, 0, 6 * PP_LINE * 8, t->stream));
     // merge positions (a lane per record, the segments' size deltas by
     // atomics), then the touched segments' verify (saving each one's
     // unchanged-prefix MD5 state) and the inner nodes of their paths
@@ -1632,6 +1634,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
     ma.klen = t->pg.m.klen;
     ma.vlen = t->pg.m.vlen;
+    const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
     {
         const DevTree d = view(t);
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
@@ -1639,81 +1642,90 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                (const uint64_t *)nullptr, S, t->mark);
         CHK(ensure_perm_any(t));
         // then the per-segment sums and the runs' prefix sums by each run's first lane (no atomics, no scan)
-        const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
         LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
                (SegSums *)nullptr, (uint8_t *)nullptr, (unsigned long long *)nullptr, pb);
         // each run summed and its page planned by the run's first lane (in place
-        // or moved; a rejected segment's plan is dropped by k_path_status below)
+        // or moved; a rejected segment's plan is dropped by k_page_place below)
         LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
                (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
                (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
-               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps, pb);
+               (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps, pb, (const uint32_t *)nullptr);
         CHK(verify_levels(t, t->H + 1));
-        LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
-               (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr, mode, (void *)rsz,
-               sizeof(PlanSums), dirty);
     }
-    if (in.clevel_out) LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n,
-                              (const uint8_t *)reject, in.clevel_out);
-    ma.seg_reject = reject;
-    // in place or to a new page; the moves' places in the append region
-    PlanSums tot(0);
+    // the plan settled (rejections, places in the append region, totals),
+    // the merge, the dirty-path rehash, then ONE read of the totals: a batch
+    // whose moves did not fit the append region was not merged (k_page_merge
+    // checks the totals itself) -- the pages are rebuilt with room for them
+    // and the batch planned and merged again
     for (int pass = 0;; pass++) {
-        if (pass) {   // the pages were rebuilt: plan again against their new capacities
-            HIPCHK(hipMemsetAsync(mode, 0, S, t->stream));
-            HIPCHK(hipMemsetAsync(rsz, 0, (S + 1) * sizeof(PlanSums), t->stream));
+        if (pass) {
+            HIPCHK(hipMemsetAsync(acc, 0, 5 * PP_LINE * 8, t->stream));
             LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
                    n, (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
                    (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
-            LAUNCH(t, "path_status", k_path_status, grid_for(S), 256, 0, view(t), t->H + 1, (const uint64_t *)bp.bseg_off,
-                   (const uint64_t *)nullptr, S, (const uint8_t *)t->ok, reject, (uint32_t *)nullptr, mode, (void *)rsz,
-                   sizeof(PlanSums), dirty);
         }
-        CHK(exclusive_scan<PlanSums>(t, rsz, rbase, S + 1));
-        CHK(d2h(t, &tot, rbase + S, sizeof(PlanSums)));
+        LAUNCH(t, "page_place", k_page_place, (uint32_t)((S + 256 * PP_ITER - 1) / (256 * PP_ITER)), 256, 0, view(t), (const uint64_t *)bp.bseg_off,
+               (const uint8_t *)t->ok, reject, mode, dirty, (const PlanSums *)rsz, rbase, acc);
+        if (!pass && in.clevel_out)
+            LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, (const uint8_t *)reject,
+                   in.clevel_out);
+        ma.seg_reject = reject;
         const Pages &g = t->pg;
-        if (g.use_e + tot.v[0] + 1 <= g.cap_e && g.use_k + tot.v[1] <= g.cap_k && g.use_v + tot.v[2] <= g.cap_v) break;
+        PageMergeArgs pa;
+        pa.a = ma;
+        pa.m = g.m;
+        pa.koff = g.koff; pa.voff = g.voff; pa.kheap = g.kheap; pa.vheap = g.vheap;
+        pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = sm; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
+        pa.e0 = g.use_e; pa.k0 = g.use_k; pa.v0 = g.use_v;
+        pa.ce = g.cap_e; pa.ck = g.cap_k; pa.cv = g.cap_v;
+        pa.acc = acc;
+        pa.chk = nullptr;
+        // uniform pages a record of another length turns mixed: their offsets first
+        LAUNCH(t, "page_merge", k_page_materialize, grid_for(S, 256, 4096), 256, 0, g.m, g.koff, g.voff,
+               (const uint8_t *)mode, (const uint8_t *)reject, S);
+        if (!t->pg_check) {
+            LAUNCH(t, "page_merge", k_page_merge<false>, grid_for(S), 256, 0, pa);
+        } else {   // checked build (debug knob): merges that would leave their pages reported, not performed
+            pa.chk = chk;   // (the pre-batch check found nothing: zero)
+            LAUNCH(t, "page_merge", k_page_merge<true>, grid_for(S), 256, 0, pa);
+            LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, g.m, (const uint64_t *)g.koff,
+                   (const uint64_t *)g.voff, S, g.cap_e, g.cap_k, g.cap_v, pa.chk);
+            CHK(page_check_report(t, chk, "after the merge"));
+        }
+        // dirty-path rehash over the pages, each segment from its unchanged
+        // prefix's MD5 state (a batch not merged hashes its old content again:
+        // the same hashes)
+        HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
+        LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
+        CHK(rehash_all(t, t->mark, ps));
+        if (!pass && in.clevel_out && in.count_rejected)
+            LAUNCH(t, "key_status", k_count_nonzero, grid_for(n), 256, 0, (const uint32_t *)in.clevel_out, n,
+                   acc + 5 * PP_LINE);
+        unsigned long long accv[6 * PP_LINE], tot[6];
+        CHK(d2h(t, accv, acc, sizeof(accv)));
+        for (int q = 0; q < 6; q++) tot[q] = accv[q * PP_LINE];
+        if (!pass && in.clevel_out && in.count_rejected) { in.n_rejected = tot[5]; in.rejected_counted = true; }
+        if (g.use_e + tot[0] + 1 <= g.cap_e && g.use_k + tot[1] <= g.cap_k && g.use_v + tot[2] <= g.cap_v) {
+            t->pg.use_e += tot[0]; t->pg.use_k += tot[1]; t->pg.use_v += tot[2];
+            t->pg.reloc_e += tot[0];
+            t->pg.touched_v += tot[4];
+            t->pg.batches++;
+            t->n += tot[3];
+            break;
+        }
         if (pass) { g_err = "page build left no room for the batch's moves"; return ST_EDEVICE; }
         // rebuild: every page gets fresh slack, the append region room for these moves
         PageSums want(0);
-        for (int q = 0; q < 3; q++) want.v[q] = 2 * tot.v[q];
+        for (int q = 0; q < 3; q++) want.v[q] = 2 * tot[q];
         CHK(pages_build(t, t->pg_slack, want));
         ma = merge_args(view(t), in, bp, reject, S);
         ma.klen = t->pg.m.klen;
         ma.vlen = t->pg.m.vlen;
     }
-    PageMergeArgs pa;
-    pa.a = ma;
-    pa.m = t->pg.m;
-    pa.koff = t->pg.koff; pa.voff = t->pg.voff; pa.kheap = t->pg.kheap; pa.vheap = t->pg.vheap;
-    pa.pos = mpos; pa.rat = rat; pa.bx = bx; pa.ss = sm; pa.mode = mode; pa.rbase = rbase; pa.rsz = rsz;
-    pa.e0 = t->pg.use_e; pa.k0 = t->pg.use_k; pa.v0 = t->pg.use_v;
-    pa.chk = nullptr;
-    // uniform pages a record of another length turns mixed: their offsets first
-    LAUNCH(t, "page_merge", k_page_materialize, grid_for(S, 256, 4096), 256, 0, t->pg.m, t->pg.koff, t->pg.voff,
-           (const uint8_t *)mode, (const uint8_t *)reject, S);
-    if (!t->pg_check) {
-        LAUNCH(t, "page_merge", k_page_merge<false>, grid_for(S), 256, 0, pa);
-    } else {   // checked build (debug knob): merges that would leave their pages reported, not performed
-        pa.chk = chk;   // (the pre-batch check found nothing: zero)
-        LAUNCH(t, "page_merge", k_page_merge<true>, grid_for(S), 256, 0, pa);
-        LAUNCH(t, "page_check", k_page_validate, grid_for(S), 256, 0, t->pg.m, (const uint64_t *)t->pg.koff,
-               (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, pa.chk);
-        CHK(page_check_report(t, chk, "after the merge"));
-    }
-    t->pg.use_e += tot.v[0]; t->pg.use_k += tot.v[1]; t->pg.use_v += tot.v[2];
-    t->pg.reloc_e += tot.v[0];
-    t->pg.touched_v += tot.v[4];
-    t->pg.batches++;
-    t->n += tot.v[3];
     t->perm_valid = false;
     t->tiles_valid = false;
     t->tiles_wanted = false;
-    // dirty-path rehash over the pages, each segment from its unchanged prefix's MD5 state
-    HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
-    LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
-    CHK(rehash_all(t, t->mark, ps));
     t->fresh = false;
     return ST_OK;
 }
@@ -2287,6 +2299,7 @@ static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8
     uint8_t *tv = nullptr, *krec = nullptr;
     uint64_t *dko = nullptr, *dvo = nullptr;
     uint32_t *dcl = nullptr;
+    bool dcl_counted = false;
     int r = ST_OK;
     if (!on_device) {
         r = dalloc_t(t, &tk, n);
@@ -2309,10 +2322,11 @@ static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8
     if (!r) {
         IngestIn in{};
         in.n = n; in.krec = krec; in.koff = dko; in.vheap = dvals; in.voff = dvo;
-        in.verify_rehash = true; in.clevel_out = dcl;
+        in.verify_rehash = true; in.clevel_out = dcl; in.count_rejected = dcl != nullptr;
         r = ingest(t, in);
+        if (!r && in.rejected_counted) { *n_corrupted = in.n_rejected; dcl_counted = true; }
     }
-    if (!r && n_corrupted && dcl) {
+    if (!r && n_corrupted && dcl && !dcl_counted) {
         // count per-key rejections on the device (8 bytes back, not n statuses)
         if (hipMemsetAsync(t->cnt64, 0, 8, t->stream) != hipSuccess) { r = ST_EDEVICE; g_err = "memset"; }
         if (!r) {

@@ -43,7 +43,7 @@ for k, v in batches[:2]:
 torch.cuda.synchronize()
 names = ['key_segment', 'bucket', 'run_sort', 'mark_paths', 'segment_verify', 'verify_pos', 'level_verify',
          'path_status', 'key_status', 'merge_count', 'merge_write', 'merge_touched', 'mark_dirty', 'seg_perm',
-         'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_merge', 'page_fold']
+         'segment_hash', 'level_rehash', 'pack_int64', 'page_build', 'page_plan', 'page_place', 'page_merge', 'page_fold']
 t.set_timing(True)
 t.kernel_stats('*reset*')
 t0 = time.perf_counter()
