@@ -288,12 +288,29 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, uint32_t lane) {
     }
     return x;
 }
+//
+// It also lists the segments the batch changes for the dirty-path hash, by
+// the MD5 blocks each has left after its verified prefix (PrefixState.k, the
+// merged value bytes sm[s].v[2]): HB bins, longest first, bin b's entries at
+// hlist[b * hcap ...], counted in hcnt[b * PP_LINE] -- a list in block-count
+// order without a pass of its own (k_segment_hash_perm, HashBins).
 #define PP_ITER 4    // segments per thread: a workgroup owns 1024 consecutive segments, one atomic per quantity
 #define PP_LINE 16   // acc quantities a 128-byte line apart (no two atomics' addresses share a line)
+#define HB 64        // hash-list bins: blocks left 63+, 62, ..., 0
+__device__ __forceinline__ uint32_t hb_bin(uint64_t vbytes, uint64_t k) {
+    const uint64_t rem = (vbytes + 8) / 64 + 1 - k;
+    return rem >= HB - 1 ? 0u : (uint32_t)(HB - 1 - rem);
+}
 __global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *bseg_off, const uint8_t *ok,
                                                     uint8_t *reject, uint8_t *mode, uint8_t *dirty, const PlanSums *rsz,
-                                                    PlanSums *rbase, unsigned long long *acc) {
+                                                    PlanSums *rbase, unsigned long long *acc, const PrefixState *ps,
+                                                    const SegSums *sm, uint32_t *hlist, uint64_t hcap,
+                                                    unsigned long long *hcnt) {
     __shared__ uint64_t wt[PP_ITER][4][3], wr[4][2], base[3];
+    __shared__ uint32_t hh[HB], hbase[HB];
+    if (threadIdx.x < HB) hh[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t hbin[PP_ITER], hrank[PP_ITER];
     const uint32_t L = t.H + 1, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t s0 = (uint64_t)blockIdx.x * 256 * PP_ITER;
     uint64_t c[PP_ITER][3], x[PP_ITER][3], r3 = 0, r4 = 0;
@@ -301,6 +318,7 @@ __global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *b
     for (int it = 0; it < PP_ITER; it++) {
         const uint64_t s = s0 + (uint64_t)it * 256 + tid;
         c[it][0] = c[it][1] = c[it][2] = 0;
+        hbin[it] = HB;
         if (s < t.S) {
             if (bseg_off[s] == bseg_off[s + 1]) {
                 reject[s] = 0; mode[s] = 0; dirty[s] = 0;
@@ -316,6 +334,8 @@ __global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *b
                     const PlanSums z = rsz[s];
                     if ((md & 3) == 2) { c[it][0] = z.v[0]; c[it][1] = z.v[1]; c[it][2] = z.v[2]; }
                     r3 += z.v[3]; r4 += z.v[4];
+                    hbin[it] = hb_bin(sm[s].v[2], ps[s].k);
+                    hrank[it] = atomicAdd(&hh[hbin[it]], 1u);
                 }
             }
         }
@@ -339,6 +359,7 @@ __global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *b
         const uint64_t b0 = tot ? atomicAdd(&acc[tid * PP_LINE], (unsigned long long)tot) : 0;
         if (tid < 3) base[tid] = b0;
     }
+    if (tid < HB) hbase[tid] = hh[tid] ? (uint32_t)atomicAdd(&hcnt[tid * PP_LINE], (unsigned long long)hh[tid]) : 0u;
     __syncthreads();
     uint64_t run[3] = {base[0], base[1], base[2]};
 #pragma unroll
@@ -353,6 +374,7 @@ __global__ void __launch_bounds__(256) k_page_place(DevTree t, const uint64_t *b
                 run[q] += wt[it][v][q];
             }
         }
+        if (hbin[it] < HB) hlist[hbin[it] * hcap + hbase[hbin[it]] + hrank[it]] = (uint32_t)s;
         if (s < t.S && (c[it][0] | c[it][1] | c[it][2])) {   // a moved page (its caps are never all zero)
             PlanSums R(0);
             R.v[0] = before[0]; R.v[1] = before[1]; R.v[2] = before[2];

@@ -790,8 +790,7 @@ struct PrefixState {
 // the merge.
 // pb.chk (checked mode): a segment whose value span lies outside the value
 // array is reported (code 32) and not hashed.
-// ntot (optional): perm is a list of *ntot segments (k_hash_list_* over the
-// touched ones, longest first: no lane idles on an untouched segment), not all S.
+// ntot (optional): perm is a list of *ntot segments, not all S.
 __global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *perm, const uint8_t *mask, uint8_t *ok,
                                                     const unsigned long long *fpos, PrefixState *ps,
                                                     PageBounds pb = PageBounds{0, 0, 0, nullptr},
@@ -2008,62 +2007,6 @@ __global__ void k_clamp_runs(uint64_t *bseg_off, uint64_t S, uint64_t lo, uint64
     }
 }
 
-// The dirty-path hash of a streaming batch: the changed segments only (mask
-// at their level), ordered by the blocks each still has to hash from its
-// saved prefix state (PrefixState.k) -- a lane per segment, so a wave's lanes
-// run alike-long loops and no lane idles on an unchanged segment.
-__device__ __forceinline__ uint32_t hash_bin(const DevTree &t, const uint8_t *mask, const PrefixState *ps, uint64_t s) {
-    if (!mask[t.base[t.H + 1] + s]) return PERM_BINS;   // not in the list
-    if (t.seg_off[s] == t.seg_end[s]) return PERM_BINS - 1;
-    const uint64_t blocks = (t.seg_vend[s] - t.seg_voff[s] + 8) / 64 + 1 - (ps ? ps[s].k : 0);
-    return blocks >= PERM_BINS - 1 ? 0u : (uint32_t)(PERM_BINS - 1 - blocks);
-}
-__global__ void __launch_bounds__(256) k_hash_list_count(DevTree t, const uint8_t *mask, const PrefixState *ps,
-                                                         uint32_t *gcount) {
-    __shared__ uint32_t h[PERM_BINS];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint64_t s = gtid(); s < t.S; s += gstride()) {
-        const uint32_t bin = hash_bin(t, mask, ps, s);
-        if (bin < PERM_BINS) atomicAdd(&h[bin], 1u);
-    }
-    __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&gcount[threadIdx.x], h[threadIdx.x]);
-}
-// exclusive scan of the bins (one workgroup); the list's length into gcount[PERM_BINS]
-__global__ void __launch_bounds__(256) k_hash_list_scan(uint32_t *gcount) {
-    __shared__ uint32_t h[PERM_BINS];
-    h[threadIdx.x] = gcount[threadIdx.x];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < PERM_BINS; b++) { const uint32_t c = h[b]; h[b] = acc; acc += c; }
-        gcount[PERM_BINS] = acc;
-    }
-    __syncthreads();
-    gcount[threadIdx.x] = h[threadIdx.x];
-}
-__global__ void __launch_bounds__(256) k_hash_list_scatter(DevTree t, const uint8_t *mask, const PrefixState *ps,
-                                                           uint32_t *gcur, uint32_t *list) {
-    __shared__ uint32_t h[PERM_BINS], base[PERM_BINS];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t chunk = (t.S + gridDim.x - 1) / gridDim.x;
-    const uint64_t a = blockIdx.x * chunk, b = (a + chunk < t.S) ? a + chunk : t.S;
-    for (uint64_t s = a + threadIdx.x; s < b; s += blockDim.x) {
-        const uint32_t bin = hash_bin(t, mask, ps, s);
-        if (bin < PERM_BINS) atomicAdd(&h[bin], 1u);
-    }
-    __syncthreads();
-    base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&gcur[threadIdx.x], h[threadIdx.x]) : 0;
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint64_t s = a + threadIdx.x; s < b; s += blockDim.x) {
-        const uint32_t bin = hash_bin(t, mask, ps, s);
-        if (bin < PERM_BINS) list[base[bin] + atomicAdd(&h[bin], 1u)] = (uint32_t)s;
-    }
-}
-
 // Pass 1: per-workgroup histograms reserved from global bin counters.
 __global__ void __launch_bounds__(256) k_seg_perm_count(DevTree t, uint32_t *gcount) {
     __shared__ uint32_t h[PERM_BINS];
@@ -2105,15 +2048,45 @@ __global__ void __launch_bounds__(256) k_seg_perm_scatter(DevTree t, uint32_t *g
     }
 }
 
+// A list in bins (k_page_place, pages.h): bin b's cnt[b * line] entries at list[b * cap ...].
+struct HashBins {
+    const uint32_t *list;
+    const unsigned long long *cnt;
+    uint64_t cap;
+    uint32_t nbins, line;
+};
+
 // K1 segment_hash over the block-count order.
 // ps (optional): per segment, the MD5 state of its unchanged prefix (PrefixState, k_verify_cap).
-// ntot (optional): perm is a list of *ntot segments (k_hash_list_*), not all S.
+// ntot (optional): perm is a list of *ntot segments, not all S.
+// hb.list (optional): the list in bins instead (perm unused; a streaming batch's changed segments).
 __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint32_t *perm, const uint8_t *mask,
-                                                           const PrefixState *ps, const uint32_t *ntot = nullptr) {
+                                                           const PrefixState *ps, const uint32_t *ntot = nullptr,
+                                                           HashBins hb = HashBins{nullptr, nullptr, 0, 0, 0}) {
     const uint32_t L1 = t.H + 1;
-    const uint64_t n = ntot ? (uint64_t)*ntot : t.S;
+    __shared__ uint32_t pre[257];
+    uint64_t n = ntot ? (uint64_t)*ntot : t.S;
+    if (hb.list) {   // the bins' starts in the list order
+        if (threadIdx.x == 0) {
+            uint32_t a = 0;
+            for (uint32_t b = 0; b < hb.nbins; b++) { pre[b] = a; a += (uint32_t)hb.cnt[b * hb.line]; }
+            pre[hb.nbins] = a;
+        }
+        __syncthreads();
+        n = pre[hb.nbins];
+    }
     for (uint64_t i = gtid(); i < n; i += gstride()) {
-        const uint64_t s = perm[i];
+        uint64_t s;
+        if (hb.list) {
+            uint32_t lo = 0, hi = hb.nbins;   // the last bin with pre[b] <= i
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pre[mid] <= i) lo = mid; else hi = mid;
+            }
+            s = hb.list[lo * hb.cap + (i - pre[lo])];
+        } else {
+            s = perm[i];
+        }
         const uint64_t slot = t.base[L1] + s;
         if (mask && !mask[slot]) continue;
         if (t.seg_off[s] == t.seg_end[s]) {

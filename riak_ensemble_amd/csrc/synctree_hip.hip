@@ -1227,8 +1227,10 @@ static int rehash_tiled(st_tree *t) {
 // pages) in block-count order (k_segment_hash_perm), then the marked inner
 // nodes: W == 16, H >= 3: k_levels3_16 per level-(H-2) subtree + the
 // per-level kernels above; other geometries: one k_level_hash launch per level.
-// ps: the prefix states of a streaming batch's verify (k_verify_pos) or NULL.
-static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr) {
+// ps: the prefix states of a streaming batch's verify (k_verify_cap) or NULL.
+// hb (a streaming batch's list, k_page_place): the changed segments in bins by blocks left.
+static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr,
+                      HashBins hb = HashBins{nullptr, nullptr, 0, 0, 0}) {
     if (!mask) {
         // The first full rehash after a mutation hashes straight from the
         // CSR (a lane per segment, no tile build: the repair path's
@@ -1245,17 +1247,9 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
         return rehash_levels(t, t->H, nullptr);
     }
     DevTree d = view(t);
-    if (ps) {   // a streaming batch: its changed segments, by the blocks left after their prefixes
-        Scratch sc(t);
-        uint32_t *cnt = nullptr, *list = nullptr;
-        CHK(sc.alloc(&cnt, PERM_BINS + 1));
-        CHK(sc.alloc(&list, t->S));
-        HIPCHK(hipMemsetAsync(cnt, 0, (PERM_BINS + 1) * 4, t->stream));
-        LAUNCH(t, "segment_hash", k_hash_list_count, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt);
-        LAUNCH(t, "segment_hash", k_hash_list_scan, 1, 256, 0, cnt);
-        LAUNCH(t, "segment_hash", k_hash_list_scatter, grid_for(t->S, 256, 1024), 256, 0, d, mask, ps, cnt, list);
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)list, mask, ps,
-               (const uint32_t *)(cnt + PERM_BINS));
+    if (hb.list) {
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)nullptr, mask, ps,
+               (const uint32_t *)nullptr, hb);
     } else {
         CHK(ensure_perm(t));
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask,
@@ -1597,7 +1591,11 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
     PrefixState *ps = nullptr;
-    unsigned long long *acc = nullptr;
+    unsigned long long *acc = nullptr, *hcnt = nullptr;
+    uint32_t *hlist = nullptr;
+    const uint64_t hcap = std::min<uint64_t>(S, n);   // a changed segment has a run
+    CHK(sc.alloc(&hlist, (uint64_t)HB * hcap));
+    CHK(sc.alloc(&hcnt, (uint64_t)HB * PP_LINE));
     CHK(sc.alloc(&reject, S));
     CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
@@ -1659,6 +1657,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // checks the totals itself) -- the pages are rebuilt with room for them
     // and the batch planned and merged again
     for (int pass = 0;; pass++) {
+        HIPCHK(hipMemsetAsync(hcnt, 0, HB * PP_LINE * 8, t->stream));
         if (pass) {
             HIPCHK(hipMemsetAsync(acc, 0, 5 * PP_LINE * 8, t->stream));
             LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
@@ -1666,7 +1665,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                    (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
         }
         LAUNCH(t, "page_place", k_page_place, (uint32_t)((S + 256 * PP_ITER - 1) / (256 * PP_ITER)), 256, 0, view(t), (const uint64_t *)bp.bseg_off,
-               (const uint8_t *)t->ok, reject, mode, dirty, (const PlanSums *)rsz, rbase, acc);
+               (const uint8_t *)t->ok, reject, mode, dirty, (const PlanSums *)rsz, rbase, acc, (const PrefixState *)ps,
+               (const SegSums *)sm, hlist, hcap, hcnt);
         if (!pass && in.clevel_out)
             LAUNCH(t, "key_status", k_key_status, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, (const uint8_t *)reject,
                    in.clevel_out);
@@ -1698,7 +1698,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         // the same hashes)
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
-        CHK(rehash_all(t, t->mark, ps));
+        CHK(rehash_all(t, t->mark, ps, HashBins{hlist, hcnt, hcap, HB, PP_LINE}));
         if (!pass && in.clevel_out && in.count_rejected)
             LAUNCH(t, "key_status", k_count_nonzero, grid_for(n), 256, 0, (const uint32_t *)in.clevel_out, n,
                    acc + 5 * PP_LINE);
