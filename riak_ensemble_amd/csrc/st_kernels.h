@@ -204,8 +204,10 @@ __global__ void k_pack_int64(const int64_t *keys, uint64_t n, uint8_t *kheap, ui
 // K1a key_segment: get_segment/2 (synctree.erl:251-253) — md5 of the key's
 // ensure_binary bytes read as a big-endian 128-bit integer, rem Segments
 // (a power of two: the low bits of digest bytes 8..15).
+// cnt / rank (optional): the bucketing's histogram, each record's rank in its
+// segment's bucket from the same atomic (k_seg_hist).
 __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64_t n, uint64_t segmask,
-                              uint32_t *seg_out) {
+                              uint32_t *seg_out, unsigned long long *cnt = nullptr, uint32_t *rank = nullptr) {
     for (uint64_t i = gtid(); i < n; i += gstride()) {
         const uint64_t o = koff[i];
         const uint64_t len = koff[i + 1] - o;
@@ -230,20 +232,24 @@ __global__ void k_key_segment(const uint8_t *kheap, const uint64_t *koff, uint64
             stmd5::md5_global_pf<true>(sp, sl, d);
         }
         const uint64_t lo = ((uint64_t)__builtin_bswap32(d[2]) << 32) | (uint64_t)__builtin_bswap32(d[3]);
-        seg_out[i] = (uint32_t)(lo & segmask);
+        const uint32_t s = (uint32_t)(lo & segmask);
+        seg_out[i] = s;
+        if (cnt) rank[i] = (uint32_t)atomicAdd(&cnt[s], 1ull);
     }
 }
 
-// Bucketing of a batch by segment (a counting sort: histogram, scan = the
-// run bounds, scatter).  The order inside a run is whatever the atomics
-// give; k_run_sort then orders every run by (key, batch index).
-__global__ void k_seg_hist(const uint32_t *seg, uint64_t n, unsigned long long *cnt) {
-    for (uint64_t i = gtid(); i < n; i += gstride()) atomicAdd(&cnt[seg[i]], 1ull);
+// Bucketing of a batch by segment (a counting sort: histogram with each
+// record's rank in its bucket from the same atomic, scan = the run bounds,
+// scatter to bound + rank: no second atomic pass).  The order inside a run is
+// whatever the atomics give; k_run_sort then orders every run by (key, batch index).
+__global__ void k_seg_hist(const uint32_t *seg, uint64_t n, unsigned long long *cnt, uint32_t *rank) {
+    for (uint64_t i = gtid(); i < n; i += gstride()) rank[i] = (uint32_t)atomicAdd(&cnt[seg[i]], 1ull);
 }
-__global__ void k_seg_scatter(const uint32_t *seg, uint64_t n, unsigned long long *cur, uint32_t *sseg, uint32_t *perm) {
+__global__ void k_seg_scatter(const uint32_t *seg, const uint32_t *rank, uint64_t n, const uint64_t *bseg_off,
+                              uint32_t *sseg, uint32_t *perm) {
     for (uint64_t i = gtid(); i < n; i += gstride()) {
         const uint32_t s = seg[i];
-        const unsigned long long p = atomicAdd(&cur[s], 1ull);
+        const uint64_t p = bseg_off[s] + rank[i];
         sseg[p] = s;
         perm[p] = (uint32_t)i;
     }
@@ -252,7 +258,30 @@ __global__ void k_seg_scatter(const uint32_t *seg, uint64_t n, unsigned long lon
 struct BatchView {
     const uint8_t *kheap;
     const uint64_t *koff;
+    bool int9;   // every record an int64 key (insert_int64): record i at kheap + 9 i, koff not read
 };
+
+// A 9-byte key record's tag and big-endian payload in ONE round trip: three
+// dword loads of its aligned window (its bytes and up to 3 of the next
+// record's; heaps keep slack).
+__device__ __forceinline__ void krec9_load(const uint8_t *p, uint32_t &tag, uint64_t &pv) {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+    const uint32_t o = (uint32_t)(ad & 3);
+    const uint32_t ST_GAS *w = reinterpret_cast<const uint32_t ST_GAS *>(ad - o);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, o), y = __builtin_amdgcn_alignbyte(w2, w1, o);
+    const uint32_t z = (uint32_t)(((uint64_t)w2 >> (8 * o)) & 0xffu);
+    tag = x & 0xffu;
+    // payload bytes 1..8 little-endian in (lo32, hi32), then big-endian order
+    const uint32_t p0 = (x >> 8) | (y << 24), p1 = (y >> 8) | (z << 24);
+    pv = ((uint64_t)__builtin_bswap32(p0) << 32) | __builtin_bswap32(p1);
+}
+__device__ __forceinline__ void cas_kx(uint64_t &ka, uint32_t &ia, uint64_t &kb, uint32_t &ib) {
+    const bool sw = kb < ka || (kb == ka && ib < ia);
+    const uint64_t k = sw ? kb : ka, k2 = sw ? ka : kb;
+    const uint32_t i = sw ? ib : ia, i2 = sw ? ia : ib;
+    ka = k; kb = k2; ia = i; ib = i2;
+}
 
 __device__ __forceinline__ int batch_cmp(const BatchView &b, uint32_t x, uint32_t y) {
     int c = rec_cmp(b.kheap + b.koff[x], b.koff[x + 1] - b.koff[x], b.kheap + b.koff[y], b.koff[y + 1] - b.koff[y]);
@@ -280,6 +309,29 @@ __global__ void k_run_sort(BatchView bv, uint32_t *perm, const uint64_t *bseg_of
         if (a == b) continue;
         uint32_t *r = perm + a;
         const uint64_t n = b - a;
+        if (bv.int9 && n <= 4) {
+            // int64 keys, a run of <= 4 (nearly all of them): the keys in
+            // registers (one round trip), a sorting network on (key, index)
+            uint64_t k[4];
+            uint32_t x[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) { x[q] = q < (int)n ? r[q] : ~0u; k[q] = ~0ull; }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < (int)n) { uint32_t tg; krec9_load(bv.kheap + 9ull * x[q], tg, k[q]); }
+            cas_kx(k[0], x[0], k[1], x[1]);
+            cas_kx(k[2], x[2], k[3], x[3]);
+            cas_kx(k[0], x[0], k[2], x[2]);
+            cas_kx(k[1], x[1], k[3], x[3]);
+            cas_kx(k[1], x[1], k[2], x[2]);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (q < (int)n) {
+                    r[q] = x[q];
+                    keep[a + q] = (q + 1 == (int)n || k[q] != k[q + 1 < 4 ? q + 1 : 3]) ? 1 : 0;
+                }
+            continue;
+        }
         if (n <= 32) {
             for (uint64_t i = 1; i < n; i++) {
                 uint32_t x = r[i];
@@ -679,16 +731,9 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             bool hit = false;
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
-                const uintptr_t ad = reinterpret_cast<uintptr_t>(k0 + 9 * mid);
-                const uint32_t o = (uint32_t)(ad & 3);
-                const uint32_t ST_GAS *w = reinterpret_cast<const uint32_t ST_GAS *>(ad - o);
-                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-                const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, o), y = __builtin_amdgcn_alignbyte(w2, w1, o);
-                const uint32_t z = (uint32_t)(((uint64_t)w2 >> (8 * o)) & 0xffu);
-                const uint32_t tag = x & 0xffu;
-                // payload bytes 1..8 little-endian in (lo32, hi32), then big-endian order
-                const uint32_t p0 = (x >> 8) | (y << 24), p1 = (y >> 8) | (z << 24);
-                const uint64_t pv = ((uint64_t)__builtin_bswap32(p0) << 32) | __builtin_bswap32(p1);
+                uint32_t tag;
+                uint64_t pv;
+                krec9_load(k0 + 9 * mid, tag, pv);
                 const int c = tag != KEYTAG_INT ? (tag < KEYTAG_INT ? -1 : 1) : (pv < kv ? -1 : (pv > kv ? 1 : 0));
                 hit |= c == 0;
                 if (c < 0) lo = mid + 1; else hi = mid;

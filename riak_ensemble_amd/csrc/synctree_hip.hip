@@ -1311,6 +1311,7 @@ struct IngestIn {
     uint32_t *clevel_out;
     uint32_t *seg_out;
     uint64_t n_rejected;
+    bool int9;               // every record an int64 key (insert_int64's packing: record i at krec + 9 i)
     bool count_rejected;     // the caller wants clevel_out's nonzero count ...
     bool rejected_counted;   // ... and the paged path counted it with its totals (n_rejected)
 };
@@ -1331,23 +1332,26 @@ static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
     CHK(sc.alloc(&bp.sseg, n));
     CHK(sc.alloc(&bp.perm, n));
     CHK(sc.alloc(&bp.bseg_off, S + 1));
+    // bucket by segment: histogram + ranks (with the key's segment), scan (=
+    // the runs' bounds), scatter
+    unsigned long long *cnt = nullptr;
+    uint32_t *rank = nullptr;
+    CHK(sc.alloc(&cnt, S + 1));
+    CHK(sc.alloc(&rank, n));
+    HIPCHK(hipMemsetAsync(cnt, 0, (S + 1) * 8, t->stream));
     if (in.seg_given) {
         HIPCHK(hipMemcpyAsync(bp.seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
+        LAUNCH(t, "bucket", k_seg_hist, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cnt, rank);
     } else {
-        LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, bp.seg);
+        LAUNCH(t, "key_segment", k_key_segment, grid_for(n), 256, 0, in.krec, in.koff, n, S - 1, bp.seg, cnt, rank);
     }
     if (in.seg_out) HIPCHK(hipMemcpyAsync(in.seg_out, bp.seg, n * 4, hipMemcpyDeviceToDevice, t->stream));
-    // bucket by segment: histogram, scan (= the runs' bounds), scatter
-    unsigned long long *cur = nullptr;
-    CHK(sc.alloc(&cur, S + 1));
-    HIPCHK(hipMemsetAsync(cur, 0, (S + 1) * 8, t->stream));
-    LAUNCH(t, "bucket", k_seg_hist, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cur);
-    CHK(exclusive_scan<uint64_t>(t, reinterpret_cast<const uint64_t *>(cur), bp.bseg_off, S + 1));
-    HIPCHK(hipMemcpyAsync(cur, bp.bseg_off, S * 8, hipMemcpyDeviceToDevice, t->stream));
-    LAUNCH(t, "bucket", k_seg_scatter, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cur, bp.sseg, bp.perm);
+    CHK(exclusive_scan<uint64_t>(t, reinterpret_cast<const uint64_t *>(cnt), bp.bseg_off, S + 1));
+    LAUNCH(t, "bucket", k_seg_scatter, grid_for(n), 256, 0, (const uint32_t *)bp.seg, (const uint32_t *)rank, n,
+           (const uint64_t *)bp.bseg_off, bp.sseg, bp.perm);
     if (t->partitioned)
         LAUNCH(t, "clamp_runs", k_clamp_runs, grid_for(S + 1), 256, 0, bp.bseg_off, S, t->part_lo, t->part_hi);
-    BatchView bv{in.krec, in.koff};
+    BatchView bv{in.krec, in.koff, in.int9};
     LAUNCH(t, "run_sort", k_run_sort, grid_for(S), 256, 0, bv, bp.perm, (const uint64_t *)bp.bseg_off, S, bp.keep);
     return ST_OK;
 }
@@ -1385,7 +1389,7 @@ static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPre
     ma.bop = in.bop;
     ma.seg_reject = reject;
     ma.seg_replace = in.seg_replace;
-    ma.bv = BatchView{in.krec, in.koff};
+    ma.bv = BatchView{in.krec, in.koff, in.int9};
     ma.bvoff = in.voff;
     ma.bvheap = in.vheap;
     ma.klen = nullptr;
@@ -2322,7 +2326,7 @@ static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8
     if (!r) {
         IngestIn in{};
         in.n = n; in.krec = krec; in.koff = dko; in.vheap = dvals; in.voff = dvo;
-        in.verify_rehash = true; in.clevel_out = dcl; in.count_rejected = dcl != nullptr;
+        in.verify_rehash = true; in.clevel_out = dcl; in.count_rejected = dcl != nullptr; in.int9 = true;
         r = ingest(t, in);
         if (!r && in.rejected_counted) { *n_corrupted = in.n_rejected; dcl_counted = true; }
     }
