@@ -19,7 +19,10 @@
 // Layout per segment s: entries [beg[s], end[s]) (slot end[s] holds the
 // ends of the last entry's key and value), entry capacity up to ecap[s]
 // (end[s] < ecap[s]), key bytes [koff[beg], koff[end]) below kcap[s], value
-// bytes [vbeg[s] = voff[beg], vend[s] = voff[end]) below vcap[s].
+// bytes [vbeg[s] = voff[beg], vend[s] = voff[end]) below vcap[s]; kbeg[s] =
+// koff[beg] (the page's first key byte: the per-segment kernels read the
+// page bounds from these S-wide arrays, consecutive segments side by side,
+// not from the entry slots a page apart).
 //
 // UNIFORM pages: when every key record of a segment has one length L (klen)
 // and every value one length V (vlen) -- int64 keys and 17-byte ObjHash
@@ -34,6 +37,7 @@
 
 struct PageMeta {
     uint64_t *beg, *end, *vbeg, *vend;   // S each: the DevTree view's seg_off / seg_end / seg_voff / seg_vend
+    uint64_t *kbeg;                      // S: koff[beg]
     uint64_t *ecap, *kcap, *vcap;        // S each: page capacities (entry slot end, key / value byte ends)
     uint16_t *klen;                      // S: the length every key record of the segment has (KLEN_MIXED: not
                                          // one length, KLEN_NONE: no entries) -- fixed-stride merge positions
@@ -152,6 +156,7 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
                 d.m.beg[s] = De;
                 d.m.end[s] = De + c;
                 d.m.vbeg[s] = Dv;
+                d.m.kbeg[s] = Dk;
                 d.m.vend[s] = Dv + (t.voff[e] - vb0);
                 d.m.ecap[s] = De + Z.v[0];
                 d.m.kcap[s] = Dk + Z.v[1];
@@ -245,14 +250,16 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
         }
         dirty[s] = 1;
         fpos[s] = fp;
-        const uint64_t b = m.beg[s], e = m.end[s];
+        // the page's bounds from the S-wide arrays (a uniform page's key bytes by stride)
+        const uint64_t b = m.beg[s], e = m.end[s], kb = m.kbeg[s], vb = m.vbeg[s], ve = m.vend[s];
+        const uint64_t kbytes = e == b ? 0 : (page_uniform(kl0, vl0) ? (uint64_t)kl0 * (e - b) : koff[e] - kb);
         SegSums x;
         x.v[0] = (e - b) + d.v[0];
-        x.v[1] = (koff[e] - koff[b]) + d.v[1];
-        x.v[2] = (voff[e] - voff[b]) + d.v[2];
+        x.v[1] = kbytes + d.v[1];
+        x.v[2] = (ve - vb) + d.v[2];
         x.v[3] = d.v[3];
         sm[s] = x;
-        const bool fits = b + x.v[0] < m.ecap[s] && koff[b] + x.v[1] <= m.kcap[s] && voff[b] + x.v[2] <= m.vcap[s];
+        const bool fits = b + x.v[0] < m.ecap[s] && kb + x.v[1] <= m.kcap[s] && vb + x.v[2] <= m.vcap[s];
         uint8_t md = fits && grow ? 1 : 2;
         const bool expl = !page_uniform(kl, vl);
         md |= (expl ? 4 : 0) | (expl && page_uniform(kl0, vl0) && e > b ? 8 : 0);
@@ -262,7 +269,7 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
             r.v[0] = c.v[0]; r.v[1] = c.v[1]; r.v[2] = c.v[2];
         }
         r.v[3] = x.v[3];
-        r.v[4] = voff[e] - voff[b];
+        r.v[4] = ve - vb;
         mode[s] = md;
         reloc[s] = r;
     }
@@ -644,7 +651,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
         if (live) {
             j0 = a.bseg_off[s]; je = a.bseg_off[s + 1];
             b = p.m.beg[s]; c = p.m.end[s] - b;
-            Kb = p.koff[b]; Vb = p.voff[b];
+            Kb = p.m.kbeg[s]; Vb = p.m.vbeg[s];
             X = p.ss[s];
             De = b; Dk = Kb; Dv = Vb; EC = p.m.ecap[s]; KC = p.m.kcap[s]; VC = p.m.vcap[s];
             if (md == 2) {
@@ -661,7 +668,8 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
         // the page as it is: uniform = entry i's offsets by stride (its slots between the first and the end are stale)
         const uint32_t L0 = live ? p.m.klen[s] : KLEN_MIXED, V0 = live ? p.m.vlen[s] : KLEN_MIXED;
         const bool stride = page_uniform(L0, V0);
-        uint64_t hi = c, khi = live ? p.koff[b + c] : 0, vhi = live ? p.voff[b + c] : 0;   // the current piece's end
+        uint64_t hi = c, khi = live ? (stride ? Kb + (uint64_t)L0 * c : p.koff[b + c]) : 0,
+                 vhi = live ? p.m.vend[s] : 0;   // the current piece's end
         uint64_t j = je;
         while (__ballot(live && j > j0)) {
             const bool mine = live && j > j0;
@@ -742,6 +750,7 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
             if (md == 2) {
                 p.m.beg[s] = De;
                 p.m.vbeg[s] = Dv;
+                p.m.kbeg[s] = Dk;
                 p.m.ecap[s] = EC;
                 p.m.kcap[s] = KC;
                 p.m.vcap[s] = VC;
@@ -759,7 +768,8 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
         if (!pg_ok(chk, b <= e && e < m.ecap[s] && m.ecap[s] <= cap_e, 20, s, e, m.ecap[s])) continue;
         if (!pg_ok(chk, koff[b] <= koff[e] && koff[e] <= m.kcap[s] && m.kcap[s] <= cap_k, 21, s, koff[e], m.kcap[s])) continue;
         if (!pg_ok(chk, voff[b] <= voff[e] && voff[e] <= m.vcap[s] && m.vcap[s] <= cap_v, 22, s, voff[e], m.vcap[s])) continue;
-        if (!pg_ok(chk, m.vbeg[s] == voff[b] && m.vend[s] == voff[e], 23, s, m.vbeg[s], voff[b])) continue;
+        if (!pg_ok(chk, m.vbeg[s] == voff[b] && m.vend[s] == voff[e] && m.kbeg[s] == koff[b], 23, s, m.vbeg[s], voff[b]))
+            continue;
         const uint32_t L = m.klen[s], V = m.vlen[s];   // the uniform lengths, if any, hold
         if (!pg_ok(chk, (L != KLEN_NONE && V != KLEN_NONE) || b == e, 25, s, e - b, L)) continue;
         if (page_uniform(L, V)) {   // offsets by stride: only the first and end slots are kept

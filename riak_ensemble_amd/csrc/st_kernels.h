@@ -607,6 +607,7 @@ struct MergeArgs {
     BatchView bv;
     const uint64_t *bvoff;
     const uint8_t *bvheap;
+    const uint64_t *kbeg;       // NULL or per segment (PageMeta::kbeg): koff[seg_off[s]]
     const uint16_t *klen;       // NULL or per segment (pages.h PageMeta::klen): every key record this long
     const uint16_t *vlen;       // NULL or per segment (PageMeta::vlen): every value this long (with klen: a uniform
                                 // page, whose per-entry offsets are by stride, pages.h)
@@ -726,7 +727,7 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             // loads of the aligned window -- a record's bytes and up to 3 of
             // its neighbour's, heaps keep slack); a different tag decides
             // by itself (its first order byte).
-            const uint8_t *k0 = a.kheap + a.koff[i0];
+            const uint8_t *k0 = a.kheap + (a.kbeg ? a.kbeg[s] : a.koff[i0]);
             const uint64_t kv = krec_be64(kb + 1);
             bool hit = false;
             while (lo < hi) {
@@ -741,7 +742,7 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             eq = hit;   // the keys of a segment are unique: an equal probe is where the search ends
             ke = L;
         } else if (L != KLEN_MIXED_) {   // every old key L bytes: entry i's key at k0 + L i, no offset loads
-            const uint8_t *k0 = a.kheap + a.koff[i0];
+            const uint8_t *k0 = a.kheap + (a.kbeg ? a.kbeg[s] : a.koff[i0]);
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
                 if (rec_cmp(k0 + L * mid, L, kb, kl) < 0) lo = mid + 1; else hi = mid;

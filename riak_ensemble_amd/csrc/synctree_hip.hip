@@ -1392,6 +1392,7 @@ static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPre
     ma.bv = BatchView{in.krec, in.koff, in.int9};
     ma.bvoff = in.voff;
     ma.bvheap = in.vheap;
+    ma.kbeg = nullptr;
     ma.klen = nullptr;
     ma.vlen = nullptr;
     ma.S = S;
@@ -1473,7 +1474,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
 // the canonical CSR first (flush_all).
 
 static void pages_free(st_tree *t, Pages &g) {
-    for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.ecap, (void *)g.m.kcap,
+    for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.kbeg, (void *)g.m.ecap, (void *)g.m.kcap,
                     (void *)g.m.vcap, (void *)g.m.klen, (void *)g.m.vlen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
     const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e, tv = g.touched_v;
@@ -1525,7 +1526,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
         st_tree *t; Pages &g; bool done = false;
         ~Undo() { if (!done) pages_free(t, g); }
     } undo{t, g};
-    for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
+    for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.kbeg, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
     CHK(dalloc_t(t, &g.m.klen, S));
     CHK(dalloc_t(t, &g.m.vlen, S));
     CHK(dalloc_t(t, &g.koff, g.cap_e));
@@ -1634,6 +1635,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         CHK(page_check_report(t, chk, "before the batch"));
     }
     MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
+    ma.kbeg = t->pg.m.kbeg;
     ma.klen = t->pg.m.klen;
     ma.vlen = t->pg.m.vlen;
     const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
@@ -1724,6 +1726,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         for (int q = 0; q < 3; q++) want.v[q] = 2 * tot[q];
         CHK(pages_build(t, t->pg_slack, want));
         ma = merge_args(view(t), in, bp, reject, S);
+        ma.kbeg = t->pg.m.kbeg;
         ma.klen = t->pg.m.klen;
         ma.vlen = t->pg.m.vlen;
     }
