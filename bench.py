@@ -395,28 +395,43 @@ def group_kernel_trace(args):
         return {'error': 'rocprofv3 not found'}
     env = dict(os.environ, TMPDIR=tempfile.gettempdir())
     d = tempfile.mkdtemp(prefix='trace_')
-    cmd = ['timeout', '-s', 'KILL', '240', prof, '--kernel-trace', '--kernel-include-regex', 'k_rehash_fused', '-f', 'csv',
-           '-d', d, '-o', 'tr', '--', sys.executable, os.path.abspath(__file__), '--trace-probe', '--ensembles',
+    cmd = ['timeout', '-s', 'KILL', '240', prof, '--kernel-trace', '--kernel-include-regex', 'k_rehash_fused|k_level16_group',
+           '-f', 'csv', '-d', d, '-o', 'tr', '--', sys.executable, os.path.abspath(__file__), '--trace-probe', '--ensembles',
            str(args.ensembles), '--ensemble-keys', str(args.ensemble_keys)]
     t0 = time.perf_counter()
     r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
-    durs = []
+    rows = []
     import csv
     for root, _, files in os.walk(d):
         for f in files:
             if f.endswith('kernel_trace.csv'):
                 for row in csv.DictReader(open(os.path.join(root, f))):
-                    if 'k_rehash_fused' in row.get('Kernel_Name', ''):
-                        durs.append((int(row['Start_Timestamp']), int(row['End_Timestamp']) - int(row['Start_Timestamp'])))
+                    nm = row.get('Kernel_Name', '')
+                    if 'k_rehash_fused' in nm or 'k_level16_group' in nm:
+                        rows.append((int(row['Start_Timestamp']), int(row['End_Timestamp']), 'k_rehash_fused' in nm))
     shutil.rmtree(d, ignore_errors=True)
-    if r.returncode != 0 or len(durs) < 3:
-        return {'error': 'rc=%d, %d launches: %s' % (r.returncode, len(durs), r.stderr.decode()[-300:])}
-    durs.sort()
-    ms = [x[1] / 1e6 for x in durs[2:]]
+    # one st_rehash_group = the fused launch (K1 + level H of every window)
+    # and one k_level16_group launch per level above: its kernels' summed
+    # durations, and its GPU span (first start to last end)
+    rows.sort()
+    calls = []
+    for st, en, fused in rows:
+        if fused or not calls:
+            calls.append([st, en, 0.0, 0])
+        c = calls[-1]
+        c[1] = max(c[1], en)
+        c[2] += (en - st) / 1e6
+        c[3] += 1
+    if r.returncode != 0 or len(calls) < 3:
+        return {'error': 'rc=%d, %d calls: %s' % (r.returncode, len(calls), r.stderr.decode()[-300:])}
+    ms = [c[2] for c in calls[2:]]
+    span = [(c[1] - c[0]) / 1e6 for c in calls[2:]]
     return {'kernel_ms_mean': round(sum(ms) / len(ms), 4), 'kernel_ms_min': round(min(ms), 4),
-            'kernel_ms_max': round(max(ms), 4), 'launches': len(ms), 'pass_s': round(time.perf_counter() - t0, 1),
-            'what': 'rocprofv3 --kernel-trace of a child process: the group launch (k_rehash_fused<GROUP>) over the '
-                    'same %d x %d-key ensembles, launches 3..10' % (args.ensembles, args.ensemble_keys)}
+            'kernel_ms_max': round(max(ms), 4), 'span_ms_mean': round(sum(span) / len(span), 4),
+            'launches_per_call': calls[2][3], 'calls': len(ms), 'pass_s': round(time.perf_counter() - t0, 1),
+            'what': 'rocprofv3 --kernel-trace of a child process: each group rehash over the same %d x %d-key ensembles '
+                    '(the fused launch k_rehash_fused<GROUP> + one k_level16_group launch per level above level H), '
+                    'its kernels\' summed durations; calls 3..10' % (args.ensembles, args.ensemble_keys)}
 
 
 # ---------------------------------------------------------------- legs
@@ -877,7 +892,7 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, trace=Non
         synctree_hip.rehash_group(trees)
     g_n, g_ms = trees[0].kernel_stats('rehash_group')
     trees[0].set_timing(False)
-    g_evt = g_ms / max(g_n, 1)
+    g_evt = g_ms / max(reps, 1)   # a group rehash: the fused launch + a level launch per level above level H
     S = trees[0].segments
     H = trees[0].height
     # SURVEY §8(d) bytes per tree: 17 B per key (values) + a 17-B entry per
@@ -893,7 +908,7 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, trace=Non
     # the roofline's launch time: rocprof's mean of the group launch (a child
     # process traced on this box) when available, else the span below
     k_ms = trace['kernel_ms_mean'] if trace and 'kernel_ms_mean' in trace else g_avg
-    k_src = ('rocprofv3 --kernel-trace mean of the group launch (ensembles.kernel_trace)' if k_ms is not g_avg else
+    k_src = ('rocprofv3 --kernel-trace mean of a group rehash\'s kernels (ensembles.kernel_trace)' if k_ms is not g_avg else
              'GPU span of %d back-to-back group rehashes on trees[0]\'s stream / %d (host preparation between them '
              'included: an upper bound of the launch)' % (reps, reps))
     g_gbs = E * tree_bytes / (k_ms / 1e3) / 1e9 if k_ms > 0 else 0.0
@@ -918,7 +933,8 @@ def _bench_ensembles(synctree_hip, dist, coll_dev, args, local, torch, trace=Non
                          'bytes_per_tree': tree_bytes, 'bytes_per_tree_incl_metadata': meta_bytes,
                          'tile_bytes_per_tree': mem0['tiles'],
                          'sample_nonempty_segments': nonempty, 'sample_present_inner': pinner,
-                         'kernel': K1_KERNEL + '<GROUP, 8 waves per window, 6 waves per SIMD>',
+                         'kernel': K1_KERNEL + '<GROUP, 8 waves per window, 6 waves per SIMD> (K1 + level H) + k_level16_group '
+                                   '(one launch per level above)',
                          'note': 'SURVEY §8(d): per tree 17 B of value per key + a 17-B entry per present node '
                                  '(non-empty segments + present inner nodes, mean of %d sampled trees)' % len(samp)},
             'kernel_trace': trace,

@@ -313,6 +313,10 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
             rw_global(GROUP ? group[gi].tag : t.tag)[slot] = (uint16_t)tg;
             if (l == 1) { rw_global(GROUP ? group[gi].md5 : t.md5)[0] = e; rw_global(GROUP ? group[gi].tag : t.tag)[0] = (uint16_t)tg; }
         }
+        // a group stops after level H: the levels above, every tree's nodes of
+        // a level at once, are k_level16_group's (the window's 16- and 1-lane
+        // chains held its LDS and its place on the CU for ~13 us)
+        if (GROUP) break;
         if (l <= lmin) break;
         if (ph == 0) {          // level-H entries into the H-1 messages
             if (act && tg) {
@@ -396,4 +400,23 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
     }
 #undef RFT
 #undef RF_STAMP
+}
+
+// The levels above level H of a group rehash (st_rehash_group: its fused
+// launch stops after level H): level l of every tree of the group in one
+// launch, a lane per node (hash_node16 from the children's slot entries),
+// node i of the launch = tree i / nper, node i % nper of the level.
+__global__ void __launch_bounds__(64) k_level16_group(DevTree t0, const TreeTiles *__restrict__ group, uint32_t ntrees,
+                                                      uint32_t l) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
+    const uint64_t nper = t0.base[l + 1] - t0.base[l];
+    const uint64_t total = nper * ntrees;
+    for (uint64_t i = gtid(); i < total; i += gstride()) {
+        const uint32_t gi = (uint32_t)(i / nper);
+        DevTree d = t0;
+        d.md5 = rw_global(group[gi].md5);
+        d.tag = rw_global(group[gi].tag);
+        hash_node16(d, l, i - (uint64_t)gi * nper, reg);
+    }
 }

@@ -1141,6 +1141,57 @@ static int levels16(st_tree *t, uint32_t top, const uint8_t *mask) {
     return ST_OK;
 }
 
+// ST_LEVEL_STAMPS=1: the fused rehash's per-window phase stamps (100 MHz
+// wall clock + shader cycles, 32 words a window) summarised to stderr.
+static void fused_stamps_report(const std::vector<uint64_t> &h, uint32_t nwg) {
+    uint64_t t0 = ~0ull;
+    for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 32]);
+    if (const char *dump = getenv("ST_STAMP_DUMP")) {   // raw per-window stamps (ticks from t0)
+        if (FILE *f = fopen(dump, "a")) {
+            for (uint32_t w = 0; w < nwg; w++) {
+                for (int k = 0; k < 16; k++) fprintf(f, "%lld ", h[w * 32 + k] ? (long long)(h[w * 32 + k] - t0) : -1ll);
+                fprintf(f, "\n");
+            }
+            fclose(f);
+        }
+    }
+    static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
+                                    "H-2 hashed", "mail stored", "cnt won", "mail read", "climb 1st hashed",
+                                    "-", "-", "-", "climb last hashed", "exit"};
+    for (int k = 0; k < 16; k++) {
+        std::vector<double> v;
+        for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
+        if (v.empty()) continue;
+        std::sort(v.begin(), v.end());
+        fprintf(stderr, "fused stamp %d %-15s n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, names[k], v.size(), v[0],
+                v[v.size() / 2], v.back());
+    }
+    // shader cycles and clock (s_memtime / s_memrealtime) over the hash intervals
+    const int iv[5][2] = {{1, 2}, {3, 4}, {5, 6}, {9, 10}, {10, 14}};
+    for (auto &q : iv) {
+        double cyc = 0, us = 0;
+        int m = 0;
+        for (uint32_t w = 0; w < nwg; w++) {
+            const uint64_t *r = &h[w * 32];
+            if (!r[q[0]] || !r[q[1]]) continue;
+            cyc += (double)(r[16 + q[1]] - r[16 + q[0]]);
+            us += (r[q[1]] - r[q[0]]) / 100.0;
+            m++;
+        }
+        if (m) fprintf(stderr, "fused cycles %s -> %s: %.0f cycles, %.2f us, %.2f GHz (n=%d)\n", names[q[0]], names[q[1]],
+                       cyc / m, us / m, cyc / us / 1e3, m);
+    }
+    for (int k = 1; k < 16; k++) {   // each phase from its window's own start (a group's windows start over the launch)
+        std::vector<double> dur;
+        for (uint32_t w = 0; w < nwg; w++)
+            if (h[w * 32] && h[w * 32 + k]) dur.push_back((h[w * 32 + k] - h[w * 32]) / 100.0);
+        if (dur.empty()) continue;
+        std::sort(dur.begin(), dur.end());
+        fprintf(stderr, "fused from start %-17s n=%zu min %7.2f med %7.2f p90 %7.2f max %7.2f us\n", names[k], dur.size(),
+                dur[0], dur[dur.size() / 2], dur[dur.size() * 9 / 10], dur.back());
+    }
+}
+
 // Full rehash.  W == 16, H >= 3: ONE launch of k_rehash_fused, a workgroup
 // per level-(H-2) window: K1 over the window's tiles, its levels H..H-2 from
 // LDS, the levels above by last-arriving workgroups.  Other geometries: K1
@@ -1175,43 +1226,7 @@ static int rehash_tiled(st_tree *t) {
         std::vector<uint64_t> h((uint64_t)nwg * 32);
         HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, t->stream));
         CHK(tsync(t));
-        uint64_t t0 = ~0ull;
-        for (uint32_t w = 0; w < nwg; w++) t0 = std::min(t0, h[w * 32]);
-        if (const char *dump = getenv("ST_STAMP_DUMP")) {   // raw per-window stamps (ticks from t0)
-            if (FILE *f = fopen(dump, "a")) {
-                for (uint32_t w = 0; w < nwg; w++) {
-                    for (int k = 0; k < 16; k++) fprintf(f, "%lld ", h[w * 32 + k] ? (long long)(h[w * 32 + k] - t0) : -1ll);
-                    fprintf(f, "\n");
-                }
-                fclose(f);
-            }
-        }
-        static const char *names[16] = {"start", "K1 done", "H hashed", "H barrier", "H-1 hashed", "H-1 barrier",
-                                        "H-2 hashed", "mail stored", "cnt won", "mail read", "climb 1st hashed",
-                                        "-", "-", "-", "climb last hashed", "exit"};
-        for (int k = 0; k < 16; k++) {
-            std::vector<double> v;
-            for (uint32_t w = 0; w < nwg; w++) if (h[w * 32 + k]) v.push_back((h[w * 32 + k] - t0) / 100.0);
-            if (v.empty()) continue;
-            std::sort(v.begin(), v.end());
-            fprintf(stderr, "fused stamp %d %-15s n=%4zu min %7.2f med %7.2f max %7.2f us\n", k, names[k], v.size(), v[0],
-                    v[v.size() / 2], v.back());
-        }
-        // shader cycles and clock (s_memtime / s_memrealtime) over the hash intervals
-        const int iv[5][2] = {{1, 2}, {3, 4}, {5, 6}, {9, 10}, {10, 14}};
-        for (auto &q : iv) {
-            double cyc = 0, us = 0;
-            int m = 0;
-            for (uint32_t w = 0; w < nwg; w++) {
-                const uint64_t *r = &h[w * 32];
-                if (!r[q[0]] || !r[q[1]]) continue;
-                cyc += (double)(r[16 + q[1]] - r[16 + q[0]]);
-                us += (r[q[1]] - r[q[0]]) / 100.0;
-                m++;
-            }
-            if (m) fprintf(stderr, "fused cycles %s -> %s: %.0f cycles, %.2f us, %.2f GHz (n=%d)\n", names[q[0]], names[q[1]],
-                           cyc / m, us / m, cyc / us / 1e3, m);
-        }
+        fused_stamps_report(h, nwg);
         return ST_OK;
     }
     const uint64_t ntl = num_tiles(t);
@@ -2608,8 +2623,26 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     uint32_t mh = 0;
     for (uint32_t i = 0; i < n; i++) mh = std::max(mh, trees[i]->mh_bytes);
     const uint32_t mhb = fused_mh_bytes(mh, nwin);
-    LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(mhb), view(t), h[0],
-           (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr, mhb);
+    static const int stamp = getenv("ST_LEVEL_STAMPS") ? atoi(getenv("ST_LEVEL_STAMPS")) : 0;
+    if (!stamp) {
+        LAUNCH(t, "rehash_group", (k_rehash_fused<false, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(mhb), view(t), h[0],
+               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, (uint64_t *)nullptr, mhb);
+    } else {   // diagnostic: the per-window phase stamps (fused_stamps_report)
+        uint64_t *st = nullptr;
+        CHK(sc.alloc(&st, nwg * 32));
+        HIPCHK(hipMemsetAsync(st, 0, nwg * 32 * 8, t->stream));
+        LAUNCH(t, "rehash_group", (k_rehash_fused<true, true, 8>), (uint32_t)nwg, 512, fused_lds_bytes(mhb), view(t), h[0],
+               (const TreeTiles *)dtt, nwin, (uint64_t)0, 1u, st, mhb);
+        std::vector<uint64_t> hs(nwg * 32);
+        HIPCHK(hipMemcpyAsync(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost, t->stream));
+        CHK(tsync(t));
+        fused_stamps_report(hs, (uint32_t)nwg);
+    }
+    // the levels above level H: every tree's nodes of a level in one launch
+    const DevTree d0 = view(t);
+    for (uint32_t l = t->H - 1; l >= 1; l--)
+        LAUNCH(t, "rehash_group", k_level16_group, grid_for((d0.base[l + 1] - d0.base[l]) * n, 64, 65536), 64,
+               (size_t)64 * lane_region_bytes(16), d0, (const TreeTiles *)dtt, n, l);
     // every tree's device-error word is checked (tsync): a tree whose climb
     // timed out is left in error (ST_EDEVICE returned), the others are clean
     int first = ST_OK;

@@ -110,14 +110,14 @@ def test_mailbox_timeout_is_a_device_error(segments, skip):
     dev.rehash()                      # a clean full rehash clears the error
     dev.sync()
     _level_parity(dev, ora)
-    # the same through the group rehash: only the faulted tree is in error
+    # the group rehash hands no window root over through a mailbox (its
+    # levels above level H are launches of their own, k_level16_group): the
+    # knob leaves it untouched, and both trees get their oracle's levels
     other, ora2 = _pair(segments, 50_000, workload.SEED ^ 0xB0C ^ segments)
     dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, skip)
-    with pytest.raises(_lib.DeviceError, match='mailbox'):
-        synctree_hip.rehash_group([other, dev])
+    synctree_hip.rehash_group([other, dev])
+    _level_parity(dev, ora)
     _level_parity(other, ora2)
-    with pytest.raises(_lib.DeviceError):
-        dev.top_hash()
     dev.debug_knob(_lib.ST_DBG_SKIP_MAIL, -1)
     synctree_hip.rehash_group([other, dev])
     _level_parity(dev, ora)
