@@ -1253,24 +1253,22 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
         // tree unchanged since, builds the tiles for the fused kernel.
         if (t->tiles_valid || t->tiles_wanted || t->partitioned) return rehash_tiled(t);
         t->tiles_wanted = true;
-        DevTree d = view(t);
         CHK(ensure_perm_any(t));
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm,
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)t->seg_perm,
                (const uint8_t *)nullptr, (const PrefixState *)nullptr, (const uint32_t *)nullptr);
-        if (t->H == 0) return ST_OK;
-        if (t->W == 16) return levels16(t, t->H, nullptr);
-        return rehash_levels(t, t->H, nullptr);
-    }
-    DevTree d = view(t);
-    if (hb.list) {
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)nullptr, mask, ps,
+    } else if (hb.list) {
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)nullptr, mask, ps,
                (const uint32_t *)nullptr, hb);
     } else {
         CHK(ensure_perm(t));
-        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, d, (const uint32_t *)t->seg_perm, mask,
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)t->seg_perm, mask,
                ps, (const uint32_t *)nullptr);
     }
     if (t->H == 0) return ST_OK;
+    // the inner levels (mask NULL: every node).  W == 16, H >= 3: levels
+    // H..H-2 of each level-(H-2) subtree in one workgroup from LDS, then the
+    // per-level kernels above
+    const DevTree d = view(t);
     if (t->W == 16 && t->H >= 3) {
         LAUNCH(t, "level_rehash", k_levels3_16, (uint32_t)(t->base[t->H - 1] - t->base[t->H - 2]), 256, levels3_16_lds_bytes(),
                d, mask);
