@@ -89,7 +89,12 @@ int st_create(uint64_t width, uint64_t segments, int device, st_tree **out);
 void st_destroy(st_tree *t);
 
 /* Enqueue this tree's work on an external hipStream_t (e.g. torch's
- * current stream); NULL restores the tree's own stream. */
+ * current stream); NULL restores the tree's own stream.  The library tracks
+ * only the work it enqueues itself: work the CALLER puts on that stream
+ * (or any other) must be complete, or ordered by the caller, before a
+ * multi-tree call (st_rehash_group, st_tops_to_device*) reads the tree --
+ * those calls skip the synchronisation of a tree with nothing of the
+ * library's pending. */
 int st_set_stream(st_tree *t, void *hip_stream);
 int st_sync(st_tree *t);
 
