@@ -657,6 +657,9 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
     tb2.insert_batch([k for k, _ in mut2], [v for _, v in mut2])
     ta = synctree_hip.DeviceTree(device=local)
     ta.insert_int64_device(keys_d.data_ptr(), vals_d.data_ptr(), n, 17)
+    # a peer exchanges over and over: the local tree's compare state (its
+    # first compare allocates it) is warmed by a plan-only exchange first
+    assert ta.exchange_plan(tb2)[0] == 'ok'
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res_apply = ta.exchange_apply(tb2)
@@ -682,7 +685,8 @@ def _bench_compare(synctree_hip, tree_a, keys_d, vals_d, n, local, torch, reps=2
             'ms_per_compare_incl_python_decode': round(dt_host * 1e3, 4),
             'exchange_apply_ms': round(dt_apply * 1e3, 4),
             'exchange_apply': 'st_exchange_apply: compare + valid_obj_hash select + one batched insert/3 of the %d '
-                              'newer remote values (dirty-path rehash); trees converge (equal top hashes)' % len(mut2),
+                              'newer remote values (dirty-path rehash); trees converge (equal top hashes); one call, '
+                              'the local tree\'s compare state warmed by an exchange_plan first' % len(mut2),
             'what': 'config3: 10M vs 10M keys, every 1000th non-empty segment differs; K3 in one launch (frontier, '
                     'verify + merge-join, each wave\'s records placed after the higher waves\' by their published '
                     'counts) with the ordered diff records left on the device; one host round trip per compare'}
