@@ -612,6 +612,7 @@ struct MergeArgs {
     const uint16_t *vlen;       // NULL or per segment (PageMeta::vlen): every value this long (with klen: a uniform
                                 // page, whose per-entry offsets are by stride, pages.h)
     uint64_t S;
+    uint64_t plo, phi;          // the segments the batch keeps: [0, S), or a partition's (k_clamp_runs)
 };
 
 // Running sums of the merge: per sorted batch record (BatchSums: eq = kept and
@@ -693,9 +694,13 @@ struct RecAt {
 __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint32_t *pos, BatchSums *bs, RecAt *rat,
                              SegSums *sd = nullptr, uint8_t *dirty = nullptr, unsigned long long *fpos = nullptr,
                              PageBounds pb = PageBounds{0, 0, 0, nullptr}) {
+    // a record is kept iff it lies in the kept segments' records [A, B) (the
+    // runs are sorted by segment, and k_clamp_runs empties the runs outside
+    // [plo, phi)): a wave-uniform check, not a load of its own run's bounds
+    const uint64_t A = a.bseg_off[a.plo], B = a.bseg_off[a.phi];
     for (uint64_t j = gtid(); j < n; j += gstride()) {
+        if (j < A || j >= B) continue;
         const uint64_t s = sseg[j];
-        if (j < a.bseg_off[s] || j >= a.bseg_off[s + 1]) continue;
         BatchSums f(0);
         if (a.seg_reject && a.seg_reject[s]) { pos[j] = 0; bs[j] = f; continue; }
         const uint64_t i0 = a.seg_off ? a.seg_off[s] : 0;

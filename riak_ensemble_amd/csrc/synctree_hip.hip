@@ -1388,7 +1388,8 @@ static int verify_batch_paths(st_tree *t, const BatchPrep &bp, Scratch &sc, uint
     return ST_OK;
 }
 
-static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPrep &bp, const uint8_t *reject, uint64_t S) {
+static MergeArgs merge_args(const st_tree *t, const DevTree &d, const IngestIn &in, const BatchPrep &bp, const uint8_t *reject,
+                            uint64_t S) {
     MergeArgs ma;
     ma.seg_off = d.seg_off;
     ma.seg_end = d.seg_end;
@@ -1409,6 +1410,8 @@ static MergeArgs merge_args(const DevTree &d, const IngestIn &in, const BatchPre
     ma.klen = nullptr;
     ma.vlen = nullptr;
     ma.S = S;
+    ma.plo = t->partitioned ? t->part_lo : 0;   // the runs batch_prepare kept (k_clamp_runs)
+    ma.phi = t->partitioned ? t->part_hi : S;
     return ma;
 }
 
@@ -1427,7 +1430,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
     }
 
     // merge (k_merge_pos / k_merge_old / k_merge_new): count, scan, write
-    MergeArgs ma = merge_args(view(t), in, bp, reject, S);
+    MergeArgs ma = merge_args(t, view(t), in, bp, reject, S);
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *ss = nullptr, *sx = nullptr;
     CHK(sc.alloc(&ss, S + 1));
@@ -1647,7 +1650,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
                (const uint64_t *)t->pg.voff, S, t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk);
         CHK(page_check_report(t, chk, "before the batch"));
     }
-    MergeArgs ma = merge_args(view(t), in, bp, nullptr, S);
+    MergeArgs ma = merge_args(t, view(t), in, bp, nullptr, S);
     ma.kbeg = t->pg.m.kbeg;
     ma.klen = t->pg.m.klen;
     ma.vlen = t->pg.m.vlen;
@@ -1738,7 +1741,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         PageSums want(0);
         for (int q = 0; q < 3; q++) want.v[q] = 2 * tot[q];
         CHK(pages_build(t, t->pg_slack, want));
-        ma = merge_args(view(t), in, bp, reject, S);
+        ma = merge_args(t, view(t), in, bp, reject, S);
         ma.kbeg = t->pg.m.kbeg;
         ma.klen = t->pg.m.klen;
         ma.vlen = t->pg.m.vlen;
