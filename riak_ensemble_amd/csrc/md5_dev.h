@@ -487,7 +487,9 @@ __device__ __forceinline__ void node16_block(int k, const uint32_t pf[16], const
 // One compress in a rolled loop: these kernels run a few waves per CU once
 // through the code, so straight-line unrolled MD5 (~14 KB) would be bound by
 // instruction-cache misses.
-template <bool UNROLL = false>
+// TPUT: the throughput form of the compression (a level of many nodes hashed
+// at once, k_level16_group) instead of the latency form (a chain)
+template <bool UNROLL = false, bool TPUT = false>
 __device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[16], uint32_t out[4], uint32_t n = 16) {
     uint32_t st[4];
     init(st);
@@ -495,7 +497,8 @@ __device__ __forceinline__ void md5_node16(const uint32_t pf[16], const uint4 h[
     for (int k = 0; k < 5; k++) {
         uint32_t m[16];
         node16_block(k, pf, h, m, n);
-        compress_lat(st, m);
+        if (TPUT) compress<true>(st, m);
+        else compress_lat(st, m);
     }
     out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; out[3] = st[3];
 }

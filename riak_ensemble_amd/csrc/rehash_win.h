@@ -404,19 +404,76 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
 
 // The levels above level H of a group rehash (st_rehash_group: its fused
 // launch stops after level H): level l of every tree of the group in one
-// launch, a lane per node (hash_node16 from the children's slot entries),
-// node i of the launch = tree i / nper, node i % nper of the level.
+// launch, a lane per node, node i of the launch = tree i / nper, node i % nper
+// of the level.  A node with all 16 children present (nearly every node of
+// these levels) hashes from registers (md5_node16); the others stage their
+// packed message in one of 16 LDS regions the wave's partial nodes take in
+// turns, so a 64-lane workgroup holds 5.6 KB of LDS, not 22 KB (which had
+// capped the launch at 7 waves a CU).
+#define LG_REGIONS 16
+__host__ __device__ __forceinline__ uint32_t level16_group_lds_bytes() { return LG_REGIONS * lane_region_bytes(16); }
 __global__ void __launch_bounds__(64) k_level16_group(DevTree t0, const TreeTiles *__restrict__ group, uint32_t ntrees,
                                                       uint32_t l) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t *reg = lds + threadIdx.x * lane_region_bytes(16);
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t nper = t0.base[l + 1] - t0.base[l];
     const uint64_t total = nper * ntrees;
-    for (uint64_t i = gtid(); i < total; i += gstride()) {
-        const uint32_t gi = (uint32_t)(i / nper);
-        DevTree d = t0;
-        d.md5 = rw_global(group[gi].md5);
-        d.tag = rw_global(group[gi].tag);
-        hash_node16(d, l, i - (uint64_t)gi * nper, reg);
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 64; i0 < total; i0 += (uint64_t)gridDim.x * 64) {   // wave-uniform
+        const uint64_t i = i0 + lane;
+        const bool valid = i < total;
+        const uint32_t gi = valid ? (uint32_t)(i / nper) : 0u;
+        const uint64_t b = valid ? i - (uint64_t)gi * nper : 0;
+        uint4 ST_GAS *md5 = rw_global(group[gi].md5);
+        uint16_t ST_GAS *tag = rw_global(group[gi].tag);
+        const uint64_t slot = t0.base[l] + b, c0 = t0.base[l + 1] + b * 16;
+        uint32_t tg[16];
+        uint4 h[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            tg[j] = valid ? tag[c0 + j] : 0u;
+            h[j] = valid ? md5[c0 + j] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        uint32_t full = valid ? 1u : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; j++) full &= (tg[j] >> 8) & 1u;
+        uint32_t dg[4] = {0u, 0u, 0u, 0u};
+        uint32_t len = 0;
+        if (full) {
+            uint32_t pf[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) pf[j] = tg[j] & 0xffu;
+            stmd5::md5_node16<true, true>(pf, h, dg);
+            len = 1;
+        }
+        // the partial nodes, 16 at a time through the shared regions (their
+        // children loaded again: the registers above are free by then)
+        const uint64_t pm = __ballot(valid && !full);
+        const uint32_t rank = __builtin_popcountll(pm & ((1ull << lane) - 1ull));
+        const uint32_t np = __builtin_popcountll(pm);
+        for (uint32_t r0 = 0; r0 < np; r0 += LG_REGIONS) {
+            if (valid && !full && rank >= r0 && rank < r0 + LG_REGIONS) {
+                uint8_t *reg = lds + (rank - r0) * lane_region_bytes(16);
+                MsgWriter mw;
+                mw.init(reg);
+                for (int j = 0; j < 16; j++) {
+                    const uint32_t g = tag[c0 + j];
+                    if (g & TAG_PRESENT) mw.entry(g, md5[c0 + j]);
+                }
+                len = mw.finish();
+                if (len) stmd5::md5_lds(reg, len, dg);
+            }
+            __builtin_amdgcn_wave_barrier();   // the regions are reused by the next 16
+        }
+        if (valid) {
+            uint32_t ot = 0;
+            uint4 e = make_uint4(0u, 0u, 0u, 0u);
+            if (len) {
+                e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+                ot = TAG_PRESENT;
+                md5[slot] = e;
+            }
+            tag[slot] = (uint16_t)ot;
+            if (l == 1) { md5[0] = e; tag[0] = (uint16_t)ot; }
+        }
     }
 }

@@ -2643,7 +2643,7 @@ extern "C" int st_rehash_group(st_tree **trees, uint32_t n) {
     const DevTree d0 = view(t);
     for (uint32_t l = t->H - 1; l >= 1; l--)
         LAUNCH(t, "rehash_group", k_level16_group, grid_for((d0.base[l + 1] - d0.base[l]) * n, 64, 65536), 64,
-               (size_t)64 * lane_region_bytes(16), d0, (const TreeTiles *)dtt, n, l);
+               (size_t)level16_group_lds_bytes(), d0, (const TreeTiles *)dtt, n, l);
     // every tree's device-error word is checked (tsync): a tree whose climb
     // timed out is left in error (ST_EDEVICE returned), the others are clean
     int first = ST_OK;
