@@ -2136,7 +2136,7 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
             }
             s = hb.list[lo * hb.cap + (i - pre[lo])];
         } else {
-            s = perm[i];
+            s = perm ? perm[i] : i;   // no perm: segment order (a few marked segments)
         }
         const uint64_t slot = t.base[L1] + s;
         if (mask && !mask[slot]) continue;

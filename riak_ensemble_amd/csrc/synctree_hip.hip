@@ -1244,8 +1244,11 @@ static int rehash_tiled(st_tree *t) {
 // per-level kernels above; other geometries: one k_level_hash launch per level.
 // ps: the prefix states of a streaming batch's verify (k_verify_cap) or NULL.
 // hb (a streaming batch's list, k_page_place): the changed segments in bins by blocks left.
+// few (mask): so few segments are marked that ordering them by length costs
+// more than it saves (the length permutation is stale after every merge):
+// they are hashed in segment order.
 static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = nullptr,
-                      HashBins hb = HashBins{nullptr, nullptr, 0, 0, 0}) {
+                      HashBins hb = HashBins{nullptr, nullptr, 0, 0, 0}, bool few = false) {
     if (!mask) {
         // The first full rehash after a mutation hashes straight from the
         // CSR (a lane per segment, no tile build: the repair path's
@@ -1259,6 +1262,9 @@ static int rehash_all(st_tree *t, const uint8_t *mask, const PrefixState *ps = n
     } else if (hb.list) {
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)nullptr, mask, ps,
                (const uint32_t *)nullptr, hb);
+    } else if (few && !t->perm_valid) {
+        LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)nullptr, mask, ps,
+               (const uint32_t *)nullptr);
     } else {
         CHK(ensure_perm(t));
         LAUNCH(t, "segment_hash", k_segment_hash_perm, grid_for(t->S), 256, 0, view(t), (const uint32_t *)t->seg_perm, mask,
@@ -1474,7 +1480,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
         // dirty-path rehash: segments whose content changed and their ancestors
         HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         LAUNCH(t, "mark_dirty", k_mark_from_segments, grid_for(S), 256, 0, view(t), (const uint8_t *)dirty, t->mark);
-        CHK(rehash_all(t, t->mark));
+        CHK(rehash_all(t, t->mark, nullptr, HashBins{nullptr, nullptr, 0, 0, 0}, n * 64 <= S));   // <= n segments dirty
     }
     t->fresh = false;
     return ST_OK;
