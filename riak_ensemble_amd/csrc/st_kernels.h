@@ -829,6 +829,13 @@ __global__ void k_merge_sums(MergeArgs a, const BatchSums *bs, const uint32_t *p
 // The MD5 state of a segment's values before the first block its merge
 // changes (k = that block; k == 0: none kept), saved by the verify of a
 // streaming batch for the hash after the merge.
+// The MD5 form of the lane-per-segment span hashes (verify, dirty hash): the
+// latency form (add3), measured faster here than the throughput form that
+// K1 uses -- these lanes wait on their own chains (config-5 batch: hash 0.301
+// -> 0.287 ms, verify 0.381 -> 0.377 ms; profiles/r06ak_span_md5_form_ab/).
+#ifndef ST_SPAN_TPUT
+#define ST_SPAN_TPUT false
+#endif
 struct PrefixState {
     uint4 st;
     uint64_t k;
@@ -869,7 +876,7 @@ __global__ void __launch_bounds__(256) k_verify_cap(DevTree t, const uint32_t *p
             const uint64_t first = fpos[s];
             const uint64_t ck = first == ~0ull ? ~0ull : first / 64;
             const uint64_t v0 = t.seg_voff[s];
-            stmd5::md5_global_span<true>(t.vheap + v0, t.seg_vend[s] - v0, 0, st, ck, cap);
+            stmd5::md5_global_span<ST_SPAN_TPUT>(t.vheap + v0, t.seg_vend[s] - v0, 0, st, ck, cap);
             const uint4 e = t.md5[eslot];
             good = (et == TAG_PRESENT) && e.x == st[0] && e.y == st[1] && e.z == st[2] && e.w == st[3];
             if (ck != ~0ull && ck > 0) {
@@ -2155,7 +2162,7 @@ __global__ void __launch_bounds__(256) k_segment_hash_perm(DevTree t, const uint
         } else {
             stmd5::init(dg);
         }
-        stmd5::md5_global_span<true>(t.vheap + v0, t.seg_vend[s] - v0, k0, dg, ~0ull, cap);
+        stmd5::md5_global_span<ST_SPAN_TPUT>(t.vheap + v0, t.seg_vend[s] - v0, k0, dg, ~0ull, cap);
         const uint4 e = make_uint4(dg[0], dg[1], dg[2], dg[3]);
         t.md5[slot] = e;
         t.tag[slot] = TAG_PRESENT;
