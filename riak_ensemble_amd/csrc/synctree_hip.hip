@@ -1568,6 +1568,9 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     pages_free(t, t->pg);
     t->pg = g;
     undo.done = true;
+    // while the pages hold the segments no merge writes a CSR: the spare set
+    // (a whole retired CSR) is released, the fold back allocates its own
+    csr_free(t, t->spare);
     t->perm_valid = false;
     return ST_OK;
 }
