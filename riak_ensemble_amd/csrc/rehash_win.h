@@ -119,6 +119,9 @@ __device__ __forceinline__ T *rw_global(T *p) {
     return p;
 }
 #endif
+#ifndef RW_K1_TPUT
+#define RW_K1_TPUT true   // K1's MD5 in the throughput form (§3.1 cost model)
+#endif
 template <bool STAMP, bool GROUP, int NW>
 __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree t, TreeTiles tt0, const TreeTiles *__restrict__ group,
                                                           uint32_t nwin, uint64_t root0, uint32_t lmin, uint64_t *stamps,
@@ -235,11 +238,11 @@ __global__ void __launch_bounds__(NW * 64, GROUP ? 6 : 1) k_rehash_fused(DevTree
                             y2 = r + 2 >= b.R ? tile_synth(r + 2, b.ln) : b.x2, y3 = tile_synth(r + 3, b.ln);
                 const uint32_t m[16] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w,
                                         y2.x, y2.y, y2.z, y2.w, y3.x, y3.y, y3.z, y3.w};
-                if (b.k < nb) stmd5::compress<true>(st, m);
+                if (b.k < nb) stmd5::compress<RW_K1_TPUT>(st, m);
             } else {             // the common case: the loaded registers feed the compression as they are
                 const uint32_t m[16] = {b.x0.x, b.x0.y, b.x0.z, b.x0.w, b.x1.x, b.x1.y, b.x1.z, b.x1.w,
                                         b.x2.x, b.x2.y, b.x2.z, b.x2.w, b.x3.x, b.x3.y, b.x3.z, b.x3.w};
-                if (b.k < nb) stmd5::compress<true>(st, m);
+                if (b.k < nb) stmd5::compress<RW_K1_TPUT>(st, m);
             }
             if (b.k + 1 == b.B) {
                 if (nb) put_entry(b.li, st);
