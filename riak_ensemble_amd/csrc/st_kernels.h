@@ -187,17 +187,39 @@ __device__ __forceinline__ void copy_bytes(uint8_t *d, const uint8_t *s, uint64_
 // Ingest helpers
 
 // int64 keys -> key records (9 bytes: tag 0, <<K:64/big>> with sign bit flipped)
+// slack: zero bytes the heap keeps after the records (over-reads), written here
 __global__ void k_pack_int64(const int64_t *keys, uint64_t n, uint8_t *kheap, uint64_t *koff, uint64_t *voff,
-                             uint32_t vlen) {
+                             uint32_t vlen, uint32_t slack = 0) {
     for (uint64_t i = gtid(); i <= n; i += gstride()) {
         koff[i] = 9 * i;
         voff[i] = (uint64_t)vlen * i;
-        if (i == n) break;
+        if (i == n) {
+            for (uint32_t b = 0; b < slack; b++) kheap[9 * n + b] = 0;
+            break;
+        }
         uint64_t k = (uint64_t)keys[i] ^ 0x8000000000000000ull;
         uint8_t *p = kheap + 9 * i;
         p[0] = KEYTAG_INT;
         uint64_t be = __builtin_bswap64(k);
         __builtin_memcpy(p + 1, &be, 8);
+    }
+}
+
+// Several buffers zeroed by one launch (each a memset kernel of its own
+// otherwise, ~5 us apiece on a batch's critical path).  Spans start 16-byte
+// aligned (device allocations); a span's last n % 16 bytes go byte by byte.
+#define ZS_MAX 6
+struct ZeroSpans {
+    uint8_t *p[ZS_MAX];
+    uint64_t n[ZS_MAX];
+    uint32_t k;
+};
+__global__ void __launch_bounds__(256) k_zero_spans(ZeroSpans z) {
+    for (uint32_t q = 0; q < z.k; q++) {
+        uint4 *w = reinterpret_cast<uint4 *>(z.p[q]);
+        const uint64_t nw = z.n[q] / 16;
+        for (uint64_t i = gtid(); i < nw; i += gstride()) w[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t i = nw * 16 + gtid(); i < z.n[q]; i += gstride()) z.p[q][i] = 0;
     }
 }
 

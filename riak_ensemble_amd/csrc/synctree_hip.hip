@@ -1344,7 +1344,9 @@ struct BatchPrep {
     uint8_t *keep = nullptr;
 };
 
-static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
+// zero (optional): more buffers the caller needs zeroed, cleared by the same
+// launch as the histogram's counters
+static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp, const ZeroSpans *zero = nullptr) {
     const uint64_t n = in.n, S = t->S;
     CHK(sc.alloc(&bp.keep, n));
     CHK(sc.alloc(&bp.seg, n));
@@ -1357,7 +1359,13 @@ static int batch_prepare(st_tree *t, IngestIn &in, Scratch &sc, BatchPrep &bp) {
     uint32_t *rank = nullptr;
     CHK(sc.alloc(&cnt, S + 1));
     CHK(sc.alloc(&rank, n));
-    HIPCHK(hipMemsetAsync(cnt, 0, (S + 1) * 8, t->stream));
+    {
+        ZeroSpans z{};
+        if (zero) z = *zero;
+        z.p[z.k] = reinterpret_cast<uint8_t *>(cnt);
+        z.n[z.k++] = (S + 1) * 8;
+        LAUNCH(t, "bucket", k_zero_spans, grid_for((S + 1) / 2), 256, 0, z);
+    }
     if (in.seg_given) {
         HIPCHK(hipMemcpyAsync(bp.seg, in.seg_given, n * 4, hipMemcpyDeviceToDevice, t->stream));
         LAUNCH(t, "bucket", k_seg_hist, grid_for(n), 256, 0, (const uint32_t *)bp.seg, n, cnt, rank);
@@ -1611,8 +1619,19 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     const uint64_t n = in.n, S = t->S;
     if (!t->pg.on) CHK(pages_build(t, t->pg_slack, PageSums(0)));
     Scratch sc(t);
+    // acc: the batch's totals (k_page_place, a line apart), then the rejected
+    // records (insert_int64's count, read with them); hcnt: the hash list's
+    // bin counts; both and the path marks zeroed with the bucketing's counters
+    unsigned long long *acc = nullptr, *hcnt = nullptr;
+    CHK(sc.alloc(&acc, 6 * PP_LINE));
+    CHK(sc.alloc(&hcnt, (uint64_t)HB * PP_LINE));
+    ZeroSpans z{};
+    z.p[0] = reinterpret_cast<uint8_t *>(acc); z.n[0] = 6 * PP_LINE * 8;
+    z.p[1] = reinterpret_cast<uint8_t *>(hcnt); z.n[1] = HB * PP_LINE * 8;
+    z.p[2] = t->mark; z.n[2] = t->nslots;
+    z.k = 3;
     BatchPrep bp;
-    CHK(batch_prepare(t, in, sc, bp));
+    CHK(batch_prepare(t, in, sc, bp, &z));
     uint8_t *reject = nullptr, *dirty = nullptr, *mode = nullptr;
     BatchSums *bs = nullptr, *bx = nullptr;
     SegSums *sm = nullptr;
@@ -1621,11 +1640,9 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     uint32_t *mpos = nullptr;
     RecAt *rat = nullptr;
     PrefixState *ps = nullptr;
-    unsigned long long *acc = nullptr, *hcnt = nullptr;
     uint32_t *hlist = nullptr;
     const uint64_t hcap = std::min<uint64_t>(S, n);   // a changed segment has a run
     CHK(sc.alloc(&hlist, (uint64_t)HB * hcap));
-    CHK(sc.alloc(&hcnt, (uint64_t)HB * PP_LINE));
     CHK(sc.alloc(&reject, S));
     CHK(sc.alloc(&ps, S));
     CHK(sc.alloc(&rat, n));
@@ -1638,12 +1655,9 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     CHK(sc.alloc(&mpos, n));
     CHK(sc.alloc(&bs, n + 1));
     CHK(sc.alloc(&bx, n));
-    CHK(sc.alloc(&acc, 6 * PP_LINE));
     // No memsets of the per-segment plan: k_run_plan writes every segment
     // with a run, k_page_place every other one; the per-record sums are read
-    // only inside runs.  acc: the batch's totals (k_page_place, a line
-    // apart), then the rejected records (insert_int64's count, read with them).
-    HIPCHK(hipMemsetAsync(acc, 0, 6 * PP_LINE * 8, t->stream));
+    // only inside runs.
     // merge positions (a lane per record, the segments' size deltas by
     // atomics), then the touched segments' verify (saving each one's
     // unchanged-prefix MD5 state) and the inner nodes of their paths
@@ -1666,9 +1680,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     const PageBounds pb{t->pg.cap_e, t->pg.cap_k, t->pg.cap_v, chk};
     {
         const DevTree d = view(t);
-        HIPCHK(hipMemsetAsync(t->mark, 0, t->nslots, t->stream));
         LAUNCH(t, "mark_paths", k_mark_paths, grid_for(S), 256, 0, d, t->H + 1, (const uint64_t *)bp.bseg_off,
-               (const uint64_t *)nullptr, S, t->mark);
+               (const uint64_t *)nullptr, S, t->mark);   // (the marks were zeroed with the bucketing's counters)
         CHK(ensure_perm_any(t));
         // then the per-segment sums and the runs' prefix sums by each run's first lane (no atomics, no scan)
         LAUNCH(t, "merge_count", k_merge_keys, grid_for(n), 256, 0, ma, (const uint32_t *)bp.sseg, n, mpos, bs, rat,
@@ -1688,8 +1701,8 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
     // checks the totals itself) -- the pages are rebuilt with room for them
     // and the batch planned and merged again
     for (int pass = 0;; pass++) {
-        HIPCHK(hipMemsetAsync(hcnt, 0, HB * PP_LINE * 8, t->stream));
         if (pass) {
+            HIPCHK(hipMemsetAsync(hcnt, 0, HB * PP_LINE * 8, t->stream));
             HIPCHK(hipMemsetAsync(acc, 0, 5 * PP_LINE * 8, t->stream));
             LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
                    n, (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
@@ -2346,9 +2359,9 @@ static int insert_int64(st_tree *t, uint64_t n, const int64_t *keys, const uint8
     if (!r) r = dalloc_t(t, &dvo, n + 1);
     if (!r && n_corrupted) r = dalloc_t(t, &dcl, n);
     if (!r) {
-        (void)hipMemsetAsync(krec + 9 * n, 0, HEAP_SLACK, t->stream);
-        TimedLaunch tl(t, "pack_int64");
-        hipLaunchKernelGGL(k_pack_int64, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, dkeys, n, krec, dko, dvo, vlen);
+        TimedLaunch tl(t, "pack_int64");   // (it zeroes the key heap's slack too)
+        hipLaunchKernelGGL(k_pack_int64, dim3(grid_for(n + 1)), dim3(256), 0, t->stream, dkeys, n, krec, dko, dvo, vlen,
+                           (uint32_t)HEAP_SLACK);
         if (hipGetLastError() != hipSuccess) { r = ST_EDEVICE; g_err = "pack_int64 launch"; }
     }
     if (!r) {
