@@ -298,6 +298,7 @@ __device__ __forceinline__ void krec9_load(const uint8_t *p, uint32_t &tag, uint
     const uint32_t p0 = (x >> 8) | (y << 24), p1 = (y >> 8) | (z << 24);
     pv = ((uint64_t)__builtin_bswap32(p0) << 32) | __builtin_bswap32(p1);
 }
+#define MI_W 16   // k_merge_keys' interpolation window (keys): 144 bytes, one round trip
 __device__ __forceinline__ void cas_kx(uint64_t &ka, uint32_t &ia, uint64_t &kb, uint32_t &ib) {
     const bool sw = kb < ka || (kb == ka && ib < ia);
     const uint64_t k = sw ? kb : ka, k2 = sw ? ka : kb;
@@ -757,6 +758,43 @@ __global__ void k_merge_keys(MergeArgs a, const uint32_t *sseg, uint64_t n, uint
             const uint8_t *k0 = a.kheap + (a.kbeg ? a.kbeg[s] : a.koff[i0]);
             const uint64_t kv = krec_be64(kb + 1);
             bool hit = false;
+#ifndef ST_NO_INTERP
+            // INTERPOLATION first (a segment's keys are a uniform sample of the
+            // key space: the segment is the key's MD5): the page's first and
+            // last keys (one round trip), then a window of MI_W keys around the
+            // interpolated position (one more); the bisection below only
+            // finishes a miss, inside the side the window leaves.  Every bound
+            // is a probed key, so the position and `hit` are the bisection's.
+            if (nold >= MI_W + 2) {
+                uint32_t tf, tl;
+                uint64_t pf, pl;
+                krec9_load(k0, tf, pf);
+                krec9_load(k0 + 9 * (nold - 1), tl, pl);
+                if (tf == KEYTAG_INT && tl == KEYTAG_INT) {   // every key int-tagged (sorted: first and last are)
+                    if (kv <= pf) {
+                        hit = kv == pf; hi = 0;                 // position 0
+                    } else if (kv >= pl) {
+                        hit = kv == pl; lo = hi = kv == pl ? nold - 1 : nold;
+                    } else {                                    // position in [1, nold - 1]
+                        const double fr = (double)(kv - pf) / (double)(pl - pf);
+                        const int64_t g = (int64_t)(fr * (double)(nold - 1)) - MI_W / 2;
+                        const uint64_t w0 = g < 1 ? 1 : ((uint64_t)g + MI_W + 1 > nold ? nold - 1 - MI_W : (uint64_t)g);
+                        uint32_t c = 0;
+#pragma unroll
+                        for (int q = 0; q < MI_W; q++) {
+                            uint32_t tg;
+                            uint64_t pv;
+                            krec9_load(k0 + 9 * (w0 + q), tg, pv);
+                            c += pv < kv ? 1u : 0u;
+                            hit |= pv == kv;
+                        }
+                        if (c == 0) { lo = 1; hi = w0; }                       // key[w0] >= kv was probed
+                        else if (c == MI_W) { lo = w0 + MI_W; hi = nold - 1; } // key[nold - 1] > kv
+                        else { lo = hi = w0 + c; }
+                    }
+                }
+            }
+#endif
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
                 uint32_t tag;
