@@ -21,13 +21,26 @@ def _vals(seqs):
     return v
 
 
+def _skewed(n, rng):
+    """95 % of the keys small, 5 % near 2^62: inside a segment the first and
+    last keys span the outliers, so the positions' interpolation guesses far
+    off and its bisection finishes from either side of the window."""
+    small = rng.choice(10_000_000, n - n // 20, replace=False).astype(np.int64)
+    big = (np.int64(1) << 62) + rng.choice(1 << 40, n // 20, replace=False).astype(np.int64)
+    return np.concatenate([small, big])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('W,S,n0,batch', [(16, 256, 20000, 600), (4, 64, 4000, 120), (16, 16, 2000, 60)])
-def test_int64_runs_last_writer_wins(W, S, n0, batch):
+@pytest.mark.parametrize('W,S,n0,batch,skew', [(16, 256, 20000, 600, False), (4, 64, 4000, 120, False),
+                                               (16, 16, 2000, 60, False), (16, 64, 8000, 240, True)])
+def test_int64_runs_last_writer_wins(W, S, n0, batch, skew):
     import oracle_c as C
     from riak_ensemble_amd import synctree_hip
     rng = np.random.default_rng(S)
-    base = workload.keys_int63(n0, workload.SEED ^ (0x77 + S)).astype(np.int64)
+    if skew:
+        base = _skewed(n0, rng)
+    else:
+        base = workload.keys_int63(n0, workload.SEED ^ (0x77 + S)).astype(np.int64)
     base[:4] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, -1, 0]
     pool = np.concatenate([base, -base[4:200]])                 # negative keys too
     dev = synctree_hip.DeviceTree(W, S)
