@@ -32,7 +32,7 @@ def _skewed(n, rng):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('W,S,n0,batch,skew', [(16, 256, 20000, 600, False), (4, 64, 4000, 120, False),
-                                               (16, 16, 2000, 60, False), (16, 64, 8000, 240, True)])
+                                               (16, 16, 2000, 60, False), (16, 256, 20000, 600, True)])
 def test_int64_runs_last_writer_wins(W, S, n0, batch, skew):
     import oracle_c as C
     from riak_ensemble_amd import synctree_hip
