@@ -423,6 +423,15 @@ int st_kernel_stats(st_tree *t, const char *kernel, uint64_t *launches, double *
 /* ST_DBG_PAGE_POISON: fault injection for the checked mode: segment `value`'s
  * page (pages on) claims entries past its capacity. */
 #define ST_DBG_PAGE_POISON 4
+/* ST_DBG_PAGE_DOWN: which in-place page merges shift the entries before the
+ * batch's insert positions down into the page's head slack instead of those
+ * after them up into its tail slack: 0 (default) never -- pages then keep
+ * all their slack after their content --, 1 when that moves fewer bytes, 2
+ * whenever the growth fits the head (tests, A/B; pages built from then on
+ * split their slack).  Measured slower: a page shifted down
+ * starts its values off 16-byte alignment, and the verify and the hash of
+ * its segment then read every MD5 block unaligned. */
+#define ST_DBG_PAGE_DOWN 5
 int st_debug_knob(st_tree *t, int knob, int64_t value);
 
 /* The paged segment layout of streaming insert batches (no reference

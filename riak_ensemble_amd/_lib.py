@@ -115,7 +115,7 @@ _SIGS = {
     'st_get1_multi': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 4),
 }
-ST_DBG_SKIP_MAIL, ST_DBG_PAGES, ST_DBG_PAGE_CHECK, ST_DBG_PAGE_POISON = 1, 2, 3, 4
+ST_DBG_SKIP_MAIL, ST_DBG_PAGES, ST_DBG_PAGE_CHECK, ST_DBG_PAGE_POISON, ST_DBG_PAGE_DOWN = 1, 2, 3, 4, 5
 
 EXPORTED = sorted(_SIGS)
 _lib = None

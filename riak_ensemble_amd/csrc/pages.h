@@ -22,7 +22,16 @@
 // bytes [vbeg[s] = voff[beg], vend[s] = voff[end]) below vcap[s]; kbeg[s] =
 // koff[beg] (the page's first key byte: the per-segment kernels read the
 // page bounds from these S-wide arrays, consecutive segments side by side,
-// not from the entry slots a page apart).
+// not from the entry slots a page apart).  With st_debug_knob
+// ST_DBG_PAGE_DOWN a page's slack is split: half after its content, half
+// before it (ebot <= beg, kbot <= kbeg, vbot <= vbeg), and a batch that
+// inserts into a page may shift the entries before its last insert position
+// down into the head slack (mode 3) instead of those after its first one up
+// into the tail slack (mode 1) -- half the moved bytes for an insert at a
+// uniform position.  Off by default: measured slower, because a page shifted
+// down no longer starts its values 16-byte aligned and every MD5 block of
+// its verify and hash is then an unaligned read.  Without
+// it ebot = beg etc. and every merge shifts up.
 //
 // UNIFORM pages: when every key record of a segment has one length L (klen)
 // and every value one length V (vlen) -- int64 keys and 17-byte ObjHash
@@ -39,6 +48,8 @@ struct PageMeta {
     uint64_t *beg, *end, *vbeg, *vend;   // S each: the DevTree view's seg_off / seg_end / seg_voff / seg_vend
     uint64_t *kbeg;                      // S: koff[beg]
     uint64_t *ecap, *kcap, *vcap;        // S each: page capacities (entry slot end, key / value byte ends)
+    uint64_t *ebot, *kbot, *vbot;        // S each: the page's first entry slot and key / value bytes (its content
+                                         // starts at or above them: the head slack a merge may shift down into)
     uint16_t *klen;                      // S: the length every key record of the segment has (KLEN_MIXED: not
                                          // one length, KLEN_NONE: no entries) -- fixed-stride merge positions
     uint16_t *vlen;                      // S: the same for its values
@@ -61,18 +72,34 @@ typedef USum<5> PlanSums;   // k_run_plan: a moved segment's new page (entries, 
 // Page capacity for a segment of c entries, kb key bytes and vb value bytes
 // (slack_pct: percent of slack; < 0: none, a gap-free CSR).  Byte caps are
 // 16-byte multiples so every page starts 16-byte aligned.
+__host__ __device__ __forceinline__ PageSums page_slack(uint64_t c, uint64_t kb, uint64_t vb, int slack_pct) {
+    PageSums r(0);
+    r.v[0] = c ? (c * (uint64_t)slack_pct / 100 > 4 ? c * (uint64_t)slack_pct / 100 : 4) : 0;
+    r.v[1] = c ? (kb * (uint64_t)slack_pct / 100 > 32 ? kb * (uint64_t)slack_pct / 100 : 32) : 0;
+    r.v[2] = c ? (vb * (uint64_t)slack_pct / 100 > 48 ? vb * (uint64_t)slack_pct / 100 : 48) : 0;
+    return r;
+}
 __host__ __device__ __forceinline__ PageSums page_caps(uint64_t c, uint64_t kb, uint64_t vb, int slack_pct) {
     PageSums r(0);
     if (slack_pct < 0) {
         r.v[0] = c; r.v[1] = kb; r.v[2] = vb;   // canonical: the next segment's first entry is this one's end
         return r;
     }
-    const uint64_t se = c ? (c * (uint64_t)slack_pct / 100 > 4 ? c * (uint64_t)slack_pct / 100 : 4) : 0;
-    const uint64_t sk = c ? (kb * (uint64_t)slack_pct / 100 > 32 ? kb * (uint64_t)slack_pct / 100 : 32) : 0;
-    const uint64_t sv = c ? (vb * (uint64_t)slack_pct / 100 > 48 ? vb * (uint64_t)slack_pct / 100 : 48) : 0;
-    r.v[0] = c + 1 + se;
-    r.v[1] = (kb + sk + 15) & ~15ull;
-    r.v[2] = (vb + sv + 15) & ~15ull;
+    const PageSums x = page_slack(c, kb, vb, slack_pct);
+    r.v[0] = c + 1 + x.v[0];
+    r.v[1] = (kb + x.v[1] + 15) & ~15ull;
+    r.v[2] = (vb + x.v[2] + 15) & ~15ull;
+    return r;
+}
+// The head of such a page (before its content): half its slack (bytes in
+// 16-byte units, so the content starts 16-byte aligned where the page does).
+__host__ __device__ __forceinline__ PageSums page_head(uint64_t c, uint64_t kb, uint64_t vb, int slack_pct) {
+    PageSums r(0);
+    if (slack_pct < 0) return r;
+    const PageSums x = page_slack(c, kb, vb, slack_pct);
+    r.v[0] = x.v[0] / 2;
+    r.v[1] = (x.v[1] / 2) & ~15ull;
+    r.v[2] = (x.v[2] / 2) & ~15ull;
     return r;
 }
 
@@ -118,6 +145,7 @@ struct PageDst {
     PageMeta m;                      // paged destination (m.beg != nullptr)
     uint64_t *cseg_off, *cseg_voff;  // canonical destination
     uint64_t e0, k0, v0;             // bases added to the scanned offsets
+    int slack_pct;                   // paged destination: the pages' slack (page_head)
 };
 // sm: the source's page metadata when the source is paged (its uniform pages
 // keep no per-entry offsets: generated here), else nullptr (a CSR).
@@ -128,8 +156,9 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
     for (uint64_t s = w0; s < t.S; s += nw) {
         const uint64_t b = t.seg_off[s], e = t.seg_end[s], c = e - b;
         const PageSums B = base[s];
-        const uint64_t De = d.e0 + B.v[0], Dk = d.k0 + B.v[1], Dv = d.v0 + B.v[2];
         const uint64_t kb0 = t.koff[b], vb0 = t.voff[b];
+        const PageSums Hd = d.m.beg ? page_head(c, t.koff[e] - kb0, t.voff[e] - vb0, d.slack_pct) : PageSums(0);
+        const uint64_t De = d.e0 + B.v[0] + Hd.v[0], Dk = d.k0 + B.v[1] + Hd.v[1], Dv = d.v0 + B.v[2] + Hd.v[2];
         const uint32_t SL = sklen ? sklen[s] : KLEN_MIXED, SV = svlen ? svlen[s] : KLEN_MIXED;
         const bool gen = sklen && page_uniform(SL, SV) && c;   // a uniform source page: offsets by stride
         const uint64_t l0 = c ? (gen ? SL : t.koff[b + 1] - kb0) : 0;
@@ -158,9 +187,12 @@ __global__ void __launch_bounds__(256) k_page_copy(DevTree t, const PageSums *ba
                 d.m.vbeg[s] = Dv;
                 d.m.kbeg[s] = Dk;
                 d.m.vend[s] = Dv + (t.voff[e] - vb0);
-                d.m.ecap[s] = De + Z.v[0];
-                d.m.kcap[s] = Dk + Z.v[1];
-                d.m.vcap[s] = Dv + Z.v[2];
+                d.m.ebot[s] = De - Hd.v[0];
+                d.m.kbot[s] = Dk - Hd.v[1];
+                d.m.vbot[s] = Dv - Hd.v[2];
+                d.m.ecap[s] = d.m.ebot[s] + Z.v[0];
+                d.m.kcap[s] = d.m.kbot[s] + Z.v[1];
+                d.m.vcap[s] = d.m.vbot[s] + Z.v[2];
             } else {
                 d.cseg_off[s] = De;
                 d.cseg_voff[s] = Dv;
@@ -203,9 +235,13 @@ __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *
 // first record sums the run (its BatchSums' inclusive prefix sums into bxl
 // -- k_page_merge's growth before and through each group --, the segment's
 // size deltas, dirty, fpos = the smallest value offset a kept record
-// changes) and plans its page: merge in place (1) or move to a new page (2)
-// -- in place needs room in the page and every prefix of the run adding >=
-// 0 key and value bytes (the moves run from the highest address down) --,
+// changes) and plans its page: merge in place shifting up (1) or down (3),
+// or move to a new page (2) -- in place up needs room after the content and
+// every prefix of the run adding >= 0 key and value bytes (the moves run
+// from the highest address down), in place down room before the content and
+// every suffix adding >= 0 (the moves run from the lowest address up); with
+// both possible the side with fewer bytes to move wins (down: 0 never, 1 by
+// the bytes, 2 whenever it fits) --,
 // reloc = the new page's sizes (mode 2, scanned for its place in the append
 // region, k_page_place), v[3] its new keys, v[4] its value bytes before the
 // merge; mode bit 4: the merged page keeps per-entry offsets (not uniform),
@@ -215,7 +251,7 @@ __global__ void __launch_bounds__(256) k_page_materialize(PageMeta m, uint64_t *
 __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint64_t n, const BatchSums *bs,
                            const RecAt *rat, PageMeta m, const uint64_t *koff, const uint64_t *voff, int slack_pct,
                            uint8_t *dirty, unsigned long long *fpos, BatchSums *bxl, SegSums *sm, uint8_t *mode,
-                           PlanSums *reloc) {
+                           PlanSums *reloc, int down) {
     for (uint64_t j = gtid(); j < n; j += gstride()) {
         const uint64_t s = sseg[j];
         if (j != bseg_off[s]) continue;
@@ -224,7 +260,8 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
         BatchSums acc(0);
         uint64_t fp = ~0ull;
         bool grow = true;
-        int64_t dk = 0, dv = 0;
+        int64_t dk = 0, dv = 0, mk = 0, mv = 0;   // the growth so far and its largest prefix
+        uint64_t up_cost = ~0ull, down_cost = 0;   // bytes after the first / before the last shifting record's position
         const uint32_t kl0 = m.klen[s], vl0 = m.vlen[s];
         uint32_t kl = kl0, vl = vl0;
         for (uint64_t r = j; r < je; r++) {
@@ -234,6 +271,13 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
             dk += (int64_t)f.v[BS_KN] - (int64_t)f.v[BS_KE];
             dv += (int64_t)f.v[BS_VN] - (int64_t)f.v[BS_VE];
             grow = grow && dk >= 0 && dv >= 0;
+            mk = dk > mk ? dk : mk;
+            mv = dv > mv ? dv : mv;
+            if (f.v[BS_NE] != f.v[BS_EQ] || f.v[BS_KN] != f.v[BS_KE] || f.v[BS_VN] != f.v[BS_VE]) {
+                const RecAt q = rat[r];   // the run is in key order: positions ascend
+                if (up_cost == ~0ull) up_cost = q.ku + q.vu;   // (made relative to the page's end below)
+                down_cost = q.ku + q.vu;
+            }
             if (f.v[BS_NE]) { kl = klen_add(kl, f.v[BS_KN]); vl = klen_add(vl, f.v[BS_VN]); }
             if (!f.v[BS_NE] && !f.v[BS_EQ]) continue;
             d.v[0] += f.v[BS_NE] - f.v[BS_EQ];
@@ -260,7 +304,12 @@ __global__ void k_run_plan(const uint32_t *sseg, const uint64_t *bseg_off, uint6
         x.v[3] = d.v[3];
         sm[s] = x;
         const bool fits = b + x.v[0] < m.ecap[s] && kb + x.v[1] <= m.kcap[s] && vb + x.v[2] <= m.vcap[s];
+        // down: the growth fits before the content and no suffix of the run shrinks
+        const bool dfits = down && dk >= 0 && dv >= 0 && mk <= dk && mv <= dv && b - m.ebot[s] >= d.v[0] &&
+                           kb - m.kbot[s] >= (uint64_t)dk && vb - m.vbot[s] >= (uint64_t)dv;
+        up_cost = up_cost == ~0ull ? 0 : kbytes + (ve - vb) - up_cost;
         uint8_t md = fits && grow ? 1 : 2;
+        if (dfits && (md == 2 || down == 2 || down_cost < up_cost)) md = 3;
         const bool expl = !page_uniform(kl, vl);
         md |= (expl ? 4 : 0) | (expl && page_uniform(kl0, vl0) && e > b ? 8 : 0);
         PlanSums r(0);
@@ -420,6 +469,7 @@ struct PageMergeArgs {
     uint64_t e0, k0, v0;          // the append region's bases
     uint64_t ce, ck, cv;          // ... and its ends
     const unsigned long long *acc;   // the batch's totals (k_page_place): no room, no merge
+    int slack_pct;                // the pages' slack (a moved page's head, page_head)
     unsigned long long *chk;      // checked build (st_debug_knob ST_DBG_PAGE_CHECK): [0] violations, [1..4] the first
 };
 
@@ -435,6 +485,7 @@ __device__ __forceinline__ bool pg_ok(unsigned long long *chk, bool ok, uint32_t
 struct PieceJob {
     uint64_t kd, ks, nk, vd, vs, nv, ko, vo, a, e, de, dk, dv, fl;   // fl: bit 0 keys, 1 values, 2 key offs, 3 value offs
 };
+#define PM_ASC 16u   // PieceJob::fl: the piece moves down (dst <= src): its units run bottom up
 // The jobs' memory accesses.  A job's addresses are rebuilt from readlanes,
 // so the compiler cannot tell their address space: as generic pointers every
 // access was a FLAT one, and the waits FLAT needs serialised a unit's loads
@@ -513,11 +564,22 @@ __device__ __forceinline__ void pm_heap_offs(uint64_t n, uint64_t u, uint32_t la
         t = lane;
     }
 }
+// A piece moving down (PM_ASC) takes the mirror image of the same units:
+// byte x of the top-down order is byte n - 1 - x, entry i is entry a + e - 1 - i,
+// so unit u covers the lowest bytes and entries not yet moved, the clamped
+// chunk is the top one and the byte unit holds the top bytes.
 __device__ __forceinline__ void pm_load(const PmJob &q, uint64_t u, uint32_t lane, PmUnit &d) {
     pm_heap_offs(q.nk, u, lane, d.kc, d.kt);
     pm_heap_offs(q.nv, u, lane, d.vc, d.vt);
     const uint64_t top = q.e - std::min(q.e - q.a, 64 * u);
-    const uint32_t oo = top > q.a + lane ? (uint32_t)(8 * (top - 1 - lane)) : PM_OOB;
+    uint32_t oo = top > q.a + lane ? (uint32_t)(8 * (top - 1 - lane)) : PM_OOB;
+    if (q.fl & PM_ASC) {
+        if (d.kc != PM_OOB) d.kc = (uint32_t)q.nk - 16 - d.kc;
+        if (d.vc != PM_OOB) d.vc = (uint32_t)q.nv - 16 - d.vc;
+        if (d.kt != PM_OOB) d.kt = (uint32_t)q.nk - 1 - d.kt;
+        if (d.vt != PM_OOB) d.vt = (uint32_t)q.nv - 1 - d.vt;
+        if (oo != PM_OOB) oo = (uint32_t)(8 * (q.a + q.e - 1)) - oo;
+    }
     d.ok = (q.fl & 4) ? oo : PM_OOB;
     d.ov = (q.fl & 8) ? oo : PM_OOB;
     d.kx = __builtin_amdgcn_raw_buffer_load_b128(q.KS, d.kc, 0, 0);
@@ -644,73 +706,101 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
         const uint64_t s = sb + lane;
         const uint8_t mb = s < a.S ? p.mode[s] : 0, md = mb & 3;
         const bool expl = (mb & 4) != 0;   // the merged page keeps per-entry offsets (pages.h: uniform pages do not)
-        uint64_t j0 = 0, je = 0, b = 0, c = 0, Kb = 0, Vb = 0, De = 0, Dk = 0, Dv = 0, EC = 0, KC = 0, VC = 0;
-        SegSums X(0);
+        uint64_t j0 = 0, je = 0, b = 0, Kb = 0, Vb = 0, De = 0, Dk = 0, Dv = 0;
+        bool nz = false;   // the merged segment has entries
         const BatchSums B0(0);   // the growth before the run's first record (pm_bx: run-local sums)
         bool live = md != 0;
-        if (live) {
-            j0 = a.bseg_off[s]; je = a.bseg_off[s + 1];
-            b = p.m.beg[s]; c = p.m.end[s] - b;
-            Kb = p.m.kbeg[s]; Vb = p.m.vbeg[s];
-            X = p.ss[s];
-            De = b; Dk = Kb; Dv = Vb; EC = p.m.ecap[s]; KC = p.m.kcap[s]; VC = p.m.vcap[s];
-            if (md == 2) {
-                const PlanSums R = p.rbase[s], Z = p.rsz[s];
-                De = p.e0 + R.v[0]; Dk = p.k0 + R.v[1]; Dv = p.v0 + R.v[2];
-                EC = De + Z.v[0]; KC = Dk + Z.v[1]; VC = Dv + Z.v[2];
-            }
-            // the merged segment fits its (new) page: every move below stays inside it
-            live = pg_ok(chk, De + X.v[0] < EC && Dk + X.v[1] <= KC && Dv + X.v[2] <= VC, 14, s, De + X.v[0], EC);
-
-        }
-        uint32_t kl = (live && X.v[0]) ? p.m.klen[s] : KLEN_NONE;   // the merged segment's uniform key length
-        uint32_t vl = (live && X.v[0]) ? p.m.vlen[s] : KLEN_NONE;   // ... and value length
         // the page as it is: uniform = entry i's offsets by stride (its slots between the first and the end are stale)
         const uint32_t L0 = live ? p.m.klen[s] : KLEN_MIXED, V0 = live ? p.m.vlen[s] : KLEN_MIXED;
         const bool stride = page_uniform(L0, V0);
-        uint64_t hi = c, khi = live ? (stride ? Kb + (uint64_t)L0 * c : p.koff[b + c]) : 0,
-                 vhi = live ? p.m.vend[s] : 0;   // the current piece's end
-        uint64_t j = je;
-        while (__ballot(live && j > j0)) {
-            const bool mine = live && j > j0;
+        uint64_t hi = 0, khi = 0, vhi = 0;   // the current piece's end (modes 1, 2) or start (mode 3)
+        if (live) {
+            j0 = a.bseg_off[s]; je = a.bseg_off[s + 1];
+            b = p.m.beg[s];
+            const uint64_t c = p.m.end[s] - b;
+            Kb = p.m.kbeg[s]; Vb = p.m.vbeg[s];
+            hi = c; khi = stride ? Kb + (uint64_t)L0 * c : p.koff[b + c]; vhi = p.m.vend[s];
+            const SegSums X = p.ss[s];   // (read again at the end: not kept in registers through the merge)
+            nz = X.v[0] != 0;
+            uint64_t EC = p.m.ecap[s], KC = p.m.kcap[s], VC = p.m.vcap[s];
+            De = b; Dk = Kb; Dv = Vb;
+            uint64_t EB = b, KB = Kb, VB = Vb;   // the lowest entry slot / key byte / value byte a store may touch
+            if (md == 2) {
+                const PlanSums R = p.rbase[s], Z = p.rsz[s];
+                const PageSums Hd = page_head(X.v[0], X.v[1], X.v[2], p.slack_pct);
+                EB = p.e0 + R.v[0]; KB = p.k0 + R.v[1]; VB = p.v0 + R.v[2];
+                De = EB + Hd.v[0]; Dk = KB + Hd.v[1]; Dv = VB + Hd.v[2];
+                EC = EB + Z.v[0]; KC = KB + Z.v[1]; VC = VB + Z.v[2];
+            } else if (md == 3) {   // the content's end stays, its start moves down by the growth
+                De = b - (X.v[0] - c); Dk = Kb - (X.v[1] - (khi - Kb)); Dv = Vb - (X.v[2] - (vhi - Vb));
+                EB = p.m.ebot[s]; KB = p.m.kbot[s]; VB = p.m.vbot[s];
+                hi = 0; khi = Kb; vhi = Vb;
+            }
+            // the merged segment fits its (new) page: every move below stays inside it
+            live = pg_ok(chk, De + X.v[0] < EC && Dk + X.v[1] <= KC && Dv + X.v[2] <= VC, 14, s, De + X.v[0], EC) &&
+                   pg_ok(chk, De >= EB && Dk >= KB && Dv >= VB, 15, s, De, EB);
+        }
+        uint32_t kl = (live && nz) ? p.m.klen[s] : KLEN_NONE;   // the merged segment's uniform key length
+        uint32_t vl = (live && nz) ? p.m.vlen[s] : KLEN_NONE;   // ... and value length
+        // modes 1, 2: the groups from the last down, each piece above its group
+        // moved up first; mode 3: from the first up, each piece below its group
+        // moved down first
+        const bool upw = md != 3;
+        uint64_t j = upw ? je : j0;
+        while (__ballot(live && (upw ? j > j0 : j < je))) {
+            const bool mine = live && (upw ? j > j0 : j < je);
             PieceJob J{};
             bool has = false;
-            uint64_t u = 0, g0 = 0, ku = 0, vu = 0;
+            uint64_t u = 0, g0 = 0, g1 = 0, ku = 0, vu = 0;
             if (mine) {
-                u = p.pos[j - 1];
-                g0 = j - 1;
-                while (g0 > j0 && p.pos[g0 - 1] == u) g0--;
-                const BatchSums Bj = pm_bx(p, j0, j);
-                const bool eq = Bj.v[BS_EQ] != pm_bx(p, j0, j - 1).v[BS_EQ];   // the group's last record replaces entry u
-                const uint64_t lo = u + (eq ? 1 : 0);
-                const uint64_t de = (Bj.v[BS_NE] - B0.v[BS_NE]) - (Bj.v[BS_EQ] - B0.v[BS_EQ]);
-                const uint64_t dk = (Bj.v[BS_KN] - B0.v[BS_KN]) - (Bj.v[BS_KE] - B0.v[BS_KE]);
-                const uint64_t dv = (Bj.v[BS_VN] - B0.v[BS_VN]) - (Bj.v[BS_VE] - B0.v[BS_VE]);
-                const RecAt R = p.rat[j - 1];   // entry u's old offsets, page-relative (read before any rewrite)
+                if (upw) {
+                    g1 = j;
+                    u = p.pos[g1 - 1];
+                    g0 = g1 - 1;
+                    while (g0 > j0 && p.pos[g0 - 1] == u) g0--;
+                } else {
+                    g0 = j;
+                    u = p.pos[g0];
+                    g1 = g0 + 1;
+                    while (g1 < je && p.pos[g1] == u) g1++;
+                }
+                // the group's last record replaces entry u
+                const bool eq = pm_bx(p, j0, g1).v[BS_EQ] != pm_bx(p, j0, g1 - 1).v[BS_EQ];
+                const RecAt R = p.rat[g1 - 1];   // entry u's old offsets, page-relative (read before any rewrite)
                 ku = Kb + R.ku;
                 vu = Vb + R.vu;
-                if (lo < hi) {
-                    const uint64_t k0 = stride ? Kb + (uint64_t)L0 * lo : p.koff[b + lo];
-                    const uint64_t v0 = stride ? Vb + (uint64_t)V0 * lo : p.voff[b + lo];
-                    J.kd = (uint64_t)(p.kheap + Dk + (k0 - Kb) + dk); J.ks = (uint64_t)(p.kheap + k0); J.nk = khi - k0;
-                    J.vd = (uint64_t)(p.vheap + Dv + (v0 - Vb) + dv); J.vs = (uint64_t)(p.vheap + v0); J.nv = vhi - v0;
+                // the piece: above the group up to hi, shifted by the growth through
+                // it (modes 1, 2), or from hi up to the group, shifted by the growth
+                // before it (mode 3)
+                const uint64_t pa = upw ? u + (eq ? 1 : 0) : hi, pe = upw ? hi : u;
+                if (pa < pe) {
+                    const BatchSums Bg = pm_bx(p, j0, upw ? g1 : g0);
+                    const uint64_t de = (Bg.v[BS_NE] - B0.v[BS_NE]) - (Bg.v[BS_EQ] - B0.v[BS_EQ]);
+                    const uint64_t dk = (Bg.v[BS_KN] - B0.v[BS_KN]) - (Bg.v[BS_KE] - B0.v[BS_KE]);
+                    const uint64_t dv = (Bg.v[BS_VN] - B0.v[BS_VN]) - (Bg.v[BS_VE] - B0.v[BS_VE]);
+                    const uint64_t k0 = !upw ? khi : stride ? Kb + (uint64_t)L0 * pa : p.koff[b + pa];
+                    const uint64_t v0 = !upw ? vhi : stride ? Vb + (uint64_t)V0 * pa : p.voff[b + pa];
+                    const uint64_t k1 = upw ? khi : ku, v1 = upw ? vhi : vu;
+                    J.kd = (uint64_t)(p.kheap + Dk + (k0 - Kb) + dk); J.ks = (uint64_t)(p.kheap + k0); J.nk = k1 - k0;
+                    J.vd = (uint64_t)(p.vheap + Dv + (v0 - Vb) + dv); J.vs = (uint64_t)(p.vheap + v0); J.nv = v1 - v0;
                     J.ko = (uint64_t)(p.koff + b); J.vo = (uint64_t)(p.voff + b);
-                    J.a = lo; J.e = hi; J.de = (De - b) + de; J.dk = (Dk - Kb) + dk; J.dv = (Dv - Vb) + dv;
-                    J.fl = ((md == 2 || dk) ? 1u : 0u) | ((md == 2 || dv) ? 2u : 0u) |
-                           (expl && (md == 2 || de || dk) ? 4u : 0u) | (expl && (md == 2 || de || dv) ? 8u : 0u);
+                    J.a = pa; J.e = pe; J.de = (De - b) + de; J.dk = (Dk - Kb) + dk; J.dv = (Dv - Vb) + dv;
+                    J.fl = ((md == 2 || J.dk) ? 1u : 0u) | ((md == 2 || J.dv) ? 2u : 0u) |
+                           (expl && (md == 2 || J.de || J.dk) ? 4u : 0u) | (expl && (md == 2 || J.de || J.dv) ? 8u : 0u);
                     has = J.fl != 0;
+                    J.fl |= upw ? 0u : PM_ASC;
                 }
             }
             wave_run_jobs(J, has, lane);
             if (mine) {
-                for (uint64_t r = j; r > g0; r--) {   // the group's records that produce an entry, highest first
+                for (uint64_t r = g1; r > g0; r--) {   // the group's records that produce an entry, highest first
                     const BatchSums Br = pm_bx(p, j0, r - 1), Bn = pm_bx(p, j0, r);
                     if (Bn.v[BS_NE] == Br.v[BS_NE]) continue;
                     const uint64_t nwi = De + u + (Br.v[BS_NE] - B0.v[BS_NE]) - (Br.v[BS_EQ] - B0.v[BS_EQ]);
                     const uint64_t nk = Dk + (ku - Kb) + (Br.v[BS_KN] - B0.v[BS_KN]) - (Br.v[BS_KE] - B0.v[BS_KE]);
                     const uint64_t nv = Dv + (vu - Vb) + (Br.v[BS_VN] - B0.v[BS_VN]) - (Br.v[BS_VE] - B0.v[BS_VE]);
                     const RecAt Q = p.rat[r - 1];
-                    if (X.v[0]) {
+                    if (nz) {
                         kl = klen_add(kl, Bn.v[BS_KN] - Br.v[BS_KN]);
                         vl = klen_add(vl, Bn.v[BS_VN] - Br.v[BS_VN]);
                     }
@@ -721,8 +811,17 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
                     copy2_disjoint(p.kheap + nk, a.bv.kheap + Q.bk, Bn.v[BS_KN] - Br.v[BS_KN], p.vheap + nv,
                                    a.bvheap + Q.bv, Bn.v[BS_VN] - Br.v[BS_VN]);
                 }
-                hi = u; khi = ku; vhi = vu;
-                j = g0;
+                if (upw) {
+                    hi = u; khi = ku; vhi = vu;
+                    j = g0;
+                } else {   // the next piece starts after entry u if the group replaced it (its old offsets: not
+                           // yet overwritten, every store so far went below it)
+                    const bool eq = pm_bx(p, j0, g1).v[BS_EQ] != pm_bx(p, j0, g1 - 1).v[BS_EQ];
+                    hi = u + (eq ? 1 : 0);
+                    khi = !eq ? ku : stride ? Kb + (uint64_t)L0 * hi : p.koff[b + hi];
+                    vhi = !eq ? vu : stride ? Vb + (uint64_t)V0 * hi : p.voff[b + hi];
+                    j = g1;
+                }
             }
         }
         {   // mode 2: the entries before the first record, unshifted, into the new page
@@ -737,30 +836,38 @@ __global__ void __launch_bounds__(256, PM_WAVES) k_page_merge(PageMergeArgs p) {
             wave_run_jobs(J, has, lane);
         }
         if (live) {
+            const SegSums X = p.ss[s];
             if (kl != p.m.klen[s]) p.m.klen[s] = (uint16_t)kl;
             if (vl != p.m.vlen[s]) p.m.vlen[s] = (uint16_t)vl;
             p.koff[De + X.v[0]] = Dk + X.v[1];   // the end slot
             p.voff[De + X.v[0]] = Dv + X.v[2];
-            if (md == 2) {   // the first slot (a uniform page keeps no other)
+            if (md >= 2) {   // the first slot (a uniform page keeps no other)
                 p.koff[De] = Dk;
                 p.voff[De] = Dv;
             }
             p.m.end[s] = De + X.v[0];
             p.m.vend[s] = Dv + X.v[2];
-            if (md == 2) {
+            if (md >= 2) {
                 p.m.beg[s] = De;
                 p.m.vbeg[s] = Dv;
                 p.m.kbeg[s] = Dk;
-                p.m.ecap[s] = EC;
-                p.m.kcap[s] = KC;
-                p.m.vcap[s] = VC;
+            }
+            if (md == 2) {   // the new page's bounds
+                const PlanSums R = p.rbase[s], Z = p.rsz[s];
+                p.m.ebot[s] = p.e0 + R.v[0];
+                p.m.kbot[s] = p.k0 + R.v[1];
+                p.m.vbot[s] = p.v0 + R.v[2];
+                p.m.ecap[s] = p.e0 + R.v[0] + Z.v[0];
+                p.m.kcap[s] = p.k0 + R.v[1] + Z.v[1];
+                p.m.vcap[s] = p.v0 + R.v[2] + Z.v[2];
             }
         }
     }
 }
 
 // Checked build: every segment's page is consistent (entries and bytes
-// inside its capacities, offsets nondecreasing, the view's value bounds).
+// inside its capacities, above its bottoms, offsets nondecreasing, the view's
+// value bounds).
 __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t *voff, uint64_t S, uint64_t cap_e,
                                 uint64_t cap_k, uint64_t cap_v, unsigned long long *chk) {
     for (uint64_t s = gtid(); s < S; s += gstride()) {
@@ -770,6 +877,7 @@ __global__ void k_page_validate(PageMeta m, const uint64_t *koff, const uint64_t
         if (!pg_ok(chk, voff[b] <= voff[e] && voff[e] <= m.vcap[s] && m.vcap[s] <= cap_v, 22, s, voff[e], m.vcap[s])) continue;
         if (!pg_ok(chk, m.vbeg[s] == voff[b] && m.vend[s] == voff[e] && m.kbeg[s] == koff[b], 23, s, m.vbeg[s], voff[b]))
             continue;
+        if (!pg_ok(chk, m.ebot[s] <= b && m.kbot[s] <= koff[b] && m.vbot[s] <= voff[b], 27, s, b, m.ebot[s])) continue;
         const uint32_t L = m.klen[s], V = m.vlen[s];   // the uniform lengths, if any, hold
         if (!pg_ok(chk, (L != KLEN_NONE && V != KLEN_NONE) || b == e, 25, s, e - b, L)) continue;
         if (page_uniform(L, V)) {   // offsets by stride: only the first and end slots are kept

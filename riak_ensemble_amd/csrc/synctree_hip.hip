@@ -116,6 +116,8 @@ struct st_tree {
     int pg_slack = 25;
     uint32_t pg_streak = 0;   // streaming batches since the last other call (pages are built at the second)
     bool pg_check = false;   // st_debug_knob ST_DBG_PAGE_CHECK: the checked page merge + a layout check per batch
+    int pg_down = 0;         // st_debug_knob ST_DBG_PAGE_DOWN: in-place merges shift down 0 never, 1 by the bytes, 2 when they
+                             // fit (pages built while it is 0 keep all their slack after their content)
     bool fresh = true;
     uint32_t *seg_perm = nullptr;   // segments by MD5 block count (K1 order)
     bool perm_valid = false;
@@ -859,6 +861,11 @@ extern "C" int st_debug_knob(st_tree *t, int knob, int64_t value) {
         t->pg_check = value != 0;
         return ST_OK;
     }
+    if (knob == ST_DBG_PAGE_DOWN) {
+        if (value < 0 || value > 2) { g_err = "ST_DBG_PAGE_DOWN takes 0, 1 or 2"; return ST_EINVAL; }
+        t->pg_down = (int)value;
+        return ST_OK;
+    }
     if (knob == ST_DBG_PAGE_POISON) {   // a page whose entries leave its capacity (the checked mode must refuse it)
         if (!t->pg.on || value < 0 || (uint64_t)value >= t->S) { g_err = "no pages / segment out of range"; return ST_EINVAL; }
         LAUNCH(t, "page_poison", k_page_poison, 1, 64, 0, t->pg.m, (uint64_t)value);
@@ -1505,7 +1512,7 @@ static int ingest_direct(st_tree *t, IngestIn &in) {
 
 static void pages_free(st_tree *t, Pages &g) {
     for (void *p : {(void *)g.m.beg, (void *)g.m.end, (void *)g.m.vbeg, (void *)g.m.vend, (void *)g.m.kbeg, (void *)g.m.ecap, (void *)g.m.kcap,
-                    (void *)g.m.vcap, (void *)g.m.klen, (void *)g.m.vlen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
+                    (void *)g.m.vcap, (void *)g.m.ebot, (void *)g.m.kbot, (void *)g.m.vbot, (void *)g.m.klen, (void *)g.m.vlen, (void *)g.koff, (void *)g.voff, (void *)g.kheap, (void *)g.vheap})
         dfree(t, p);
     const uint64_t b = g.batches, bu = g.builds, f = g.folds, r = g.reloc_e, tv = g.touched_v;
     g = Pages();
@@ -1556,7 +1563,9 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
         st_tree *t; Pages &g; bool done = false;
         ~Undo() { if (!done) pages_free(t, g); }
     } undo{t, g};
-    for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.kbeg, &g.m.ecap, &g.m.kcap, &g.m.vcap}) CHK(dalloc_t(t, a, S));
+    for (uint64_t **a : {&g.m.beg, &g.m.end, &g.m.vbeg, &g.m.vend, &g.m.kbeg, &g.m.ecap, &g.m.kcap, &g.m.vcap, &g.m.ebot,
+                         &g.m.kbot, &g.m.vbot})
+        CHK(dalloc_t(t, a, S));
     CHK(dalloc_t(t, &g.m.klen, S));
     CHK(dalloc_t(t, &g.m.vlen, S));
     CHK(dalloc_t(t, &g.koff, g.cap_e));
@@ -1567,6 +1576,7 @@ static int pages_build(st_tree *t, int slack_pct, const PageSums &reserve) {
     HIPCHK(hipMemsetAsync(g.vheap + g.cap_v, 0, HEAP_SLACK, t->stream));
     PageDst d{};
     d.koff = g.koff; d.voff = g.voff; d.kheap = g.kheap; d.vheap = g.vheap; d.m = g.m;
+    d.slack_pct = t->pg_down ? slack_pct : -1;   // head slack only for merges that may shift down (page_head)
     LAUNCH(t, "page_build", k_page_copy, grid, 256, 0, src, (const PageSums *)base, (const PageSums *)sz, d, sklen, svlen);
     g.use_e = tot.v[0]; g.use_k = tot.v[1]; g.use_v = tot.v[2];
     g.on = true;
@@ -1690,7 +1700,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         // or moved; a rejected segment's plan is dropped by k_page_place below)
         LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off, n,
                (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
-               (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
+               (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz, t->pg_down);
         LAUNCH(t, "segment_verify", k_verify_cap, grid_for(S), 256, 0, d, (const uint32_t *)t->seg_perm,
                (const uint8_t *)t->mark, t->ok, (const unsigned long long *)fpos, ps, pb, (const uint32_t *)nullptr);
         CHK(verify_levels(t, t->H + 1));
@@ -1706,7 +1716,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
             HIPCHK(hipMemsetAsync(acc, 0, 5 * PP_LINE * 8, t->stream));
             LAUNCH(t, "page_plan", k_run_plan, grid_for(n), 256, 0, (const uint32_t *)bp.sseg, (const uint64_t *)bp.bseg_off,
                    n, (const BatchSums *)bs, (const RecAt *)rat, t->pg.m, (const uint64_t *)t->pg.koff,
-                   (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz);
+                   (const uint64_t *)t->pg.voff, t->pg_slack, dirty, fpos, bx, sm, mode, rsz, t->pg_down);
         }
         LAUNCH(t, "page_place", k_page_place, (uint32_t)((S + 256 * PP_ITER - 1) / (256 * PP_ITER)), 256, 0, view(t), (const uint64_t *)bp.bseg_off,
                (const uint8_t *)t->ok, reject, mode, dirty, (const PlanSums *)rsz, rbase, acc, (const PrefixState *)ps,
@@ -1724,6 +1734,7 @@ static int ingest_paged(st_tree *t, IngestIn &in) {
         pa.e0 = g.use_e; pa.k0 = g.use_k; pa.v0 = g.use_v;
         pa.ce = g.cap_e; pa.ck = g.cap_k; pa.cv = g.cap_v;
         pa.acc = acc;
+        pa.slack_pct = t->pg_down ? t->pg_slack : -1;
         pa.chk = nullptr;
         // uniform pages a record of another length turns mixed: their offsets first
         LAUNCH(t, "page_merge", k_page_materialize, grid_for(S, 256, 4096), 256, 0, g.m, g.koff, g.voff,

@@ -7,7 +7,10 @@ pages back into the canonical CSR.  Every batch is checked against the C or
 Python restatement of insert/3 (synctree.erl:189-209, sequential inserts,
 last writer wins): top hash and entry count after every batch, every level's
 entries, and after folding the segments themselves (get, compare).  Small
-slack (st_debug_knob ST_DBG_PAGES) makes the tests cross moves and rebuilds.
+slack (st_debug_knob ST_DBG_PAGES) makes the tests cross moves and rebuilds;
+ST_DBG_PAGE_DOWN = 2 makes every in-place merge that fits shift the entries
+before its insert positions down into the page's head slack (1: when that
+moves fewer bytes; the default, 0, never shifts down).
 Needs an MI355X."""
 import numpy as np
 import pytest
@@ -34,14 +37,17 @@ def _obj(seqs, epoch=1):
     return v
 
 
-@pytest.mark.parametrize('segments,n0,batch,slack,check', [
-    (1 << 16, 300_000, 4_000, 1, True),      # H = 4, minimal slack: moves every batch, rebuilds
-    (1 << 16, 300_000, 4_000, 25, True),     # the default slack
-    (1 << 20, 1_000_000, 20_000, 2, True),   # H = 5, the config-5 geometry at 1/100 scale
-    (4096, 500_000, 6_000, 25, True),        # H = 3, ~120 entries a segment: pieces of kilobytes
-    (1 << 16, 300_000, 4_000, 2, False),     # the production merge (no checked stores), rebuilds and deletes
+@pytest.mark.parametrize('segments,n0,batch,slack,check,down', [
+    (1 << 16, 300_000, 4_000, 1, True, 0),      # H = 4, minimal slack: moves every batch, rebuilds
+    (1 << 16, 300_000, 4_000, 25, True, 0),     # the default slack
+    (1 << 20, 1_000_000, 20_000, 2, True, 0),   # H = 5, the config-5 geometry at 1/100 scale
+    (4096, 500_000, 6_000, 25, True, 0),        # H = 3, ~120 entries a segment: pieces of kilobytes
+    (1 << 16, 300_000, 4_000, 2, False, 0),     # the production merge (no checked stores), rebuilds and deletes
+    (4096, 500_000, 6_000, 25, True, 2),        # every in-place merge that fits shifts down (head slack)
+    (1 << 16, 300_000, 4_000, 2, False, 2),     # ... in the unchecked merge, with rebuilds
+    (4096, 500_000, 6_000, 25, True, 1),        # down when that moves fewer bytes
 ])
-def test_int_keys_stream_through_pages(segments, n0, batch, slack, check):
+def test_int_keys_stream_through_pages(segments, n0, batch, slack, check, down):
     rng = np.random.default_rng(segments ^ n0 ^ slack)
     keys = workload.keys_int63(n0 + 40 * batch, workload.SEED ^ 0xDE17A)
     dev = synctree_hip.DeviceTree(16, segments)
@@ -50,6 +56,7 @@ def test_int_keys_stream_through_pages(segments, n0, batch, slack, check):
     ora.bulk_load_int64(keys[:n0], _obj(range(n0)))
     dev.debug_knob(_lib.ST_DBG_PAGES, slack)
     dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1 if check else 0)   # every page store bounds-checked, every page validated
+    dev.debug_knob(_lib.ST_DBG_PAGE_DOWN, down)
     nxt = n0
     for b in range(30):
         old = rng.integers(0, nxt, batch // 2)                 # overwrites (Seq + 1), some repeated in the batch
@@ -127,8 +134,8 @@ def _rand_bin(rng, lo, hi):
     return bytes(rng.integers(0, 256, int(rng.integers(lo, hi + 1)), dtype=np.uint8))
 
 
-@pytest.mark.parametrize('slack', [1, 25])
-def test_variable_keys_and_values_through_pages(slack):
+@pytest.mark.parametrize('slack,down', [(1, 0), (25, 0), (1, 2), (25, 2)])
+def test_variable_keys_and_values_through_pages(slack, down):
     """Binary keys of 1..24 bytes and values of 0..40 bytes: overwrites that
     grow and shrink a value (tails moving right and left inside a page),
     empty values, segments outgrowing their pages."""
@@ -144,6 +151,7 @@ def test_variable_keys_and_values_through_pages(slack):
     ora.bulk_load(ks, [base[k] for k in ks])
     dev.debug_knob(_lib.ST_DBG_PAGES, slack)
     dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)   # every page store bounds-checked, every page validated
+    dev.debug_knob(_lib.ST_DBG_PAGE_DOWN, down)
     for b in range(12):
         bk = [ks[i] for i in rng.integers(0, len(ks), 300)] + [_rand_bin(rng, 1, 24) for _ in range(300)]
         bv = [_rand_bin(rng, 0, 40) for _ in bk]
@@ -161,7 +169,8 @@ def test_variable_keys_and_values_through_pages(slack):
     dev.close()
 
 
-def test_uniform_pages_turning_mixed():
+@pytest.mark.parametrize('down', [0, 2])
+def test_uniform_pages_turning_mixed(down):
     """Int keys with 17-byte values: every page is UNIFORM (one key length,
     one value length: only its first and end offset slots are kept, pages.h).
     Batches that put a longer value, a shorter value or a binary key into
@@ -175,6 +184,7 @@ def test_uniform_pages_turning_mixed():
     ora.bulk_load_int64(keys[:n0], _obj(range(n0)))
     dev.debug_knob(_lib.ST_DBG_PAGES, 3)
     dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
+    dev.debug_knob(_lib.ST_DBG_PAGE_DOWN, down)
     nxt = n0
     for b in range(16):
         if b % 4 == 3:   # a mixed batch: other value lengths, term keys, overwrites of uniform entries
@@ -203,7 +213,8 @@ def test_uniform_pages_turning_mixed():
     dev.close()
 
 
-def test_equal_numbers_through_pages():
+@pytest.mark.parametrize('down', [0, 2])
+def test_equal_numbers_through_pages(down):
     """1 and 1.0 are ONE key (synctree.erl:206 orddict:store compares with
     ==): a streamed float form replaces the integer entry with a longer key
     record, and the integer form replaces it back -- key byte shifts of both
@@ -219,6 +230,7 @@ def test_equal_numbers_through_pages():
     assert all(x is None for x in dev.insert_batch(ks, vs))
     dev.debug_knob(_lib.ST_DBG_PAGES, 5)
     dev.debug_knob(_lib.ST_DBG_PAGE_CHECK, 1)
+    dev.debug_knob(_lib.ST_DBG_PAGE_DOWN, down)
     pairs = [(a, b) for a, b in _same_segment_pairs(S, 40) if isinstance(a, int) and a < 3000]
     assert len(pairs) >= 10
     for b in range(8):

@@ -2,7 +2,8 @@
 range), then per-kernel times (HIP events on the library's stream,
 st_kernel_stats) over K timed 1M-key batches (50 % overwrites, 50 % new), then the wall
 time of K more such batches with no per-kernel events.
-Usage: python tools/part_breakdown.py [tree_keys] [batches] [csr]   (csr: pages off)"""
+Usage: python tools/part_breakdown.py [tree_keys] [batches] [csr|downN]
+(csr: pages off; downN: st_debug_knob ST_DBG_PAGE_DOWN = N)"""
 import os
 import sys
 import time
@@ -22,6 +23,9 @@ t = synctree_hip.DeviceTree()
 if len(sys.argv) > 3 and sys.argv[3] == 'csr':   # pages off: every batch merged into the CSR
     from riak_ensemble_amd import _lib  # noqa: E402
     t.debug_knob(_lib.ST_DBG_PAGES, -1)
+if len(sys.argv) > 3 and sys.argv[3].startswith('down'):   # which in-place merges shift down (pages.h)
+    from riak_ensemble_amd import _lib  # noqa: E402
+    t.debug_knob(_lib.ST_DBG_PAGE_DOWN, int(sys.argv[3][4:]))
 seed = 0x5EED0005
 for a in range(0, N, 10_000_000):
     m = min(10_000_000, N - a)
