@@ -25,7 +25,31 @@ __device__ __forceinline__ void load_block_join(const uint8_t *p, uint32_t m[16]
     for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], mis);
 }
 
-template <int MODE>   // 0: md5_global_span's loads; 1: joined dword loads
+// one 64-byte block from 16-byte aligned loads: 5 x 16 B, a dword shift by
+// (p & 12) / 4 in two conditional rounds, then v_alignbyte by p & 3
+__device__ __forceinline__ void load_block_shift(const uint8_t *p, uint32_t m[16]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(a & 15);
+    const uint4 *w = reinterpret_cast<const uint4 *>(a - sh);
+    uint32_t x[20];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint4 v = w[q];
+        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+    }
+    // the selects as bit-field inserts with all-ones / zero masks (a select of
+    // array elements became a dynamically indexed array in scratch)
+    const uint32_t M2 = (sh & 8) ? ~0u : 0u, M1 = (sh & 4) ? ~0u : 0u;
+    uint32_t y[18], z[17];
+#pragma unroll
+    for (int i = 0; i < 18; i++) y[i] = (x[i + 2] & M2) | (x[i] & ~M2);
+#pragma unroll
+    for (int i = 0; i < 17; i++) z[i] = (y[i + 1] & M1) | (y[i] & ~M1);
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_alignbyte(z[i + 1], z[i], sh & 3);
+}
+
+template <int MODE>   // 0: md5_global_span's loads; 1: joined dword loads; 2: 16-byte loads, shifted
 __global__ void __launch_bounds__(256) k(const uint8_t *base, uint32_t mis, uint32_t len, uint32_t *out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t *p = base + (uint64_t)i * 2048 + mis;
@@ -33,13 +57,15 @@ __global__ void __launch_bounds__(256) k(const uint8_t *base, uint32_t mis, uint
     stmd5::init(st);
     const uint32_t nblk = len / 64;
     uint32_t nx[16];
-    if (MODE == 0) stmd5::load_block_global(p, nx); else load_block_join(p, nx);
+    if (MODE == 0) stmd5::load_block_global(p, nx); else if (MODE == 1) load_block_join(p, nx); else load_block_shift(p, nx);
     for (uint32_t b = 0; b < nblk; b++) {
         uint32_t m[16];
 #pragma unroll
         for (int w = 0; w < 16; w++) m[w] = nx[w];
         if (b + 1 < nblk) {
-            if (MODE == 0) stmd5::load_block_global(p + 64 * (b + 1), nx); else load_block_join(p + 64 * (b + 1), nx);
+            if (MODE == 0) stmd5::load_block_global(p + 64 * (b + 1), nx);
+            else if (MODE == 1) load_block_join(p + 64 * (b + 1), nx);
+            else load_block_shift(p + 64 * (b + 1), nx);
         }
         stmd5::compress_lat(st, m);
     }
@@ -56,16 +82,18 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char *names[] = {"aligned 16", "aligned 4", "odd byte", "odd byte, joined dword loads", "aligned 16, joined"};
-    const uint32_t miss[] = {0, 4, 1, 1, 0};
-    const int modes[] = {0, 0, 0, 1, 1};
+    const char *names[] = {"aligned 16", "aligned 4", "odd byte", "odd byte, joined dword loads", "aligned 16, joined",
+                           "odd byte, 16 B loads shifted", "byte 7, 16 B loads shifted", "aligned 16, shifted"};
+    const uint32_t miss[] = {0, 4, 1, 1, 0, 1, 7, 0};
+    const int modes[] = {0, 0, 0, 1, 1, 2, 2, 2};
     for (int rep = 0; rep < 2; rep++)
-        for (int v = 0; v < 5; v++) {
+        for (int v = 0; v < 8; v++) {
             float best = 1e9f;
             for (int it = 0; it < 5; it++) {
                 hipEventRecord(a);
                 if (modes[v] == 0) hipLaunchKernelGGL(k<0>, dim3(n / 256), dim3(256), 0, 0, buf, miss[v], len, out);
-                else hipLaunchKernelGGL(k<1>, dim3(n / 256), dim3(256), 0, 0, buf, miss[v], len, out);
+                else if (modes[v] == 1) hipLaunchKernelGGL(k<1>, dim3(n / 256), dim3(256), 0, 0, buf, miss[v], len, out);
+                else hipLaunchKernelGGL(k<2>, dim3(n / 256), dim3(256), 0, 0, buf, miss[v], len, out);
                 hipEventRecord(b);
                 hipEventSynchronize(b);
                 float ms;
