@@ -298,7 +298,10 @@ __device__ __forceinline__ void krec9_load(const uint8_t *p, uint32_t &tag, uint
     const uint32_t p0 = (x >> 8) | (y << 24), p1 = (y >> 8) | (z << 24);
     pv = ((uint64_t)__builtin_bswap32(p0) << 32) | __builtin_bswap32(p1);
 }
-#define MI_W 16   // k_merge_keys' interpolation window (keys): 144 bytes, one round trip
+#ifndef MI_W
+#define MI_W 8    // k_merge_keys' interpolation window (keys): 72 bytes, one round trip (16: 0.19, 8: 0.175 ms
+                  // a config-5 batch's positions; 4: 0.186, 24: 0.24 -- profiles/r06ba_interp_window_ab/)
+#endif
 __device__ __forceinline__ void cas_kx(uint64_t &ka, uint32_t &ia, uint64_t &kb, uint32_t &ib) {
     const bool sw = kb < ka || (kb == ka && ib < ia);
     const uint64_t k = sw ? kb : ka, k2 = sw ? ka : kb;
